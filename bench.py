@@ -1,0 +1,237 @@
+"""Throughput bench: packet-steps/s @ 512^2 field, 1e6 packets per GPU.
+
+Workload (BASELINE.json configs[3], the metric's config): two-layer QG
+background (qg2layersw_raytrace.m: L = 20, wavenumbers scaled by 2*pi/L,
+shear_strength 0.5, packets advected in layer 1 so interpolate's y-period is
+2*nx), two spectral snapshots (prev_qk, qk) prepared on the GPU by grid_U
+(swrt_set_field_qk), 1e6 packets on the omega0 = 4f ring (f = 3, Cg = 1,
+Ug = 0.2) per GPU.  One bench step = one PDE interval dt = 0.25*dx/U0
+(CFL_fraction of qg2layersw_raytrace.m:31) advanced by `--substeps` fused
+leapfrog steps with the interpolate_U time blend.  Synthetic data: random
+phase ring spectrum 10 < |k| <= 30 (initial_q's ring), normalised so
+max|U| = Ug; a second snapshot with slightly rotated phases.
+
+Multi-GPU: one process per GPU (torch.distributed.run), packets sharded by
+rank (weak scaling: 1e6 per GPU), field replicated, no data-path collective;
+barrier + device sync around the timed region, max time over ranks.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+# torch first: libswrt must bind to the HIP runtime torch loads (one runtime).
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import swraytracing_amd as sw  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (spec)
+BYTES_STEADY = 1792          # 32+32 state + 1 snap * 6 fields * 36 taps * 8 B
+BYTES_BLEND = 3520           # 32+32 state + 2 snaps * 6 * 36 * 8 B
+
+
+def ring_spectrum(nx, kmin, kmax_ring, rng, phase_shift=0.0):
+    """Half-plane qk with unit-amplitude random phases on kmin < |k| <= kmax_ring."""
+    kmax = nx // 2 - 1
+    qk = np.zeros((2 * kmax + 1, kmax + 1), dtype=np.complex128)
+    ph = rng.uniform(0, 2 * np.pi, qk.shape) + phase_shift
+    kx = np.arange(-kmax, kmax + 1)[:, None]
+    ky = np.arange(0, kmax + 1)[None, :]
+    r2 = kx * kx + ky * ky
+    mask = (r2 > kmin * kmin) & (r2 <= kmax_ring * kmax_ring)
+    qk[mask] = np.exp(1j * ph[mask])
+    return qk
+
+
+def build_workload(ctx, args, rng):
+    nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
+    K_d2 = f / Cg
+    ks = 2 * np.pi / L
+    qk1 = ring_spectrum(nx, 10, 30, rng)
+    rng2 = np.random.default_rng(args.seed + 1)
+    qk2 = qk1 * np.exp(1j * rng2.normal(0, 0.05, qk1.shape))
+    # normalise to max|U| = Ug (initial_q, qg2layersw_raytrace.m:279-280)
+    ctx.set_field_qk(0, qk1, nx, L, K_d2, 0.0, ks, 2 * nx)
+    p = ctx.get_field_grid(0, nx)
+    scale = Ug / math.sqrt(float((p[0] ** 2 + p[1] ** 2).max()))
+    qk1 *= scale
+    qk2 *= scale
+    shear = 0.5
+    nslots = 1 if args.mode == "steady" else 2
+    ctx.set_field_qk(0, qk1, nx, L, K_d2, shear, ks, 2 * nx)
+    if nslots == 2:
+        ctx.set_field_qk(1, qk2, nx, L, K_d2, shear, ks, 2 * nx)
+    p = ctx.get_field_grid(0, nx)
+    U0 = math.sqrt(float((p[0] ** 2 + p[1] ** 2).max()))
+    dt = 0.25 * (L / nx) / U0  # qg2layersw_raytrace.m:31,78
+    N = args.packets
+    w0 = 4.0
+    wf = math.sqrt((w0 ** 2 - 1) * f ** 2 / Cg ** 2)
+    i = np.arange(1, N + 1, dtype=np.float64) + args.rank * N
+    Ntot = N * args.world
+    k = np.stack([wf * np.cos(2 * np.pi * i / Ntot), wf * np.sin(2 * np.pi * i / Ntot)], axis=1)
+    x = L * rng.random((N, 2)) - L / 2
+    return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
+                K_d2=K_d2, ks=ks, shear=shear)
+
+
+def step(ctx, w, sub):
+    h = w["dt"] / sub
+    ctx.advance(h, sub, w["f"], w["gH"], nslots=w["nslots"], alpha0=0.5 / sub, dalpha=1.0 / sub,
+                bump=sw.BUMP_QG)
+
+
+def cpu_baseline(ctx, w, target_s):
+    """The C oracle (OpenMP) on this host: same fields, same algorithm."""
+    from oracle import cbind
+    cbind.build()
+    nx = w["nx"]
+    p0 = ctx.get_field_grid(0, nx)
+    p1 = ctx.get_field_grid(1, nx) if w["nslots"] == 2 else None
+    threads = cbind.lib().oracle_num_threads()
+
+    def run(n, steps):
+        x = w["x"][:n]
+        k = w["k"][:n]
+        t0 = time.perf_counter()
+        cbind.leapfrog(p0, p1, 0.5, 0.0, nx, 2 * nx, w["L"] / nx, sw.BUMP_QG, x, k, w["dt"], steps,
+                       w["f"], w["gH"])
+        return time.perf_counter() - t0
+
+    n = min(20000, w["x"].shape[0])
+    t = run(n, 1)
+    rate = n / max(t, 1e-9)
+    steps = max(1, int(target_s * rate / n))
+    t = run(n, steps)
+    return {"value": n * steps / t, "unit": "packet-steps/s", "cores": int(threads), "kind": "port",
+            "sample": f"{n} packets x {steps} leapfrog steps of the same {nx}^2 two-snapshot field "
+                      f"(oracle/swrt_oracle.c, OpenMP {threads} threads, {t:.1f} s)"}
+
+
+def load_traffic(config_key):
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        return d.get(config_key)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nx", type=int, default=512)
+    ap.add_argument("--packets", type=int, default=1_000_000, help="packets per GPU (weak scaling)")
+    ap.add_argument("--substeps", type=int, default=1, help="leapfrog steps per bench step")
+    ap.add_argument("--mode", choices=["blend", "steady"], default="blend")
+    ap.add_argument("--seed", type=int, default=146)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    args.world, args.rank = world, rank
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+
+    ctx = sw.Context(local)
+    rng = np.random.default_rng(args.seed + rank)
+    w = build_workload(ctx, args, rng)
+    ctx.packets_set(w["x"], w["k"])
+
+    def barrier_sync():
+        ctx.synchronize()
+        torch.cuda.synchronize(dev)
+        if distributed:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step(ctx, w, args.substeps)
+    barrier_sync()
+    ctx.kernel_time(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(ctx, w, args.substeps)
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if distributed:
+        dist.barrier()
+    elapsed = t1 - t0
+    kms, launches = ctx.kernel_time(reset=True)
+    if distributed:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    xg, kg = ctx.packets_get()
+    finite = bool(np.isfinite(xg).all() and np.isfinite(kg).all())
+
+    N = args.packets
+    total_ps = N * world * args.substeps * args.steps
+    value = total_ps / elapsed
+    B = BYTES_BLEND if w["nslots"] == 2 else BYTES_STEADY
+    avg_launch_s = (kms / 1e3) / max(launches, 1)
+    ps_per_launch = N * args.substeps  # one launch advances all local packets by `substeps` steps
+    achieved_gbs = ps_per_launch * B / avg_launch_s / 1e9
+    # fp64 VALU work per packet-step of the exact-order stencil
+    key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}"
+    traffic = load_traffic(key)
+    out = {
+        "metric": "packet-steps/sec @ 512² field, 1e6 packets; 1/2/4/8-GPU scaling",
+        "value": value,
+        "unit": "packet-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic",
+        "config": {"workload": "qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
+                               f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, "
+                               f"{args.nx}^2x2 field, {N} packets/GPU, leapfrog",
+                   "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
+                   "mode": args.mode, "parallelism": f"packets sharded x{world}, field replicated"},
+        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "bytes_per_packet_step": B, "avg_launch_ms": avg_launch_s * 1e3,
+                     "launches": launches},
+        "finite": finite,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(ctx, w, args.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

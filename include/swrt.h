@@ -1,0 +1,155 @@
+/*
+ * swrt.h — C ABI of the MI355X-native wave-packet ray-tracing hot path
+ * (ndefilippis/SWRaytracing, qg_flow_ray_trace hot loop).
+ *
+ * The reference is MATLAB and has no native interface; each entry point below
+ * names the MATLAB function (file:line, paths relative to the reference root)
+ * whose behaviour it replaces.  A MEX gateway (matlab/swrt_mex.cpp) and the
+ * Python ctypes front-end (swraytracing_amd/) bind exactly these symbols.
+ *
+ * Conventions
+ *  - Every function returns an int status: SWRT_OK (0) or a SWRT_ERR_* code;
+ *    swrt_last_error(ctx) returns a message for the last failure on ctx.
+ *    No C++ exception or longjmp crosses this ABI.
+ *  - Host buffers are caller-owned, fp64, MATLAB column-major, and are never
+ *    retained after a call returns.  The context owns all device memory.
+ *  - Packet arrays are N x 2 column-major: x(:,1) (all x) then x(:,2) (all y),
+ *    the layout of packet_x / packet_k in qgsw_raytrace.m:54-55 and of one
+ *    frame of packet_x.bin (write_field.m:38).
+ *  - Gridded fields are nx x nx column-major, first index = x: F(ig, jg) at
+ *    x = (ig-1)*dx, y = (jg-1)*dx (k2g.m / interpolate.m conventions).
+ *  - One context per host thread; calls are synchronous with respect to the
+ *    host (stream-ordered internally); not re-entrant on the same context.
+ */
+#ifndef SWRT_H
+#define SWRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SWRT_OK 0
+#define SWRT_ERR_ARG 1   /* invalid argument (shape, slot, null pointer) */
+#define SWRT_ERR_HIP 2   /* HIP runtime error */
+#define SWRT_ERR_STATE 3 /* call out of order (e.g. field not set) */
+#define SWRT_ERR_ALLOC 4 /* allocation failure */
+
+#define SWRT_MAX_SLOTS 2 /* snapshot slots: 0 = flow1 / steady, 1 = flow2 */
+
+typedef struct swrt_ctx swrt_ctx;
+
+/* ABI version (major*10000 + minor*100 + patch). */
+int swrt_version(void);
+
+/* Create a context bound to HIP device `device` (one process per GPU). */
+int swrt_create(int device, swrt_ctx** out);
+void swrt_destroy(swrt_ctx* ctx);
+const char* swrt_last_error(const swrt_ctx* ctx);
+
+/* ---------------------------------------------------------------------------
+ * Background flow (L1/L2: field preparation, once per snapshot)
+ * ------------------------------------------------------------------------ */
+
+/* Six gridded fields (u, v, u_x, u_y, v_x, v_y), each nx*nx column-major,
+ * concatenated.  Replaces holding SpectralScheme.U_field / GradU_field
+ * (SpectralScheme.m:29-35) or a grid_U output struct (grid_U.m:11-17).
+ * ny_period: the y-period of interpolate.m's mod (interpolate.m:15,22): nx for
+ * a single layer, nlayers*nx for the 2-layer call (qg2layersw_raytrace.m:187-188)
+ * where F is nx x nx x 2 and only layer 1 is read.  0 means nx. */
+int swrt_set_field_grid(swrt_ctx* ctx, int slot, const double* fields6, int64_t nx, double L,
+                        int64_t ny_period);
+
+/* SpectralScheme(L, nx, psi_field) constructor (SpectralScheme.m:6-36):
+ * psik = g2k(psi); u = k2g(-i ky psik), v = k2g(i kx psik), gradients by
+ * i kx / i ky; integer wavenumbers regardless of L.  FFTs run on the GPU.
+ * The filtered psi grid k2g(g2k(psi)) is kept for swrt_get_psi_grid. */
+int swrt_set_field_psi(swrt_ctx* ctx, int slot, const double* psi_grid, int64_t nx, double L);
+
+/* grid_U(qk, K_d2, K2, kx_, ky_, shear_strength) (grid_U.m:1-18) for one
+ * layer: psik = -qk./(K_d2+K2), six derivative spectra, k2g on the GPU,
+ * u += shear.  qk: (2kmax+1) x (kmax+1) complex, column-major, interleaved
+ * (re, im) (MATLAB -R2018a interleaved complex).  k_scale multiplies the
+ * integer wavenumbers (1 for qgsw_raytrace.m:19, 2*pi/L for
+ * qg2layersw_raytrace.m:20-21).  ny_period as in swrt_set_field_grid. */
+int swrt_set_field_qk(swrt_ctx* ctx, int slot, const double* qk_interleaved, int64_t nx, double L,
+                      double K_d2, double shear, double k_scale, int64_t ny_period);
+
+/* g2k(fg) (g2k.m:5-9): nx x nx real grid (column-major) -> the
+ * (2kmax+1) x (kmax+1) half-plane spectrum fftshift(fft2(fg))/nx^2 cropped,
+ * interleaved complex, column-major.  GPU FFT. */
+int swrt_g2k(swrt_ctx* ctx, const double* fg, int64_t nx, double* fk_interleaved_out);
+/* k2g(fk) (k2g.m:5-6 + fulspec.m): half-plane spectrum -> nx x nx real grid
+ * nx^2*ifft2(ifftshift(fulspec(fk))) (real part), column-major.  GPU FFT. */
+int swrt_k2g(swrt_ctx* ctx, const double* fk_interleaved, int64_t nx, double* fg_out);
+
+/* Download slot's six fields (nx*nx column-major each) — for checks/plots. */
+int swrt_get_field_grid(swrt_ctx* ctx, int slot, double* fields6_out);
+/* Download the filtered psi grid of the last swrt_set_field_psi (nx*nx). */
+int swrt_get_psi_grid(swrt_ctx* ctx, int slot, double* psi_out);
+
+/* ---------------------------------------------------------------------------
+ * Point evaluation (L2 boundary API)
+ * ------------------------------------------------------------------------ */
+
+/* interpolate(x, y, F, dx, dy) (interpolate.m:1-50) of an arbitrary nx x nyF
+ * grid field F (only the first nx columns are read when nyF > nx, as MATLAB's
+ * 2-subscript F(ig,jg) does), with the given bump (1e-10:
+ * qg_flow_ray_trace/interpolate.m:13; 1e-13: ray_trace_sw/interpolate.m:13). */
+int swrt_interpolate(swrt_ctx* ctx, const double* F, int64_t nx, int64_t nyF, double dx, double dy,
+                     double bump, const double* x, const double* y, int64_t n, double* out);
+
+/* U and grad U at n points from the slot fields: out is 6 x n row-major
+ * (u, v, u_x, u_y, v_x, v_y).  nslots = 1: slot 0 only (SpectralScheme.U /
+ * grad_U, SpectralScheme.m:45-68).  nslots = 2: interpolate_U's blend
+ * (1-alpha)*slot0 + alpha*slot1 (interpolate_U.m:5-23). */
+int swrt_eval(swrt_ctx* ctx, const double* x, const double* y, int64_t n, int nslots, double alpha,
+              double bump, double* out6);
+
+/* ---------------------------------------------------------------------------
+ * Packets and the fused symplectic integrator (L3)
+ * ------------------------------------------------------------------------ */
+
+/* Upload / download packet state (N x 2 column-major x and k). */
+int swrt_packets_set(swrt_ctx* ctx, const double* x, const double* k, int64_t n);
+int swrt_packets_get(swrt_ctx* ctx, double* x, double* k);
+int64_t swrt_packets_count(const swrt_ctx* ctx);
+
+/* Advance the device-resident packets by nsteps leapfrog steps
+ * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
+ * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of
+ * step s uses alpha = alpha0 + s*dalpha when nslots == 2.  bump: Lagrange
+ * bump.  If save_every > 0 a frame (N x 2 x, then N x 2 k) is recorded on the
+ * device after every save_every steps (frames appended to the history
+ * buffer, see swrt_history_*). */
+int swrt_advance(swrt_ctx* ctx, double dt, int64_t nsteps, double f, double gH, int nslots,
+                 double alpha0, double dalpha, double bump, int64_t save_every);
+
+/* History frames recorded by swrt_advance since the last swrt_history_reset. */
+int64_t swrt_history_frames(const swrt_ctx* ctx);
+int swrt_history_get(swrt_ctx* ctx, int64_t first, int64_t count, double* hist_x, double* hist_k);
+int swrt_history_reset(swrt_ctx* ctx);
+
+/* Host convenience = packets_set + advance + packets_get (+ history): the
+ * drop-in for ode_symplectic(x0,k0,dt,T,f,gH,scheme) (ode_symplectic.m:1-31).
+ * hist_x / hist_k may be NULL; otherwise they receive nsteps/save_every frames
+ * of N x 2 each. */
+int swrt_leapfrog(swrt_ctx* ctx, double* x, double* k, int64_t n, double dt, int64_t nsteps,
+                  double f, double gH, int nslots, double alpha0, double dalpha, double bump,
+                  int64_t save_every, double* hist_x, double* hist_k);
+
+/* ---------------------------------------------------------------------------
+ * Runtime helpers
+ * ------------------------------------------------------------------------ */
+int swrt_synchronize(swrt_ctx* ctx);
+/* The hipStream_t all of ctx's work is ordered on (for external event timing). */
+int swrt_get_stream(swrt_ctx* ctx, void** stream_out);
+/* Sum of HIP-event-measured durations of the packet kernel launches since the
+ * last reset (synchronizes). */
+int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SWRT_H */

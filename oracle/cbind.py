@@ -1,0 +1,74 @@
+"""ctypes binding of the C oracle (oracle/build/libswrt_oracle.so).
+
+TEST INFRASTRUCTURE ONLY — used by tests/ and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "libswrt_oracle.so")
+_lib = None
+
+_D = ctypes.c_double
+_I = ctypes.c_int64
+_P = ctypes.POINTER(ctypes.c_double)
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.oracle_eval.argtypes = [_P, _P, _D, _I, _D, _D, _D, _P, _P, _I, _P]
+        L.oracle_eval.restype = None
+        L.oracle_leapfrog.argtypes = [_P, _P, _D, _D, _I, _D, _D, _D, _P, _P, _I, _D, _I, _D, _D,
+                                      _I, _P, _P]
+        L.oracle_leapfrog.restype = None
+        L.oracle_num_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_P) if a is not None else None
+
+
+def planes_of(fields):
+    """dict of 6 grids (u,v,ux,uy,vx,vy) -> contiguous 6 x nx*nx column-major planes."""
+    from .swrt_oracle import FIELD_ORDER  # noqa: E402  (package-relative when imported as oracle.cbind)
+    return np.ascontiguousarray(np.stack([np.asarray(fields[n], dtype=np.float64).ravel(order="F")
+                                          for n in FIELD_ORDER]))
+
+
+def eval6(planes0, planes1, alpha, nx, nyF, dx, bump, x, y):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    out = np.empty((6, x.size))
+    lib().oracle_eval(_ptr(planes0), _ptr(planes1), alpha, nx, float(nyF), dx, bump, _ptr(x), _ptr(y),
+                      x.size, _ptr(out))
+    return out
+
+
+def leapfrog(planes0, planes1, alpha0, dalpha, nx, nyF, dx, bump, x, k, dt, nsteps, f, gH,
+             save_every=0):
+    """State x, k: N x 2 (any order) -> returns new (x, k) N x 2 and history frames."""
+    x = np.asfortranarray(x, dtype=np.float64).copy(order="F")
+    k = np.asfortranarray(k, dtype=np.float64).copy(order="F")
+    n = x.shape[0]
+    nfr = nsteps // save_every if save_every else 0
+    hx = np.empty((nfr, 2, n)) if nfr else None
+    hk = np.empty((nfr, 2, n)) if nfr else None
+    lib().oracle_leapfrog(_ptr(planes0), _ptr(planes1), alpha0, dalpha, nx, float(nyF), dx, bump,
+                          x.ctypes.data_as(_P), k.ctypes.data_as(_P), n, dt, nsteps, f, gH,
+                          save_every if nfr else 0, _ptr(hx), _ptr(hk))
+    return x, k, hx, hk

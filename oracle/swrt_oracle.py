@@ -1,0 +1,555 @@
+"""CPU oracle for the qg_flow_ray_trace hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is a plain-numpy restatement of the MATLAB reference
+(ndefilippis/SWRaytracing) for the wave-packet ray-tracing hot loop.  It exists
+to *check* the HIP product path; it is never imported by the product package
+(`swraytracing_amd/`), only by `tests/`, `__graft_entry__.smoke()` and the
+`cpu_baseline` leg of `bench.py`.
+
+Parity status: the reference is MATLAB and cannot run
+in this container (no MATLAB/Octave), and it ships no numeric golden vectors,
+fixtures or tests.  This restatement is therefore pinned by analytic known
+answers only (zero background flow, single Fourier mode, the closed-form
+random Fourier field of scratch/fourier_interpolate_test.m, k2g(g2k(f)) == f,
+Lagrange-weight identities) — "parity pinned to analytic KATs; no
+reference-produced vectors exist".
+
+Every function follows the cited .m file line by line, including operation
+order (so that the same IEEE-754 double operations happen in the same order as
+in MATLAB's scalar loops), MATLAB `mod` semantics and the 1-based index maths
+(done here 0-based with identical results).
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+IORD = 2  # interpolate.m:12 — 6x6 Lagrange stencil
+BUMP_QG = 1e-10  # qg_flow_ray_trace/interpolate.m:13
+BUMP_SW = 1e-13  # ray_trace_sw/interpolate.m:13 (SpectralScheme path via addpath, SpectralScheme.m:7-8)
+
+
+# ----------------------------------------------------------------------------
+# MATLAB primitives
+# ----------------------------------------------------------------------------
+def matlab_mod(a, m):
+    """MATLAB mod(a, m) = a - floor(a./m).*m for m > 0 (documented definition).
+
+    With integer m (always the case here: m = nx or nlayers*nx) MATLAB's
+    round-off compensation for non-integer divisors does not apply.
+    """
+    a = np.asarray(a, dtype=np.float64)
+    return a - np.floor(a / m) * m
+
+
+# ----------------------------------------------------------------------------
+# L1 spectral utilities — qg_flow_ray_trace/{g2k,k2g,fulspec,apply_3d}.m
+# ----------------------------------------------------------------------------
+def g2k(fg):
+    """g2k.m:5-9: fk = fftshift(fft2(fg))/nx^2, rows 2:end, cols kmax+2:end."""
+    fg = np.asarray(fg, dtype=np.float64)
+    nx = fg.shape[0]
+    kmax = nx // 2 - 1
+    fkt = np.fft.fftshift(np.fft.fft2(fg)) / nx**2
+    return fkt[1:, kmax + 1:].copy()
+
+
+def fulspec(fk):
+    """fulspec.m:10-19: Hermitian completion of the upper-half spectrum."""
+    fk = np.asarray(fk, dtype=np.complex128)
+    nkx, nky = fk.shape
+    nx = nkx + 1
+    kmax = nky - 1
+    fkf = np.zeros((nx, nx), dtype=np.complex128)
+    fup = fk.copy()
+    # fup(kmax:-1:1,1) = conj(fup(kmax+2:nkx,1))      (fulspec.m:16)
+    fup[kmax - 1::-1, 0] = np.conj(fup[kmax + 1:nkx, 0])
+    # fdn = conj(fup(nkx:-1:1,nky:-1:2))              (fulspec.m:17)
+    fdn = np.conj(fup[::-1, nky - 1:0:-1])
+    fkf[1:nx, nky:nx] = fup  # fulspec.m:18
+    fkf[1:nx, 1:nky] = fdn  # fulspec.m:19
+    return fkf
+
+
+def k2g(fk):
+    """k2g.m:5-6: fg = nx^2*ifft2(ifftshift(fulspec(fk))).
+
+    The completed spectrum is Hermitian except possibly an imaginary DC part;
+    MATLAB would then return a complex array whose real part is what every
+    consumer (interpolate) effectively uses.  We return the real part.
+    """
+    fk = np.asarray(fk, dtype=np.complex128)
+    nx = fk.shape[0] + 1
+    fg = nx**2 * np.fft.ifft2(np.fft.ifftshift(fulspec(fk)))
+    return np.ascontiguousarray(fg.real)
+
+
+def apply_3d(x, f):
+    """apply_3d.m:1-7 — apply f per layer along the 3rd dimension."""
+    x = np.asarray(x)
+    if x.ndim == 2:
+        return f(x)
+    first = f(x[:, :, 0])
+    y = np.zeros(first.shape + (x.shape[2],), dtype=first.dtype)
+    for i in range(x.shape[2]):
+        y[:, :, i] = f(x[:, :, i])
+    return y
+
+
+def wavenumber_grids(nx, L=2 * math.pi, scale=False):
+    """[kx_,ky_] = ndgrid(-kmax:kmax, 0:kmax) (qgsw_raytrace.m:18-20).
+
+    With scale=True multiply by 2*pi/L (qg2layersw_raytrace.m:19-22).
+    """
+    kmax = nx // 2 - 1
+    kx_, ky_ = np.meshgrid(np.arange(-kmax, kmax + 1, dtype=np.float64),
+                           np.arange(0, kmax + 1, dtype=np.float64), indexing="ij")
+    if scale:
+        kx_ = kx_ * (2 * math.pi / L)
+        ky_ = ky_ * (2 * math.pi / L)
+    K2 = kx_**2 + ky_**2
+    return kx_, ky_, K2
+
+
+def grid_U(qk, K_d2, K2, kx_, ky_, shear_strength=0.0):
+    """grid_U.m:1-18 (6th argument defaults to 0: the 5-arg call sites at
+    qgsw_raytrace.m:63,141-142 predate it).  Returns dict of 6 grid fields."""
+    qk = np.asarray(qk, dtype=np.complex128)
+    if qk.ndim == 3:
+        K2b, kxb, kyb = K2[:, :, None], kx_[:, :, None], ky_[:, :, None]
+    else:
+        K2b, kxb, kyb = K2, kx_, ky_
+    psik = -qk / (K_d2 + K2b)
+    vk = 1j * kxb * psik
+    uk = -1j * kyb * psik
+    ukx = 1j * kxb * uk
+    uky = 1j * kyb * uk
+    vkx = 1j * kxb * vk
+    vky = 1j * kyb * vk
+    return {
+        "u": apply_3d(uk, k2g) + shear_strength,
+        "v": apply_3d(vk, k2g),
+        "ux": apply_3d(ukx, k2g),
+        "uy": apply_3d(uky, k2g),
+        "vx": apply_3d(vkx, k2g),
+        "vy": apply_3d(vky, k2g),
+    }
+
+
+def spectral_scheme_fields(L, nx, psi_field):
+    """SpectralScheme.m:6-36 constructor: psi grid -> 7 grid fields.
+
+    Integer wavenumbers regardless of L (SpectralScheme.m:12-13)."""
+    kmax = nx // 2 - 1
+    kx_, ky_ = np.meshgrid(np.arange(-kmax, kmax + 1, dtype=np.float64),
+                           np.arange(0, kmax + 1, dtype=np.float64), indexing="ij")
+    psik = g2k(psi_field)
+    ugk = -1j * ky_ * psik
+    vgk = 1j * kx_ * psik
+    ugxk = 1j * kx_ * ugk
+    ugyk = 1j * ky_ * ugk
+    vgxk = 1j * kx_ * vgk
+    vgyk = 1j * ky_ * vgk
+    return {
+        "psi": k2g(psik),
+        "u": k2g(ugk),
+        "v": k2g(vgk),
+        "ux": k2g(ugxk),
+        "uy": k2g(ugyk),
+        "vx": k2g(vgxk),
+        "vy": k2g(vgyk),
+    }
+
+
+FIELD_ORDER = ("u", "v", "ux", "uy", "vx", "vy")
+
+
+# ----------------------------------------------------------------------------
+# L2 — periodic 6x6 Lagrange interpolation (interpolate.m:1-50)
+# ----------------------------------------------------------------------------
+def lagrange_weights(a, bump):
+    """interpolate.m:33-41: w(i) = prod_{j!=i} (a - j + bump)/(j - i), i,j in -2..3.
+
+    Evaluated exactly in the reference order (j inner, running product,
+    multiply-then-divide)."""
+    a = np.asarray(a, dtype=np.float64)
+    w = [np.ones_like(a) for _ in range(2 * (IORD + 1))]
+    for i in range(-IORD, IORD + 2):
+        for j in range(-IORD, IORD + 2):
+            if i != j:
+                w[i + IORD] = w[i + IORD] * (a - float(j) + bump) / float(j - i)
+    return w
+
+
+def _cell_and_frac(x, dx, period):
+    """interpolate.m:21-31: xl = mod(x/dx, n); i0 = 1+floor(xl); a = 1+xl-i0.
+
+    Returns 0-based cell index (i0-1, may equal `period` after round-up of
+    mod) and the fractional offset a."""
+    xl = matlab_mod(np.asarray(x, dtype=np.float64) / dx, float(period))
+    fl = np.floor(xl)
+    i0 = 1.0 + fl
+    a = (1.0 + xl) - i0
+    return fl.astype(np.int64), a
+
+
+def interpolate(x, y, F, dx, dy, bump=BUMP_QG):
+    """interpolate.m:1-50 vectorised over packets (per-packet arithmetic is
+    bit-identical to the scalar loop: same ops, same order).
+
+    F: nx x ny grid (first index = x).  A 3-D nx x nx x nz F reproduces the
+    2-layer call (CS3): [nx,ny]=size(F) gives ny = nx*nz for the y-mod and
+    2-subscript F(ig,jg) with jg<=nx reads layer 1."""
+    F = np.asarray(F, dtype=np.float64)
+    nx = F.shape[0]
+    ny = int(np.prod(F.shape[1:]))
+    F2 = F if F.ndim == 2 else F[:, :, 0]
+    x = np.asarray(x, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    shape = x.shape
+    x = x.ravel()
+    y = y.ravel()
+    ic, ax = _cell_and_frac(x, dx, nx)
+    jc, ay = _cell_and_frac(y, dy, ny)
+    wx = lagrange_weights(ax, bump)
+    wy = lagrange_weights(ay, bump)
+    FI = np.zeros_like(x)
+    for i in range(-IORD, IORD + 2):
+        ig = np.mod(ic + i, nx)  # ig = 1 + mod(i0 + i - 1, nx)
+        for j in range(-IORD, IORD + 2):
+            jg = np.mod(jc + j, nx)  # jg = 1 + mod(j0 + j - 1, nx)  (nx, not ny: :46)
+            FI = FI + wx[i + IORD] * wy[j + IORD] * F2[ig, jg]
+    return FI.reshape(shape)
+
+
+def interpolate_fields(x, y, fields, dx, bump, nyF=None):
+    """Interpolate the 6 fields (FIELD_ORDER) at the points: 6 x N array.
+
+    Same arithmetic as 6 calls of `interpolate` (the Lagrange weights and the
+    2-D weight products are identical across calls)."""
+    return np.stack([interpolate(x, y, _as_F(fields[name], nyF), dx, dx, bump)
+                     for name in FIELD_ORDER])
+
+
+def _as_F(f, nyF):
+    f = np.asarray(f, dtype=np.float64)
+    if nyF is None or f.ndim == 3:
+        return f
+    nz = nyF // f.shape[0]
+    if nz == 1:
+        return f
+    # present as a 3-D array so interpolate() uses ny = nz*nx in the y-mod
+    out = np.zeros(f.shape + (nz,))
+    out[:, :, 0] = f
+    return out
+
+
+def interpolate_U(flow1, flow2, alpha, x, h, bump=BUMP_QG, nyF=None):
+    """interpolate_U.m:1-24 — 12 interpolations and the linear time blend.
+
+    x: N x 2.  Returns U (N x 2) and dict u_x,u_y,v_x,v_y (N,)."""
+    xx = x[:, 0]
+    yy = x[:, 1]
+    I1 = {n: interpolate(xx, yy, _as_F(flow1[n], nyF), h, h, bump) for n in FIELD_ORDER}
+    I2 = {n: interpolate(xx, yy, _as_F(flow2[n], nyF), h, h, bump) for n in FIELD_ORDER}
+    U1 = np.stack([I1["u"], I1["v"]], axis=1)
+    U2 = np.stack([I2["u"], I2["v"]], axis=1)
+    U = (1 - alpha) * U1 + alpha * U2
+    nab = {
+        "u_x": (1 - alpha) * I1["ux"] + alpha * I2["ux"],
+        "u_y": (1 - alpha) * I1["uy"] + alpha * I2["uy"],
+        "v_x": (1 - alpha) * I1["vx"] + alpha * I2["vx"],
+        "v_y": (1 - alpha) * I1["vy"] + alpha * I2["vy"],
+    }
+    return U, nab
+
+
+# ----------------------------------------------------------------------------
+# L2 boundary API — RaytracingScheme.m / SpectralScheme.m
+# ----------------------------------------------------------------------------
+class SpectralSchemeOracle:
+    """SpectralScheme(L, nx, psi_field) (SpectralScheme.m:1-70) + the concrete
+    RaytracingScheme methods (RaytracingScheme.m:9-26).
+
+    `interpolate` resolves to ray_trace_sw/interpolate.m after the
+    constructor's addpath (CS2), hence bump = 1e-13."""
+
+    def __init__(self, L, nx, psi_field, bump=BUMP_SW):
+        self.L = L
+        self.nx = nx
+        self.bump = bump
+        fl = spectral_scheme_fields(L, nx, psi_field)
+        self.psi_field = fl.pop("psi")
+        self.fields = fl  # u, v, ux, uy, vx, vy
+
+    @property
+    def dx(self):
+        return self.L / self.psi_field.shape[0]  # SpectralScheme.m:46
+
+    def streamfunction(self, x, y, t=0.0):
+        return interpolate(x, y, self.psi_field, self.dx, self.dx, self.bump)
+
+    def U(self, x, t=0.0):
+        """x: M x 2 x P (or N x 2) -> same shape (SpectralScheme.m:45-54)."""
+        x = np.asarray(x, dtype=np.float64)
+        xx = x[:, 0, ...]
+        yy = x[:, 1, ...]
+        u = np.zeros_like(x)
+        u[:, 0, ...] = interpolate(xx, yy, self.fields["u"], self.dx, self.dx, self.bump)
+        u[:, 1, ...] = interpolate(xx, yy, self.fields["v"], self.dx, self.dx, self.bump)
+        return u
+
+    def grad_U(self, x, t=0.0):
+        """SpectralScheme.m:56-68 — struct of column vectors (numel(x)/2)."""
+        x = np.asarray(x, dtype=np.float64)
+        xx = np.ravel(x[:, 0, ...], order="F")
+        yy = np.ravel(x[:, 1, ...], order="F")
+        d = self.dx
+        return {
+            "u_x": interpolate(xx, yy, self.fields["ux"], d, d, self.bump),
+            "u_y": interpolate(xx, yy, self.fields["uy"], d, d, self.bump),
+            "v_x": interpolate(xx, yy, self.fields["vx"], d, d, self.bump),
+            "v_y": interpolate(xx, yy, self.fields["vy"], d, d, self.bump),
+        }
+
+    def grad_U_times_k(self, x, k, t=0.0):
+        """RaytracingScheme.m:9-16."""
+        nab = self.grad_U(x, t)
+        k = np.asarray(k, dtype=np.float64)
+        kk = np.ravel(k[:, 0, ...], order="F")
+        ll = np.ravel(k[:, 1, ...], order="F")
+        out = np.zeros_like(k)
+        shp = k[:, 0, ...].shape
+        out[:, 0, ...] = np.reshape(nab["u_x"] * kk + nab["v_x"] * ll, shp, order="F")
+        out[:, 1, ...] = np.reshape(nab["u_y"] * kk + nab["v_y"] * ll, shp, order="F")
+        return out
+
+    def vorticity(self, x, t=0.0):
+        nab = self.grad_U(x, t)
+        return nab["v_x"] - nab["u_y"]  # RaytracingScheme.m:18-21
+
+    def strain(self, x, t=0.0):
+        nab = self.grad_U(x, t)  # RaytracingScheme.m:23-26
+        return np.sqrt((nab["u_x"] - nab["v_y"]) ** 2 + (nab["v_x"] + nab["u_y"]) ** 2)
+
+
+# ----------------------------------------------------------------------------
+# L3 — ode_symplectic.m (Strang / leapfrog)
+# ----------------------------------------------------------------------------
+def _omega(k1, k2, f, gH):
+    """ode_symplectic.m:10 — sqrt(f^2 + gH*dot(k,k,2))."""
+    return np.sqrt(f * f + gH * (k1 * k1 + k2 * k2))
+
+
+def ode_symplectic(x0, k0, dt, T, f, gH, scheme):
+    """ode_symplectic.m:1-31 verbatim semantics.  x0, k0: 1 x 2 x P.
+
+    Returns x, k: Nsteps x 2 x P and t: (Nsteps,)."""
+    Nsteps = int(math.floor(T / dt))
+    x0 = np.array(x0, dtype=np.float64)
+    k0 = np.array(k0, dtype=np.float64)
+    P = x0.shape[2]
+    x = np.zeros((Nsteps, 2, P))
+    k = np.zeros((Nsteps, 2, P))
+    t = np.zeros(Nsteps)
+    x[0] = x0[0]
+    k[0] = k0[0]
+
+    def group_velocity(kk):
+        w = _omega(kk[:, 0:1, :], kk[:, 1:2, :], f, gH)
+        return gH * kk / w
+
+    def phi1(xa, ka, h):
+        return xa + h * group_velocity(ka), ka
+
+    def phi2(xa, ka, h):
+        return xa + h * scheme.U(xa), ka - h * scheme.grad_U_times_k(xa, ka, 0)
+
+    for i in range(1, Nsteps):
+        x1, k1 = phi1(x0, k0, dt / 2)
+        x2, k2 = phi2(x1, k1, dt)
+        x0, k0 = phi1(x2, k2, dt / 2)
+        x[i] = x0[0]
+        k[i] = k0[0]
+        t[i] = i * dt
+    return x, k, t
+
+
+@dataclass
+class GridField:
+    """Six gridded fields (u, v, u_x, u_y, v_x, v_y) of one snapshot.
+
+    nyF is the y-period used by interpolate's mod (nx for 1 layer, nz*nx for
+    the 2-layer call of qg2layersw_raytrace.m:187-188)."""
+    fields: dict
+    dx: float
+    nyF: int | None = None
+
+
+def leapfrog(x, k, dt, nsteps, f, gH, snap0: GridField, snap1: GridField | None = None,
+             alpha0=0.0, dalpha=0.0, bump=BUMP_SW, save_every=0):
+    """Vectorised `ode_symplectic` inner loop (ode_symplectic.m:23-37) on
+    N x 2 state, generalised to a two-snapshot time blend: the kick of step s
+    evaluates U, grad U with interpolate_U's blend (interpolate_U.m:19-23) at
+    alpha = alpha0 + s*dalpha.  With snap1=None this is exactly the steady
+    SpectralScheme path (scheme time 0).
+
+    Returns (x, k, hist_x, hist_k): hist frames are N x 2 arrays after every
+    `save_every` steps (packet_x.bin frame layout, write_field.m:38)."""
+    x = np.array(x, dtype=np.float64)
+    k = np.array(k, dtype=np.float64)
+    hx, hk = [], []
+    half = dt / 2
+    for s in range(nsteps):
+        # phi1(x0, k0, dt/2)
+        w = _omega(k[:, 0], k[:, 1], f, gH)
+        x1 = np.stack([x[:, 0] + half * (gH * k[:, 0] / w),
+                       x[:, 1] + half * (gH * k[:, 1] / w)], axis=1)
+        # phi2(x1, k1, dt): U and grad U at x1
+        if snap1 is None:
+            I = interpolate_fields(x1[:, 0], x1[:, 1], snap0.fields, snap0.dx, bump, snap0.nyF)
+            u, v, ux, uy, vx, vy = I
+        else:
+            alpha = alpha0 + s * dalpha
+            U, nab = interpolate_U(snap0.fields, snap1.fields, alpha, x1, snap0.dx, bump, snap0.nyF)
+            u, v = U[:, 0], U[:, 1]
+            ux, uy, vx, vy = nab["u_x"], nab["u_y"], nab["v_x"], nab["v_y"]
+        k1, l1 = k[:, 0], k[:, 1]
+        x2 = np.stack([x1[:, 0] + dt * u, x1[:, 1] + dt * v], axis=1)
+        k2 = np.stack([k1 - dt * (ux * k1 + vx * l1), l1 - dt * (uy * k1 + vy * l1)], axis=1)
+        # phi1(x2, k2, dt/2)
+        w = _omega(k2[:, 0], k2[:, 1], f, gH)
+        x = np.stack([x2[:, 0] + half * (gH * k2[:, 0] / w),
+                      x2[:, 1] + half * (gH * k2[:, 1] / w)], axis=1)
+        k = k2
+        if save_every and (s + 1) % save_every == 0:
+            hx.append(x.copy())
+            hk.append(k.copy())
+    return x, k, hx, hk
+
+
+# ----------------------------------------------------------------------------
+# Exact Fourier-mode kick (scratch/fourier_interpolate_test.m:92-136) — KAT source
+# ----------------------------------------------------------------------------
+def fourier_velocity(x, y, amp, phase, n):
+    """fourier_interpolate_test.m:125-136: U for psi = sum A cos(Kx+Ly+phi)."""
+    u = np.zeros_like(x, dtype=np.float64)
+    v = np.zeros_like(y, dtype=np.float64)
+    for K in range(-n, n + 1):
+        for Lw in range(-n, n + 1):
+            a = amp[K + n, Lw + n]
+            s = np.sin(K * x + Lw * y + phase[K + n, Lw + n])
+            u = u + -Lw * a * -s
+            v = v + K * a * -s
+    return u, v
+
+
+def fourier_streamfunction(X, Y, amp, phase, n):
+    """fourier_interpolate_test.m:116-123."""
+    psi = np.zeros_like(X, dtype=np.float64)
+    for K in range(-n, n + 1):
+        for Lw in range(-n, n + 1):
+            psi = psi + amp[K + n, Lw + n] * np.cos(K * X + Lw * Y + phase[K + n, Lw + n])
+    return psi
+
+
+def fourier_grad(x, y, amp, phase, n):
+    """Closed-form grad U of the same field (u = -psi_y, v = psi_x)."""
+    ux = np.zeros_like(x); uy = np.zeros_like(x); vx = np.zeros_like(x); vy = np.zeros_like(x)
+    for K in range(-n, n + 1):
+        for Lw in range(-n, n + 1):
+            a = amp[K + n, Lw + n]
+            c = np.cos(K * x + Lw * y + phase[K + n, Lw + n])
+            # psi = a cos(th): psi_x = -aK sin, psi_y = -aL sin
+            # u = -psi_y = aL sin -> u_x = aLK cos, u_y = aL^2 cos
+            # v = psi_x = -aK sin -> v_x = -aK^2 cos, v_y = -aKL cos
+            ux = ux + a * Lw * K * c
+            uy = uy + a * Lw * Lw * c
+            vx = vx - a * K * K * c
+            vy = vy - a * K * Lw * c
+    return ux, uy, vx, vy
+
+
+def fourier_phi2(x0, k0, dt, amp, phase, n):
+    """fourier_interpolate_test.m:92-114 exact kick (x0,k0: N x 2)."""
+    xx, yy = x0[:, 0], x0[:, 1]
+    kk, ll = k0[:, 0], k0[:, 1]
+    ux_ = np.zeros_like(xx); uy_ = np.zeros_like(xx); uk_ = np.zeros_like(xx); ul_ = np.zeros_like(xx)
+    for K in range(-n, n + 1):
+        for Lw in range(-n, n + 1):
+            c = K * xx + Lw * yy
+            a = Lw * kk - K * ll
+            A = amp[K + n, Lw + n]
+            ph = phase[K + n, Lw + n]
+            ux_ = ux_ - dt * Lw * A * -np.sin(c + ph)
+            uy_ = uy_ + dt * K * A * -np.sin(c + ph)
+            uk_ = uk_ + dt * K * A * -np.cos(c + ph) * a
+            ul_ = ul_ + dt * Lw * A * -np.cos(c + ph) * a
+    return (np.stack([xx + ux_, yy + uy_], axis=1), np.stack([kk + uk_, ll + ul_], axis=1))
+
+
+# ----------------------------------------------------------------------------
+# I/O — write_field.m / read_field.m (raw native-endian fp64, appended frames)
+# ----------------------------------------------------------------------------
+def write_field(field, fname, frame=1):
+    """write_field.m:22-49: append column-major fp64 frame; complex = re then im."""
+    field = np.asarray(field)
+    with open(str(fname) + ".bin", "ab") as fh:
+        if np.iscomplexobj(field):
+            fh.write(np.asfortranarray(field.real, dtype=np.float64).tobytes(order="F"))
+            fh.write(np.asfortranarray(field.imag, dtype=np.float64).tobytes(order="F"))
+        else:
+            fh.write(np.asarray(field, dtype=np.float64).tobytes(order="F"))
+
+
+def read_field(fname, nx=1, ny=1, nz=1, frames=None):
+    """read_field.m:58-101 for real fields: returns nx x ny (x nz) x frames."""
+    data = np.fromfile(str(fname) + ".bin", dtype=np.float64)
+    if nx == 1:
+        return data[None, :]
+    per = nx * ny * nz
+    nfr = data.size // per
+    frames = list(range(1, nfr + 1)) if frames is None else list(frames)
+    out = np.stack([data[(fr - 1) * per: fr * per].reshape((nx, ny, nz), order="F") for fr in frames],
+                   axis=-1)
+    return np.squeeze(out)
+
+
+# ----------------------------------------------------------------------------
+# Synthetic inputs (qgsw_raytrace.m:191-214, :54-60) with a numpy RNG
+# ----------------------------------------------------------------------------
+def initial_q(nx, L, a_g, K_d2, k_min, k_max, rng):
+    """initial_q (qgsw_raytrace.m:191-214; k in (5,8]; 2-layer: (10,30],
+    qg2layersw_raytrace.m:258-281).  Grid X,Y = meshgrid(linspace(-L/2,L/2,nx))
+    as in the reference (note: linspace includes both ends, not periodic)."""
+    xs = np.linspace(-L / 2, L / 2, nx)
+    X, Y = np.meshgrid(xs, xs)  # qgsw_raytrace.m:15-16 (meshgrid)
+    q = 0 * X
+    U = 0 * X
+    V = 0 * X
+    phase = 2 * np.pi * rng.random((2 * k_max + 1, 2 * k_max + 1))
+    for k in range(-k_max, k_max + 1):
+        for l in range(-k_max, k_max + 1):
+            if k_min**2 < k**2 + l**2 <= k_max**2:
+                wave_phase = k * X + l * Y + phase[k + k_max, l + k_max]
+                U = U - l * np.sin(wave_phase)
+                V = V + k * np.sin(wave_phase)
+                q = q - (K_d2 + k**2 + l**2) * np.cos(wave_phase)
+    speed2 = U**2 + V**2
+    return a_g / np.sqrt(speed2.max()) * q
+
+
+def initial_packets(N, L, near_inertial_factor, f, Cg, rng):
+    """qgsw_raytrace.m:54-60: k on a ring, x uniform in [-L/2, L/2)^2."""
+    wf = math.sqrt((near_inertial_factor**2 - 1) * f**2 / Cg**2)
+    i = np.arange(1, N + 1, dtype=np.float64)
+    k = np.stack([wf * np.cos(2 * np.pi * i / N), wf * np.sin(2 * np.pi * i / N)], axis=1)
+    x = L * rng.random((N, 2)) - L / 2
+    return x, k
+
+
+def here():
+    return os.path.dirname(os.path.abspath(__file__))

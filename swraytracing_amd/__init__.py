@@ -1,0 +1,18 @@
+"""swraytracing_amd — MI355X-native wave-packet ray tracing (gfx950 HIP).
+
+The qg_flow_ray_trace hot loop of ndefilippis/SWRaytracing (ode_symplectic
+over SpectralScheme / interpolate_U / grid_U / g2k / k2g) as hand-written
+CDNA4 kernels behind the C ABI in include/swrt.h, with the reference's
+MATLAB call surface mirrored in Python.
+"""
+from ._lib import Context, SwrtError, load
+from .integrate import PacketEnsemble, ode_symplectic
+from .io import read_field, write_field
+from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, RaytracingScheme, SnapshotPairScheme,
+                     SpectralScheme, g2k, grid_U, interpolate, interpolate_U, k2g)
+
+__all__ = [
+    "Context", "SwrtError", "load", "PacketEnsemble", "ode_symplectic", "read_field", "write_field",
+    "BUMP_QG", "BUMP_SW", "DifferenceScheme", "RaytracingScheme", "SnapshotPairScheme",
+    "SpectralScheme", "g2k", "grid_U", "interpolate", "interpolate_U", "k2g",
+]

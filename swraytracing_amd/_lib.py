@@ -1,0 +1,267 @@
+"""ctypes binding of libswrt.so (the C ABI in include/swrt.h).
+
+There is no CPU fallback: if the HIP library is missing or the device call
+fails, the error propagates.  Build it with
+``python -c "import __graft_entry__ as g; g.build()"`` (hipcc, gfx950).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+# One HIP runtime per process: torch wheels ship their own libamdhip64.so.7.
+# Import torch (if present) before dlopen-ing libswrt so that our NEEDED
+# libamdhip64.so.7 resolves to the runtime torch already loaded, instead of a
+# second copy from /opt/rocm.
+try:  # pragma: no cover - import side effect only
+    import torch  # noqa: F401
+except Exception:  # torch absent: the system HIP runtime is used
+    pass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libswrt.so")
+
+SWRT_OK = 0
+ERRORS = {1: "SWRT_ERR_ARG", 2: "SWRT_ERR_HIP", 3: "SWRT_ERR_STATE", 4: "SWRT_ERR_ALLOC"}
+
+_D = ctypes.c_double
+_I = ctypes.c_int64
+_INT = ctypes.c_int
+_P = ctypes.POINTER(ctypes.c_double)
+_VP = ctypes.c_void_p
+
+# name -> (restype, argtypes).  Kept in the order of include/swrt.h.
+SIGNATURES = {
+    "swrt_version": (_INT, []),
+    "swrt_create": (_INT, [_INT, ctypes.POINTER(_VP)]),
+    "swrt_destroy": (None, [_VP]),
+    "swrt_last_error": (ctypes.c_char_p, [_VP]),
+    "swrt_set_field_grid": (_INT, [_VP, _INT, _P, _I, _D, _I]),
+    "swrt_set_field_psi": (_INT, [_VP, _INT, _P, _I, _D]),
+    "swrt_set_field_qk": (_INT, [_VP, _INT, _P, _I, _D, _D, _D, _D, _I]),
+    "swrt_get_field_grid": (_INT, [_VP, _INT, _P]),
+    "swrt_get_psi_grid": (_INT, [_VP, _INT, _P]),
+    "swrt_g2k": (_INT, [_VP, _P, _I, _P]),
+    "swrt_k2g": (_INT, [_VP, _P, _I, _P]),
+    "swrt_interpolate": (_INT, [_VP, _P, _I, _I, _D, _D, _D, _P, _P, _I, _P]),
+    "swrt_eval": (_INT, [_VP, _P, _P, _I, _INT, _D, _D, _P]),
+    "swrt_packets_set": (_INT, [_VP, _P, _P, _I]),
+    "swrt_packets_get": (_INT, [_VP, _P, _P]),
+    "swrt_packets_count": (_I, [_VP]),
+    "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
+    "swrt_history_frames": (_I, [_VP]),
+    "swrt_history_get": (_INT, [_VP, _I, _I, _P, _P]),
+    "swrt_history_reset": (_INT, [_VP]),
+    "swrt_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT, _D, _D, _D, _I, _P, _P]),
+    "swrt_synchronize": (_INT, [_VP]),
+    "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
+    "swrt_kernel_time": (_INT, [_VP, _INT, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
+}
+
+_lib = None
+
+
+class SwrtError(RuntimeError):
+    pass
+
+
+def load():
+    """dlopen libswrt.so (no HIP call is made by loading)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: the HIP extension is not built "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'`). "
+            "There is no CPU fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(_P)
+
+
+def _f64(a, order="C"):
+    return np.require(np.asarray(a, dtype=np.float64), requirements=[order[0] + "_CONTIGUOUS", "ALIGNED"])
+
+
+class Context:
+    """Owns one swrt_ctx (device buffers + HIP stream) on one GPU."""
+
+    def __init__(self, device: int = 0):
+        self._L = load()
+        h = _VP()
+        rc = self._L.swrt_create(int(device), ctypes.byref(h))
+        if rc != SWRT_OK:
+            raise SwrtError(f"swrt_create(device={device}) failed: {ERRORS.get(rc, rc)}")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.swrt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != SWRT_OK:
+            msg = self._L.swrt_last_error(self._h)
+            raise SwrtError(f"{what}: {ERRORS.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    # ---- fields ---------------------------------------------------------
+    def set_field_grid(self, slot, planes6, nx, L, ny_period=0):
+        planes6 = _f64(planes6)
+        assert planes6.size == 6 * nx * nx
+        self._chk(self._L.swrt_set_field_grid(self._h, slot, _p(planes6), nx, float(L), ny_period),
+                  "swrt_set_field_grid")
+
+    def set_field_psi(self, slot, psi_grid, nx, L):
+        psi = _f64(np.asarray(psi_grid, dtype=np.float64).ravel(order="F"))
+        assert psi.size == nx * nx
+        self._chk(self._L.swrt_set_field_psi(self._h, slot, _p(psi), nx, float(L)), "swrt_set_field_psi")
+
+    def set_field_qk(self, slot, qk, nx, L, K_d2, shear=0.0, k_scale=1.0, ny_period=0):
+        qk = np.asarray(qk, dtype=np.complex128)
+        kmax = nx // 2 - 1
+        assert qk.shape == (2 * kmax + 1, kmax + 1), qk.shape
+        buf = _f64(np.asfortranarray(qk).ravel(order="F").view(np.float64))
+        self._chk(self._L.swrt_set_field_qk(self._h, slot, _p(buf), nx, float(L), float(K_d2),
+                                            float(shear), float(k_scale), ny_period),
+                  "swrt_set_field_qk")
+
+    def get_field_grid(self, slot, nx):
+        out = np.empty(6 * nx * nx)
+        self._chk(self._L.swrt_get_field_grid(self._h, slot, _p(out)), "swrt_get_field_grid")
+        return out.reshape(6, nx * nx)
+
+    def get_psi_grid(self, slot, nx):
+        out = np.empty(nx * nx)
+        self._chk(self._L.swrt_get_psi_grid(self._h, slot, _p(out)), "swrt_get_psi_grid")
+        return out.reshape((nx, nx), order="F")
+
+    def g2k(self, fg):
+        fg = np.asarray(fg, dtype=np.float64)
+        nx = fg.shape[0]
+        kmax = nx // 2 - 1
+        src = _f64(fg.ravel(order="F"))
+        out = np.empty(2 * (2 * kmax + 1) * (kmax + 1))
+        self._chk(self._L.swrt_g2k(self._h, _p(src), nx, _p(out)), "swrt_g2k")
+        return out.view(np.complex128).reshape((2 * kmax + 1, kmax + 1), order="F")
+
+    def k2g(self, fk):
+        fk = np.asarray(fk, dtype=np.complex128)
+        nx = fk.shape[0] + 1
+        src = _f64(np.asfortranarray(fk).ravel(order="F").view(np.float64))
+        out = np.empty(nx * nx)
+        self._chk(self._L.swrt_k2g(self._h, _p(src), nx, _p(out)), "swrt_k2g")
+        return out.reshape((nx, nx), order="F")
+
+    # ---- evaluation -------------------------------------------------------
+    def interpolate(self, x, y, F, dx, dy, bump):
+        F = np.asarray(F, dtype=np.float64)
+        nx = F.shape[0]
+        nyF = int(np.prod(F.shape[1:]))
+        Fc = _f64(F.reshape(nx, -1, order="F")[:, :nx].ravel(order="F"))
+        x = np.asarray(x, dtype=np.float64)
+        shape = x.shape
+        xf = _f64(x.ravel())
+        yf = _f64(np.asarray(y, dtype=np.float64).ravel())
+        out = np.empty(xf.size)
+        self._chk(self._L.swrt_interpolate(self._h, _p(Fc), nx, nyF, float(dx), float(dy), float(bump),
+                                           _p(xf), _p(yf), xf.size, _p(out)), "swrt_interpolate")
+        return out.reshape(shape)
+
+    def eval(self, x, y, nslots=1, alpha=0.0, bump=1e-13):
+        xf = _f64(np.asarray(x, dtype=np.float64).ravel())
+        yf = _f64(np.asarray(y, dtype=np.float64).ravel())
+        out = np.empty((6, xf.size))
+        self._chk(self._L.swrt_eval(self._h, _p(xf), _p(yf), xf.size, nslots, float(alpha), float(bump),
+                                    _p(out)), "swrt_eval")
+        return out
+
+    # ---- packets ---------------------------------------------------------
+    def packets_set(self, x, k):
+        """x, k: N x 2 arrays (converted to column-major)."""
+        x = np.asfortranarray(x, dtype=np.float64)
+        k = np.asfortranarray(k, dtype=np.float64)
+        assert x.shape == k.shape and x.ndim == 2 and x.shape[1] == 2
+        self._chk(self._L.swrt_packets_set(self._h, _p(x), _p(k), x.shape[0]), "swrt_packets_set")
+
+    def packets_get(self):
+        n = self._L.swrt_packets_count(self._h)
+        x = np.empty((n, 2), order="F")
+        k = np.empty((n, 2), order="F")
+        self._chk(self._L.swrt_packets_get(self._h, _p(x), _p(k)), "swrt_packets_get")
+        return x, k
+
+    def advance(self, dt, nsteps, f, gH, nslots=1, alpha0=0.0, dalpha=0.0, bump=1e-13, save_every=0):
+        self._chk(self._L.swrt_advance(self._h, float(dt), int(nsteps), float(f), float(gH), int(nslots),
+                                       float(alpha0), float(dalpha), float(bump), int(save_every)),
+                  "swrt_advance")
+
+    def history(self, first=0, count=None):
+        n = self._L.swrt_packets_count(self._h)
+        total = self._L.swrt_history_frames(self._h)
+        count = total - first if count is None else count
+        hx = np.empty((count, 2, n))
+        hk = np.empty((count, 2, n))
+        self._chk(self._L.swrt_history_get(self._h, first, count, _p(hx), _p(hk)), "swrt_history_get")
+        return hx, hk
+
+    def history_reset(self):
+        self._chk(self._L.swrt_history_reset(self._h), "swrt_history_reset")
+
+    def leapfrog(self, x, k, dt, nsteps, f, gH, nslots=1, alpha0=0.0, dalpha=0.0, bump=1e-13,
+                 save_every=0):
+        x = np.array(x, dtype=np.float64, order="F")
+        k = np.array(k, dtype=np.float64, order="F")
+        n = x.shape[0]
+        nfr = nsteps // save_every if save_every else 0
+        hx = np.empty((nfr, 2, n)) if nfr else None
+        hk = np.empty((nfr, 2, n)) if nfr else None
+        self._chk(self._L.swrt_leapfrog(self._h, _p(x), _p(k), n, float(dt), int(nsteps), float(f),
+                                        float(gH), int(nslots), float(alpha0), float(dalpha),
+                                        float(bump), int(save_every) if nfr else 0, _p(hx), _p(hk)),
+                  "swrt_leapfrog")
+        return x, k, hx, hk
+
+    # ---- runtime ---------------------------------------------------------
+    def synchronize(self):
+        self._chk(self._L.swrt_synchronize(self._h), "swrt_synchronize")
+
+    def stream(self):
+        s = _VP()
+        self._chk(self._L.swrt_get_stream(self._h, ctypes.byref(s)), "swrt_get_stream")
+        return s.value
+
+    def kernel_time(self, reset=True):
+        ms = _D()
+        n = _I()
+        self._chk(self._L.swrt_kernel_time(self._h, int(reset), ctypes.byref(ms), ctypes.byref(n)),
+                  "swrt_kernel_time")
+        return ms.value, n.value
+
+
+def exported_symbols():
+    """Names the header declares (for the ABI export test)."""
+    return list(SIGNATURES)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    load()
+    print("libswrt loaded:", LIB_PATH, file=sys.stderr)

@@ -1,0 +1,750 @@
+// swrt_api.hip — the C ABI (include/swrt.h) over the gfx950 kernels.
+//
+// Host-side orchestration only: device buffers owned by the context, one HIP
+// stream per context, every call synchronous to the host and exception-free
+// across the ABI boundary.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/swrt.h"
+#include "swrt_fft.hpp"
+#include "swrt_kernels.hpp"
+
+using namespace swrt;
+
+namespace {
+
+constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
+
+struct Slot {
+  double* nodes = nullptr;  // padded interleaved records
+  double* psi = nullptr;    // filtered psi plane (swrt_set_field_psi)
+  int64_t nx = 0;
+  int64_t npad = 0;
+  int64_t ny_period = 0;
+  double L = 0.0;
+  bool set = false;
+  bool has_psi = false;
+};
+
+struct Timing {
+  std::vector<hipEvent_t> ev;  // pairs
+  size_t used = 0;             // events used (2 per launch)
+  double folded_ms = 0.0;      // elapsed of pairs already folded (ring recycled)
+  int64_t folded_n = 0;
+};
+constexpr size_t kMaxEvents = 2048;
+
+}  // namespace
+
+struct swrt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  Slot slot[SWRT_MAX_SLOTS];
+  // packets
+  double* dx = nullptr;  // 2N
+  double* dk = nullptr;  // 2N
+  int64_t n = 0;
+  int64_t cap = 0;
+  // history
+  double* hx = nullptr;
+  double* hk = nullptr;
+  int64_t hframes = 0;
+  int64_t hcap = 0;  // frames allocated
+  int64_t steps_done = 0;  // global step counter since history reset (for save cadence)
+  // scratch
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  double2* tw = nullptr;
+  int tw_n = 0;
+  Timing timing;
+};
+
+namespace {
+
+int fail(swrt_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                   \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(ctx, SWRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
+  } while (0)
+
+#define GUARD_BEGIN try {
+#define GUARD_END(ctx)                                                \
+  }                                                                   \
+  catch (const std::bad_alloc&) {                                     \
+    return fail(ctx, SWRT_ERR_ALLOC, "host allocation failed");       \
+  }                                                                   \
+  catch (...) {                                                       \
+    return fail(ctx, SWRT_ERR_STATE, "unexpected C++ exception");     \
+  }
+
+bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
+
+int ensure_scratch(swrt_ctx* c, size_t bytes) {
+  if (c->scratch_bytes >= bytes) return SWRT_OK;
+  if (c->scratch) (void)hipFree(c->scratch);
+  c->scratch = nullptr;
+  c->scratch_bytes = 0;
+  HIPCHK(c, hipMalloc(&c->scratch, bytes));
+  c->scratch_bytes = bytes;
+  return SWRT_OK;
+}
+
+int ensure_twiddles(swrt_ctx* c, int n) {
+  if (c->tw_n == n) return SWRT_OK;
+  if (c->tw) (void)hipFree(c->tw);
+  c->tw = nullptr;
+  std::vector<double2> h(n / 2);
+  for (int k = 0; k < n / 2; ++k) {
+    // exp(-2*pi*i*k/n); long double for the argument reduction
+    const long double th = -2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
+    h[k] = make_double2((double)cosl(th), (double)sinl(th));
+  }
+  HIPCHK(c, hipMalloc(&c->tw, sizeof(double2) * (n / 2)));
+  HIPCHK(c, hipMemcpyAsync(c->tw, h.data(), sizeof(double2) * (n / 2), hipMemcpyHostToDevice,
+                           c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->tw_n = n;
+  return SWRT_OK;
+}
+
+int ensure_slot(swrt_ctx* c, int slot, int64_t nx) {
+  Slot& s = c->slot[slot];
+  const int64_t npad = nx + kPadTot;
+  if (s.nodes && s.nx == nx) return SWRT_OK;
+  if (s.nodes) (void)hipFree(s.nodes);
+  if (s.psi) (void)hipFree(s.psi);
+  s.nodes = nullptr;
+  s.psi = nullptr;
+  s.set = false;
+  HIPCHK(c, hipMalloc(&s.nodes, sizeof(double) * kRec * npad * npad));
+  s.nx = nx;
+  s.npad = npad;
+  return SWRT_OK;
+}
+
+int check_slot_args(swrt_ctx* c, int slot, int64_t nx) {
+  if (!c) return SWRT_ERR_ARG;
+  if (slot < 0 || slot >= SWRT_MAX_SLOTS) return fail(c, SWRT_ERR_ARG, "slot out of range");
+  if (nx < 8 || nx > 4096 || (nx & 1)) return fail(c, SWRT_ERR_ARG, "nx must be even, 8..4096");
+  return SWRT_OK;
+}
+
+FieldView view_of(const Slot& s) {
+  FieldView v;
+  v.nodes = s.nodes;
+  v.nx = (int)s.nx;
+  v.npad = (int)s.npad;
+  v.dx = s.L / (double)s.nx;
+  v.px = (double)s.nx;
+  v.py = (double)s.ny_period;
+  v.inv_px = 1.0 / v.px;
+  v.inv_py = 1.0 / v.py;
+  v.pow2x = is_pow2(s.nx);
+  v.pow2y = is_pow2(s.ny_period);
+  return v;
+}
+
+inline unsigned nblocks(int64_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+// Pack 6 device planes (already in scratch) into the slot's node array.
+int pack_slot(swrt_ctx* c, int slot, const double* dplanes, double shear) {
+  Slot& s = c->slot[slot];
+  const int64_t tot = s.npad * s.npad;
+  hipLaunchKernelGGL(pack_nodes_kernel, dim3(nblocks(tot, 256)), dim3(256), 0, c->stream, dplanes,
+                     (int)s.nx, (int)s.npad, shear, s.nodes);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+
+int run_fft_pass(swrt_ctx* c, double2* Z, int n, int nb, int inverse) {
+  int logn = 0;
+  while ((1 << logn) < n) ++logn;
+  const size_t lds = sizeof(double2) * 2 * n;
+  hipLaunchKernelGGL(fft_vec_kernel, dim3((unsigned)(n * nb)), dim3(256), lds, c->stream, Z, n,
+                     logn, c->tw, inverse);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+
+int run_transpose(swrt_ctx* c, const double2* in, double2* out, int n, int nb) {
+  dim3 grid((n + 31) / 32, (n + 31) / 32, nb);
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(32, 8), 0, c->stream, in, out, n);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+
+// Inverse 2-D transform of nb spectra in layout [c + n*r] (ky contiguous);
+// result in layout [r + n*c] (x contiguous) in `out`.
+int inverse_2d(swrt_ctx* c, double2* Z, double2* out, int n, int nb) {
+  int rc;
+  if ((rc = run_fft_pass(c, Z, n, nb, 1))) return rc;   // along ky
+  if ((rc = run_transpose(c, Z, out, n, nb))) return rc;
+  if ((rc = run_fft_pass(c, out, n, nb, 1))) return rc;  // along kx
+  return SWRT_OK;
+}
+
+// Shared tail of set_field_psi / set_field_qk: fk half-plane in device memory.
+int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int mode, double K_d2,
+                          double kscale, double shear, int with_psi, double2* Z, double2* T) {
+  int rc;
+  const int64_t nn = (int64_t)n * n;
+  const int nb = with_psi ? 4 : 3;
+  hipLaunchKernelGGL(spectra_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, dfk, n, mode,
+                     K_d2, kscale, with_psi, Z);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = inverse_2d(c, Z, T, n, nb))) return rc;
+  // T now holds fields in [r + n*c]; unpair into planes (reuse Z as planes buffer)
+  double* planes = reinterpret_cast<double*>(Z);
+  Slot& s = c->slot[slot];
+  if (with_psi && !s.psi) HIPCHK(c, hipMalloc(&s.psi, sizeof(double) * nn));
+  hipLaunchKernelGGL(unpair_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, n, with_psi,
+                     planes, with_psi ? s.psi : nullptr);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = pack_slot(c, slot, planes, shear))) return rc;
+  s.has_psi = with_psi != 0;
+  return SWRT_OK;
+}
+
+int launch_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int nslots,
+                   double alpha0, double dalpha, double bump, int64_t save_every) {
+  StepArgs a;
+  a.f0 = view_of(c->slot[0]);
+  a.f1 = nslots == 2 ? view_of(c->slot[1]) : a.f0;
+  a.nslots = nslots;
+  a.x = c->dx;
+  a.k = c->dk;
+  a.n = c->n;
+  a.dt = dt;
+  a.half = dt / 2;
+  a.f2 = f * f;
+  a.gH = gH;
+  a.alpha0 = alpha0;
+  a.dalpha = dalpha;
+  a.bump = bump;
+  a.save_every = save_every > 0 ? save_every : 1;
+  a.hist_x = save_every > 0 ? c->hx : nullptr;
+  a.hist_k = save_every > 0 ? c->hk : nullptr;
+  a.frame0 = c->hframes;
+  const unsigned grid = nblocks(c->n, 256);
+  for (int64_t s0 = 0; s0 < nsteps; s0 += kMaxStepsPerLaunch) {
+    a.s0 = s0;
+    a.nsteps = (int)std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
+    // timing events (pairs), grown on demand; fold into a running sum when full
+    if (c->timing.used + 2 > kMaxEvents) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      for (size_t i = 0; i + 1 < c->timing.used; i += 2) {
+        float ms = 0.f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->timing.ev[i], c->timing.ev[i + 1]));
+        c->timing.folded_ms += ms;
+        c->timing.folded_n += 1;
+      }
+      c->timing.used = 0;
+    }
+    if (c->timing.used + 2 > c->timing.ev.size()) {
+      for (int e = 0; e < 64; ++e) {
+        hipEvent_t ev;
+        HIPCHK(c, hipEventCreate(&ev));
+        c->timing.ev.push_back(ev);
+      }
+    }
+    hipEvent_t e0 = c->timing.ev[c->timing.used], e1 = c->timing.ev[c->timing.used + 1];
+    c->timing.used += 2;
+    HIPCHK(c, hipEventRecord(e0, c->stream));
+    hipLaunchKernelGGL(leapfrog_kernel, dim3(grid), dim3(256), 0, c->stream, a);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(e1, c->stream));
+  }
+  return SWRT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int swrt_version(void) { return 100; }
+
+int swrt_create(int device, swrt_ctx** out) {
+  if (!out) return SWRT_ERR_ARG;
+  *out = nullptr;
+  swrt_ctx* c = nullptr;
+  try {
+    c = new swrt_ctx();
+  } catch (...) {
+    return SWRT_ERR_ALLOC;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    delete c;
+    return SWRT_ERR_HIP;
+  }
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return SWRT_ERR_HIP;
+  }
+  *out = c;
+  return SWRT_OK;
+}
+
+void swrt_destroy(swrt_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& s : c->slot) {
+    if (s.nodes) (void)hipFree(s.nodes);
+    if (s.psi) (void)hipFree(s.psi);
+  }
+  if (c->dx) (void)hipFree(c->dx);
+  if (c->dk) (void)hipFree(c->dk);
+  if (c->hx) (void)hipFree(c->hx);
+  if (c->hk) (void)hipFree(c->hk);
+  if (c->scratch) (void)hipFree(c->scratch);
+  if (c->tw) (void)hipFree(c->tw);
+  for (auto e : c->timing.ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* swrt_last_error(const swrt_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int swrt_set_field_grid(swrt_ctx* c, int slot, const double* fields6, int64_t nx, double L,
+                        int64_t ny_period) {
+  int rc = check_slot_args(c, slot, nx);
+  if (rc) return rc;
+  GUARD_BEGIN
+  if (!fields6) return fail(c, SWRT_ERR_ARG, "fields6 is NULL");
+  if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
+  if (ny_period == 0) ny_period = nx;
+  if (ny_period % nx) return fail(c, SWRT_ERR_ARG, "ny_period must be a multiple of nx");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_slot(c, slot, nx))) return rc;
+  const size_t bytes = sizeof(double) * 6 * nx * nx;
+  if ((rc = ensure_scratch(c, bytes))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->scratch, fields6, bytes, hipMemcpyHostToDevice, c->stream));
+  if ((rc = pack_slot(c, slot, (const double*)c->scratch, 0.0))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  Slot& s = c->slot[slot];
+  s.L = L;
+  s.ny_period = ny_period;
+  s.has_psi = false;
+  s.set = true;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_set_field_psi(swrt_ctx* c, int slot, const double* psi_grid, int64_t nx, double L) {
+  int rc = check_slot_args(c, slot, nx);
+  if (rc) return rc;
+  GUARD_BEGIN
+  if (!psi_grid) return fail(c, SWRT_ERR_ARG, "psi_grid is NULL");
+  if (!is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two for the GPU FFT");
+  if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_slot(c, slot, nx))) return rc;
+  if ((rc = ensure_twiddles(c, (int)nx))) return rc;
+  const int n = (int)nx;
+  const int64_t nn = nx * nx;
+  const int kmax = n / 2 - 1;
+  const int64_t nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
+  // scratch: Z (4 nn complex) | T (4 nn complex) | fk (nhalf complex) | raw (nn double)
+  const size_t zb = sizeof(double2) * 4 * nn;
+  const size_t bytes = 2 * zb + sizeof(double2) * nhalf + sizeof(double) * nn;
+  if ((rc = ensure_scratch(c, bytes))) return rc;
+  char* base = (char*)c->scratch;
+  double2* Z = (double2*)base;
+  double2* T = (double2*)(base + zb);
+  double2* fk = (double2*)(base + 2 * zb);
+  double* raw = (double*)(base + 2 * zb + sizeof(double2) * nhalf);
+  HIPCHK(c, hipMemcpyAsync(raw, psi_grid, sizeof(double) * nn, hipMemcpyHostToDevice, c->stream));
+  // g2k: forward FFT2 of the real grid (layout [r + n*c], r = x index)
+  hipLaunchKernelGGL(real_to_complex_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, raw,
+                     Z, nn);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = run_fft_pass(c, Z, n, 1, 0))) return rc;  // along x
+  if ((rc = run_transpose(c, Z, T, n, 1))) return rc;
+  if ((rc = run_fft_pass(c, T, n, 1, 0))) return rc;  // along y; T: [c + n*r]
+  hipLaunchKernelGGL(crop_half_kernel, dim3(nblocks(nhalf, 256)), dim3(256), 0, c->stream, T, n, fk);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = fields_from_halfplane(c, slot, fk, n, 0, 0.0, 1.0, 0.0, 1, Z, T))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  Slot& s = c->slot[slot];
+  s.L = L;
+  s.ny_period = nx;
+  s.set = true;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_set_field_qk(swrt_ctx* c, int slot, const double* qk_interleaved, int64_t nx, double L,
+                      double K_d2, double shear, double k_scale, int64_t ny_period) {
+  int rc = check_slot_args(c, slot, nx);
+  if (rc) return rc;
+  GUARD_BEGIN
+  if (!qk_interleaved) return fail(c, SWRT_ERR_ARG, "qk is NULL");
+  if (!is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two for the GPU FFT");
+  if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
+  if (ny_period == 0) ny_period = nx;
+  if (ny_period % nx) return fail(c, SWRT_ERR_ARG, "ny_period must be a multiple of nx");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_slot(c, slot, nx))) return rc;
+  if ((rc = ensure_twiddles(c, (int)nx))) return rc;
+  const int n = (int)nx;
+  const int64_t nn = nx * nx;
+  const int kmax = n / 2 - 1;
+  const int64_t nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
+  const size_t zb = sizeof(double2) * 3 * nn;
+  const size_t bytes = 2 * zb + sizeof(double2) * nhalf;
+  if ((rc = ensure_scratch(c, bytes))) return rc;
+  char* base = (char*)c->scratch;
+  double2* Z = (double2*)base;
+  double2* T = (double2*)(base + zb);
+  double2* fk = (double2*)(base + 2 * zb);
+  HIPCHK(c, hipMemcpyAsync(fk, qk_interleaved, sizeof(double2) * nhalf, hipMemcpyHostToDevice,
+                           c->stream));
+  if ((rc = fields_from_halfplane(c, slot, fk, n, 1, K_d2, k_scale, shear, 0, Z, T))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  Slot& s = c->slot[slot];
+  s.L = L;
+  s.ny_period = ny_period;
+  s.set = true;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_g2k(swrt_ctx* c, const double* fg, int64_t nx, double* fk_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!fg || !fk_out) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  if (nx < 8 || nx > 4096 || !is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two, 8..4096");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_twiddles(c, (int)nx))) return rc;
+  const int n = (int)nx;
+  const int64_t nn = nx * nx;
+  const int kmax = n / 2 - 1;
+  const int64_t nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
+  const size_t zb = sizeof(double2) * nn;
+  if ((rc = ensure_scratch(c, 2 * zb + sizeof(double2) * nhalf + sizeof(double) * nn))) return rc;
+  char* base = (char*)c->scratch;
+  double2* Z = (double2*)base;
+  double2* T = (double2*)(base + zb);
+  double2* fk = (double2*)(base + 2 * zb);
+  double* raw = (double*)(base + 2 * zb + sizeof(double2) * nhalf);
+  HIPCHK(c, hipMemcpyAsync(raw, fg, sizeof(double) * nn, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(real_to_complex_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, raw, Z, nn);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = run_fft_pass(c, Z, n, 1, 0))) return rc;
+  if ((rc = run_transpose(c, Z, T, n, 1))) return rc;
+  if ((rc = run_fft_pass(c, T, n, 1, 0))) return rc;
+  hipLaunchKernelGGL(crop_half_kernel, dim3(nblocks(nhalf, 256)), dim3(256), 0, c->stream, T, n, fk);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(fk_out, fk, sizeof(double2) * nhalf, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_k2g(swrt_ctx* c, const double* fk_in, int64_t nx, double* fg_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!fk_in || !fg_out) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  if (nx < 8 || nx > 4096 || !is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two, 8..4096");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_twiddles(c, (int)nx))) return rc;
+  const int n = (int)nx;
+  const int64_t nn = nx * nx;
+  const int kmax = n / 2 - 1;
+  const int64_t nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
+  const size_t zb = sizeof(double2) * nn;
+  if ((rc = ensure_scratch(c, 2 * zb + sizeof(double2) * nhalf + sizeof(double) * nn))) return rc;
+  char* base = (char*)c->scratch;
+  double2* Z = (double2*)base;
+  double2* T = (double2*)(base + zb);
+  double2* fk = (double2*)(base + 2 * zb);
+  double* raw = (double*)(base + 2 * zb + sizeof(double2) * nhalf);
+  HIPCHK(c, hipMemcpyAsync(fk, fk_in, sizeof(double2) * nhalf, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(fulspec_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, fk, n, Z);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = inverse_2d(c, Z, T, n, 1))) return rc;
+  hipLaunchKernelGGL(real_part_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, raw, nn);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(fg_out, raw, sizeof(double) * nn, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_get_field_grid(swrt_ctx* c, int slot, double* out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (slot < 0 || slot >= SWRT_MAX_SLOTS || !c->slot[slot].set)
+    return fail(c, SWRT_ERR_STATE, "slot not set");
+  if (!out) return fail(c, SWRT_ERR_ARG, "out is NULL");
+  HIPCHK(c, hipSetDevice(c->device));
+  Slot& s = c->slot[slot];
+  const int64_t nn = s.nx * s.nx;
+  int rc;
+  if ((rc = ensure_scratch(c, sizeof(double) * 6 * nn))) return rc;
+  hipLaunchKernelGGL(unpack_nodes_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, s.nodes,
+                     (int)s.nx, (int)s.npad, (double*)c->scratch);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, c->scratch, sizeof(double) * 6 * nn, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_get_psi_grid(swrt_ctx* c, int slot, double* out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (slot < 0 || slot >= SWRT_MAX_SLOTS || !c->slot[slot].set || !c->slot[slot].has_psi)
+    return fail(c, SWRT_ERR_STATE, "slot has no psi grid (use swrt_set_field_psi)");
+  if (!out) return fail(c, SWRT_ERR_ARG, "out is NULL");
+  HIPCHK(c, hipSetDevice(c->device));
+  Slot& s = c->slot[slot];
+  HIPCHK(c, hipMemcpyAsync(out, s.psi, sizeof(double) * s.nx * s.nx, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_interpolate(swrt_ctx* c, const double* F, int64_t nx, int64_t nyF, double dx, double dy,
+                     double bump, const double* x, const double* y, int64_t n, double* out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (n < 0) return fail(c, SWRT_ERR_ARG, "n < 0");
+  if (n == 0) return SWRT_OK;
+  if (!F || !x || !y || !out) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  if (nx < 6 || nyF < nx) return fail(c, SWRT_ERR_ARG, "need nx >= 6 and nyF >= nx");
+  if (!(dx > 0) || !(dy > 0)) return fail(c, SWRT_ERR_ARG, "dx, dy must be > 0");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t fb = sizeof(double) * nx * nx;  // only the first nx columns are read
+  const size_t bytes = fb + sizeof(double) * 3 * n;
+  int rc;
+  if ((rc = ensure_scratch(c, bytes))) return rc;
+  double* dF = (double*)c->scratch;
+  double* dxp = dF + nx * nx;
+  double* dyp = dxp + n;
+  double* dout = dyp + n;
+  HIPCHK(c, hipMemcpyAsync(dF, F, fb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dxp, x, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dyp, y, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  const double py = (double)nyF;
+  hipLaunchKernelGGL(interp1_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, dF, (int)nx, py,
+                     1.0 / py, (int)is_pow2(nyF), dx, dy, bump, dxp, dyp, n, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_eval(swrt_ctx* c, const double* x, const double* y, int64_t n, int nslots, double alpha,
+              double bump, double* out6) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (n < 0) return fail(c, SWRT_ERR_ARG, "n < 0");
+  if (n == 0) return SWRT_OK;
+  if (!x || !y || !out6) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  if (nslots != 1 && nslots != 2) return fail(c, SWRT_ERR_ARG, "nslots must be 1 or 2");
+  for (int s = 0; s < nslots; ++s)
+    if (!c->slot[s].set) return fail(c, SWRT_ERR_STATE, "field slot not set");
+  if (nslots == 2 && (c->slot[1].nx != c->slot[0].nx || c->slot[1].L != c->slot[0].L ||
+                      c->slot[1].ny_period != c->slot[0].ny_period))
+    return fail(c, SWRT_ERR_ARG, "slots 0 and 1 have different grids");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_scratch(c, sizeof(double) * 8 * n))) return rc;
+  double* dxp = (double*)c->scratch;
+  double* dyp = dxp + n;
+  double* dout = dyp + n;
+  HIPCHK(c, hipMemcpyAsync(dxp, x, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dyp, y, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  FieldView f0 = view_of(c->slot[0]);
+  FieldView f1 = nslots == 2 ? view_of(c->slot[1]) : f0;
+  hipLaunchKernelGGL(eval_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, f0, f1, nslots,
+                     alpha, bump, dxp, dyp, n, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out6, dout, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (n < 0) return fail(c, SWRT_ERR_ARG, "n < 0");
+  if (n > 0 && (!x || !k)) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (n > c->cap) {
+    if (c->dx) (void)hipFree(c->dx);
+    if (c->dk) (void)hipFree(c->dk);
+    c->dx = c->dk = nullptr;
+    c->cap = 0;
+    HIPCHK(c, hipMalloc(&c->dx, sizeof(double) * 2 * n));
+    HIPCHK(c, hipMalloc(&c->dk, sizeof(double) * 2 * n));
+    c->cap = n;
+  }
+  c->n = n;
+  if (n > 0) {
+    HIPCHK(c, hipMemcpyAsync(c->dx, x, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->dk, k, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // a new ensemble starts a new history
+  c->hframes = 0;
+  c->steps_done = 0;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (c->n == 0) return SWRT_OK;
+  if (!x || !k) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipMemcpyAsync(x, c->dx, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(k, c->dk, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int64_t swrt_packets_count(const swrt_ctx* c) { return c ? c->n : -1; }
+
+int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int nslots,
+                 double alpha0, double dalpha, double bump, int64_t save_every) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (nsteps < 0) return fail(c, SWRT_ERR_ARG, "nsteps < 0");
+  if (nslots != 1 && nslots != 2) return fail(c, SWRT_ERR_ARG, "nslots must be 1 or 2");
+  if (save_every < 0) return fail(c, SWRT_ERR_ARG, "save_every < 0");
+  for (int s = 0; s < nslots; ++s)
+    if (!c->slot[s].set) return fail(c, SWRT_ERR_STATE, "field slot not set");
+  if (nslots == 2 && (c->slot[1].nx != c->slot[0].nx || c->slot[1].L != c->slot[0].L ||
+                      c->slot[1].ny_period != c->slot[0].ny_period))
+    return fail(c, SWRT_ERR_ARG, "slots 0 and 1 have different grids");
+  if (c->n == 0 || nsteps == 0) return SWRT_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  int64_t new_frames = save_every > 0 ? nsteps / save_every : 0;
+  if (save_every > 0 && nsteps % save_every)
+    return fail(c, SWRT_ERR_ARG, "nsteps must be a multiple of save_every");
+  if (new_frames > 0 && c->hframes + new_frames > c->hcap) {
+    // grow (keeps existing frames)
+    const int64_t ncap = std::max<int64_t>(c->hframes + new_frames, 2 * c->hcap);
+    double *nx_ = nullptr, *nk_ = nullptr;
+    HIPCHK(c, hipMalloc(&nx_, sizeof(double) * 2 * c->n * ncap));
+    HIPCHK(c, hipMalloc(&nk_, sizeof(double) * 2 * c->n * ncap));
+    if (c->hframes > 0) {
+      HIPCHK(c, hipMemcpyAsync(nx_, c->hx, sizeof(double) * 2 * c->n * c->hframes,
+                               hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(nk_, c->hk, sizeof(double) * 2 * c->n * c->hframes,
+                               hipMemcpyDeviceToDevice, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    if (c->hx) (void)hipFree(c->hx);
+    if (c->hk) (void)hipFree(c->hk);
+    c->hx = nx_;
+    c->hk = nk_;
+    c->hcap = ncap;
+  }
+  int rc = launch_advance(c, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every);
+  if (rc) return rc;
+  c->hframes += new_frames;
+  c->steps_done += nsteps;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int64_t swrt_history_frames(const swrt_ctx* c) { return c ? c->hframes : -1; }
+
+int swrt_history_get(swrt_ctx* c, int64_t first, int64_t count, double* hist_x, double* hist_k) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (first < 0 || count < 0 || first + count > c->hframes)
+    return fail(c, SWRT_ERR_ARG, "history frame range out of bounds");
+  if (count == 0) return SWRT_OK;
+  if (!hist_x || !hist_k) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t fb = sizeof(double) * 2 * c->n;
+  HIPCHK(c, hipMemcpyAsync(hist_x, (char*)c->hx + fb * first, fb * count, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(hist_k, (char*)c->hk + fb * first, fb * count, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_history_reset(swrt_ctx* c) {
+  if (!c) return SWRT_ERR_ARG;
+  c->hframes = 0;
+  c->steps_done = 0;
+  return SWRT_OK;
+}
+
+int swrt_leapfrog(swrt_ctx* c, double* x, double* k, int64_t n, double dt, int64_t nsteps, double f,
+                  double gH, int nslots, double alpha0, double dalpha, double bump,
+                  int64_t save_every, double* hist_x, double* hist_k) {
+  if (!c) return SWRT_ERR_ARG;
+  int rc;
+  if ((rc = swrt_packets_set(c, x, k, n))) return rc;
+  const int64_t se = (hist_x && hist_k) ? save_every : 0;
+  if ((rc = swrt_advance(c, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, se))) return rc;
+  if ((rc = swrt_packets_get(c, x, k))) return rc;
+  if (se > 0) {
+    if ((rc = swrt_history_get(c, 0, c->hframes, hist_x, hist_k))) return rc;
+  }
+  return SWRT_OK;
+}
+
+int swrt_synchronize(swrt_ctx* c) {
+  if (!c) return SWRT_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+}
+
+int swrt_get_stream(swrt_ctx* c, void** out) {
+  if (!c || !out) return SWRT_ERR_ARG;
+  *out = (void*)c->stream;
+  return SWRT_OK;
+}
+
+int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches) {
+  if (!c) return SWRT_ERR_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  double tot = c->timing.folded_ms;
+  for (size_t i = 0; i + 1 < c->timing.used; i += 2) {
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->timing.ev[i], c->timing.ev[i + 1]));
+    tot += ms;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = c->timing.folded_n + (int64_t)(c->timing.used / 2);
+  if (reset) {
+    c->timing.used = 0;
+    c->timing.folded_ms = 0.0;
+    c->timing.folded_n = 0;
+  }
+  return SWRT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,192 @@
+// swrt_fft.hpp — field preparation on the GPU (g2k / fulspec / k2g / grid_U).
+//
+// Replaces MATLAB's fft2/ifft2/fftshift in qg_flow_ray_trace/{g2k,k2g,fulspec}.m
+// and the spectral algebra of grid_U.m / SpectralScheme.m:12-35.  A 2-D
+// transform is two passes of a batched 1-D radix-2 Stockham FFT (one 256-lane
+// workgroup per length-n vector, ping-pong in LDS) with a tiled LDS transpose
+// in between.  Runs once per snapshot (amortised over all packets).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swrt {
+
+// Batched length-n complex FFT over contiguous vectors data[b*n + i].
+// tw[k] = exp(-2*pi*i*k/n), k < n/2.  inverse: conjugate twiddles, no scaling.
+// Stockham autosort, radix 2: stage with stride s, half-length m = n/(2s):
+//   y[q + s*2p] = a + b,  y[q + s*(2p+1)] = (a - b) * w^(p*s),
+//   a = x[q + s*p], b = x[q + s*(p+m)].
+__global__ void __launch_bounds__(256) fft_vec_kernel(double2* data, int n, int logn,
+                                                      const double2* tw, int inverse) {
+  extern __shared__ double2 sbuf[];
+  double2* xa = sbuf;
+  double2* ya = sbuf + n;
+  double2* v = data + (size_t)blockIdx.x * n;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) xa[i] = v[i];
+  __syncthreads();
+  const int half = n >> 1;
+  int s = 1, logs = 0;
+  for (int st = 0; st < logn; ++st) {
+    const int m = half >> logs;  // half-length of the current sub-transform
+    for (int b = threadIdx.x; b < half; b += blockDim.x) {
+      const int q = b & (s - 1);
+      const int p = b >> logs;
+      const double2 a = xa[q + s * p];
+      const double2 c = xa[q + s * (p + m)];
+      double2 w = tw[p * s];
+      if (inverse) w.y = -w.y;
+      const double2 d = make_double2(a.x - c.x, a.y - c.y);
+      ya[q + s * (2 * p)] = make_double2(a.x + c.x, a.y + c.y);
+      ya[q + s * (2 * p + 1)] = make_double2(d.x * w.x - d.y * w.y, d.x * w.y + d.y * w.x);
+    }
+    __syncthreads();
+    double2* t = xa; xa = ya; ya = t;
+    s <<= 1;
+    ++logs;
+  }
+  for (int i = threadIdx.x; i < n; i += blockDim.x) v[i] = xa[i];
+}
+
+// out[c + n*r] = in[r + n*c] for batch of nb n x n complex matrices.
+__global__ void transpose_kernel(const double2* in, double2* out, int n) {
+  __shared__ double2 tile[32][33];
+  const size_t boff = (size_t)blockIdx.z * n * n;
+  const int r0 = blockIdx.x * 32, c0 = blockIdx.y * 32;
+  for (int dy = threadIdx.y; dy < 32; dy += blockDim.y) {
+    const int r = r0 + threadIdx.x, c = c0 + dy;
+    if (r < n && c < n) tile[dy][threadIdx.x] = in[boff + r + (size_t)n * c];
+  }
+  __syncthreads();
+  for (int dy = threadIdx.y; dy < 32; dy += blockDim.y) {
+    const int c = c0 + threadIdx.x, r = r0 + dy;
+    if (r < n && c < n) out[boff + c + (size_t)n * r] = tile[threadIdx.x][dy];
+  }
+}
+
+// real column-major grid -> complex
+__global__ void real_to_complex_kernel(const double* g, double2* z, int64_t cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cnt) z[i] = make_double2(g[i], 0.0);
+}
+
+// FFT-order index -> signed wavenumber for even n (Nyquist -> n/2).
+__device__ __forceinline__ int signed_k(int r, int n) { return r <= n / 2 ? (r == n / 2 ? n / 2 : r) : r - n; }
+
+// g2k.m:8-9 crop of the forward spectrum.  F (forward FFT2 of the grid) is in
+// layout [c + n*r] (r: kx FFT index, c: ky FFT index).  Output fk is the
+// (2kmax+1) x (kmax+1) column-major half plane (row kx+kmax, col ky), /nx^2.
+__global__ void crop_half_kernel(const double2* F, int n, double2* fk) {
+  const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)nkx * (kmax + 1)) return;
+  const int row = (int)(idx % nkx), col = (int)(idx / nkx);
+  const int kx = row - kmax, ky = col;
+  const int r = kx < 0 ? kx + n : kx, c = ky;
+  const double nn = (double)n * (double)n;
+  const double2 v = F[c + (size_t)n * r];
+  fk[idx] = make_double2(v.x / nn, v.y / nn);
+}
+
+// Complex helpers matching MATLAB's (i*k).*z and (-i*k).*z evaluation.
+__device__ __forceinline__ double2 mul_ik(double k, double2 z) { return make_double2(-(k * z.y), k * z.x); }
+__device__ __forceinline__ double2 mul_mik(double k, double2 z) { return make_double2(k * z.y, -(k * z.x)); }
+
+// Build the full Hermitian spectra (fulspec.m:10-19 + ifftshift) of the six
+// derivative fields (grid_U.m:2-9 / SpectralScheme.m:16-25), packed two real
+// fields per complex transform: Z0 = u + i v, Z1 = u_x + i u_y,
+// Z2 = v_x + i v_y, and (if with_psi) Z3 = psi.  Output layout [c + n*r]
+// (ky FFT index c contiguous), each Zk an n*n block.
+// mode 0: psik = fk (SpectralScheme path); mode 1: psik = -qk./(K_d2 + K2).
+__global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, double kscale,
+                               int with_psi, double2* Z) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nn = (int64_t)n * n;
+  if (idx >= nn) return;
+  const int c = (int)(idx % n), r = (int)(idx / n);
+  const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int kx = signed_k(r, n), ky = signed_k(c, n);
+  double2 z[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) z[q] = make_double2(0.0, 0.0);
+  const bool inband = (kx >= -kmax && kx <= kmax && ky >= -kmax && ky <= kmax);
+  if (inband) {
+    // Half-plane representative (kx', ky' >= 0 side) and whether to conjugate.
+    int hx = kx, hy = ky;
+    bool cj = false;
+    if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
+    double2 q = fk[(hx + kmax) + (int64_t)nkx * hy];
+    const double kxs = (double)hx * kscale, kys = (double)hy * kscale;
+    double2 ps;
+    if (mode == 0) {
+      ps = q;
+    } else {
+      const double den = K_d2 + (kxs * kxs + kys * kys);
+      ps = make_double2(-q.x / den, -q.y / den);
+    }
+    const double2 u = mul_mik(kys, ps);
+    const double2 v = mul_ik(kxs, ps);
+    double2 a[7] = {u, v, mul_ik(kxs, u), mul_ik(kys, u), mul_ik(kxs, v), mul_ik(kys, v), ps};
+    if (hx == 0 && hy == 0) {
+      // DC: only its real part reaches the real output of k2g.
+#pragma unroll
+      for (int t = 0; t < 7; ++t) a[t].y = 0.0;
+    }
+    if (cj) {
+#pragma unroll
+      for (int t = 0; t < 7; ++t) a[t].y = -a[t].y;
+    }
+    // pack: Z = A + i*B
+    z[0] = make_double2(a[0].x - a[1].y, a[0].y + a[1].x);
+    z[1] = make_double2(a[2].x - a[3].y, a[2].y + a[3].x);
+    z[2] = make_double2(a[4].x - a[5].y, a[4].y + a[5].x);
+    z[3] = a[6];
+  }
+  Z[idx] = z[0];
+  Z[nn + idx] = z[1];
+  Z[2 * nn + idx] = z[2];
+  if (with_psi) Z[3 * nn + idx] = z[3];
+}
+
+// After the inverse 2-D transform Z is in layout [r + n*c] (x contiguous):
+// unpack to six column-major planes (+ psi plane).
+__global__ void unpair_kernel(const double2* Z, int n, int with_psi, double* planes, double* psi) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nn = (int64_t)n * n;
+  if (idx >= nn) return;
+  const double2 z0 = Z[idx], z1 = Z[nn + idx], z2 = Z[2 * nn + idx];
+  planes[idx] = z0.x;
+  planes[nn + idx] = z0.y;
+  planes[2 * nn + idx] = z1.x;
+  planes[3 * nn + idx] = z1.y;
+  planes[4 * nn + idx] = z2.x;
+  planes[5 * nn + idx] = z2.y;
+  if (with_psi) psi[idx] = Z[3 * nn + idx].x;
+}
+
+// fulspec.m:10-19 + ifftshift of ONE field: full Hermitian spectrum in layout
+// [c + n*r] (ky FFT index contiguous).  DC keeps its real part only.
+__global__ void fulspec_kernel(const double2* fk, int n, double2* Z) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nn = (int64_t)n * n;
+  if (idx >= nn) return;
+  const int c = (int)(idx % n), r = (int)(idx / n);
+  const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int kx = signed_k(r, n), ky = signed_k(c, n);
+  double2 z = make_double2(0.0, 0.0);
+  if (kx >= -kmax && kx <= kmax && ky >= -kmax && ky <= kmax) {
+    int hx = kx, hy = ky;
+    bool cj = false;
+    if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
+    z = fk[(hx + kmax) + (int64_t)nkx * hy];
+    if (hx == 0 && hy == 0) z.y = 0.0;
+    if (cj) z.y = -z.y;
+  }
+  Z[idx] = z;
+}
+
+__global__ void real_part_kernel(const double2* Z, double* out, int64_t cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cnt) out[i] = Z[i].x;
+}
+
+}  // namespace swrt

@@ -1,0 +1,242 @@
+// swrt_kernels.hpp — device code of the packet hot path (gfx950 / CDNA4).
+//
+// One lane per packet.  The six background fields of a snapshot live in HBM
+// as a halo-padded, node-interleaved array: node (ix, iy) holds the 48 B
+// record {u, v, u_x, u_y, v_x, v_y} and iy is the fast index, so one row of
+// the 6x6 Lagrange stencil (fixed ix, six consecutive iy) is one contiguous
+// 288 B segment and no tap needs a periodic wrap (2 ghost nodes below, 3
+// above in each direction).
+//
+// Arithmetic is fp64 in exactly the reference's operation order (see
+// oracle/swrt_oracle.c for the CPU twin); this translation unit is compiled
+// with -ffp-contract=off so no FMA is formed behind our back.  Divisions and
+// square roots are IEEE correctly rounded.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swrt {
+
+constexpr int kNT = 6;            // taps per direction (Iord = 2, interpolate.m:12)
+constexpr int kPadLo = 2;         // ghost nodes below (offset -2)
+constexpr int kPadTot = 5;        // npad = nx + 5 (offsets -2..+3 from cells 0..nx-1)
+constexpr int kRec = 6;           // doubles per node record
+
+struct FieldView {
+  const double* nodes;  // (nx+5) x (nx+5) records, x-major, y contiguous
+  int nx;               // grid size (periodic in x and y with nx nodes)
+  int npad;             // nx + 5
+  double dx;            // L / nx (interpolate.m dx = dy = h)
+  double px, py;        // mod periods of x/dx and y/dy (nx, ny_period)
+  double inv_px, inv_py;
+  int pow2x, pow2y;     // period is a power of two: a/m == a*(1/m) exactly
+};
+
+// interpolate.m:21-31 — xl = mod(x/dx, n); i0 = 1 + floor(xl); a = 1 + xl - i0.
+// Returns the 0-based cell reduced mod nx and the fractional offset a.
+__device__ __forceinline__ int cell_frac(double x, double dx, double period, double inv_period,
+                                         int pow2, int nx, double& a) {
+  const double q = x / dx;
+  const double r = pow2 ? q * inv_period : q / period;
+  const double xl = q - floor(r) * period;   // MATLAB mod (a - floor(a/m)*m)
+  const double fl = floor(xl);
+  a = (1.0 + xl) - (1.0 + fl);
+  // NaN/Inf positions: keep the index in range (the result is NaN anyway).
+  int c = (fl >= 0.0 && fl <= period) ? (int)fl : 0;
+  c = c % nx;  // i0 may equal the period after round-up of mod, and the
+               // 2-layer y-period is 2*nx (interpolate.m:45-46 wrap by nx)
+  return c;
+}
+
+// interpolate.m:33-41 — w(i) = prod_{j != i} (a - j + bump)/(j - i), running
+// product in the reference order.  Divisions by the constants +-1,+-2,+-4 are
+// exact scalings; the compiler keeps IEEE division for +-3, +-5.
+__device__ __forceinline__ void lagrange_w(double a, double bump, double w[kNT]) {
+  double t[kNT];
+#pragma unroll
+  for (int j = -2; j <= 3; ++j) t[j + 2] = (a - (double)j) + bump;
+#pragma unroll
+  for (int i = -2; i <= 3; ++i) {
+    double wi = 1.0;
+#pragma unroll
+    for (int j = -2; j <= 3; ++j) {
+      if (i != j) wi = wi * t[j + 2] / (double)(j - i);
+    }
+    w[i + 2] = wi;
+  }
+}
+
+// Six-field stencil sum at (x, y): out[f] = sum_i sum_j (wx_i * wy_j) * F_f[ig, jg]
+// accumulated i-outer / j-inner exactly as interpolate.m:43-49 does per field.
+__device__ __forceinline__ void interp6(const FieldView& fv, double x, double y, double bump,
+                                        double out[kRec]) {
+  double ax, ay;
+  const int ic = cell_frac(x, fv.dx, fv.px, fv.inv_px, fv.pow2x, fv.nx, ax);
+  const int jc = cell_frac(y, fv.dx, fv.py, fv.inv_py, fv.pow2y, fv.nx, ay);
+  double wx[kNT], wy[kNT];
+  lagrange_w(ax, bump, wx);
+  lagrange_w(ay, bump, wy);
+#pragma unroll
+  for (int f = 0; f < kRec; ++f) out[f] = 0.0;
+  const double* base = fv.nodes + ((size_t)ic * fv.npad + jc) * kRec;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+    const double2* row = reinterpret_cast<const double2*>(base + (size_t)i * fv.npad * kRec);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const double2 a0 = row[3 * j + 0];
+      const double2 a1 = row[3 * j + 1];
+      const double2 a2 = row[3 * j + 2];
+      const double wij = wx[i] * wy[j];
+      out[0] = out[0] + wij * a0.x;
+      out[1] = out[1] + wij * a0.y;
+      out[2] = out[2] + wij * a1.x;
+      out[3] = out[3] + wij * a1.y;
+      out[4] = out[4] + wij * a2.x;
+      out[5] = out[5] + wij * a2.y;
+    }
+  }
+}
+
+// interpolate_U.m:19-23 — (1 - alpha)*U1 + alpha*U2, per field.
+__device__ __forceinline__ void eval_flow(const FieldView& f0, const FieldView& f1, int nslots,
+                                          double alpha, double x, double y, double bump,
+                                          double I[kRec]) {
+  interp6(f0, x, y, bump, I);
+  if (nslots == 2) {
+    double J[kRec];
+    interp6(f1, x, y, bump, J);
+    const double oma = 1 - alpha;
+#pragma unroll
+    for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
+  }
+}
+
+struct StepArgs {
+  FieldView f0, f1;
+  int nslots;
+  double* x;  // N x 2 column-major
+  double* k;
+  int64_t n;
+  double dt, half, f2, gH;  // f2 = f*f
+  double alpha0, dalpha;
+  int64_t s0;               // global index of the first step of this launch
+  int nsteps;
+  double bump;
+  int64_t save_every;
+  double* hist_x;           // frames of N x 2 (NULL: no history)
+  double* hist_k;
+  int64_t frame0;           // history frame index of global step save_every-1
+};
+
+// ode_symplectic.m:13-37 fused: drift(dt/2) -> kick(dt) -> drift(dt/2), nsteps
+// times with the packet held in registers.
+__global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.n) return;
+  double x0 = a.x[p], y0 = a.x[a.n + p];
+  double k0 = a.k[p], l0 = a.k[a.n + p];
+  for (int s = 0; s < a.nsteps; ++s) {
+    const int64_t sg = a.s0 + s;
+    // phi1(x0, k0, dt/2): x + (dt/2) * (gH*k/omega(k))   (ode_symplectic.m:10-16)
+    double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
+    const double x1 = x0 + a.half * (a.gH * k0 / w);
+    const double y1 = y0 + a.half * (a.gH * l0 / w);
+    // phi2(x1, k1, dt): U and (grad U)^T k at x1  (ode_symplectic.m:18-21)
+    double I[kRec];
+    eval_flow(a.f0, a.f1, a.nslots, a.alpha0 + (double)sg * a.dalpha, x1, y1, a.bump, I);
+    const double x2 = x1 + a.dt * I[0];
+    const double y2 = y1 + a.dt * I[1];
+    const double k2 = k0 - a.dt * (I[2] * k0 + I[4] * l0);  // RaytracingScheme.m:14
+    const double l2 = l0 - a.dt * (I[3] * k0 + I[5] * l0);  // RaytracingScheme.m:15
+    // phi1(x2, k2, dt/2)
+    w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
+    x0 = x2 + a.half * (a.gH * k2 / w);
+    y0 = y2 + a.half * (a.gH * l2 / w);
+    k0 = k2;
+    l0 = l2;
+    if (a.hist_x != nullptr && ((sg + 1) % a.save_every) == 0) {
+      const int64_t fr = a.frame0 + (sg + 1) / a.save_every - 1;
+      double* hx = a.hist_x + fr * 2 * a.n;
+      double* hk = a.hist_k + fr * 2 * a.n;
+      hx[p] = x0; hx[a.n + p] = y0;
+      hk[p] = k0; hk[a.n + p] = l0;
+    }
+  }
+  a.x[p] = x0; a.x[a.n + p] = y0;
+  a.k[p] = k0; a.k[a.n + p] = l0;
+}
+
+// U, grad U at points: out 6 x n (SpectralScheme.U/grad_U, interpolate_U).
+__global__ void __launch_bounds__(256) eval_kernel(FieldView f0, FieldView f1, int nslots,
+                                                   double alpha, double bump, const double* x,
+                                                   const double* y, int64_t n, double* out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  double I[kRec];
+  eval_flow(f0, f1, nslots, alpha, x[p], y[p], bump, I);
+#pragma unroll
+  for (int q = 0; q < kRec; ++q) out[(int64_t)q * n + p] = I[q];
+}
+
+// Generic interpolate(x, y, F, dx, dy) of one nx x nyF column-major grid
+// (reads only columns < nx, as F(ig,jg) with jg <= nx does).
+__global__ void __launch_bounds__(256) interp1_kernel(const double* F, int nx, double pyF,
+                                                      double inv_py, int pow2y, double dx,
+                                                      double dy, double bump, const double* x,
+                                                      const double* y, int64_t n, double* out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const double px = (double)nx;
+  const int pow2x = (nx & (nx - 1)) == 0;
+  double ax, ay;
+  const int ic = cell_frac(x[p], dx, px, 1.0 / px, pow2x, nx, ax);
+  const int jc = cell_frac(y[p], dy, pyF, inv_py, pow2y, nx, ay);
+  double wx[kNT], wy[kNT];
+  lagrange_w(ax, bump, wx);
+  lagrange_w(ay, bump, wy);
+  double FI = 0.0;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+    int ig = ic + i - 2;
+    ig = ig < 0 ? ig + nx : (ig >= nx ? ig - nx : ig);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      int jg = jc + j - 2;
+      jg = jg < 0 ? jg + nx : (jg >= nx ? jg - nx : jg);
+      FI = FI + wx[i] * wy[j] * F[ig + (size_t)nx * jg];
+    }
+  }
+  out[p] = FI;
+}
+
+// Pack 6 column-major planes (F[ig + nx*jg]) into the padded interleaved
+// node array with periodic ghosts; u gets `shear` added (grid_U.m:11).
+__global__ void pack_nodes_kernel(const double* planes, int nx, int npad, double shear,
+                                  double* nodes) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)npad * npad;
+  if (idx >= tot) return;
+  const int ip = (int)(idx / npad), jp = (int)(idx % npad);
+  int ig = ip - kPadLo, jg = jp - kPadLo;
+  ig = ((ig % nx) + nx) % nx;
+  jg = ((jg % nx) + nx) % nx;
+  const int64_t plane = (int64_t)nx * nx;
+  const int64_t src = ig + (int64_t)nx * jg;
+  double* dst = nodes + idx * kRec;
+#pragma unroll
+  for (int f = 0; f < kRec; ++f) dst[f] = planes[f * plane + src] + (f == 0 ? shear : 0.0);
+}
+
+// Inverse of pack for downloads: nodes -> 6 column-major planes.
+__global__ void unpack_nodes_kernel(const double* nodes, int nx, int npad, double* planes) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t plane = (int64_t)nx * nx;
+  if (idx >= plane) return;
+  const int ig = (int)(idx % nx), jg = (int)(idx / nx);
+  const double* src = nodes + ((int64_t)(ig + kPadLo) * npad + (jg + kPadLo)) * kRec;
+#pragma unroll
+  for (int f = 0; f < kRec; ++f) planes[f * plane + idx] = src[f];
+}
+
+}  // namespace swrt

@@ -1,0 +1,59 @@
+"""The C-ABI library loads and exports every symbol include/swrt.h declares
+(CPU only: no compute call is made)."""
+import os
+import re
+import subprocess
+
+import pytest
+
+from tests.conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "swrt.h")
+LIB = os.path.join(ROOT, "swraytracing_amd", "libswrt.so")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(swrt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ("swrt_create", "swrt_set_field_psi", "swrt_set_field_qk", "swrt_eval", "swrt_advance",
+                 "swrt_leapfrog", "swrt_interpolate", "swrt_g2k", "swrt_k2g"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    import swraytracing_amd._lib as L
+    lib = L.load()  # dlopen only
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (swrt_\w+)", out))
+    assert set(declared_functions()) <= exported
+    # the ctypes table binds exactly the header's functions
+    assert set(L.SIGNATURES) == set(declared_functions())
+
+
+def test_library_is_gfx950_code_object():
+    data = open(LIB, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_product_package_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "swraytracing_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                txt = open(os.path.join(dirpath, f)).read()
+                assert "from oracle" not in txt and "import oracle" not in txt, f
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    import swraytracing_amd._lib as L
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(ImportError):
+        L.load()

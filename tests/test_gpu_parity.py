@@ -1,0 +1,345 @@
+"""GPU parity: the HIP path through the C ABI vs the CPU oracle.
+
+Packet kernels (interpolate / eval / leapfrog) are bit-exact: same IEEE fp64
+operations in the same order, no FMA contraction, correctly rounded div/sqrt.
+Field preparation (g2k / k2g / grid_U / SpectralScheme ctor) uses a different
+FFT than numpy, so it is compared within a stated fp64 tolerance:
+  FIELD_RTOL = 1e-13 of the field's max-abs (FFT round-off ~ log2(n) eps).
+Trajectories built on GPU-prepared fields inherit that round-off; over <= 100
+steps they are compared at TRAJ_ATOL = 1e-10 (BASELINE.md parity row).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import swrt_oracle as orc
+from tests.conftest import ROOT, periodic_grid
+
+pytestmark = pytest.mark.gpu
+
+FIELD_RTOL = 1e-13
+TRAJ_ATOL = 1e-10
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def _planes(flow):
+    return np.ascontiguousarray(np.stack([np.asarray(flow[n]).ravel(order="F") for n in orc.FIELD_ORDER]))
+
+
+def _edge_points(nx, L, rng, n=4096):
+    dx = L / nx
+    pts = [0.0, -0.0, -1e-17, 1e-17, L, -L, L / 2, -L / 2, 3 * dx, -5 * dx, 1e3 * L + dx / 3,
+           -7e2 * L - 1e-9, np.nextafter(dx, 0), np.nextafter(dx, 1), 1e6, -1e6]
+    x = np.concatenate([rng.uniform(-3 * L, 3 * L, n), np.array(pts)])
+    y = np.concatenate([rng.uniform(-3 * L, 3 * L, n), np.array(pts[::-1])])
+    return x, y
+
+
+def test_eval_bitexact(ctx, oracle_lib, qg_case):
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    pl = _planes(c["flow"])
+    ctx.set_field_grid(0, pl, nx, L)
+    rng = np.random.default_rng(7)
+    x, y = _edge_points(nx, L, rng)
+    for bump in (orc.BUMP_SW, orc.BUMP_QG):
+        g = ctx.eval(x, y, nslots=1, bump=bump)
+        o = oracle_lib.eval6(pl, None, 0.0, nx, nx, L / nx, bump, x, y)
+        np.testing.assert_array_equal(g, o)
+    # numpy oracle agrees too (independent restatement)
+    I = orc.interpolate_fields(x[:300], y[:300], c["flow"], L / nx, orc.BUMP_QG)
+    np.testing.assert_array_equal(ctx.eval(x[:300], y[:300], bump=orc.BUMP_QG), I)
+
+
+def test_eval_blend_two_layer_bitexact(ctx, oracle_lib, qg_case):
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    fl2 = {n: np.asarray(v) * 0.9 + 0.01 for n, v in c["flow"].items()}
+    p0, p1 = _planes(c["flow"]), _planes(fl2)
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    rng = np.random.default_rng(8)
+    x, y = _edge_points(nx, L, rng)
+    for alpha in (0.0, 0.37, 1.0):
+        g = ctx.eval(x, y, nslots=2, alpha=alpha, bump=orc.BUMP_QG)
+        o = oracle_lib.eval6(p0, p1, alpha, nx, 2 * nx, L / nx, orc.BUMP_QG, x, y)
+        np.testing.assert_array_equal(g, o)
+
+
+def test_interpolate_generic_matches_numpy_oracle(ctx):
+    nx, L = 48, 20.0  # non-power-of-two grid, qg2layer domain length
+    X, Y = periodic_grid(nx, L)
+    F = np.zeros((nx, nx, 2))
+    F[:, :, 0] = np.sin(2 * np.pi * X / L) * np.cos(4 * np.pi * Y / L)
+    F[:, :, 1] = -3.0
+    rng = np.random.default_rng(9)
+    x, y = _edge_points(nx, L, rng, 2000)
+    for FF in (F, F[:, :, 0]):
+        g = ctx.interpolate(x, y, FF, L / nx, L / nx, orc.BUMP_QG)
+        o = orc.interpolate(x, y, FF, L / nx, L / nx, orc.BUMP_QG)
+        np.testing.assert_array_equal(g, o)
+
+
+def test_leapfrog_bitexact_steady_with_history(ctx, oracle_lib, qg_case):
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    pl = _planes(c["flow"])
+    ctx.set_field_grid(0, pl, nx, L)
+    nsteps = 150  # > one launch (64 steps): exercises the chunked launch path
+    xg, kg, hxg, hkg = ctx.leapfrog(c["x"], c["k"], c["dt"], nsteps, c["f"], 1.0, bump=orc.BUMP_SW,
+                                    save_every=10)
+    xo, ko, hxo, hko = oracle_lib.leapfrog(pl, None, 0, 0, nx, nx, L / nx, orc.BUMP_SW, c["x"], c["k"],
+                                           c["dt"], nsteps, c["f"], 1.0, save_every=10)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
+    np.testing.assert_array_equal(hxg, hxo)
+    np.testing.assert_array_equal(hkg, hko)
+
+
+def test_leapfrog_blend_bitexact(ctx, oracle_lib, qg_case):
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    fl2 = {n: np.asarray(v) * 1.1 for n, v in c["flow"].items()}
+    p0, p1 = _planes(c["flow"]), _planes(fl2)
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    nsub = 8
+    xg, kg, _, _ = ctx.leapfrog(c["x"], c["k"], c["dt"] / nsub, nsub, c["f"], 1.0, nslots=2,
+                                alpha0=0.5 / nsub, dalpha=1.0 / nsub, bump=orc.BUMP_QG)
+    xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.5 / nsub, 1.0 / nsub, nx, 2 * nx, L / nx, orc.BUMP_QG,
+                                       c["x"], c["k"], c["dt"] / nsub, nsub, c["f"], 1.0)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
+
+
+def test_golden_fixtures_bitexact(ctx):
+    g = np.load(os.path.join(GOLD, "golden_steady.npz"))
+    nx = int(g["nx"])
+    ctx.set_field_grid(0, g["planes"], nx, float(g["L"]))
+    x, k, hx, hk = ctx.leapfrog(g["x0"], g["k0"], float(g["dt"]), int(g["nsteps"]), float(g["f"]),
+                                float(g["gH"]), bump=float(g["bump"]), save_every=int(g["save_every"]))
+    np.testing.assert_array_equal(x, g["x"])
+    np.testing.assert_array_equal(k, g["k"])
+    np.testing.assert_array_equal(hx, g["hist_x"].transpose(0, 2, 1))
+    np.testing.assert_array_equal(hk, g["hist_k"].transpose(0, 2, 1))
+    b = np.load(os.path.join(GOLD, "golden_blend.npz"))
+    nx = int(b["nx"])
+    ctx.set_field_grid(0, b["planes0"], nx, float(b["L"]), int(b["ny_period"]))
+    ctx.set_field_grid(1, b["planes1"], nx, float(b["L"]), int(b["ny_period"]))
+    x, k, _, _ = ctx.leapfrog(b["x0"], b["k0"], float(b["dt"]), int(b["nsteps"]), float(b["f"]),
+                              float(b["gH"]), nslots=2, alpha0=float(b["alpha0"]), dalpha=float(b["dalpha"]),
+                              bump=float(b["bump"]))
+    np.testing.assert_array_equal(x, b["x"])
+    np.testing.assert_array_equal(k, b["k"])
+
+
+def _close_field(a, b, rtol=FIELD_RTOL):
+    scale = max(np.abs(b).max(), 1e-300)
+    err = np.abs(np.asarray(a) - np.asarray(b)).max() / scale
+    assert err <= rtol, f"relative field error {err:.3e} > {rtol:.1e}"
+
+
+@pytest.mark.parametrize("nx", [32, 64, 256, 512])
+def test_g2k_k2g_vs_numpy(ctx, nx):
+    X, Y = periodic_grid(nx)
+    rng = np.random.default_rng(nx)
+    f = np.zeros_like(X)
+    for _ in range(20):
+        kx, ky = rng.integers(-nx // 2 + 1, nx // 2, 2)
+        f += rng.normal() * np.cos(kx * X + ky * Y + rng.uniform(0, 6))
+    f += rng.normal(size=f.shape) * 1e-3  # broadband (incl. Nyquist content)
+    fk_g = ctx.g2k(f)
+    fk_o = orc.g2k(f)
+    _close_field(fk_g, fk_o)
+    _close_field(ctx.k2g(fk_o), orc.k2g(fk_o))
+
+
+def test_golden_field_preparation(ctx):
+    g = np.load(os.path.join(GOLD, "golden_fields.npz"))
+    nx = g["psi_in"].shape[0]
+    ctx.set_field_psi(0, g["psi_in"], nx, 2 * np.pi)
+    got = ctx.get_field_grid(0, nx)
+    for i in range(6):
+        _close_field(got[i], g["planes_psi"][i])
+    _close_field(ctx.get_psi_grid(0, nx), g["psi"])
+    ctx.set_field_qk(0, g["qk"], nx, 2 * np.pi, float(g["K_d2"]))
+    got = ctx.get_field_grid(0, nx)
+    for i in range(6):
+        _close_field(got[i], g["planes_qk"][i])
+    ctx.set_field_qk(0, g["qk"], nx, 2 * np.pi, float(g["K_d2"]), shear=0.5)
+    got = ctx.get_field_grid(0, nx)
+    for i in range(6):
+        _close_field(got[i], g["planes_qk_shear"][i])
+
+
+def test_grid_U_scaled_wavenumbers_two_layer(ctx):
+    # qg2layersw_raytrace.m: L = 20, k scaled by 2*pi/L, shear 0.5, 2 layers.
+    import swraytracing_amd as sw
+    nx, L = 64, 20.0
+    kx_, ky_, K2 = orc.wavenumber_grids(nx, L, scale=True)
+    rng = np.random.default_rng(5)
+    X, Y = periodic_grid(nx, L)
+    q1 = np.cos(2 * np.pi * (3 * X + 2 * Y) / L) + 0.3 * np.sin(2 * np.pi * (5 * X - 4 * Y) / L)
+    qk = np.stack([orc.g2k(q1), orc.g2k(-q1)], axis=2)
+    fo = orc.grid_U(qk, 3.0, K2, kx_, ky_, 0.5)
+    fg = sw.grid_U(qk, 3.0, K2, kx_, ky_, 0.5, ctx=ctx)
+    for n in orc.FIELD_ORDER:
+        assert fg[n].shape == (nx, nx, 2)
+        _close_field(fg[n], fo[n])
+
+
+def test_spectral_scheme_api_matches_oracle(qg_case):
+    import swraytracing_amd as sw
+    c = qg_case
+    psi = orc.k2g(-c["qk"] / (c["K_d2"] + c["K2"]))
+    gs = sw.SpectralScheme(c["L"], c["nx"], psi)
+    os_ = orc.SpectralSchemeOracle(c["L"], c["nx"], psi)
+    P = 33
+    x = c["x"][:P].T[None].copy()
+    k = c["k"][:P].T[None].copy()
+    scaleU = np.abs(os_.fields["u"]).max()
+    scaleG = np.abs(os_.fields["ux"]).max()
+    np.testing.assert_allclose(gs.U(x), os_.U(x), rtol=0, atol=1e-13 * scaleU)
+    gg, go = gs.grad_U(x), os_.grad_U(x)
+    for n in ("u_x", "u_y", "v_x", "v_y"):
+        np.testing.assert_allclose(gg[n], go[n], rtol=0, atol=1e-13 * scaleG)
+    np.testing.assert_allclose(gs.grad_U_times_k(x, k), os_.grad_U_times_k(x, k), rtol=0,
+                               atol=1e-12 * scaleG)
+    np.testing.assert_allclose(gs.vorticity(x), os_.vorticity(x), rtol=0, atol=1e-12 * scaleG)
+    np.testing.assert_allclose(gs.strain(x), os_.strain(x), rtol=0, atol=1e-12 * scaleG)
+    sp = gs.streamfunction(x[0, 0], x[0, 1])
+    np.testing.assert_allclose(sp, os_.streamfunction(x[0, 0], x[0, 1]), rtol=0,
+                               atol=1e-13 * np.abs(psi).max())
+    assert gs.U_field["u"].shape == (c["nx"], c["nx"])
+
+
+def test_ode_symplectic_gpu_vs_oracle(qg_case):
+    import swraytracing_amd as sw
+    c = qg_case
+    psi = orc.k2g(-c["qk"] / (c["K_d2"] + c["K2"]))
+    gs = sw.SpectralScheme(c["L"], c["nx"], psi)
+    os_ = orc.SpectralSchemeOracle(c["L"], c["nx"], psi)
+    P = 40
+    x0 = c["x"][:P].T[None].copy()
+    k0 = c["k"][:P].T[None].copy()
+    T = c["dt"] * 100.5
+    xg, kg, tg = sw.ode_symplectic(x0, k0, c["dt"], T, c["f"], 1.0, gs)
+    xo, ko, to = orc.ode_symplectic(x0, k0, c["dt"], T, c["f"], 1.0, os_)
+    assert xg.shape == xo.shape == (100, 2, P)
+    np.testing.assert_array_equal(tg, to)
+    np.testing.assert_allclose(xg, xo, rtol=0, atol=TRAJ_ATOL)
+    np.testing.assert_allclose(kg, ko, rtol=0, atol=TRAJ_ATOL * 10)
+    # same fields -> bit-exact: run the oracle on the GPU's own fields
+    snap = orc.GridField({n: v for n, v in gs._fields().items()}, gs.dx)
+    xl, kl, hx, hk = orc.leapfrog(x0[0].T, k0[0].T, c["dt"], 99, c["f"], 1.0, snap, bump=orc.BUMP_SW,
+                                  save_every=1)
+    np.testing.assert_array_equal(xg[1:], np.stack(hx).transpose(0, 2, 1))
+    np.testing.assert_array_equal(kg[1:], np.stack(hk).transpose(0, 2, 1))
+
+
+def test_full_size_subset_parity(ctx, oracle_lib):
+    """BASELINE size: 512^2 field, 1e6 packets.  Packets are independent, so
+    a random subset run through the oracle must match the GPU bit for bit."""
+    nx, L = 512, 2 * np.pi
+    rng = np.random.default_rng(146)
+    X, Y = periodic_grid(nx, L)
+    psi = np.zeros_like(X)
+    for _ in range(40):
+        kx, ky = rng.integers(-30, 31, 2)
+        psi += rng.normal() / (1 + kx * kx + ky * ky) * np.cos(kx * X + ky * Y + rng.uniform(0, 6))
+    ctx.set_field_psi(0, psi, nx, L)
+    planes = ctx.get_field_grid(0, nx)
+    N = 1_000_000
+    x, k = orc.initial_packets(N, L, 4.0, 3.0, 1.0, rng)
+    ctx.packets_set(x, k)
+    dt, steps = 0.004, 12
+    ctx.advance(dt, steps, 3.0, 1.0, bump=orc.BUMP_SW)
+    xg, kg = ctx.packets_get()
+    assert np.isfinite(xg).all() and np.isfinite(kg).all()
+    idx = np.sort(rng.choice(N, 3000, replace=False))
+    xo, ko, _, _ = oracle_lib.leapfrog(planes, None, 0, 0, nx, nx, L / nx, orc.BUMP_SW, x[idx], k[idx], dt,
+                                       steps, 3.0, 1.0)
+    np.testing.assert_array_equal(xg[idx], xo)
+    np.testing.assert_array_equal(kg[idx], ko)
+
+
+def test_edge_cases(ctx, qg_case):
+    import swraytracing_amd as sw
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    ctx.set_field_grid(0, _planes(c["flow"]), nx, L)
+    # empty ensemble
+    x, k, _, _ = ctx.leapfrog(np.zeros((0, 2)), np.zeros((0, 2)), 0.01, 5, 3.0, 1.0)
+    assert x.shape == (0, 2)
+    # single packet, zero steps
+    x1 = np.array([[0.1, 0.2]])
+    k1 = np.array([[3.0, -1.0]])
+    xs, ks, _, _ = ctx.leapfrog(x1, k1, 0.01, 0, 3.0, 1.0)
+    np.testing.assert_array_equal(xs, x1)
+    # NaN / Inf packets do not fault and stay non-finite; others unaffected
+    xb = np.array([[np.nan, 0.0], [np.inf, 1.0], [0.3, 0.4]])
+    kb = np.array([[1.0, 1.0], [1.0, 1.0], [1.0, 2.0]])
+    xs, ks, _, _ = ctx.leapfrog(xb, kb, 0.01, 3, 3.0, 1.0)
+    assert not np.isfinite(xs[0]).all() and not np.isfinite(xs[1]).all()
+    xr, kr, _, _ = ctx.leapfrog(xb[2:], kb[2:], 0.01, 3, 3.0, 1.0)
+    np.testing.assert_array_equal(xs[2:], xr)
+    # argument errors surface as SwrtError, not crashes
+    with pytest.raises(sw.SwrtError):
+        ctx.advance(0.01, 1, 3.0, 1.0, nslots=3)
+    with pytest.raises(sw.SwrtError):
+        ctx.set_field_grid(2, _planes(c["flow"]), nx, L)
+    fresh = sw.Context(0)
+    fresh.packets_set(x1, k1)
+    with pytest.raises(sw.SwrtError):
+        fresh.advance(0.01, 1, 3.0, 1.0)
+    fresh.close()
+
+
+def test_packet_ensemble_driver_frames(tmp_path, qg_case):
+    """PacketEnsemble writes packet_x/k/time.bin frames that read_field and
+    load_data.m's layout accept (N x 2 column-major per frame, wrapped x)."""
+    import swraytracing_amd as sw
+    c = qg_case
+    nx = c["nx"]
+    ens = sw.PacketEnsemble(c["x"], c["k"], c["L"], c["f"], c["Cg"], nx, c["K_d2"])
+    qk2 = c["qk"] * 1.01
+    ens.set_snapshots(c["qk"], qk2)
+    d = str(tmp_path)
+    ens.write_frame(0.0, d)
+    ens.advance(c["dt"], nsub=4)
+    ens.write_frame(c["dt"], d)
+    t = sw.read_field(os.path.join(d, "packet_time"))
+    assert t.shape == (1, 2)
+    xs = sw.read_field(os.path.join(d, "packet_x"), c["x"].shape[0], 2, 1, [1, 2])
+    assert xs.shape == (c["x"].shape[0], 2, 2)
+    assert np.all(xs >= -c["L"] / 2) and np.all(xs < c["L"] / 2)
+    # advance == oracle blend on the GPU-built fields
+    fo0 = orc.grid_U(c["qk"], c["K_d2"], c["K2"], c["kx_"], c["ky_"])
+    fo1 = orc.grid_U(qk2, c["K_d2"], c["K2"], c["kx_"], c["ky_"])
+    xo, ko, _, _ = orc.leapfrog(c["x"], c["k"], c["dt"] / 4, 4, c["f"], 1.0, orc.GridField(fo0, c["L"] / nx),
+                                orc.GridField(fo1, c["L"] / nx), 0.125, 0.25, bump=orc.BUMP_QG)
+    xg, kg = ens.state()
+    np.testing.assert_allclose(xg, xo, rtol=0, atol=TRAJ_ATOL)
+    np.testing.assert_allclose(kg, ko, rtol=0, atol=TRAJ_ATOL)
+
+
+def test_sqrt_div_correctly_rounded_on_device(ctx):
+    """Zero-flow drift exercises sqrt and division only: must equal the
+    host's IEEE results bit for bit over a wide range of k."""
+    nx = 16
+    ctx.set_field_grid(0, np.zeros((6, nx * nx)), nx, 2 * np.pi)
+    rng = np.random.default_rng(11)
+    n = 200000
+    k = rng.normal(size=(n, 2)) * np.exp(rng.uniform(-20, 20, (n, 1)))
+    x = rng.uniform(-1, 1, (n, 2))
+    f, gH, dt = 3.0, 0.7, 0.01
+    xg, kg, _, _ = ctx.leapfrog(x, k, dt, 1, f, gH)
+    w = np.sqrt(f * f + gH * (k[:, 0] * k[:, 0] + k[:, 1] * k[:, 1]))
+    half = dt / 2
+    x1 = x + half * (gH * k / w[:, None])
+    x2 = x1 + dt * 0.0
+    xo = x2 + half * (gH * k / w[:, None])
+    np.testing.assert_array_equal(kg, k)
+    np.testing.assert_array_equal(xg, xo)
