@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--seed", type=int, default=146)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rebin-every", type=int, default=8, help="steps between spatial re-binning (0: off)")
+    ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -157,6 +159,7 @@ def main():
     dev = torch.device("cuda", local)
 
     ctx = sw.Context(local)
+    ctx.set_locality(args.rebin_every, args.tile)
     rng = np.random.default_rng(args.seed + rank)
     w = build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
@@ -215,7 +218,8 @@ def main():
                                f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, "
                                f"{args.nx}^2x2 field, {N} packets/GPU, leapfrog",
                    "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
-                   "mode": args.mode, "parallelism": f"packets sharded x{world}, field replicated"},
+                   "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile,
+                   "parallelism": f"packets sharded x{world}, field replicated"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_packet_step": B, "avg_launch_ms": avg_launch_s * 1e3,

@@ -116,6 +116,13 @@ int swrt_packets_set(swrt_ctx* ctx, const double* x, const double* k, int64_t n)
 int swrt_packets_get(swrt_ctx* ctx, double* x, double* k);
 int64_t swrt_packets_count(const swrt_ctx* ctx);
 
+/* Locality tuning: the packets are kept counting-sorted by spatial tile
+ * (tile x tile cells of slot 0's grid) and re-binned every `rebin_every`
+ * steps (0 disables binning; tile 0 picks a size automatically).  Binning
+ * changes only the device-side order: results, downloads and history frames
+ * are identical and in the original packet order. */
+int swrt_set_locality(swrt_ctx* ctx, int64_t rebin_every, int64_t tile);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

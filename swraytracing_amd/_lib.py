@@ -51,6 +51,7 @@ SIGNATURES = {
     "swrt_packets_set": (_INT, [_VP, _P, _P, _I]),
     "swrt_packets_get": (_INT, [_VP, _P, _P]),
     "swrt_packets_count": (_I, [_VP]),
+    "swrt_set_locality": (_INT, [_VP, _I, _I]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
     "swrt_history_get": (_INT, [_VP, _I, _I, _P, _P]),
@@ -208,6 +209,9 @@ class Context:
         k = np.empty((n, 2), order="F")
         self._chk(self._L.swrt_packets_get(self._h, _p(x), _p(k)), "swrt_packets_get")
         return x, k
+
+    def set_locality(self, rebin_every=8, tile=0):
+        self._chk(self._L.swrt_set_locality(self._h, int(rebin_every), int(tile)), "swrt_set_locality")
 
     def advance(self, dt, nsteps, f, gH, nslots=1, alpha0=0.0, dalpha=0.0, bump=1e-13, save_every=0):
         self._chk(self._L.swrt_advance(self._h, float(dt), int(nsteps), float(f), float(gH), int(nslots),

@@ -8,11 +8,14 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
+#include <climits>
 #include <new>
 #include <string>
 #include <vector>
 
 #include "../../include/swrt.h"
+#include "swrt_bin.hpp"
 #include "swrt_fft.hpp"
 #include "swrt_kernels.hpp"
 
@@ -48,11 +51,21 @@ struct swrt_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   Slot slot[SWRT_MAX_SLOTS];
-  // packets
+  // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
   double* dk = nullptr;  // 2N
+  int* perm = nullptr;   // N
+  double* dx2 = nullptr;  // scatter targets of the binning pass
+  double* dk2 = nullptr;
+  int* perm2 = nullptr;
+  int* keys = nullptr;   // N
+  int* bins = nullptr;   // 2 * kMaxBins (counts | cursor)
   int64_t n = 0;
   int64_t cap = 0;
+  int64_t rebin_every = 8;  // steps between spatial re-binning (0: never)
+  int64_t tile = 0;         // cells per tile side (0: automatic)
+  int64_t steps_since_bin = 0;
+  bool bin_valid = false;
   // history
   double* hx = nullptr;
   double* hk = nullptr;
@@ -219,14 +232,79 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
   return SWRT_OK;
 }
 
-int launch_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int nslots,
-                   double alpha0, double dalpha, double bump, int64_t save_every) {
+// Record a timing event pair around one leapfrog launch.
+int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid) {
+  // timing events (pairs), grown on demand; fold into a running sum when full
+  if (c->timing.used + 2 > kMaxEvents) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (size_t i = 0; i + 1 < c->timing.used; i += 2) {
+      float ms = 0.f;
+      HIPCHK(c, hipEventElapsedTime(&ms, c->timing.ev[i], c->timing.ev[i + 1]));
+      c->timing.folded_ms += ms;
+      c->timing.folded_n += 1;
+    }
+    c->timing.used = 0;
+  }
+  if (c->timing.used + 2 > c->timing.ev.size()) {
+    for (int e = 0; e < 64; ++e) {
+      hipEvent_t ev;
+      HIPCHK(c, hipEventCreate(&ev));
+      c->timing.ev.push_back(ev);
+    }
+  }
+  hipEvent_t e0 = c->timing.ev[c->timing.used], e1 = c->timing.ev[c->timing.used + 1];
+  c->timing.used += 2;
+  HIPCHK(c, hipEventRecord(e0, c->stream));
+  hipLaunchKernelGGL(leapfrog_kernel, dim3(grid), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(e1, c->stream));
+  return SWRT_OK;
+}
+
+int tile_cells(const swrt_ctx* c, int64_t nx) {
+  if (c->tile > 0) return (int)std::min<int64_t>(c->tile, nx);
+  // default: 8x8-cell tiles, coarser on big grids so bins stay <= 4096
+  int t = 8;
+  while ((nx + t - 1) / t > 64) t *= 2;
+  return t;
+}
+
+// Counting-sort the packets by spatial tile of slot 0's grid (swrt_bin.hpp).
+int rebin(swrt_ctx* c) {
+  const Slot& s = c->slot[0];
+  const FieldView v = view_of(s);
+  BinGeom g;
+  g.dx = v.dx; g.px = v.px; g.py = v.py; g.inv_px = v.inv_px; g.inv_py = v.inv_py;
+  g.pow2x = v.pow2x; g.pow2y = v.pow2y; g.nx = v.nx;
+  g.tile = tile_cells(c, s.nx);
+  g.ntx = (int)((s.nx + g.tile - 1) / g.tile);
+  const int nbins = g.ntx * g.ntx;
+  if (nbins > kMaxBins) return fail(c, SWRT_ERR_ARG, "too many spatial bins (raise tile size)");
+  const int64_t n = c->n;
+  HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * nbins, c->stream));
+  const unsigned grid = nblocks(n, 256);
+  hipLaunchKernelGGL(bin_count_kernel, dim3(grid), dim3(256), sizeof(int) * nbins, c->stream, g, c->dx, n,
+                     nbins, c->keys, c->bins);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins);
+  HIPCHK(c, hipGetLastError());
+  hipLaunchKernelGGL(bin_scatter_kernel, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream, c->dx,
+                     c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2);
+  HIPCHK(c, hipGetLastError());
+  std::swap(c->dx, c->dx2);
+  std::swap(c->dk, c->dk2);
+  std::swap(c->perm, c->perm2);
+  c->steps_since_bin = 0;
+  c->bin_valid = true;
+  return SWRT_OK;
+}
+
+int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int nslots,
+                double alpha0, double dalpha, double bump, int64_t save_every) {
   StepArgs a;
   a.f0 = view_of(c->slot[0]);
   a.f1 = nslots == 2 ? view_of(c->slot[1]) : a.f0;
   a.nslots = nslots;
-  a.x = c->dx;
-  a.k = c->dk;
   a.n = c->n;
   a.dt = dt;
   a.half = dt / 2;
@@ -240,33 +318,25 @@ int launch_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, 
   a.hist_k = save_every > 0 ? c->hk : nullptr;
   a.frame0 = c->hframes;
   const unsigned grid = nblocks(c->n, 256);
-  for (int64_t s0 = 0; s0 < nsteps; s0 += kMaxStepsPerLaunch) {
+  int64_t s0 = 0;
+  while (s0 < nsteps) {
+    int64_t chunk = std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
+    if (c->rebin_every > 0) {
+      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every) {
+        int rc = rebin(c);
+        if (rc) return rc;
+      }
+      chunk = std::min<int64_t>(chunk, c->rebin_every - c->steps_since_bin);
+    }
+    a.x = c->dx;
+    a.k = c->dk;
+    a.perm = c->perm;
     a.s0 = s0;
-    a.nsteps = (int)std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
-    // timing events (pairs), grown on demand; fold into a running sum when full
-    if (c->timing.used + 2 > kMaxEvents) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      for (size_t i = 0; i + 1 < c->timing.used; i += 2) {
-        float ms = 0.f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->timing.ev[i], c->timing.ev[i + 1]));
-        c->timing.folded_ms += ms;
-        c->timing.folded_n += 1;
-      }
-      c->timing.used = 0;
-    }
-    if (c->timing.used + 2 > c->timing.ev.size()) {
-      for (int e = 0; e < 64; ++e) {
-        hipEvent_t ev;
-        HIPCHK(c, hipEventCreate(&ev));
-        c->timing.ev.push_back(ev);
-      }
-    }
-    hipEvent_t e0 = c->timing.ev[c->timing.used], e1 = c->timing.ev[c->timing.used + 1];
-    c->timing.used += 2;
-    HIPCHK(c, hipEventRecord(e0, c->stream));
-    hipLaunchKernelGGL(leapfrog_kernel, dim3(grid), dim3(256), 0, c->stream, a);
-    HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipEventRecord(e1, c->stream));
+    a.nsteps = (int)chunk;
+    int rc = timed_launch(c, a, grid);
+    if (rc) return rc;
+    c->steps_since_bin += chunk;
+    s0 += chunk;
   }
   return SWRT_OK;
 }
@@ -309,8 +379,9 @@ void swrt_destroy(swrt_ctx* c) {
     if (s.nodes) (void)hipFree(s.nodes);
     if (s.psi) (void)hipFree(s.psi);
   }
-  if (c->dx) (void)hipFree(c->dx);
-  if (c->dk) (void)hipFree(c->dk);
+  for (void* p : {(void*)c->dx, (void*)c->dk, (void*)c->perm, (void*)c->dx2, (void*)c->dk2,
+                  (void*)c->perm2, (void*)c->keys, (void*)c->bins})
+    if (p) (void)hipFree(p);
   if (c->hx) (void)hipFree(c->hx);
   if (c->hk) (void)hipFree(c->hk);
   if (c->scratch) (void)hipFree(c->scratch);
@@ -590,27 +661,39 @@ int swrt_eval(swrt_ctx* c, const double* x, const double* y, int64_t n, int nslo
 int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
-  if (n < 0) return fail(c, SWRT_ERR_ARG, "n < 0");
+  if (n < 0 || n > INT32_MAX) return fail(c, SWRT_ERR_ARG, "n out of range (0..2^31-1)");
   if (n > 0 && (!x || !k)) return fail(c, SWRT_ERR_ARG, "NULL buffer");
   HIPCHK(c, hipSetDevice(c->device));
   if (n > c->cap) {
-    if (c->dx) (void)hipFree(c->dx);
-    if (c->dk) (void)hipFree(c->dk);
-    c->dx = c->dk = nullptr;
+    for (void** p : {(void**)&c->dx, (void**)&c->dk, (void**)&c->perm, (void**)&c->dx2, (void**)&c->dk2,
+                     (void**)&c->perm2, (void**)&c->keys}) {
+      if (*p) (void)hipFree(*p);
+      *p = nullptr;
+    }
     c->cap = 0;
     HIPCHK(c, hipMalloc(&c->dx, sizeof(double) * 2 * n));
     HIPCHK(c, hipMalloc(&c->dk, sizeof(double) * 2 * n));
+    HIPCHK(c, hipMalloc(&c->dx2, sizeof(double) * 2 * n));
+    HIPCHK(c, hipMalloc(&c->dk2, sizeof(double) * 2 * n));
+    HIPCHK(c, hipMalloc(&c->perm, sizeof(int) * n));
+    HIPCHK(c, hipMalloc(&c->perm2, sizeof(int) * n));
+    HIPCHK(c, hipMalloc(&c->keys, sizeof(int) * n));
     c->cap = n;
   }
+  if (!c->bins) HIPCHK(c, hipMalloc(&c->bins, sizeof(int) * 2 * kMaxBins));
   c->n = n;
   if (n > 0) {
     HIPCHK(c, hipMemcpyAsync(c->dx, x, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(c->dk, k, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(iota_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, c->perm, n);
+    HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  // a new ensemble starts a new history
+  // a new ensemble starts a new history and needs binning before the next step
   c->hframes = 0;
   c->steps_done = 0;
+  c->bin_valid = false;
+  c->steps_since_bin = 0;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -621,11 +704,24 @@ int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
   if (c->n == 0) return SWRT_OK;
   if (!x || !k) return fail(c, SWRT_ERR_ARG, "NULL buffer");
   HIPCHK(c, hipSetDevice(c->device));
-  HIPCHK(c, hipMemcpyAsync(x, c->dx, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipMemcpyAsync(k, c->dk, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
+  // un-permute into the scatter buffers, then download in original order
+  hipLaunchKernelGGL(unpermute_kernel, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, c->dx, c->dk,
+                     c->perm, c->n, c->dx2, c->dk2);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(x, c->dx2, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(k, c->dk2, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SWRT_OK;
   GUARD_END(c)
+}
+
+int swrt_set_locality(swrt_ctx* c, int64_t rebin_every, int64_t tile) {
+  if (!c) return SWRT_ERR_ARG;
+  if (rebin_every < 0 || tile < 0) return fail(c, SWRT_ERR_ARG, "negative locality parameter");
+  c->rebin_every = rebin_every;
+  c->tile = tile;
+  c->bin_valid = false;
+  return SWRT_OK;
 }
 
 int64_t swrt_packets_count(const swrt_ctx* c) { return c ? c->n : -1; }
@@ -666,7 +762,7 @@ int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, in
     c->hk = nk_;
     c->hcap = ncap;
   }
-  int rc = launch_advance(c, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every);
+  int rc = run_advance(c, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every);
   if (rc) return rc;
   c->hframes += new_frames;
   c->steps_done += nsteps;

@@ -1,0 +1,133 @@
+// swrt_bin.hpp — spatial binning of packets (locality for the stencil gather).
+//
+// Packets are independent, so their order in device memory is free: every
+// `rebin_every` steps they are counting-sorted by spatial tile (TILE x TILE
+// cells, tiles in row-major order) so that the lanes of a wavefront, the
+// waves of a workgroup and the workgroups of one XCD gather from the same
+// few cache lines of the field.  A permutation array keeps each packet's
+// original index; downloads and history frames are written in the original
+// order, so results are independent of the binning (and bit-identical).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "swrt_kernels.hpp"
+
+namespace swrt {
+
+struct BinGeom {
+  double dx, px, py, inv_px, inv_py;
+  int pow2x, pow2y, nx;
+  int tile;     // cells per tile side
+  int ntx;      // tiles per side
+};
+
+__device__ __forceinline__ int tile_of(const BinGeom& g, double x, double y) {
+  double a;
+  const int cx = cell_frac(x, g.dx, g.px, g.inv_px, g.pow2x, g.nx, a);
+  const int cy = cell_frac(y, g.dx, g.py, g.inv_py, g.pow2y, g.nx, a);
+  return (cx / g.tile) * g.ntx + (cy / g.tile);
+}
+
+// Pass 1: key per packet + histogram (LDS-aggregated, one global atomic per
+// (block, occupied bin)).  nbins <= kMaxBins.
+constexpr int kMaxBins = 16384;
+
+__global__ void __launch_bounds__(256) bin_count_kernel(BinGeom g, const double* x, int64_t n,
+                                                        int nbins, int* keys, int* counts) {
+  extern __shared__ int hist[];
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) {
+    const int key = tile_of(g, x[p], x[n + p]);
+    keys[p] = key;
+    atomicAdd(&hist[key], 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+    const int c = hist[b];
+    if (c) atomicAdd(&counts[b], c);
+  }
+}
+
+// Pass 2: exclusive scan of counts -> cursor (single workgroup, nbins <= 16384).
+__global__ void __launch_bounds__(1024) bin_scan_kernel(const int* counts, int nbins, int* cursor) {
+  __shared__ int part[1024];
+  const int per = (nbins + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  int s = 0;
+  for (int i = 0; i < per; ++i) {
+    const int b = b0 + i;
+    if (b < nbins) s += counts[b];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  // Hillis-Steele inclusive scan over the 1024 partials
+  for (int off = 1; off < 1024; off <<= 1) {
+    const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
+  for (int i = 0; i < per; ++i) {
+    const int b = b0 + i;
+    if (b < nbins) {
+      cursor[b] = run;
+      run += counts[b];
+    }
+  }
+}
+
+// Pass 3: scatter.  Each block ranks its packets per bin in LDS, reserves one
+// contiguous range per occupied bin with a single global atomic, then writes.
+__global__ void __launch_bounds__(256) bin_scatter_kernel(const double* x, const double* k,
+                                                          const int* perm, const int* keys, int64_t n,
+                                                          int nbins, int* cursor, double* x2,
+                                                          double* k2, int* perm2) {
+  extern __shared__ int sh[];
+  int* cnt = sh;            // nbins
+  int* base = sh + nbins;   // nbins
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) cnt[b] = 0;
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int key = 0, local = 0;
+  if (p < n) {
+    key = keys[p];
+    local = atomicAdd(&cnt[key], 1);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+    const int c = cnt[b];
+    if (c) base[b] = atomicAdd(&cursor[b], c);
+  }
+  __syncthreads();
+  if (p < n) {
+    const int64_t d = (int64_t)base[key] + local;
+    x2[d] = x[p];
+    x2[n + d] = x[n + p];
+    k2[d] = k[p];
+    k2[n + d] = k[n + p];
+    perm2[d] = perm[p];
+  }
+}
+
+__global__ void iota_kernel(int* perm, int64_t n) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) perm[p] = (int)p;
+}
+
+// Binned (device) order -> original order.
+__global__ void unpermute_kernel(const double* x, const double* k, const int* perm, int64_t n,
+                                 double* xo, double* ko) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int64_t d = perm[p];
+  xo[d] = x[p];
+  xo[n + d] = x[n + p];
+  ko[d] = k[p];
+  ko[n + d] = k[n + p];
+}
+
+}  // namespace swrt

@@ -127,12 +127,22 @@ struct StepArgs {
   double* hist_x;           // frames of N x 2 (NULL: no history)
   double* hist_k;
   int64_t frame0;           // history frame index of global step save_every-1
+  const int* perm;          // device order -> original packet index (history)
 };
+
+// XCD-aware block order: the dispatcher deals blocks round-robin over the 8
+// XCDs (b and b+8 share one); remap so each XCD walks one contiguous range of
+// the (spatially binned) packet array and its L2 holds one band of the field.
+// Bijective for any grid size (cdna_hip_programming.md §5 "XCD swizzle").
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nblk) {
+  const int64_t q = nblk / 8, r = nblk % 8, xcd = b % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
 
 // ode_symplectic.m:13-37 fused: drift(dt/2) -> kick(dt) -> drift(dt/2), nsteps
 // times with the packet held in registers.
 __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (p >= a.n) return;
   double x0 = a.x[p], y0 = a.x[a.n + p];
   double k0 = a.k[p], l0 = a.k[a.n + p];
@@ -159,8 +169,9 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
       const int64_t fr = a.frame0 + (sg + 1) / a.save_every - 1;
       double* hx = a.hist_x + fr * 2 * a.n;
       double* hk = a.hist_k + fr * 2 * a.n;
-      hx[p] = x0; hx[a.n + p] = y0;
-      hk[p] = k0; hk[a.n + p] = l0;
+      const int64_t o = a.perm[p];  // frames are stored in the original packet order
+      hx[o] = x0; hx[a.n + o] = y0;
+      hk[o] = k0; hk[a.n + o] = l0;
     }
   }
   a.x[p] = x0; a.x[a.n + p] = y0;

@@ -343,3 +343,25 @@ def test_sqrt_div_correctly_rounded_on_device(ctx):
     xo = x2 + half * (gH * k / w[:, None])
     np.testing.assert_array_equal(kg, k)
     np.testing.assert_array_equal(xg, xo)
+
+
+@pytest.mark.parametrize("rebin_every,tile", [(0, 0), (1, 4), (3, 8), (8, 0), (64, 16)])
+def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, tile):
+    """Binning only permutes the device order: final state and history frames
+    are bit-identical to the oracle and in the original packet order."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    pl = _planes(c["flow"])
+    ctx.set_field_grid(0, pl, nx, L)
+    ctx.set_locality(rebin_every, tile)
+    try:
+        xg, kg, hxg, hkg = ctx.leapfrog(c["x"], c["k"], c["dt"] * 4, 30, c["f"], 1.0, bump=orc.BUMP_SW,
+                                        save_every=5)
+    finally:
+        ctx.set_locality(8, 0)
+    xo, ko, hxo, hko = oracle_lib.leapfrog(pl, None, 0, 0, nx, nx, L / nx, orc.BUMP_SW, c["x"], c["k"],
+                                           c["dt"] * 4, 30, c["f"], 1.0, save_every=5)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
+    np.testing.assert_array_equal(hxg, hxo)
+    np.testing.assert_array_equal(hkg, hko)
