@@ -255,7 +255,10 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid) {
   hipEvent_t e0 = c->timing.ev[c->timing.used], e1 = c->timing.ev[c->timing.used + 1];
   c->timing.used += 2;
   HIPCHK(c, hipEventRecord(e0, c->stream));
-  hipLaunchKernelGGL(leapfrog_kernel, dim3(grid), dim3(256), 0, c->stream, a);
+  if (a.nslots == 2)
+    hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
+  else
+    hipLaunchKernelGGL(leapfrog_kernel<false>, dim3(grid), dim3(256), 0, c->stream, a);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipEventRecord(e1, c->stream));
   return SWRT_OK;

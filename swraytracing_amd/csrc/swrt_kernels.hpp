@@ -48,68 +48,142 @@ __device__ __forceinline__ int cell_frac(double x, double dx, double period, dou
   return c;
 }
 
+// x / d for a small integer constant d, correctly rounded (== IEEE x/d).
+// |d| in {1,2,4}: exact scaling.  |d| in {3,5}: Markstein's correction,
+//   q0 = RN(x*RN(1/d)), r = fma(-q0, d, x) (exact), q = RN(q0 + r*RN(1/d)),
+// which is the correctly rounded quotient because x/d is never within
+// 1/(2|d|) ulp of a rounding midpoint (its binary expansion is periodic with
+// period |d|-1), far more than the 2^-52-relative error of the correction.
+template <int D>
+__device__ __forceinline__ double div_const(double x) {
+  constexpr int A = D < 0 ? -D : D;
+  static_assert(A >= 1 && A <= 5, "divisor");
+  double q;
+  if constexpr (A == 1 || A == 2 || A == 4) {
+    q = x * (1.0 / (double)A);
+  } else {
+    constexpr double R = 1.0 / (double)A;  // RN(1/A), evaluated in double
+    const double q0 = x * R;
+    const double r = __builtin_fma(-q0, (double)A, x);
+    q = __builtin_fma(r, R, q0);
+  }
+  return D < 0 ? -q : q;
+}
+
 // interpolate.m:33-41 — w(i) = prod_{j != i} (a - j + bump)/(j - i), running
-// product in the reference order.  Divisions by the constants +-1,+-2,+-4 are
-// exact scalings; the compiler keeps IEEE division for +-3, +-5.
+// product in the reference order (multiply, then divide by the constant).
+template <int I, int J>
+__device__ __forceinline__ double wstep(double w, const double* t) {
+  if constexpr (I == J) {
+    return w;
+  } else {
+    return div_const<J - I>(w * t[J + 2]);
+  }
+}
+
+template <int I>
+__device__ __forceinline__ double lagrange_wi(const double* t) {
+  double w = 1.0;
+  w = wstep<I, -2>(w, t);
+  w = wstep<I, -1>(w, t);
+  w = wstep<I, 0>(w, t);
+  w = wstep<I, 1>(w, t);
+  w = wstep<I, 2>(w, t);
+  w = wstep<I, 3>(w, t);
+  return w;
+}
+
 __device__ __forceinline__ void lagrange_w(double a, double bump, double w[kNT]) {
   double t[kNT];
 #pragma unroll
   for (int j = -2; j <= 3; ++j) t[j + 2] = (a - (double)j) + bump;
-#pragma unroll
-  for (int i = -2; i <= 3; ++i) {
-    double wi = 1.0;
-#pragma unroll
-    for (int j = -2; j <= 3; ++j) {
-      if (i != j) wi = wi * t[j + 2] / (double)(j - i);
-    }
-    w[i + 2] = wi;
-  }
+  w[0] = lagrange_wi<-2>(t);
+  w[1] = lagrange_wi<-1>(t);
+  w[2] = lagrange_wi<0>(t);
+  w[3] = lagrange_wi<1>(t);
+  w[4] = lagrange_wi<2>(t);
+  w[5] = lagrange_wi<3>(t);
 }
 
-// Six-field stencil sum at (x, y): out[f] = sum_i sum_j (wx_i * wy_j) * F_f[ig, jg]
-// accumulated i-outer / j-inner exactly as interpolate.m:43-49 does per field.
-__device__ __forceinline__ void interp6(const FieldView& fv, double x, double y, double bump,
-                                        double out[kRec]) {
-  double ax, ay;
-  const int ic = cell_frac(x, fv.dx, fv.px, fv.inv_px, fv.pow2x, fv.nx, ax);
-  const int jc = cell_frac(y, fv.dx, fv.py, fv.inv_py, fv.pow2y, fv.nx, ay);
+// Cell and 1-D weights of a point: shared by every field and snapshot of the
+// same grid (the reference recomputes them per interpolate call; the values
+// are identical).
+struct Stencil {
+  int ic, jc;
   double wx[kNT], wy[kNT];
-  lagrange_w(ax, bump, wx);
-  lagrange_w(ay, bump, wy);
+};
+
+__device__ __forceinline__ void stencil_at(const FieldView& fv, double x, double y, double bump,
+                                           Stencil& s) {
+  double ax, ay;
+  s.ic = cell_frac(x, fv.dx, fv.px, fv.inv_px, fv.pow2x, fv.nx, ax);
+  s.jc = cell_frac(y, fv.dx, fv.py, fv.inv_py, fv.pow2y, fv.nx, ay);
+  lagrange_w(ax, bump, s.wx);
+  lagrange_w(ay, bump, s.wy);
+}
+
+// Six-field stencil sums of one or two snapshots:
+//   out[f] = sum_i sum_j (wx_i * wy_j) * F_f[ig, jg]
+// accumulated i-outer / j-inner exactly as interpolate.m:43-49 does per field.
+template <bool TWO>
+__device__ __forceinline__ void gather6(const double* nodes0, const double* nodes1, int npad,
+                                        const Stencil& s, double o0[kRec], double o1[kRec]) {
 #pragma unroll
-  for (int f = 0; f < kRec; ++f) out[f] = 0.0;
-  const double* base = fv.nodes + ((size_t)ic * fv.npad + jc) * kRec;
+  for (int f = 0; f < kRec; ++f) { o0[f] = 0.0; o1[f] = 0.0; }
+  const size_t off = ((size_t)s.ic * npad + s.jc) * kRec;
 #pragma unroll
   for (int i = 0; i < kNT; ++i) {
-    const double2* row = reinterpret_cast<const double2*>(base + (size_t)i * fv.npad * kRec);
+    const size_t ro = off + (size_t)i * npad * kRec;
+    const double2* r0 = reinterpret_cast<const double2*>(nodes0 + ro);
+    const double2* r1 = reinterpret_cast<const double2*>(nodes1 + ro);
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
-      const double2 a0 = row[3 * j + 0];
-      const double2 a1 = row[3 * j + 1];
-      const double2 a2 = row[3 * j + 2];
-      const double wij = wx[i] * wy[j];
-      out[0] = out[0] + wij * a0.x;
-      out[1] = out[1] + wij * a0.y;
-      out[2] = out[2] + wij * a1.x;
-      out[3] = out[3] + wij * a1.y;
-      out[4] = out[4] + wij * a2.x;
-      out[5] = out[5] + wij * a2.y;
+      const double wij = s.wx[i] * s.wy[j];
+      const double2 a0 = r0[3 * j + 0], a1 = r0[3 * j + 1], a2 = r0[3 * j + 2];
+      o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
+      o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
+      o0[4] = o0[4] + wij * a2.x; o0[5] = o0[5] + wij * a2.y;
+      if constexpr (TWO) {
+        const double2 b0 = r1[3 * j + 0], b1 = r1[3 * j + 1], b2 = r1[3 * j + 2];
+        o1[0] = o1[0] + wij * b0.x; o1[1] = o1[1] + wij * b0.y;
+        o1[2] = o1[2] + wij * b1.x; o1[3] = o1[3] + wij * b1.y;
+        o1[4] = o1[4] + wij * b2.x; o1[5] = o1[5] + wij * b2.y;
+      }
     }
   }
 }
 
-// interpolate_U.m:19-23 — (1 - alpha)*U1 + alpha*U2, per field.
-__device__ __forceinline__ void eval_flow(const FieldView& f0, const FieldView& f1, int nslots,
-                                          double alpha, double x, double y, double bump,
-                                          double I[kRec]) {
-  interp6(f0, x, y, bump, I);
-  if (nslots == 2) {
-    double J[kRec];
-    interp6(f1, x, y, bump, J);
+__device__ __forceinline__ void interp6(const FieldView& fv, double x, double y, double bump,
+                                        double out[kRec]) {
+  Stencil s;
+  stencil_at(fv, x, y, bump, s);
+  double dummy[kRec];
+  gather6<false>(fv.nodes, fv.nodes, fv.npad, s, out, dummy);
+}
+
+// interpolate_U.m:19-23 — (1 - alpha)*U1 + alpha*U2, per field.  Both
+// snapshots live on the same grid (checked on the host).
+template <bool TWO>
+__device__ __forceinline__ void eval_flow_t(const FieldView& f0, const FieldView& f1, double alpha,
+                                            double x, double y, double bump, double I[kRec]) {
+  Stencil s;
+  stencil_at(f0, x, y, bump, s);
+  double J[kRec];
+  gather6<TWO>(f0.nodes, f1.nodes, f0.npad, s, I, J);
+  if constexpr (TWO) {
     const double oma = 1 - alpha;
 #pragma unroll
     for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
   }
+}
+
+__device__ __forceinline__ void eval_flow(const FieldView& f0, const FieldView& f1, int nslots,
+                                          double alpha, double x, double y, double bump,
+                                          double I[kRec]) {
+  if (nslots == 2)
+    eval_flow_t<true>(f0, f1, alpha, x, y, bump, I);
+  else
+    eval_flow_t<false>(f0, f1, alpha, x, y, bump, I);
 }
 
 struct StepArgs {
@@ -141,6 +215,7 @@ __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nblk) {
 
 // ode_symplectic.m:13-37 fused: drift(dt/2) -> kick(dt) -> drift(dt/2), nsteps
 // times with the packet held in registers.
+template <bool TWO>
 __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
   const int64_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   if (p >= a.n) return;
@@ -154,7 +229,7 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
     const double y1 = y0 + a.half * (a.gH * l0 / w);
     // phi2(x1, k1, dt): U and (grad U)^T k at x1  (ode_symplectic.m:18-21)
     double I[kRec];
-    eval_flow(a.f0, a.f1, a.nslots, a.alpha0 + (double)sg * a.dalpha, x1, y1, a.bump, I);
+    eval_flow_t<TWO>(a.f0, a.f1, a.alpha0 + (double)sg * a.dalpha, x1, y1, a.bump, I);
     const double x2 = x1 + a.dt * I[0];
     const double y2 = y1 + a.dt * I[1];
     const double k2 = k0 - a.dt * (I[2] * k0 + I[4] * l0);  // RaytracingScheme.m:14
