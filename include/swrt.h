@@ -123,6 +123,12 @@ int64_t swrt_packets_count(const swrt_ctx* ctx);
  * are identical and in the original packet order. */
 int swrt_set_locality(swrt_ctx* ctx, int64_t rebin_every, int64_t tile);
 
+/* Packet-kernel variant (same results, bit for bit): 0 = automatic (the
+ * LDS-tiled kernel whenever binning is on and nx >= 32), 1 = one lane per
+ * packet gathering from the global node array, 2 = LDS-tiled kernel (16x16-
+ * cell tiles, field window staged in LDS, in-tile cell sort). */
+int swrt_set_kernel(swrt_ctx* ctx, int variant);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

@@ -52,6 +52,7 @@ SIGNATURES = {
     "swrt_packets_get": (_INT, [_VP, _P, _P]),
     "swrt_packets_count": (_I, [_VP]),
     "swrt_set_locality": (_INT, [_VP, _I, _I]),
+    "swrt_set_kernel": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
     "swrt_history_get": (_INT, [_VP, _I, _I, _P, _P]),
@@ -212,6 +213,9 @@ class Context:
 
     def set_locality(self, rebin_every=8, tile=0):
         self._chk(self._L.swrt_set_locality(self._h, int(rebin_every), int(tile)), "swrt_set_locality")
+
+    def set_kernel(self, variant=0):
+        self._chk(self._L.swrt_set_kernel(self._h, int(variant)), "swrt_set_kernel")
 
     def advance(self, dt, nsteps, f, gH, nslots=1, alpha0=0.0, dalpha=0.0, bump=1e-13, save_every=0):
         self._chk(self._L.swrt_advance(self._h, float(dt), int(nsteps), float(f), float(gH), int(nslots),

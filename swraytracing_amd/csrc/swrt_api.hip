@@ -18,12 +18,16 @@
 #include "swrt_bin.hpp"
 #include "swrt_fft.hpp"
 #include "swrt_kernels.hpp"
+#include "swrt_tile.hpp"
 
 using namespace swrt;
 
 namespace {
 
 constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
+constexpr int kTile = 16;               // LDS tile kernel: cells per tile side
+constexpr int kMargin = 2;              // LDS tile kernel: drift margin (cells)
+constexpr int kTileThreads = 512;
 
 struct Slot {
   double* nodes = nullptr;  // padded interleaved records
@@ -59,7 +63,9 @@ struct swrt_ctx {
   double* dk2 = nullptr;
   int* perm2 = nullptr;
   int* keys = nullptr;   // N
-  int* bins = nullptr;   // 2 * kMaxBins (counts | cursor)
+  int* bins = nullptr;   // counts | cursor | starts  (3 * kMaxBins + 1)
+  int kernel = 0;        // 0 auto, 1 per-packet global gather, 2 LDS tile kernel
+  int nbins = 0;         // bins of the current binning
   int64_t n = 0;
   int64_t cap = 0;
   int64_t rebin_every = 8;  // steps between spatial re-binning (0: never)
@@ -232,6 +238,9 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
   return SWRT_OK;
 }
 
+bool use_tile_kernel(const swrt_ctx* c);
+int tile_launch(swrt_ctx* c, const StepArgs& a);
+
 // Record a timing event pair around one leapfrog launch.
 int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid) {
   // timing events (pairs), grown on demand; fold into a running sum when full
@@ -255,16 +264,28 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid) {
   hipEvent_t e0 = c->timing.ev[c->timing.used], e1 = c->timing.ev[c->timing.used + 1];
   c->timing.used += 2;
   HIPCHK(c, hipEventRecord(e0, c->stream));
-  if (a.nslots == 2)
-    hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
-  else
-    hipLaunchKernelGGL(leapfrog_kernel<false>, dim3(grid), dim3(256), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
+  if (use_tile_kernel(c)) {
+    int rc = tile_launch(c, a);
+    if (rc) return rc;
+  } else {
+    if (a.nslots == 2)
+      hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
+    else
+      hipLaunchKernelGGL(leapfrog_kernel<false>, dim3(grid), dim3(256), 0, c->stream, a);
+    HIPCHK(c, hipGetLastError());
+  }
   HIPCHK(c, hipEventRecord(e1, c->stream));
   return SWRT_OK;
 }
 
+bool use_tile_kernel(const swrt_ctx* c) {
+  if (c->rebin_every <= 0) return false;
+  if (c->kernel == 2) return true;
+  return c->kernel == 0 && c->slot[0].nx >= 2 * kTile;
+}
+
 int tile_cells(const swrt_ctx* c, int64_t nx) {
+  if (use_tile_kernel(c)) return kTile;
   if (c->tile > 0) return (int)std::min<int64_t>(c->tile, nx);
   // default: 8x8-cell tiles, coarser on big grids so bins stay <= 4096
   int t = 8;
@@ -289,7 +310,8 @@ int rebin(swrt_ctx* c) {
   hipLaunchKernelGGL(bin_count_kernel, dim3(grid), dim3(256), sizeof(int) * nbins, c->stream, g, c->dx, n,
                      nbins, c->keys, c->bins);
   HIPCHK(c, hipGetLastError());
-  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins);
+  hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins,
+                     c->bins + 2 * kMaxBins);
   HIPCHK(c, hipGetLastError());
   hipLaunchKernelGGL(bin_scatter_kernel, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream, c->dx,
                      c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2);
@@ -299,6 +321,29 @@ int rebin(swrt_ctx* c) {
   std::swap(c->perm, c->perm2);
   c->steps_since_bin = 0;
   c->bin_valid = true;
+  c->nbins = nbins;
+  return SWRT_OK;
+}
+
+int tile_launch(swrt_ctx* c, const StepArgs& a) {
+  TileArgs t;
+  t.s = a;
+  t.x_out = c->dx2;
+  t.k_out = c->dk2;
+  t.perm_out = c->perm2;
+  t.starts = c->bins + 2 * kMaxBins;
+  t.ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  const unsigned grid = (unsigned)(t.ntx * t.ntx);
+  if (a.nslots == 2)
+    hipLaunchKernelGGL((tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>), dim3(grid),
+                       dim3(kTileThreads), 0, c->stream, t);
+  else
+    hipLaunchKernelGGL((tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>), dim3(grid),
+                       dim3(kTileThreads), 0, c->stream, t);
+  HIPCHK(c, hipGetLastError());
+  std::swap(c->dx, c->dx2);
+  std::swap(c->dk, c->dk2);
+  std::swap(c->perm, c->perm2);
   return SWRT_OK;
 }
 
@@ -683,7 +728,7 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
     HIPCHK(c, hipMalloc(&c->keys, sizeof(int) * n));
     c->cap = n;
   }
-  if (!c->bins) HIPCHK(c, hipMalloc(&c->bins, sizeof(int) * 2 * kMaxBins));
+  if (!c->bins) HIPCHK(c, hipMalloc(&c->bins, sizeof(int) * (3 * kMaxBins + 1)));
   c->n = n;
   if (n > 0) {
     HIPCHK(c, hipMemcpyAsync(c->dx, x, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
@@ -716,6 +761,14 @@ int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SWRT_OK;
   GUARD_END(c)
+}
+
+int swrt_set_kernel(swrt_ctx* c, int variant) {
+  if (!c) return SWRT_ERR_ARG;
+  if (variant < 0 || variant > 2) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0, 1 or 2");
+  c->kernel = variant;
+  c->bin_valid = false;
+  return SWRT_OK;
 }
 
 int swrt_set_locality(swrt_ctx* c, int64_t rebin_every, int64_t tile) {

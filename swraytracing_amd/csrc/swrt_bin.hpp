@@ -52,7 +52,8 @@ __global__ void __launch_bounds__(256) bin_count_kernel(BinGeom g, const double*
 }
 
 // Pass 2: exclusive scan of counts -> cursor (single workgroup, nbins <= 16384).
-__global__ void __launch_bounds__(1024) bin_scan_kernel(const int* counts, int nbins, int* cursor) {
+__global__ void __launch_bounds__(1024) bin_scan_kernel(const int* counts, int nbins, int* cursor,
+                                                        int* starts) {
   __shared__ int part[1024];
   const int per = (nbins + 1023) / 1024;
   const int b0 = threadIdx.x * per;
@@ -75,9 +76,11 @@ __global__ void __launch_bounds__(1024) bin_scan_kernel(const int* counts, int n
     const int b = b0 + i;
     if (b < nbins) {
       cursor[b] = run;
+      starts[b] = run;
       run += counts[b];
     }
   }
+  if (threadIdx.x == 1023) starts[nbins] = part[1023];
 }
 
 // Pass 3: scatter.  Each block ranks its packets per bin in LDS, reserves one

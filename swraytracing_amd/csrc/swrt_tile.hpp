@@ -1,0 +1,208 @@
+// swrt_tile.hpp — LDS-tiled fused leapfrog (the throughput kernel).
+//
+// Packets are counting-sorted by T x T-cell spatial tile (swrt_bin.hpp).  One
+// workgroup owns one tile per launch:
+//   1. it stages the tile's field window — (T + 5 + 2M)^2 nodes, i.e. the
+//      tile, the 6x6 stencil reach and an M-cell drift margin — for one or
+//      two snapshots into LDS (chunk-major: chunk c of node e at
+//      lds[c*WN + e], 16 B each, so lanes reading neighbouring nodes hit
+//      different LDS banks);
+//   2. it counting-sorts the tile's packets by their cell inside the tile
+//      (LDS histogram + scan) so that the 16-lane groups of a ds_read_b128
+//      read equal (broadcast) or adjacent nodes;
+//   3. each lane advances one packet: the 36-tap gathers come from LDS, or —
+//      for a packet that drifted beyond the margin since the last re-binning —
+//      from the global node array (same arithmetic, same result);
+//   4. outputs are written in the in-tile sorted order to the other state
+//      buffer (double-buffered), carrying the permutation along.
+// Arithmetic is identical to leapfrog_kernel (same Stencil / weights / blend
+// / order), so results are bit-identical to the oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "swrt_kernels.hpp"
+
+namespace swrt {
+
+struct TileArgs {
+  StepArgs s;            // fields, physics, history (s.x/s.k/s.perm are the inputs)
+  double* x_out;
+  double* k_out;
+  int* perm_out;
+  const int* starts;     // ntiles + 1 packet offsets of the tiles
+  int ntx;               // tiles per side
+};
+
+// a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
+__device__ __forceinline__ int ring_diff(int a, int b, int n) {
+  int d = a - b;
+  if (d >= n / 2) d -= n;
+  if (d < -n / 2) d += n;
+  return d;
+}
+
+template <bool TWO, int W, int WN>
+__device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const Stencil& s,
+                                            double o0[kRec], double o1[kRec]) {
+#pragma unroll
+  for (int f = 0; f < kRec; ++f) { o0[f] = 0.0; o1[f] = 0.0; }
+  const double2* p = lds + node0;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const int e = i * W + j;
+      const double wij = s.wx[i] * s.wy[j];
+      const double2 a0 = p[0 * WN + e], a1 = p[1 * WN + e], a2 = p[2 * WN + e];
+      o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
+      o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
+      o0[4] = o0[4] + wij * a2.x; o0[5] = o0[5] + wij * a2.y;
+      if constexpr (TWO) {
+        const double2 b0 = p[3 * WN + e], b1 = p[4 * WN + e], b2 = p[5 * WN + e];
+        o1[0] = o1[0] + wij * b0.x; o1[1] = o1[1] + wij * b0.y;
+        o1[2] = o1[2] + wij * b1.x; o1[3] = o1[3] + wij * b1.y;
+        o1[4] = o1[4] + wij * b2.x; o1[5] = o1[5] + wij * b2.y;
+      }
+    }
+  }
+}
+
+template <bool TWO, int T, int M, int NT>
+__global__ void __launch_bounds__(NT) tile_leapfrog_kernel(TileArgs ta) {
+  constexpr int W = T + 5 + 2 * M;  // window side in nodes
+  constexpr int WN = W * W;
+  constexpr int NCH = TWO ? 6 : 3;  // 16-B chunks per node
+  constexpr int NB = T * T + 1;     // in-tile cell bins + "elsewhere"
+  constexpr int MAXB = 2 * NT;      // packets sorted per batch
+  __shared__ double2 win[NCH * WN];
+  __shared__ int hist[NB];
+  __shared__ int kr[MAXB];          // key << 16 | rank
+  __shared__ int order[MAXB];
+
+  const StepArgs& a = ta.s;
+  const int tid = threadIdx.x;
+  const int tile = (int)xcd_block(blockIdx.x, gridDim.x);
+  const int tx = tile / ta.ntx, ty = tile % ta.ntx;
+  const int nx = a.f0.nx, npad = a.f0.npad;
+  const int ox = tx * T, oy = ty * T;  // tile origin (cells)
+
+  // 1. stage the window: node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx
+  for (int e = tid; e < WN; e += NT) {
+    const int wi = e / W, wj = e % W;
+    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
+    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
+    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec;
+    const double2* s0 = reinterpret_cast<const double2*>(a.f0.nodes + src);
+    win[0 * WN + e] = s0[0];
+    win[1 * WN + e] = s0[1];
+    win[2 * WN + e] = s0[2];
+    if constexpr (TWO) {
+      const double2* s1 = reinterpret_cast<const double2*>(a.f1.nodes + src);
+      win[3 * WN + e] = s1[0];
+      win[4 * WN + e] = s1[1];
+      win[5 * WN + e] = s1[2];
+    }
+  }
+
+  const int pbeg = ta.starts[tile], pend = ta.starts[tile + 1];
+  for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
+    const int nb = min(MAXB, pend - b0);
+    // 2. in-tile counting sort by the cell of the current position
+    for (int h = tid; h < NB; h += NT) hist[h] = 0;
+    __syncthreads();  // (also publishes the window on the first batch)
+    for (int i = tid; i < nb; i += NT) {
+      const int64_t p = b0 + i;
+      double fa;
+      const int ic = cell_frac(a.x[p], a.f0.dx, a.f0.px, a.f0.inv_px, a.f0.pow2x, nx, fa);
+      const int jc = cell_frac(a.x[a.n + p], a.f0.dx, a.f0.py, a.f0.inv_py, a.f0.pow2y, nx, fa);
+      const int dx_ = ring_diff(ic, ox, nx), dy_ = ring_diff(jc, oy, nx);
+      const int key = (dx_ >= 0 && dx_ < T && dy_ >= 0 && dy_ < T) ? dx_ * T + dy_ : T * T;
+      const int r = atomicAdd(&hist[key], 1);
+      kr[i] = (key << 16) | r;
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of NB bins by one wavefront
+      constexpr int PER = (NB + 63) / 64;
+      int loc[PER];
+      int sum = 0;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int h = tid * PER + q;
+        loc[q] = h < NB ? hist[h] : 0;
+        sum += loc[q];
+      }
+      int incl = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (tid >= off) incl += v;
+      }
+      int run = incl - sum;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int h = tid * PER + q;
+        if (h < NB) hist[h] = run;
+        run += loc[q];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nb; i += NT) {
+      const int v = kr[i];
+      order[hist[v >> 16] + (v & 0xffff)] = i;
+    }
+    __syncthreads();
+
+    // 3. advance the packets in sorted order
+    for (int r = tid; r < nb; r += NT) {
+      const int64_t pi = b0 + order[r];
+      const int64_t po = b0 + r;
+      double x0 = a.x[pi], y0 = a.x[a.n + pi];
+      double k0 = a.k[pi], l0 = a.k[a.n + pi];
+      const int orig = a.perm[pi];
+      for (int st = 0; st < a.nsteps; ++st) {
+        const int64_t sg = a.s0 + st;
+        double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
+        const double x1 = x0 + a.half * (a.gH * k0 / w);
+        const double y1 = y0 + a.half * (a.gH * l0 / w);
+        Stencil sc;
+        stencil_at(a.f0, x1, y1, a.bump, sc);
+        const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
+        double I[kRec], J[kRec];
+        if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M) {
+          gather6_lds<TWO, W, WN>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
+        } else {
+          gather6<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
+        }
+        if constexpr (TWO) {
+          const double alpha = a.alpha0 + (double)sg * a.dalpha;
+          const double oma = 1 - alpha;
+#pragma unroll
+          for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
+        }
+        const double x2 = x1 + a.dt * I[0];
+        const double y2 = y1 + a.dt * I[1];
+        const double k2 = k0 - a.dt * (I[2] * k0 + I[4] * l0);
+        const double l2 = l0 - a.dt * (I[3] * k0 + I[5] * l0);
+        w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
+        x0 = x2 + a.half * (a.gH * k2 / w);
+        y0 = y2 + a.half * (a.gH * l2 / w);
+        k0 = k2;
+        l0 = l2;
+        if (a.hist_x != nullptr && ((sg + 1) % a.save_every) == 0) {
+          const int64_t fr = a.frame0 + (sg + 1) / a.save_every - 1;
+          double* hx = a.hist_x + fr * 2 * a.n;
+          double* hk = a.hist_k + fr * 2 * a.n;
+          hx[orig] = x0; hx[a.n + orig] = y0;
+          hk[orig] = k0; hk[a.n + orig] = l0;
+        }
+      }
+      ta.x_out[po] = x0; ta.x_out[a.n + po] = y0;
+      ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
+      ta.perm_out[po] = orig;
+    }
+    __syncthreads();  // LDS sort arrays are reused by the next batch
+  }
+}
+
+}  // namespace swrt

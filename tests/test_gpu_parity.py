@@ -365,3 +365,65 @@ def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, til
     np.testing.assert_array_equal(kg, ko)
     np.testing.assert_array_equal(hxg, hxo)
     np.testing.assert_array_equal(hkg, hko)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("nslots", [1, 2])
+@pytest.mark.parametrize("dt_scale", [1.0, 40.0])
+def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, nslots, dt_scale):
+    """Per-packet (1) and LDS-tiled (2) kernels give the oracle's bits; the
+    large-dt case drives packets out of the LDS window (global fallback)."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    p0 = _planes(c["flow"])
+    p1 = _planes({n: np.asarray(v) * 0.8 for n, v in c["flow"].items()})
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    dt = c["dt"] * dt_scale
+    ctx.set_kernel(variant)
+    ctx.set_locality(5, 0)
+    try:
+        xg, kg, hxg, hkg = ctx.leapfrog(c["x"], c["k"], dt, 12, c["f"], 1.0, nslots=nslots, alpha0=0.1,
+                                        dalpha=0.07, bump=orc.BUMP_QG, save_every=3)
+    finally:
+        ctx.set_kernel(0)
+        ctx.set_locality(8, 0)
+    xo, ko, hxo, hko = oracle_lib.leapfrog(p0, p1 if nslots == 2 else None, 0.1, 0.07, nx, 2 * nx, L / nx,
+                                           orc.BUMP_QG, c["x"], c["k"], dt, 12, c["f"], 1.0, save_every=3)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
+    np.testing.assert_array_equal(hxg, hxo)
+    np.testing.assert_array_equal(hkg, hko)
+
+
+def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib):
+    """512^2 two-snapshot field, 2e5 packets, LDS kernel with re-binning every
+    3 steps over 10 steps: random subset bit-identical to the oracle."""
+    nx, L = 512, 20.0
+    rng = np.random.default_rng(2024)
+    kmax = nx // 2 - 1
+    qk = np.zeros((2 * kmax + 1, kmax + 1), complex)
+    kx = np.arange(-kmax, kmax + 1)[:, None]
+    ky = np.arange(kmax + 1)[None, :]
+    ring = (kx * kx + ky * ky > 100) & (kx * kx + ky * ky <= 900)
+    qk[ring] = np.exp(2j * np.pi * rng.random(ring.sum())) * 0.02
+    ctx.set_field_qk(0, qk, nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+    ctx.set_field_qk(1, qk * np.exp(0.05j), nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+    p0 = ctx.get_field_grid(0, nx)
+    p1 = ctx.get_field_grid(1, nx)
+    N = 200_000
+    x, k = orc.initial_packets(N, L, 4.0, 3.0, 1.0, rng)
+    ctx.set_kernel(2)
+    ctx.set_locality(3, 0)
+    try:
+        ctx.packets_set(x, k)
+        ctx.advance(0.01, 10, 3.0, 1.0, nslots=2, alpha0=0.05, dalpha=0.1, bump=orc.BUMP_QG)
+        xg, kg = ctx.packets_get()
+    finally:
+        ctx.set_kernel(0)
+        ctx.set_locality(8, 0)
+    idx = np.sort(rng.choice(N, 2000, replace=False))
+    xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.05, 0.1, nx, 2 * nx, L / nx, orc.BUMP_QG, x[idx], k[idx], 0.01,
+                                       10, 3.0, 1.0)
+    np.testing.assert_array_equal(xg[idx], xo)
+    np.testing.assert_array_equal(kg[idx], ko)
