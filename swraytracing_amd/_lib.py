@@ -22,7 +22,8 @@ except Exception:  # torch absent: the system HIP runtime is used
     pass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libswrt.so")
+# SWRT_LIB_PATH: alternative build of the same ABI (tuning experiments only)
+LIB_PATH = os.environ.get("SWRT_LIB_PATH") or os.path.join(_HERE, "libswrt.so")
 
 SWRT_OK = 0
 ERRORS = {1: "SWRT_ERR_ARG", 2: "SWRT_ERR_HIP", 3: "SWRT_ERR_STATE", 4: "SWRT_ERR_ALLOC"}

@@ -25,9 +25,18 @@ using namespace swrt;
 namespace {
 
 constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
-constexpr int kTile = 16;               // LDS tile kernel: cells per tile side
-constexpr int kMargin = 2;              // LDS tile kernel: drift margin (cells)
-constexpr int kTileThreads = 512;
+#ifndef SWRT_TILE
+#define SWRT_TILE 16
+#endif
+#ifndef SWRT_MARGIN
+#define SWRT_MARGIN 2
+#endif
+#ifndef SWRT_TILE_THREADS
+#define SWRT_TILE_THREADS 512
+#endif
+constexpr int kTile = SWRT_TILE;                // LDS tile kernel: cells per tile side
+constexpr int kMargin = SWRT_MARGIN;            // LDS tile kernel: drift margin (cells)
+constexpr int kTileThreads = SWRT_TILE_THREADS;
 
 struct Slot {
   double* nodes = nullptr;  // padded interleaved records

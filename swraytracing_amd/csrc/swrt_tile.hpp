@@ -68,8 +68,12 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
   }
 }
 
+#ifndef SWRT_TILE_MIN_WAVES
+#define SWRT_TILE_MIN_WAVES 1
+#endif
+
 template <bool TWO, int T, int M, int NT>
-__global__ void __launch_bounds__(NT) tile_leapfrog_kernel(TileArgs ta) {
+__global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
   constexpr int WN = W * W;
   constexpr int NCH = TWO ? 6 : 3;  // 16-B chunks per node
