@@ -144,7 +144,7 @@ def main():
     ap.add_argument("--seed", type=int, default=146)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--rebin-every", type=int, default=8, help="steps between spatial re-binning (0: off)")
+    ap.add_argument("--rebin-every", type=int, default=4, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
     args = ap.parse_args()

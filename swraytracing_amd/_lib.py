@@ -212,7 +212,7 @@ class Context:
         self._chk(self._L.swrt_packets_get(self._h, _p(x), _p(k)), "swrt_packets_get")
         return x, k
 
-    def set_locality(self, rebin_every=8, tile=0):
+    def set_locality(self, rebin_every=4, tile=0):
         self._chk(self._L.swrt_set_locality(self._h, int(rebin_every), int(tile)), "swrt_set_locality")
 
     def set_kernel(self, variant=0):

@@ -77,7 +77,7 @@ struct swrt_ctx {
   int nbins = 0;         // bins of the current binning
   int64_t n = 0;
   int64_t cap = 0;
-  int64_t rebin_every = 8;  // steps between spatial re-binning (0: never)
+  int64_t rebin_every = 4;  // steps between spatial re-binning (0: never)
   int64_t tile = 0;         // cells per tile side (0: automatic)
   int64_t steps_since_bin = 0;
   bool bin_valid = false;

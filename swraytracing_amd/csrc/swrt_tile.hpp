@@ -69,7 +69,7 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
 }
 
 #ifndef SWRT_TILE_MIN_WAVES
-#define SWRT_TILE_MIN_WAVES 1
+#define SWRT_TILE_MIN_WAVES 4
 #endif
 
 template <bool TWO, int T, int M, int NT>

@@ -358,7 +358,7 @@ def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, til
         xg, kg, hxg, hkg = ctx.leapfrog(c["x"], c["k"], c["dt"] * 4, 30, c["f"], 1.0, bump=orc.BUMP_SW,
                                         save_every=5)
     finally:
-        ctx.set_locality(8, 0)
+        ctx.set_locality(4, 0)
     xo, ko, hxo, hko = oracle_lib.leapfrog(pl, None, 0, 0, nx, nx, L / nx, orc.BUMP_SW, c["x"], c["k"],
                                            c["dt"] * 4, 30, c["f"], 1.0, save_every=5)
     np.testing.assert_array_equal(xg, xo)
@@ -387,7 +387,7 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, nslots, dt_
                                         dalpha=0.07, bump=orc.BUMP_QG, save_every=3)
     finally:
         ctx.set_kernel(0)
-        ctx.set_locality(8, 0)
+        ctx.set_locality(4, 0)
     xo, ko, hxo, hko = oracle_lib.leapfrog(p0, p1 if nslots == 2 else None, 0.1, 0.07, nx, 2 * nx, L / nx,
                                            orc.BUMP_QG, c["x"], c["k"], dt, 12, c["f"], 1.0, save_every=3)
     np.testing.assert_array_equal(xg, xo)
@@ -421,7 +421,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib):
         xg, kg = ctx.packets_get()
     finally:
         ctx.set_kernel(0)
-        ctx.set_locality(8, 0)
+        ctx.set_locality(4, 0)
     idx = np.sort(rng.choice(N, 2000, replace=False))
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.05, 0.1, nx, 2 * nx, L / nx, orc.BUMP_QG, x[idx], k[idx], 0.01,
                                        10, 3.0, 1.0)
