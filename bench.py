@@ -36,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import swraytracing_amd as sw  # noqa: E402
+from swraytracing_amd.dist import gather_to_root, max_over_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (spec)
@@ -147,6 +148,10 @@ def main():
     ap.add_argument("--rebin-every", type=int, default=4, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
+    ap.add_argument("--gather", action="store_true",
+                    help="after timing, gather all trajectories to rank 0 (one all_gather)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,12 +159,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     args.world, args.rank = world, rank
     distributed = world > 1
+    ndev = max(1, torch.cuda.device_count())
+    device = local % ndev
+    torch.cuda.set_device(device)
     if distributed:
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", init_method="env://")
-    dev = torch.device("cuda", local)
+        dist.init_process_group(backend=args.dist_backend, init_method="env://")
+    dev = torch.device("cuda", device)
 
-    ctx = sw.Context(local)
+    ctx = sw.Context(device)
     ctx.set_locality(args.rebin_every, args.tile)
     ctx.set_kernel(args.kernel)
     rng = np.random.default_rng(args.seed + rank)
@@ -187,11 +194,14 @@ def main():
     elapsed = t1 - t0
     kms, launches = ctx.kernel_time(reset=True)
     if distributed:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = max_over_ranks(elapsed, backend=args.dist_backend)
     xg, kg = ctx.packets_get()
     finite = bool(np.isfinite(xg).all() and np.isfinite(kg).all())
+    gathered = None
+    if distributed and args.gather:
+        full = gather_to_root(np.concatenate([xg, kg], axis=1), args.packets * world, world, rank,
+                              backend=args.dist_backend)
+        gathered = None if full is None else bool(np.isfinite(full).all() and full.shape[0] == args.packets * world)
 
     N = args.packets
     total_ps = N * world * args.substeps * args.steps
@@ -228,6 +238,8 @@ def main():
                      "launches": launches},
         "finite": finite,
     }
+    if gathered is not None:
+        out["gathered_finite"] = gathered
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, w, args.cpu_seconds)
     elif rank == 0:
