@@ -1,0 +1,159 @@
+// swrt_mex.cpp — MATLAB MEX gateway over the swrt C ABI (include/swrt.h).
+//
+// The reference-side binding a maintainer adds to ndefilippis/SWRaytracing so
+// that SpectralScheme / ode_symplectic / interpolate_U callers run on the
+// MI355X.  Deliberately thin: argument marshalling only, every error is raised
+// with mexErrMsgIdAndTxt AFTER the C call has returned (never from HIP code).
+// Build (MATLAB R2018a+, interleaved complex):
+//   mex -R2018a -I../include swrt_mex.cpp -L../swraytracing_amd -lswrt
+// Usage (see SpectralSchemeGPU.m, ode_symplectic_gpu.m):
+//   swrt_mex('create', device)
+//   swrt_mex('set_field_psi', slot, psi_grid, L)             % SpectralScheme ctor
+//   swrt_mex('set_field_qk', slot, qk, L, K_d2, shear, kscale, ny_period)   % grid_U
+//   swrt_mex('set_field_grid', slot, u, v, ux, uy, vx, vy, L, ny_period)
+//   out6 = swrt_mex('eval', x, y, nslots, alpha, bump)       % 6 x n
+//   FI   = swrt_mex('interpolate', x, y, F, dx, dy, bump)    % interpolate.m
+//   [x, k, hx, hk] = swrt_mex('leapfrog', x0, k0, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every)
+//   fk = swrt_mex('g2k', fg);  fg = swrt_mex('k2g', fk);
+//   swrt_mex('destroy')
+#include <cstring>
+#include <string>
+
+#include "mex.h"
+#include "swrt.h"
+
+static swrt_ctx* g_ctx = nullptr;
+
+static void cleanup() {
+  if (g_ctx) {
+    swrt_destroy(g_ctx);
+    g_ctx = nullptr;
+  }
+}
+
+static void check(int rc, const char* what) {
+  if (rc != SWRT_OK) {
+    std::string msg = std::string(what) + ": " + (g_ctx ? swrt_last_error(g_ctx) : "no context");
+    mexErrMsgIdAndTxt("swrt:call", "%s (code %d)", msg.c_str(), rc);
+  }
+}
+
+static double scalar(const mxArray* a) { return mxGetScalar(a); }
+
+static const double* reals(const mxArray* a, const char* name) {
+  if (!mxIsDouble(a) || mxIsComplex(a)) mexErrMsgIdAndTxt("swrt:arg", "%s must be real double", name);
+  return mxGetDoubles(a);
+}
+
+static swrt_ctx* ctx() {
+  if (!g_ctx) mexErrMsgIdAndTxt("swrt:state", "call swrt_mex('create', device) first");
+  return g_ctx;
+}
+
+void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
+  if (nrhs < 1 || !mxIsChar(prhs[0])) mexErrMsgIdAndTxt("swrt:arg", "first argument: command");
+  char cmd[64];
+  mxGetString(prhs[0], cmd, sizeof(cmd));
+
+  if (!strcmp(cmd, "create")) {
+    if (!g_ctx) {
+      const int dev = nrhs > 1 ? (int)scalar(prhs[1]) : 0;
+      const int rc = swrt_create(dev, &g_ctx);
+      if (rc != SWRT_OK) mexErrMsgIdAndTxt("swrt:create", "swrt_create failed (code %d)", rc);
+      mexAtExit(cleanup);
+      mexLock();
+    }
+    return;
+  }
+  if (!strcmp(cmd, "destroy")) {
+    cleanup();
+    if (mexIsLocked()) mexUnlock();
+    return;
+  }
+  if (!strcmp(cmd, "set_field_psi")) {  // (slot, psi, L)
+    const mxArray* psi = prhs[2];
+    const int64_t nx = (int64_t)mxGetM(psi);
+    check(swrt_set_field_psi(ctx(), (int)scalar(prhs[1]), reals(psi, "psi"), nx, scalar(prhs[3])),
+          "swrt_set_field_psi");
+    return;
+  }
+  if (!strcmp(cmd, "set_field_qk")) {  // (slot, qk, L, K_d2, shear, kscale, ny_period)
+    const mxArray* qk = prhs[2];
+    if (!mxIsComplex(qk)) mexErrMsgIdAndTxt("swrt:arg", "qk must be complex");
+    const int64_t nx = (int64_t)mxGetM(qk) + 1;
+    check(swrt_set_field_qk(ctx(), (int)scalar(prhs[1]), (const double*)mxGetComplexDoubles(qk), nx,
+                            scalar(prhs[3]), scalar(prhs[4]), scalar(prhs[5]), scalar(prhs[6]),
+                            (int64_t)scalar(prhs[7])),
+          "swrt_set_field_qk");
+    return;
+  }
+  if (!strcmp(cmd, "set_field_grid")) {  // (slot, u, v, ux, uy, vx, vy, L, ny_period)
+    const int64_t nx = (int64_t)mxGetM(prhs[2]);
+    const size_t plane = (size_t)(nx * nx);
+    mxArray* tmp = mxCreateDoubleMatrix(plane, 6, mxREAL);  // 6 planes, MATLAB-owned scratch
+    double* d = mxGetDoubles(tmp);
+    for (int f = 0; f < 6; ++f) memcpy(d + f * plane, reals(prhs[2 + f], "field"), plane * sizeof(double));
+    const int rc = swrt_set_field_grid(ctx(), (int)scalar(prhs[1]), d, nx, scalar(prhs[8]),
+                                       (int64_t)scalar(prhs[9]));
+    mxDestroyArray(tmp);
+    check(rc, "swrt_set_field_grid");
+    return;
+  }
+  if (!strcmp(cmd, "eval")) {  // (x, y, nslots, alpha, bump) -> 6 x n
+    const size_t n = mxGetNumberOfElements(prhs[1]);
+    plhs[0] = mxCreateDoubleMatrix(n, 6, mxREAL);  // column f = field f (6 x n row-major == n x 6 col-major)
+    check(swrt_eval(ctx(), reals(prhs[1], "x"), reals(prhs[2], "y"), (int64_t)n, (int)scalar(prhs[3]),
+                    scalar(prhs[4]), scalar(prhs[5]), mxGetDoubles(plhs[0])),
+          "swrt_eval");
+    return;
+  }
+  if (!strcmp(cmd, "interpolate")) {  // (x, y, F, dx, dy, bump)
+    const mxArray* F = prhs[3];
+    const int64_t nx = (int64_t)mxGetM(F);
+    const int64_t nyF = (int64_t)(mxGetNumberOfElements(F) / mxGetM(F));
+    const size_t n = mxGetNumberOfElements(prhs[1]);
+    plhs[0] = mxCreateNumericArray(mxGetNumberOfDimensions(prhs[1]), mxGetDimensions(prhs[1]),
+                                   mxDOUBLE_CLASS, mxREAL);
+    check(swrt_interpolate(ctx(), reals(F, "F"), nx, nyF, scalar(prhs[4]), scalar(prhs[5]), scalar(prhs[6]),
+                           reals(prhs[1], "x"), reals(prhs[2], "y"), (int64_t)n, mxGetDoubles(plhs[0])),
+          "swrt_interpolate");
+    return;
+  }
+  if (!strcmp(cmd, "leapfrog")) {
+    // (x0 Nx2, k0 Nx2, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every)
+    const int64_t n = (int64_t)mxGetM(prhs[1]);
+    const int64_t nsteps = (int64_t)scalar(prhs[4]);
+    const int64_t save_every = nrhs > 11 ? (int64_t)scalar(prhs[11]) : 0;
+    plhs[0] = mxDuplicateArray(prhs[1]);
+    plhs[1] = mxDuplicateArray(prhs[2]);
+    double *hx = nullptr, *hk = nullptr;
+    if (nlhs > 2 && save_every > 0) {
+      const mwSize dims[3] = {(mwSize)n, 2, (mwSize)(nsteps / save_every)};  // frames of N x 2
+      plhs[2] = mxCreateNumericArray(3, dims, mxDOUBLE_CLASS, mxREAL);
+      plhs[3] = mxCreateNumericArray(3, dims, mxDOUBLE_CLASS, mxREAL);
+      hx = mxGetDoubles(plhs[2]);
+      hk = mxGetDoubles(plhs[3]);
+    }
+    check(swrt_leapfrog(ctx(), mxGetDoubles(plhs[0]), mxGetDoubles(plhs[1]), n, scalar(prhs[3]), nsteps,
+                        scalar(prhs[5]), scalar(prhs[6]), (int)scalar(prhs[7]), scalar(prhs[8]),
+                        scalar(prhs[9]), scalar(prhs[10]), hx ? save_every : 0, hx, hk),
+          "swrt_leapfrog");
+    return;
+  }
+  if (!strcmp(cmd, "g2k")) {
+    const int64_t nx = (int64_t)mxGetM(prhs[1]);
+    const int64_t kmax = nx / 2 - 1;
+    plhs[0] = mxCreateDoubleMatrix(2 * kmax + 1, kmax + 1, mxCOMPLEX);
+    check(swrt_g2k(ctx(), reals(prhs[1], "fg"), nx, (double*)mxGetComplexDoubles(plhs[0])), "swrt_g2k");
+    return;
+  }
+  if (!strcmp(cmd, "k2g")) {
+    if (!mxIsComplex(prhs[1])) mexErrMsgIdAndTxt("swrt:arg", "fk must be complex");
+    const int64_t nx = (int64_t)mxGetM(prhs[1]) + 1;
+    plhs[0] = mxCreateDoubleMatrix(nx, nx, mxREAL);
+    check(swrt_k2g(ctx(), (const double*)mxGetComplexDoubles(prhs[1]), nx, mxGetDoubles(plhs[0])),
+          "swrt_k2g");
+    return;
+  }
+  mexErrMsgIdAndTxt("swrt:arg", "unknown command '%s'", cmd);
+}

@@ -42,7 +42,7 @@ def main():
     key = f"{mode}_nx{arg('--nx', 512)}_N{arg('--packets', 1000000)}_sub{arg('--substeps', 1)}"
     rec = {"bytes_per_launch": corr, "bytes_per_launch_raw": raw, "fetch_kib": f_kib, "write_kib": w_kib,
            "dispatches": len(fetch), "note": "median dispatch; FETCH_SIZE doubled (gfx950 half-count)"}
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "traffic.json")
+    path = os.path.join(d, "traffic.json")  # copied into profiles/traffic.json once reviewed
     db = json.load(open(path)) if os.path.exists(path) else {}
     db[key] = rec
     json.dump(db, open(path, "w"), indent=1, sort_keys=True)
