@@ -81,6 +81,7 @@ struct swrt_ctx {
   int64_t tile = 0;         // cells per tile side (0: automatic)
   int64_t steps_since_bin = 0;
   bool bin_valid = false;
+  bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
   // history
   double* hx = nullptr;
   double* hk = nullptr;
@@ -248,10 +249,10 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
 }
 
 bool use_tile_kernel(const swrt_ctx* c);
-int tile_launch(swrt_ctx* c, const StepArgs& a);
+int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next);
 
 // Record a timing event pair around one leapfrog launch.
-int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid) {
+int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next) {
   // timing events (pairs), grown on demand; fold into a running sum when full
   if (c->timing.used + 2 > kMaxEvents) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -274,9 +275,10 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid) {
   c->timing.used += 2;
   HIPCHK(c, hipEventRecord(e0, c->stream));
   if (use_tile_kernel(c)) {
-    int rc = tile_launch(c, a);
+    int rc = tile_launch(c, a, count_next);
     if (rc) return rc;
   } else {
+    c->keys_fresh = false;
     if (a.nslots == 2)
       hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
     else
@@ -314,11 +316,14 @@ int rebin(swrt_ctx* c) {
   const int nbins = g.ntx * g.ntx;
   if (nbins > kMaxBins) return fail(c, SWRT_ERR_ARG, "too many spatial bins (raise tile size)");
   const int64_t n = c->n;
-  HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * nbins, c->stream));
-  const unsigned grid = nblocks(n, 256);
-  hipLaunchKernelGGL(bin_count_kernel, dim3(grid), dim3(256), sizeof(int) * nbins, c->stream, g, c->dx, n,
-                     nbins, c->keys, c->bins);
-  HIPCHK(c, hipGetLastError());
+  const unsigned grid = nblocks(n, 256 * kBinPerThread);
+  if (!(c->keys_fresh && c->bin_valid && nbins == c->nbins)) {
+    HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * nbins, c->stream));
+    hipLaunchKernelGGL(bin_count_kernel, dim3(grid), dim3(256), sizeof(int) * nbins, c->stream, g, c->dx, n,
+                       nbins, c->keys, c->bins);
+    HIPCHK(c, hipGetLastError());
+  }
+  c->keys_fresh = false;
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins,
                      c->bins + 2 * kMaxBins);
   HIPCHK(c, hipGetLastError());
@@ -334,7 +339,7 @@ int rebin(swrt_ctx* c) {
   return SWRT_OK;
 }
 
-int tile_launch(swrt_ctx* c, const StepArgs& a) {
+int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   TileArgs t;
   t.s = a;
   t.x_out = c->dx2;
@@ -343,6 +348,13 @@ int tile_launch(swrt_ctx* c, const StepArgs& a) {
   t.starts = c->bins + 2 * kMaxBins;
   t.ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
   const unsigned grid = (unsigned)(t.ntx * t.ntx);
+  t.next_keys = nullptr;
+  t.next_counts = nullptr;
+  if (count_next && (int)grid == c->nbins) {
+    HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * grid, c->stream));
+    t.next_keys = c->keys;
+    t.next_counts = c->bins;
+  }
   if (a.nslots == 2)
     hipLaunchKernelGGL((tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>), dim3(grid),
                        dim3(kTileThreads), 0, c->stream, t);
@@ -353,6 +365,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a) {
   std::swap(c->dx, c->dx2);
   std::swap(c->dk, c->dk2);
   std::swap(c->perm, c->perm2);
+  c->keys_fresh = t.next_keys != nullptr;
   return SWRT_OK;
 }
 
@@ -390,7 +403,9 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
     a.perm = c->perm;
     a.s0 = s0;
     a.nsteps = (int)chunk;
-    int rc = timed_launch(c, a, grid);
+    // the launch that ends at a re-binning point also counts the next bins
+    const bool count_next = c->rebin_every > 0 && c->steps_since_bin + chunk >= c->rebin_every;
+    int rc = timed_launch(c, a, grid, count_next);
     if (rc) return rc;
     c->steps_since_bin += chunk;
     s0 += chunk;
@@ -471,6 +486,7 @@ int swrt_set_field_grid(swrt_ctx* c, int slot, const double* fields6, int64_t nx
   s.ny_period = ny_period;
   s.has_psi = false;
   s.set = true;
+  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -514,6 +530,7 @@ int swrt_set_field_psi(swrt_ctx* c, int slot, const double* psi_grid, int64_t nx
   s.L = L;
   s.ny_period = nx;
   s.set = true;
+  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -550,6 +567,7 @@ int swrt_set_field_qk(swrt_ctx* c, int slot, const double* qk_interleaved, int64
   s.L = L;
   s.ny_period = ny_period;
   s.set = true;
+  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -750,6 +768,7 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
   c->hframes = 0;
   c->steps_done = 0;
   c->bin_valid = false;
+  c->keys_fresh = false;
   c->steps_since_bin = 0;
   return SWRT_OK;
   GUARD_END(c)
@@ -777,6 +796,7 @@ int swrt_set_kernel(swrt_ctx* c, int variant) {
   if (variant < 0 || variant > 2) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0, 1 or 2");
   c->kernel = variant;
   c->bin_valid = false;
+  c->keys_fresh = false;
   return SWRT_OK;
 }
 
@@ -786,6 +806,7 @@ int swrt_set_locality(swrt_ctx* c, int64_t rebin_every, int64_t tile) {
   c->rebin_every = rebin_every;
   c->tile = tile;
   c->bin_valid = false;
+  c->keys_fresh = false;
   return SWRT_OK;
 }
 

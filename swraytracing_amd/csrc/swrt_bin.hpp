@@ -30,19 +30,24 @@ __device__ __forceinline__ int tile_of(const BinGeom& g, double x, double y) {
 }
 
 // Pass 1: key per packet + histogram (LDS-aggregated, one global atomic per
-// (block, occupied bin)).  nbins <= kMaxBins.
+// (block, occupied bin)).  Each block handles kBinPerThread packets per
+// thread so the per-block LDS histogram clear is amortised.
 constexpr int kMaxBins = 16384;
+constexpr int kBinPerThread = 16;
 
 __global__ void __launch_bounds__(256) bin_count_kernel(BinGeom g, const double* x, int64_t n,
                                                         int nbins, int* keys, int* counts) {
   extern __shared__ int hist[];
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) hist[b] = 0;
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < n) {
-    const int key = tile_of(g, x[p], x[n + p]);
-    keys[p] = key;
-    atomicAdd(&hist[key], 1);
+  const int64_t base = (int64_t)blockIdx.x * blockDim.x * kBinPerThread;
+  for (int q = 0; q < kBinPerThread; ++q) {
+    const int64_t p = base + (int64_t)q * blockDim.x + threadIdx.x;
+    if (p < n) {
+      const int key = tile_of(g, x[p], x[n + p]);
+      keys[p] = key;
+      atomicAdd(&hist[key], 1);
+    }
   }
   __syncthreads();
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
@@ -94,11 +99,17 @@ __global__ void __launch_bounds__(256) bin_scatter_kernel(const double* x, const
   int* base = sh + nbins;   // nbins
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) cnt[b] = 0;
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int key = 0, local = 0;
-  if (p < n) {
-    key = keys[p];
-    local = atomicAdd(&cnt[key], 1);
+  const int64_t b0 = (int64_t)blockIdx.x * blockDim.x * kBinPerThread;
+  int key[kBinPerThread], local[kBinPerThread];
+#pragma unroll
+  for (int q = 0; q < kBinPerThread; ++q) {
+    const int64_t p = b0 + (int64_t)q * blockDim.x + threadIdx.x;
+    key[q] = 0;
+    local[q] = 0;
+    if (p < n) {
+      key[q] = keys[p];
+      local[q] = atomicAdd(&cnt[key[q]], 1);
+    }
   }
   __syncthreads();
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
@@ -106,13 +117,17 @@ __global__ void __launch_bounds__(256) bin_scatter_kernel(const double* x, const
     if (c) base[b] = atomicAdd(&cursor[b], c);
   }
   __syncthreads();
-  if (p < n) {
-    const int64_t d = (int64_t)base[key] + local;
-    x2[d] = x[p];
-    x2[n + d] = x[n + p];
-    k2[d] = k[p];
-    k2[n + d] = k[n + p];
-    perm2[d] = perm[p];
+#pragma unroll
+  for (int q = 0; q < kBinPerThread; ++q) {
+    const int64_t p = b0 + (int64_t)q * blockDim.x + threadIdx.x;
+    if (p < n) {
+      const int64_t d = (int64_t)base[key[q]] + local[q];
+      x2[d] = x[p];
+      x2[n + d] = x[n + p];
+      k2[d] = k[p];
+      k2[n + d] = k[n + p];
+      perm2[d] = perm[p];
+    }
   }
 }
 

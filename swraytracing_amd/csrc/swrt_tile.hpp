@@ -32,6 +32,8 @@ struct TileArgs {
   int* perm_out;
   const int* starts;     // ntiles + 1 packet offsets of the tiles
   int ntx;               // tiles per side
+  int* next_keys;        // non-NULL: write each output packet's tile (next binning) ...
+  int* next_counts;      // ... and add it to the per-tile counts (zeroed by the host)
 };
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
@@ -83,6 +85,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   __shared__ int hist[NB];
   __shared__ int kr[MAXB];          // key << 16 | rank
   __shared__ int order[MAXB];
+  __shared__ int nbr[9];            // next-binning counts of the 3x3 neighbour tiles
 
   const StepArgs& a = ta.s;
   const int tid = threadIdx.x;
@@ -90,6 +93,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   const int tx = tile / ta.ntx, ty = tile % ta.ntx;
   const int nx = a.f0.nx, npad = a.f0.npad;
   const int ox = tx * T, oy = ty * T;  // tile origin (cells)
+  if (tid < 9) nbr[tid] = 0;
 
   // 1. stage the window: node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx
   for (int e = tid; e < WN; e += NT) {
@@ -204,8 +208,29 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       ta.x_out[po] = x0; ta.x_out[a.n + po] = y0;
       ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
       ta.perm_out[po] = orig;
+      if (ta.next_keys != nullptr) {  // fused histogram for the next re-binning
+        double fa;
+        const int ic = cell_frac(x0, a.f0.dx, a.f0.px, a.f0.inv_px, a.f0.pow2x, nx, fa);
+        const int jc = cell_frac(y0, a.f0.dx, a.f0.py, a.f0.inv_py, a.f0.pow2y, nx, fa);
+        const int ntx_ = ta.ntx;
+        const int ntx2 = ic / T, nty2 = jc / T;
+        ta.next_keys[po] = ntx2 * ntx_ + nty2;
+        const int ddx = ring_diff(ntx2, tx, ntx_), ddy = ring_diff(nty2, ty, ntx_);
+        if (ddx >= -1 && ddx <= 1 && ddy >= -1 && ddy <= 1)
+          atomicAdd(&nbr[(ddx + 1) * 3 + (ddy + 1)], 1);
+        else
+          atomicAdd(&ta.next_counts[ntx2 * ntx_ + nty2], 1);
+      }
     }
     __syncthreads();  // LDS sort arrays are reused by the next batch
+  }
+  if (ta.next_keys != nullptr) {
+    __syncthreads();
+    if (tid < 9 && nbr[tid] != 0) {
+      const int n_ = ta.ntx;
+      const int gx = ((tx + tid / 3 - 1) % n_ + n_) % n_, gy = ((ty + tid % 3 - 1) % n_ + n_) % n_;
+      atomicAdd(&ta.next_counts[gx * n_ + gy], nbr[tid]);
+    }
   }
 }
 
