@@ -33,7 +33,7 @@ __device__ __forceinline__ int tile_of(const BinGeom& g, double x, double y) {
 // (block, occupied bin)).  Each block handles kBinPerThread packets per
 // thread so the per-block LDS histogram clear is amortised.
 constexpr int kMaxBins = 16384;
-constexpr int kBinPerThread = 16;
+constexpr int kBinPerThread = 4;
 
 __global__ void __launch_bounds__(256) bin_count_kernel(BinGeom g, const double* x, int64_t n,
                                                         int nbins, int* keys, int* counts) {

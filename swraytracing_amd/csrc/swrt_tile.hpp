@@ -216,10 +216,17 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         const int ntx2 = ic / T, nty2 = jc / T;
         ta.next_keys[po] = ntx2 * ntx_ + nty2;
         const int ddx = ring_diff(ntx2, tx, ntx_), ddy = ring_diff(nty2, ty, ntx_);
+        int nb_idx = -1;
         if (ddx >= -1 && ddx <= 1 && ddy >= -1 && ddy <= 1)
-          atomicAdd(&nbr[(ddx + 1) * 3 + (ddy + 1)], 1);
+          nb_idx = (ddx + 1) * 3 + (ddy + 1);
         else
           atomicAdd(&ta.next_counts[ntx2 * ntx_ + nty2], 1);
+        // wavefront-aggregated LDS counts (same-address LDS atomics serialise)
+#pragma unroll
+        for (int b = 0; b < 9; ++b) {
+          const unsigned long long m = __ballot(nb_idx == b);
+          if (m != 0ull && (tid & 63) == (int)__builtin_ctzll(m)) atomicAdd(&nbr[b], (int)__popcll(m));
+        }
       }
     }
     __syncthreads();  // LDS sort arrays are reused by the next batch
