@@ -151,6 +151,8 @@ def main():
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
+    ap.add_argument("--timing-every", type=int, default=8,
+                    help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather all trajectories to rank 0 (one all_gather)")
     args = ap.parse_args()
@@ -183,6 +185,7 @@ def main():
     for _ in range(args.warmup):
         step(ctx, w, args.substeps)
     barrier_sync()
+    ctx.set_timing(args.timing_every)
     ctx.kernel_time(reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -236,7 +239,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_packet_step": B, "avg_launch_ms": avg_launch_s * 1e3,
-                     "launches": launches},
+                     "timed_launches": launches, "timing_every": args.timing_every},
         "finite": finite,
     }
     if gathered is not None:

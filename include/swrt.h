@@ -158,6 +158,11 @@ int swrt_leapfrog(swrt_ctx* ctx, double* x, double* k, int64_t n, double dt, int
 int swrt_synchronize(swrt_ctx* ctx);
 /* The hipStream_t all of ctx's work is ordered on (for external event timing). */
 int swrt_get_stream(swrt_ctx* ctx, void** stream_out);
+/* Bracket every `every`-th packet-kernel launch with HIP events (default 1;
+ * 0 disables).  A timestamped event between two launches costs a few µs of
+ * GPU idle, so sampled timing keeps the measurement inside the timed region
+ * without perturbing it. */
+int swrt_set_timing(swrt_ctx* ctx, int every);
 /* Sum of HIP-event-measured durations of the packet kernel launches since the
  * last reset (synchronizes). */
 int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launches);

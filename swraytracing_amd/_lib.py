@@ -61,6 +61,7 @@ SIGNATURES = {
     "swrt_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT, _D, _D, _D, _I, _P, _P]),
     "swrt_synchronize": (_INT, [_VP]),
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
+    "swrt_set_timing": (_INT, [_VP, _INT]),
     "swrt_kernel_time": (_INT, [_VP, _INT, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
 }
 
@@ -257,6 +258,9 @@ class Context:
         s = _VP()
         self._chk(self._L.swrt_get_stream(self._h, ctypes.byref(s)), "swrt_get_stream")
         return s.value
+
+    def set_timing(self, every=1):
+        self._chk(self._L.swrt_set_timing(self._h, int(every)), "swrt_set_timing")
 
     def kernel_time(self, reset=True):
         ms = _D()

@@ -94,6 +94,8 @@ struct swrt_ctx {
   double2* tw = nullptr;
   int tw_n = 0;
   Timing timing;
+  int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
+  int64_t launch_count = 0;
 };
 
 namespace {
@@ -253,6 +255,17 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next);
 
 // Record a timing event pair around one leapfrog launch.
 int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next) {
+  const bool timed = c->timing_every > 0 && (c->launch_count++ % c->timing_every) == 0;
+  if (!timed) {
+    if (use_tile_kernel(c)) return tile_launch(c, a, count_next);
+    c->keys_fresh = false;
+    if (a.nslots == 2)
+      hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
+    else
+      hipLaunchKernelGGL(leapfrog_kernel<false>, dim3(grid), dim3(256), 0, c->stream, a);
+    HIPCHK(c, hipGetLastError());
+    return SWRT_OK;
+  }
   // timing events (pairs), grown on demand; fold into a running sum when full
   if (c->timing.used + 2 > kMaxEvents) {
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -789,6 +802,14 @@ int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SWRT_OK;
   GUARD_END(c)
+}
+
+int swrt_set_timing(swrt_ctx* c, int every) {
+  if (!c) return SWRT_ERR_ARG;
+  if (every < 0) return fail(c, SWRT_ERR_ARG, "timing interval must be >= 0");
+  c->timing_every = every;
+  c->launch_count = 0;
+  return SWRT_OK;
 }
 
 int swrt_set_kernel(swrt_ctx* c, int variant) {
