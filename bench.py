@@ -211,7 +211,8 @@ def main():
     total_ps = N * world * args.substeps * args.steps
     value = total_ps / elapsed
     B = BYTES_BLEND if w["nslots"] == 2 else BYTES_STEADY
-    avg_launch_s = (kms / 1e3) / max(launches, 1)
+    # sampled HIP-event time of the packet kernel; without samples fall back to wall time per step
+    avg_launch_s = (kms / 1e3) / launches if launches > 0 else elapsed / args.steps
     ps_per_launch = N * args.substeps  # one launch advances all local packets by `substeps` steps
     achieved_gbs = ps_per_launch * B / avg_launch_s / 1e9
     # fp64 VALU work per packet-step of the exact-order stencil
