@@ -153,6 +153,23 @@ int swrt_leapfrog(swrt_ctx* ctx, double* x, double* k, int64_t n, double dt, int
                   int64_t save_every, double* hist_x, double* hist_k);
 
 /* ---------------------------------------------------------------------------
+ * Wave-action packets over an RSW background (ray_trace_sw/step_packet_xka.m)
+ * ------------------------------------------------------------------------ */
+
+/* Background of step_packet_xka(P, U, GradU, H, C0, f, dx, dy, dt)
+ * (step_packet_xka.m:1): seven nx x nx column-major planes concatenated in the
+ * order U.u, U.v, GradU.u_x, GradU.u_y, GradU.v_x, GradU.v_y, H. */
+int swrt_xka_set_fields(swrt_ctx* ctx, const double* fields7, int64_t nx, double dx, double dy);
+
+/* nsteps of Pout = step_packet_xka(P, ...) for n packets (step_packet_xka.m:
+ * 38-91 with cg_sw.m:15-32 evaluated per stencil tap; interpolate of
+ * ray_trace_sw, bump 1e-13).  state5 (in/out): n x 5 column-major
+ * [P.x P.y P.k P.l P.a].  hist5 (may be NULL): nsteps/save_every frames of
+ * n x 5 after every save_every steps. */
+int swrt_xka_step(swrt_ctx* ctx, double* state5, int64_t n, double C0, double f, double dt,
+                  int64_t nsteps, int64_t save_every, double* hist5);
+
+/* ---------------------------------------------------------------------------
  * Runtime helpers
  * ------------------------------------------------------------------------ */
 int swrt_synchronize(swrt_ctx* ctx);

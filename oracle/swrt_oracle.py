@@ -553,3 +553,95 @@ def initial_packets(N, L, near_inertial_factor, f, Cg, rng):
 
 def here():
     return os.path.dirname(os.path.abspath(__file__))
+
+
+# ----------------------------------------------------------------------------
+# ray_trace_sw/step_packet_xka.m + cg_sw.m (wave action, RSW background)
+# ----------------------------------------------------------------------------
+def cg_sw(k, l, C0, f, U, H=None):
+    """cg_sw.m:1-32 on full fields (k, l scalars; U dict u, v; H field).
+
+    Returns C (dict x, y), omega, omega_abs, divC, gradomega (dict x, y)."""
+    if H is not None:
+        gH = C0 ** 2 * np.asarray(H, dtype=np.float64)  # cg_sw.m:15-16
+    else:
+        gH = C0 ** 2
+    K2 = k ** 2 + l ** 2
+    omega = np.sqrt(f ** 2 + gH * K2)  # cg_sw.m:22
+    omega_abs = np.abs(omega)
+    C = {"x": gH * k / omega, "y": gH * l / omega}  # cg_sw.m:25-26
+    divC = gradomega = None
+    if U is not None:  # cg_sw.m:28-32
+        divC = (k * f * U["v"] - l * f * U["u"] - C["x"] ** 2 - C["y"] ** 2) / omega
+        gradomega = {"x": f * K2 * U["v"] / (2 * omega), "y": -f * K2 * U["u"] / (2 * omega)}
+    return C, omega, omega_abs, divC, gradomega
+
+
+def step_packet_xka(P, U, GradU, H, C0, f, dx, dy, dt):
+    """step_packet_xka.m:1-91 for one packet P = dict(x, y, k, l, a) (floats).
+
+    Literal restatement: cg_sw on the full fields with the packet's k, l, RK4 of
+    x through interpolate(U.u + C.x) (k frozen), then 7 interpolations at the new
+    position and RK4 of k, l and the action a with frozen coefficients.
+    `interpolate` is ray_trace_sw/interpolate.m (bump 1e-13)."""
+    b = BUMP_SW
+    C, _, _, divC, gw = cg_sw(P["k"], P["l"], C0, f, U, H)
+    Fu = U["u"] + C["x"]
+    Fv = U["v"] + C["y"]
+
+    def I(x, y, F):
+        return float(interpolate(np.array([x]), np.array([y]), F, dx, dy, b)[0])
+
+    x, y = P["x"], P["y"]
+    x1 = dt * I(x, y, Fu)
+    y1 = dt * I(x, y, Fv)
+    x2 = dt * I(x + x1 / 2, y + y1 / 2, Fu)
+    y2 = dt * I(x + x1 / 2, y + y1 / 2, Fv)
+    x3 = dt * I(x + x2 / 2, y + y2 / 2, Fu)
+    y3 = dt * I(x + x2 / 2, y + y2 / 2, Fv)
+    x4 = dt * I(x + x3, y + y3, Fu)
+    y4 = dt * I(x + x3, y + y3, Fv)
+    out = {}
+    out["x"] = x + (x1 + 2 * x2 + 2 * x3 + x4) / 6
+    out["y"] = y + (y1 + 2 * y2 + 2 * y3 + y4) / 6
+    X, Y = out["x"], out["y"]
+    u_xi = I(X, Y, GradU["u_x"])
+    u_yi = I(X, Y, GradU["u_y"])
+    v_xi = I(X, Y, GradU["v_x"])
+    v_yi = I(X, Y, GradU["v_y"])
+    omega_xi = I(X, Y, gw["x"])
+    omega_yi = I(X, Y, gw["y"])
+    divCi = I(X, Y, divC)
+    k, l = P["k"], P["l"]
+    k1 = dt * (-u_xi * k - v_xi * l - omega_xi)
+    l1 = dt * (-u_yi * k - v_yi * l - omega_yi)
+    k2 = dt * (-u_xi * (k + k1 / 2) - v_xi * (l + l1 / 2) - omega_xi)
+    l2 = dt * (-u_yi * (k + k1 / 2) - v_yi * (l + l1 / 2) - omega_yi)
+    k3 = dt * (-u_xi * (k + k2 / 2) - v_xi * (l + l2 / 2) - omega_xi)
+    l3 = dt * (-u_yi * (k + k2 / 2) - v_yi * (l + l2 / 2) - omega_yi)
+    k4 = dt * (-u_xi * (k + k3) - v_xi * (l + l3) - omega_xi)
+    l4 = dt * (-u_yi * (k + k3) - v_yi * (l + l3) - omega_yi)
+    out["k"] = k + (k1 + 2 * k2 + 2 * k3 + k4) / 6
+    out["l"] = l + (l1 + 2 * l2 + 2 * l3 + l4) / 6
+    a = P["a"]
+    a1 = dt * (-a * divCi)
+    a2 = dt * (-(a + a1 / 2) * divCi)
+    a3 = dt * (-(a + a2 / 2) * divCi)
+    a4 = dt * (-(a + a3) * divCi)
+    out["a"] = a + (a1 + 2 * a2 + 2 * a3 + a4) / 6
+    return out
+
+
+def childress_soward(nx, U0=0.1, km=4.0, a=0.25, L=2 * math.pi):
+    """ray_trace_sw/raytrace.m:30-37 analytic cellular flow on the grid
+    x = (0:nx-1)*dx (raytrace.m:26-28): returns U, GradU dicts."""
+    x = np.arange(nx) * (L / nx)
+    X, Y = np.meshgrid(x, x, indexing="ij")
+    s, c = np.sin, np.cos
+    U = {"u": -U0 * (s(km * X) * c(km * Y) - a * c(km * X) * s(km * Y)),
+         "v": U0 * (c(km * X) * s(km * Y) - a * s(km * X) * c(km * Y))}
+    G = {"u_x": -km * U0 * (c(km * X) * c(km * Y) + a * s(km * X) * s(km * Y)),
+         "u_y": km * U0 * (s(km * X) * s(km * Y) + a * c(km * X) * c(km * Y)),
+         "v_x": -km * U0 * (s(km * X) * s(km * Y) + a * c(km * X) * c(km * Y)),
+         "v_y": km * U0 * (c(km * X) * c(km * Y) + a * s(km * X) * s(km * Y))}
+    return U, G

@@ -6,13 +6,14 @@ CDNA4 kernels behind the C ABI in include/swrt.h, with the reference's
 MATLAB call surface mirrored in Python.
 """
 from ._lib import Context, SwrtError, load
-from .integrate import PacketEnsemble, ode_symplectic
+from .integrate import PacketEnsemble, ode_symplectic, raytrace_xka, step_packet_xka
 from .io import read_field, write_field
 from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, RaytracingScheme, SnapshotPairScheme,
                      SpectralScheme, g2k, grid_U, interpolate, interpolate_U, k2g)
 
 __all__ = [
-    "Context", "SwrtError", "load", "PacketEnsemble", "ode_symplectic", "read_field", "write_field",
+    "Context", "SwrtError", "load", "PacketEnsemble", "ode_symplectic", "raytrace_xka", "step_packet_xka",
+    "read_field", "write_field",
     "BUMP_QG", "BUMP_SW", "DifferenceScheme", "RaytracingScheme", "SnapshotPairScheme",
     "SpectralScheme", "g2k", "grid_U", "interpolate", "interpolate_U", "k2g",
 ]

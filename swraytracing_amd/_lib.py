@@ -59,6 +59,8 @@ SIGNATURES = {
     "swrt_history_get": (_INT, [_VP, _I, _I, _P, _P]),
     "swrt_history_reset": (_INT, [_VP]),
     "swrt_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT, _D, _D, _D, _I, _P, _P]),
+    "swrt_xka_set_fields": (_INT, [_VP, _P, _I, _D, _D]),
+    "swrt_xka_step": (_INT, [_VP, _P, _I, _D, _D, _D, _I, _I, _P]),
     "swrt_synchronize": (_INT, [_VP]),
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
@@ -249,6 +251,24 @@ class Context:
                                         float(bump), int(save_every) if nfr else 0, _p(hx), _p(hk)),
                   "swrt_leapfrog")
         return x, k, hx, hk
+
+    # ---- wave action (step_packet_xka) -------------------------------------
+    def xka_set_fields(self, U, GradU, H, dx, dy):
+        nx = np.asarray(H).shape[0]
+        planes = _f64(np.stack([np.asarray(a, dtype=np.float64).ravel(order="F") for a in
+                                (U["u"], U["v"], GradU["u_x"], GradU["u_y"], GradU["v_x"], GradU["v_y"], H)]))
+        self._chk(self._L.swrt_xka_set_fields(self._h, _p(planes), nx, float(dx), float(dy)),
+                  "swrt_xka_set_fields")
+
+    def xka_step(self, state, C0, f, dt, nsteps, save_every=0):
+        """state: n x 5 [x y k l a]; returns (new state, history frames n x 5 or None)."""
+        st = np.array(state, dtype=np.float64, order="F")
+        n = st.shape[0]
+        nfr = nsteps // save_every if save_every else 0
+        hist = np.empty((nfr, 5, n)) if nfr else None
+        self._chk(self._L.swrt_xka_step(self._h, _p(st), n, float(C0), float(f), float(dt), int(nsteps),
+                                        int(save_every) if nfr else 0, _p(hist)), "swrt_xka_step")
+        return st, (None if hist is None else hist.transpose(0, 2, 1))
 
     # ---- runtime ---------------------------------------------------------
     def synchronize(self):

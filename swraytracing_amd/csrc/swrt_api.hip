@@ -19,6 +19,7 @@
 #include "swrt_fft.hpp"
 #include "swrt_kernels.hpp"
 #include "swrt_tile.hpp"
+#include "swrt_xka.hpp"
 
 using namespace swrt;
 
@@ -93,6 +94,14 @@ struct swrt_ctx {
   size_t scratch_bytes = 0;
   double2* tw = nullptr;
   int tw_n = 0;
+  // wave-action (step_packet_xka) background and state
+  double* xka_nodes = nullptr;
+  int64_t xka_nx = 0;
+  double xka_dx = 0.0, xka_dy = 0.0;
+  double* xka_state = nullptr;  // 5n
+  int64_t xka_cap = 0;
+  double* xka_hist = nullptr;
+  int64_t xka_hcap = 0;  // doubles allocated
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -471,6 +480,8 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->hk) (void)hipFree(c->hk);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->tw) (void)hipFree(c->tw);
+  for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist})
+    if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
   delete c;
@@ -915,6 +926,94 @@ int swrt_leapfrog(swrt_ctx* c, double* x, double* k, int64_t n, double dt, int64
     if ((rc = swrt_history_get(c, 0, c->hframes, hist_x, hist_k))) return rc;
   }
   return SWRT_OK;
+}
+
+int swrt_xka_set_fields(swrt_ctx* c, const double* fields7, int64_t nx, double dx, double dy) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!fields7) return fail(c, SWRT_ERR_ARG, "fields7 is NULL");
+  if (nx < 6 || nx > 8192) return fail(c, SWRT_ERR_ARG, "nx out of range");
+  if (!(dx > 0) || !(dy > 0)) return fail(c, SWRT_ERR_ARG, "dx, dy must be > 0");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int64_t npad = nx + kPadTot;
+  if (c->xka_nx != nx) {
+    if (c->xka_nodes) (void)hipFree(c->xka_nodes);
+    c->xka_nodes = nullptr;
+    c->xka_nx = 0;
+    HIPCHK(c, hipMalloc(&c->xka_nodes, sizeof(double) * kXkaRec * npad * npad));
+    c->xka_nx = nx;
+  }
+  int rc;
+  if ((rc = ensure_scratch(c, sizeof(double) * 7 * nx * nx))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->scratch, fields7, sizeof(double) * 7 * nx * nx, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(pack_xka_kernel, dim3(nblocks(npad * npad, 256)), dim3(256), 0, c->stream,
+                     (const double*)c->scratch, (int)nx, (int)npad, c->xka_nodes);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->xka_dx = dx;
+  c->xka_dy = dy;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, double dt, int64_t nsteps,
+                  int64_t save_every, double* hist5) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!c->xka_nodes) return fail(c, SWRT_ERR_STATE, "call swrt_xka_set_fields first");
+  if (n < 0 || nsteps < 0 || save_every < 0) return fail(c, SWRT_ERR_ARG, "negative size");
+  if (n == 0) return SWRT_OK;
+  if (!state5) return fail(c, SWRT_ERR_ARG, "state is NULL");
+  if (hist5 && save_every > 0 && nsteps % save_every)
+    return fail(c, SWRT_ERR_ARG, "nsteps must be a multiple of save_every");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (n > c->xka_cap) {
+    if (c->xka_state) (void)hipFree(c->xka_state);
+    c->xka_state = nullptr;
+    c->xka_cap = 0;
+    HIPCHK(c, hipMalloc(&c->xka_state, sizeof(double) * 5 * n));
+    c->xka_cap = n;
+  }
+  const int64_t frames = (hist5 && save_every > 0) ? nsteps / save_every : 0;
+  if (frames * 5 * n > c->xka_hcap) {
+    if (c->xka_hist) (void)hipFree(c->xka_hist);
+    c->xka_hist = nullptr;
+    c->xka_hcap = 0;
+    HIPCHK(c, hipMalloc(&c->xka_hist, sizeof(double) * frames * 5 * n));
+    c->xka_hcap = frames * 5 * n;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->xka_state, state5, sizeof(double) * 5 * n, hipMemcpyHostToDevice, c->stream));
+  XkaArgs a;
+  a.nodes = c->xka_nodes;
+  a.nx = (int)c->xka_nx;
+  a.npad = (int)(c->xka_nx + kPadTot);
+  a.dx = c->xka_dx;
+  a.dy = c->xka_dy;
+  a.px = a.py = (double)c->xka_nx;
+  a.inv_px = a.inv_py = 1.0 / (double)c->xka_nx;
+  a.pow2x = a.pow2y = is_pow2(c->xka_nx);
+  a.C0sq = C0 * C0;
+  a.f = f;
+  a.f2 = f * f;
+  a.dt = dt;
+  a.bump = 1e-13;  // ray_trace_sw/interpolate.m:13
+  a.st = c->xka_state;
+  a.n = n;
+  a.save_every = save_every > 0 ? save_every : 1;
+  a.hist = frames ? c->xka_hist : nullptr;
+  for (int64_t s0 = 0; s0 < nsteps; s0 += kMaxStepsPerLaunch) {
+    a.nsteps = (int)std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
+    a.frame0 = s0 / a.save_every;
+    hipLaunchKernelGGL(xka_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, a);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipMemcpyAsync(state5, c->xka_state, sizeof(double) * 5 * n, hipMemcpyDeviceToHost, c->stream));
+  if (frames)
+    HIPCHK(c, hipMemcpyAsync(hist5, c->xka_hist, sizeof(double) * frames * 5 * n, hipMemcpyDeviceToHost,
+                             c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
 }
 
 int swrt_synchronize(swrt_ctx* c) {

@@ -1,0 +1,193 @@
+// swrt_xka.hpp — wave-action packet stepping over an RSW background.
+//
+// Replaces ray_trace_sw/step_packet_xka.m (+ cg_sw.m).  The reference builds
+// the packet-dependent fields U.u + C.x, U.v + C.y, grad(omega), div(C) on the
+// whole nx x ny grid for every packet and step (cg_sw.m:15-32, O(nx^2) per
+// packet-step) and then interpolates them.  Here each of those node values is
+// formed per stencil tap from the node's (u, v, H, u_x, u_y, v_x, v_y) with the
+// same scalar operations in the same order, so the interpolated values are
+// bit-identical while the cost drops to O(36) per interpolation.
+//
+// Node record: 8 doubles {u, v, H, 0, u_x, u_y, v_x, v_y} (64 B) in the same
+// halo-padded x-major / y-contiguous layout as the QG snapshot nodes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "swrt_kernels.hpp"
+
+namespace swrt {
+
+constexpr int kXkaRec = 8;
+
+struct XkaArgs {
+  const double* nodes;
+  int nx, npad;
+  double dx, dy, px, py, inv_px, inv_py;
+  int pow2x, pow2y;
+  double C0sq, f, f2, dt, bump;
+  double* st;          // 5 x n: x, y, k, l, a (column blocks)
+  int64_t n;
+  int nsteps;
+  int64_t save_every;
+  double* hist;        // frames of 5 x n (NULL: none)
+  int64_t frame0;
+};
+
+struct XkaStencil {
+  int ic, jc;
+  double wx[kNT], wy[kNT];
+};
+
+__device__ __forceinline__ void xka_stencil(const XkaArgs& a, double x, double y, XkaStencil& s) {
+  double ax, ay;
+  s.ic = cell_frac(x, a.dx, a.px, a.inv_px, a.pow2x, a.nx, ax);
+  s.jc = cell_frac(y, a.dy, a.py, a.inv_py, a.pow2y, a.nx, ay);
+  lagrange_w(ax, a.bump, s.wx);
+  lagrange_w(ay, a.bump, s.wy);
+}
+
+// interpolate(x, y, U.u + C.x) and interpolate(x, y, U.v + C.y)
+// (step_packet_xka.m:42-52) with C from cg_sw.m:15-26 formed per tap.
+__device__ __forceinline__ void xka_velocity(const XkaArgs& a, double x, double y, double k, double l,
+                                             double K2, double& Iu, double& Iv) {
+  XkaStencil s;
+  xka_stencil(a, x, y, s);
+  const double* base = a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec;
+  double su = 0.0, sv = 0.0;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const double2* nd = reinterpret_cast<const double2*>(base + ((size_t)i * a.npad + j) * kXkaRec);
+      const double2 uv = nd[0];
+      const double H = nd[1].x;
+      const double gH = a.C0sq * H;                   // cg_sw.m:16
+      const double w = sqrt(a.f2 + gH * K2);          // cg_sw.m:22
+      const double cx = gH * k / w;                   // cg_sw.m:25
+      const double cy = gH * l / w;                   // cg_sw.m:26
+      const double wij = s.wx[i] * s.wy[j];
+      su = su + wij * (uv.x + cx);
+      sv = sv + wij * (uv.y + cy);
+    }
+  }
+  Iu = su;
+  Iv = sv;
+}
+
+// The 7 interpolations at the new position (step_packet_xka.m:59-65):
+// u_x, u_y, v_x, v_y, gradomega.x, gradomega.y, divC.
+__device__ __forceinline__ void xka_gradients(const XkaArgs& a, double x, double y, double k, double l,
+                                              double K2, double out[7]) {
+  XkaStencil s;
+  xka_stencil(a, x, y, s);
+  const double* base = a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec;
+  const double kf = k * a.f, lf = l * a.f;        // k*f, l*f (cg_sw.m:29)
+  const double fK2 = a.f * K2, mfK2 = (-a.f) * K2;  // f*(k^2+l^2), -f*(k^2+l^2) (cg_sw.m:30-31)
+#pragma unroll
+  for (int q = 0; q < 7; ++q) out[q] = 0.0;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const double2* nd = reinterpret_cast<const double2*>(base + ((size_t)i * a.npad + j) * kXkaRec);
+      const double2 uv = nd[0];
+      const double H = nd[1].x;
+      const double2 g0 = nd[2], g1 = nd[3];  // (u_x, u_y), (v_x, v_y)
+      const double gH = a.C0sq * H;
+      const double w = sqrt(a.f2 + gH * K2);
+      const double cx = gH * k / w;
+      const double cy = gH * l / w;
+      const double divC = (((kf * uv.y - lf * uv.x) - cx * cx) - cy * cy) / w;  // cg_sw.m:29
+      const double w2 = 2 * w;
+      const double gwx = fK2 * uv.y / w2;   // cg_sw.m:30
+      const double gwy = mfK2 * uv.x / w2;  // cg_sw.m:31
+      const double wij = s.wx[i] * s.wy[j];
+      out[0] = out[0] + wij * g0.x;
+      out[1] = out[1] + wij * g0.y;
+      out[2] = out[2] + wij * g1.x;
+      out[3] = out[3] + wij * g1.y;
+      out[4] = out[4] + wij * gwx;
+      out[5] = out[5] + wij * gwy;
+      out[6] = out[6] + wij * divC;
+    }
+  }
+}
+
+// (a + 2b + 2c + d)/6 in MATLAB's left-to-right order; /6 = (/2 exact)/3.
+__device__ __forceinline__ double rk4_mean(double a, double b, double c, double d) {
+  return div_const<3>((((a + 2 * b) + 2 * c) + d) * 0.5);
+}
+
+// step_packet_xka.m:38-91 — one lane per packet, nsteps steps.
+__global__ void __launch_bounds__(256) xka_kernel(XkaArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.n) return;
+  const int64_t n = a.n;
+  double x = a.st[p], y = a.st[n + p], k = a.st[2 * n + p], l = a.st[3 * n + p], ac = a.st[4 * n + p];
+  const double dt = a.dt;
+  for (int s = 0; s < a.nsteps; ++s) {
+    const double K2 = k * k + l * l;  // cg_sw.m:22 (k^2+l^2)
+    double u, v;
+    xka_velocity(a, x, y, k, l, K2, u, v);
+    const double x1 = dt * u, y1 = dt * v;
+    xka_velocity(a, x + x1 * 0.5, y + y1 * 0.5, k, l, K2, u, v);
+    const double x2 = dt * u, y2 = dt * v;
+    xka_velocity(a, x + x2 * 0.5, y + y2 * 0.5, k, l, K2, u, v);
+    const double x3 = dt * u, y3 = dt * v;
+    xka_velocity(a, x + x3, y + y3, k, l, K2, u, v);
+    const double x4 = dt * u, y4 = dt * v;
+    const double X = x + rk4_mean(x1, x2, x3, x4);  // step_packet_xka.m:54-55
+    const double Y = y + rk4_mean(y1, y2, y3, y4);
+    double g[7];
+    xka_gradients(a, X, Y, k, l, K2, g);
+    const double uxi = g[0], uyi = g[1], vxi = g[2], vyi = g[3], oxi = g[4], oyi = g[5], dci = g[6];
+    // step_packet_xka.m:69-82
+    const double k1 = dt * (((-uxi) * k - vxi * l) - oxi);
+    const double l1 = dt * (((-uyi) * k - vyi * l) - oyi);
+    const double k2 = dt * (((-uxi) * (k + k1 * 0.5) - vxi * (l + l1 * 0.5)) - oxi);
+    const double l2 = dt * (((-uyi) * (k + k1 * 0.5) - vyi * (l + l1 * 0.5)) - oyi);
+    const double k3 = dt * (((-uxi) * (k + k2 * 0.5) - vxi * (l + l2 * 0.5)) - oxi);
+    const double l3 = dt * (((-uyi) * (k + k2 * 0.5) - vyi * (l + l2 * 0.5)) - oyi);
+    const double k4 = dt * (((-uxi) * (k + k3) - vxi * (l + l3)) - oxi);
+    const double l4 = dt * (((-uyi) * (k + k3) - vyi * (l + l3)) - oyi);
+    const double Kn = k + rk4_mean(k1, k2, k3, k4);
+    const double Ln = l + rk4_mean(l1, l2, l3, l4);
+    // step_packet_xka.m:86-91
+    const double a1 = dt * ((-ac) * dci);
+    const double a2 = dt * ((-(ac + a1 * 0.5)) * dci);
+    const double a3 = dt * ((-(ac + a2 * 0.5)) * dci);
+    const double a4 = dt * ((-(ac + a3)) * dci);
+    ac = ac + rk4_mean(a1, a2, a3, a4);
+    x = X;
+    y = Y;
+    k = Kn;
+    l = Ln;
+    if (a.hist != nullptr && ((s + 1) % a.save_every) == 0) {
+      double* h = a.hist + (a.frame0 + (s + 1) / a.save_every - 1) * 5 * n;
+      h[p] = x; h[n + p] = y; h[2 * n + p] = k; h[3 * n + p] = l; h[4 * n + p] = ac;
+    }
+  }
+  a.st[p] = x; a.st[n + p] = y; a.st[2 * n + p] = k; a.st[3 * n + p] = l; a.st[4 * n + p] = ac;
+}
+
+// 7 column-major planes (u, v, u_x, u_y, v_x, v_y, H) -> padded 8-double node records.
+__global__ void pack_xka_kernel(const double* planes, int nx, int npad, double* nodes) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t tot = (int64_t)npad * npad;
+  if (idx >= tot) return;
+  const int ip = (int)(idx / npad), jp = (int)(idx % npad);
+  const int ig = ((ip - kPadLo) % nx + nx) % nx, jg = ((jp - kPadLo) % nx + nx) % nx;
+  const int64_t plane = (int64_t)nx * nx, src = ig + (int64_t)nx * jg;
+  double* d = nodes + idx * kXkaRec;
+  d[0] = planes[0 * plane + src];  // u
+  d[1] = planes[1 * plane + src];  // v
+  d[2] = planes[6 * plane + src];  // H
+  d[3] = 0.0;
+  d[4] = planes[2 * plane + src];  // u_x
+  d[5] = planes[3 * plane + src];  // u_y
+  d[6] = planes[4 * plane + src];  // v_x
+  d[7] = planes[5 * plane + src];  // v_y
+}
+
+}  // namespace swrt

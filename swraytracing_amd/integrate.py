@@ -123,3 +123,42 @@ class PacketEnsemble:
         write_field(np.mod(x + L / 2, L) - L / 2, os.path.join(directory, "packet_x"))
         write_field(k, os.path.join(directory, "packet_k"))
         write_field(np.array([[t]]), os.path.join(directory, "packet_time"))
+
+
+def step_packet_xka(P, U, GradU, H, C0, f, dx, dy, dt, nsteps=1, ctx: Context | None = None):
+    """Pout = step_packet_xka(P, U, GradU, H, C0, f, dx, dy, dt)
+    (ray_trace_sw/step_packet_xka.m:1-91) on the GPU.
+
+    P: dict with x, y, k, l, a (scalars or equal-length arrays = many packets).
+    U: dict u, v; GradU: dict u_x, u_y, v_x, v_y; H: field (nx x nx).
+    `nsteps` > 1 repeats the step (the raytrace_sw.m:125-130 loop) on device."""
+    from .scheme import default_context
+    ctx = ctx or default_context()
+    if not np.allclose(np.asarray(H).shape, np.asarray(U["u"]).shape) or np.asarray(H).shape[0] != np.asarray(H).shape[1]:
+        raise ValueError("fields must be nx x nx")
+    ctx.xka_set_fields(U, GradU, H, dx, dy)
+    names = ("x", "y", "k", "l", "a")
+    scalar = np.ndim(P["x"]) == 0
+    st = np.stack([np.atleast_1d(np.asarray(P[n], dtype=np.float64)) for n in names], axis=1)
+    out, _ = ctx.xka_step(st, C0, f, dt, nsteps)
+    return {n: (float(out[0, i]) if scalar else out[:, i].copy()) for i, n in enumerate(names)}
+
+
+def raytrace_xka(P0, U, GradU, H, C0, f, dx, dy, dt, nsteps, ctx: Context | None = None):
+    """The packet loop of ray_trace_sw/raytrace_sw.m:124-130: P(i, 1) = P0(i),
+    P(i, j) = step_packet_xka(P(i, j-1), ...) for j = 2..nsteps.  Returns a dict
+    of (np, nsteps) arrays (column j-1 = state after j-1 steps)."""
+    from .scheme import default_context
+    ctx = ctx or default_context()
+    ctx.xka_set_fields(U, GradU, H, dx, dy)
+    names = ("x", "y", "k", "l", "a")
+    st = np.stack([np.atleast_1d(np.asarray(P0[n], dtype=np.float64)) for n in names], axis=1)
+    npk = st.shape[0]
+    out = {n: np.zeros((npk, nsteps)) for n in names}
+    for i, n in enumerate(names):
+        out[n][:, 0] = st[:, i]
+    if nsteps > 1:
+        _, hist = ctx.xka_step(st, C0, f, dt, nsteps - 1, save_every=1)
+        for i, n in enumerate(names):
+            out[n][:, 1:] = hist[:, :, i].T
+    return out

@@ -427,3 +427,41 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib):
                                        10, 3.0, 1.0)
     np.testing.assert_array_equal(xg[idx], xo)
     np.testing.assert_array_equal(kg[idx], ko)
+
+
+def _rsw_background(nx, seed=3):
+    """Childress-Soward flow (ray_trace_sw/raytrace.m:30-37) + a smooth H."""
+    U, G = orc.childress_soward(nx, U0=0.1, km=4.0, a=0.25)
+    X, Y = periodic_grid(nx)
+    H = 1.0 + 0.1 * np.cos(2 * X + Y) + 0.05 * np.sin(3 * Y)
+    return U, G, H
+
+
+@pytest.mark.parametrize("nx", [32, 64])
+def test_step_packet_xka_bitexact(ctx, nx):
+    """GPU step_packet_xka (cg_sw per tap) == the literal full-field oracle."""
+    import swraytracing_amd as sw
+    U, G, H = _rsw_background(nx)
+    dx = 2 * np.pi / nx
+    rng = np.random.default_rng(nx)
+    npk, steps, dt, C0, f = 24, 6, 0.3 * dx, 1.0, 4.0
+    P0 = {"x": rng.uniform(0, 2 * np.pi, npk), "y": rng.uniform(-7, 7, npk),
+          "k": 40 * np.cos(np.arange(npk)), "l": 40 * np.sin(np.arange(npk)), "a": np.ones(npk)}
+    hist = sw.raytrace_xka(P0, U, G, H, C0, f, dx, dx, dt, steps, ctx=ctx)
+    for i in range(npk):
+        P = {n: float(P0[n][i]) for n in "xykla"}
+        for j in range(1, steps):
+            P = orc.step_packet_xka(P, U, G, H, C0, f, dx, dx, dt)
+            for n in "xykla":
+                assert hist[n][i, j] == P[n], (i, j, n, hist[n][i, j], P[n])
+
+
+def test_step_packet_xka_scalar_api(ctx):
+    import swraytracing_amd as sw
+    nx = 32
+    U, G, H = _rsw_background(nx)
+    dx = 2 * np.pi / nx
+    P = {"x": 0.3, "y": 1.7, "k": 12.0, "l": -5.0, "a": 2.0}
+    g = sw.step_packet_xka(P, U, G, H, 1.0, 4.0, dx, dx, 0.02, ctx=ctx)
+    o = orc.step_packet_xka(P, U, G, H, 1.0, 4.0, dx, dx, 0.02)
+    assert g == o
