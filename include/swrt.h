@@ -170,6 +170,26 @@ int swrt_xka_step(swrt_ctx* ctx, double* state5, int64_t n, double C0, double f,
                   int64_t nsteps, int64_t save_every, double* hist5);
 
 /* ---------------------------------------------------------------------------
+ * Exact spectral evaluator (scratch/fourier_interpolate_test.m:92-136)
+ * ------------------------------------------------------------------------ */
+
+/* psi(x,y) = sum_{i,j} Re(C[i,j] exp(1i*(kx_i x + ky_j y))), kx_i = (kx0+i)*s,
+ * ky_j = (ky0+j)*s; C nkx x nky column-major interleaved complex.  The
+ * half-plane spectrum of g2k maps to C = 2*psik (ky = 0, kx < 0 zeroed, DC
+ * real, kx0 = -kmax, ky0 = 0); the scratch test's amp/phase field to
+ * C = amp.*exp(1i*phase) (kx0 = ky0 = -n, s = 1). */
+int swrt_spectral_set_modes(swrt_ctx* ctx, const double* C_interleaved, int64_t nkx, int64_t nky,
+                            double kx0, double ky0, double s);
+/* Exact U and grad U (6 x n, as swrt_eval) by the direct mode sum;
+ * precision 64 (fp64) or 32 (fp32 sums, the config-5 tolerance study). */
+int swrt_spectral_eval(swrt_ctx* ctx, const double* x, const double* y, int64_t n, int precision,
+                       double* out6);
+/* Leapfrog (ode_symplectic.m:13-37) with the exact spectral kick
+ * (fourier_interpolate_test.m:73-114); x, k N x 2 column-major, in/out. */
+int swrt_spectral_leapfrog(swrt_ctx* ctx, double* x, double* k, int64_t n, double dt, int64_t nsteps,
+                           double f, double gH, int precision);
+
+/* ---------------------------------------------------------------------------
  * Runtime helpers
  * ------------------------------------------------------------------------ */
 int swrt_synchronize(swrt_ctx* ctx);

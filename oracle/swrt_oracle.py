@@ -645,3 +645,44 @@ def childress_soward(nx, U0=0.1, km=4.0, a=0.25, L=2 * math.pi):
          "v_x": -km * U0 * (s(km * X) * s(km * Y) + a * c(km * X) * c(km * Y)),
          "v_y": km * U0 * (c(km * X) * c(km * Y) + a * s(km * X) * s(km * Y))}
     return U, G
+
+
+# ----------------------------------------------------------------------------
+# Exact spectral evaluator (scratch/fourier_interpolate_test.m:92-136 generalised)
+# ----------------------------------------------------------------------------
+def spectral_direct(C, kx0, ky0, s, x, y):
+    """psi = sum Re(C[i,j] e^{i(kx_i x + ky_j y)}): returns 6 x N flow
+    (u, v, u_x, u_y, v_x, v_y) with u = -psi_y, v = psi_x (direct sincos sum)."""
+    C = np.asarray(C, dtype=np.complex128)
+    x = np.asarray(x, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    nkx, nky = C.shape
+    kx = (kx0 + np.arange(nkx)) * s
+    ky = (ky0 + np.arange(nky)) * s
+    px = np.zeros_like(x); py = np.zeros_like(x)
+    pxx = np.zeros_like(x); pxy = np.zeros_like(x); pyy = np.zeros_like(x)
+    Ex = np.exp(1j * np.outer(x, kx))  # N x nkx
+    for j in range(nky):
+        z = (Ex * np.exp(1j * ky[j] * y)[:, None]) * C[None, :, j]  # N x nkx
+        px += -(z.imag * kx).sum(axis=1)
+        py += -ky[j] * z.imag.sum(axis=1)
+        pxx += -(z.real * kx * kx).sum(axis=1)
+        pxy += -ky[j] * (z.real * kx).sum(axis=1)
+        pyy += -ky[j] ** 2 * z.real.sum(axis=1)
+    return np.stack([-py, px, -pxy, -pyy, pxx, pxy])
+
+
+def modes_from_halfplane(fk, k_scale=1.0):
+    """g2k half plane -> dense coefficient grid of the spectral evaluator
+    (k2g's point formula): C = 2 fk, ky=0/kx<0 zeroed, DC real."""
+    fk = np.asarray(fk, dtype=np.complex128)
+    kmax = fk.shape[1] - 1
+    C = 2 * fk
+    C[:kmax, 0] = 0
+    C[kmax, 0] = fk[kmax, 0].real
+    return C, -kmax, 0, k_scale
+
+
+def modes_from_amp_phase(amp, phase, n):
+    """fourier_interpolate_test.m:116-123 field: C = amp .* exp(1i*phase), K, L in -n..n."""
+    return np.asarray(amp) * np.exp(1j * np.asarray(phase)), -n, -n, 1.0

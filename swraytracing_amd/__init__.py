@@ -8,12 +8,12 @@ MATLAB call surface mirrored in Python.
 from ._lib import Context, SwrtError, load
 from .integrate import PacketEnsemble, ode_symplectic, raytrace_xka, step_packet_xka
 from .io import read_field, write_field
-from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, RaytracingScheme, SnapshotPairScheme,
+from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, FourierScheme, RaytracingScheme, SnapshotPairScheme,
                      SpectralScheme, g2k, grid_U, interpolate, interpolate_U, k2g)
 
 __all__ = [
     "Context", "SwrtError", "load", "PacketEnsemble", "ode_symplectic", "raytrace_xka", "step_packet_xka",
     "read_field", "write_field",
-    "BUMP_QG", "BUMP_SW", "DifferenceScheme", "RaytracingScheme", "SnapshotPairScheme",
+    "BUMP_QG", "BUMP_SW", "DifferenceScheme", "FourierScheme", "RaytracingScheme", "SnapshotPairScheme",
     "SpectralScheme", "g2k", "grid_U", "interpolate", "interpolate_U", "k2g",
 ]

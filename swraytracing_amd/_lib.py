@@ -61,6 +61,9 @@ SIGNATURES = {
     "swrt_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT, _D, _D, _D, _I, _P, _P]),
     "swrt_xka_set_fields": (_INT, [_VP, _P, _I, _D, _D]),
     "swrt_xka_step": (_INT, [_VP, _P, _I, _D, _D, _D, _I, _I, _P]),
+    "swrt_spectral_set_modes": (_INT, [_VP, _P, _I, _I, _D, _D, _D]),
+    "swrt_spectral_eval": (_INT, [_VP, _P, _P, _I, _INT, _P]),
+    "swrt_spectral_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT]),
     "swrt_synchronize": (_INT, [_VP]),
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
@@ -269,6 +272,29 @@ class Context:
         self._chk(self._L.swrt_xka_step(self._h, _p(st), n, float(C0), float(f), float(dt), int(nsteps),
                                         int(save_every) if nfr else 0, _p(hist)), "swrt_xka_step")
         return st, (None if hist is None else hist.transpose(0, 2, 1))
+
+    # ---- exact spectral evaluator -----------------------------------------
+    def spectral_set_modes(self, C, kx0, ky0, s):
+        C = np.asarray(C, dtype=np.complex128)
+        nkx, nky = C.shape
+        buf = _f64(np.asfortranarray(C).ravel(order="F").view(np.float64))
+        self._chk(self._L.swrt_spectral_set_modes(self._h, _p(buf), nkx, nky, float(kx0), float(ky0), float(s)),
+                  "swrt_spectral_set_modes")
+
+    def spectral_eval(self, x, y, precision=64):
+        xf = _f64(np.asarray(x, dtype=np.float64).ravel())
+        yf = _f64(np.asarray(y, dtype=np.float64).ravel())
+        out = np.empty((6, xf.size))
+        self._chk(self._L.swrt_spectral_eval(self._h, _p(xf), _p(yf), xf.size, int(precision), _p(out)),
+                  "swrt_spectral_eval")
+        return out
+
+    def spectral_leapfrog(self, x, k, dt, nsteps, f, gH, precision=64):
+        x = np.array(x, dtype=np.float64, order="F")
+        k = np.array(k, dtype=np.float64, order="F")
+        self._chk(self._L.swrt_spectral_leapfrog(self._h, _p(x), _p(k), x.shape[0], float(dt), int(nsteps),
+                                                 float(f), float(gH), int(precision)), "swrt_spectral_leapfrog")
+        return x, k
 
     # ---- runtime ---------------------------------------------------------
     def synchronize(self):

@@ -20,6 +20,7 @@
 #include "swrt_kernels.hpp"
 #include "swrt_tile.hpp"
 #include "swrt_xka.hpp"
+#include "swrt_spectral.hpp"
 
 using namespace swrt;
 
@@ -102,6 +103,11 @@ struct swrt_ctx {
   int64_t xka_cap = 0;
   double* xka_hist = nullptr;
   int64_t xka_hcap = 0;  // doubles allocated
+  // exact spectral evaluator (dense coefficient grid)
+  double2* modes = nullptr;
+  int64_t mode_cap = 0;
+  ModeGrid mg{};
+  bool modes_set = false;
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -480,7 +486,7 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->hk) (void)hipFree(c->hk);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->tw) (void)hipFree(c->tw);
-  for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist})
+  for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist, (void*)c->modes})
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -1011,6 +1017,95 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   if (frames)
     HIPCHK(c, hipMemcpyAsync(hist5, c->xka_hist, sizeof(double) * frames * 5 * n, hipMemcpyDeviceToHost,
                              c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_spectral_set_modes(swrt_ctx* c, const double* C, int64_t nkx, int64_t nky, double kx0, double ky0,
+                            double s) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!C) return fail(c, SWRT_ERR_ARG, "C is NULL");
+  if (nkx <= 0 || nky <= 0 || nkx * nky > (int64_t)1 << 28) return fail(c, SWRT_ERR_ARG, "bad mode grid");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (nkx * nky > c->mode_cap) {
+    if (c->modes) (void)hipFree(c->modes);
+    c->modes = nullptr;
+    c->mode_cap = 0;
+    HIPCHK(c, hipMalloc(&c->modes, sizeof(double2) * nkx * nky));
+    c->mode_cap = nkx * nky;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->modes, C, sizeof(double2) * nkx * nky, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->mg.C = c->modes;
+  c->mg.nkx = (int)nkx;
+  c->mg.nky = (int)nky;
+  c->mg.kx0 = kx0;
+  c->mg.ky0 = ky0;
+  c->mg.s = s;
+  c->modes_set = true;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_spectral_eval(swrt_ctx* c, const double* x, const double* y, int64_t n, int precision, double* out6) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!c->modes_set) return fail(c, SWRT_ERR_STATE, "call swrt_spectral_set_modes first");
+  if (precision != 64 && precision != 32) return fail(c, SWRT_ERR_ARG, "precision must be 64 or 32");
+  if (n < 0) return fail(c, SWRT_ERR_ARG, "n < 0");
+  if (n == 0) return SWRT_OK;
+  if (!x || !y || !out6) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_scratch(c, sizeof(double) * 8 * n))) return rc;
+  double* dxp = (double*)c->scratch;
+  double* dyp = dxp + n;
+  double* dout = dyp + n;
+  HIPCHK(c, hipMemcpyAsync(dxp, x, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dyp, y, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+  if (precision == 64)
+    hipLaunchKernelGGL(spectral_eval_kernel<double>, dim3(nblocks(n, kSpecThreads)), dim3(kSpecThreads), 0,
+                       c->stream, c->mg, dxp, dyp, n, dout);
+  else
+    hipLaunchKernelGGL(spectral_eval_kernel<float>, dim3(nblocks(n, kSpecThreads)), dim3(kSpecThreads), 0,
+                       c->stream, c->mg, dxp, dyp, n, dout);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(out6, dout, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_spectral_leapfrog(swrt_ctx* c, double* x, double* k, int64_t n, double dt, int64_t nsteps, double f,
+                           double gH, int precision) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!c->modes_set) return fail(c, SWRT_ERR_STATE, "call swrt_spectral_set_modes first");
+  if (precision != 64 && precision != 32) return fail(c, SWRT_ERR_ARG, "precision must be 64 or 32");
+  if (n < 0 || nsteps < 0) return fail(c, SWRT_ERR_ARG, "negative size");
+  if (n == 0 || nsteps == 0) return SWRT_OK;
+  if (!x || !k) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_scratch(c, sizeof(double) * 4 * n))) return rc;
+  double* dxp = (double*)c->scratch;
+  double* dkp = dxp + 2 * n;
+  HIPCHK(c, hipMemcpyAsync(dxp, x, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(dkp, k, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
+  for (int64_t s0 = 0; s0 < nsteps; s0 += kMaxStepsPerLaunch) {
+    const int ns = (int)std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
+    if (precision == 64)
+      hipLaunchKernelGGL(spectral_leapfrog_kernel<double>, dim3(nblocks(n, kSpecThreads)), dim3(kSpecThreads),
+                         0, c->stream, c->mg, dxp, dkp, n, dt, ns, f * f, gH);
+    else
+      hipLaunchKernelGGL(spectral_leapfrog_kernel<float>, dim3(nblocks(n, kSpecThreads)), dim3(kSpecThreads),
+                         0, c->stream, c->mg, dxp, dkp, n, dt, ns, f * f, gH);
+    HIPCHK(c, hipGetLastError());
+  }
+  HIPCHK(c, hipMemcpyAsync(x, dxp, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(k, dkp, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return SWRT_OK;
   GUARD_END(c)

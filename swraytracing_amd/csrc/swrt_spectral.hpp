@@ -1,0 +1,165 @@
+// swrt_spectral.hpp — exact spectral evaluator (E2 / SURVEY K3).
+//
+// Generalises the exact Fourier kick of scratch/fourier_interpolate_test.m:
+// 92-136 (psi = sum A cos(Kx + Ly + phi)) to a dense coefficient grid
+//     psi(x, y) = sum_{i,j} Re( C[i,j] * exp(1i*(kx_i*x + ky_j*y)) ),
+//     kx_i = (kx0 + i)*s, ky_j = (ky0 + j)*s,
+// which covers the half-plane spectral layout of g2k (C = 2*psik, the
+// ky = 0 / kx < 0 half-line zeroed, DC real) and the full-plane amp/phase
+// field of the scratch test (C = A*exp(1i*phi)).  U = -psi_y, V = psi_x,
+// u_x = -psi_xy, u_y = -psi_yy, v_x = psi_xx, v_y = psi_xy.
+//
+// One lane per packet; the workgroup streams coefficient rows through LDS
+// (every lane reads the same coefficient: broadcast, conflict-free) and each
+// lane walks a row with the phase recurrence e <- e*exp(1i*s*x) (re-seeded
+// with sincos at the start of every row), accumulating the five row sums
+//   A0 = sum Im z, A1 = sum kx Im z, B0 = sum Re z, B1 = sum kx Re z,
+//   B2 = sum kx^2 Re z   (z = C*e)
+// that the ky weights then combine: psi_x -= A1, psi_y -= ky*A0,
+// psi_xx -= B2, psi_xy -= ky*B1, psi_yy -= ky^2*B0.
+// FP-VALU bound (≈14 flops per mode per packet); T = double or float
+// (the fp32 tolerance study of config 5).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace swrt {
+
+struct ModeGrid {
+  const double2* C;  // nkx x nky column-major (i fastest): row j = fixed ky
+  int nkx, nky;
+  double kx0, ky0, s;
+};
+
+constexpr int kSpecThreads = 256;
+constexpr int kSpecChunk = 512;  // coefficients staged per LDS pass
+
+template <typename T>
+struct cplx {
+  T re, im;
+};
+
+// Five derivative sums of psi at (x, y) for the lanes of a workgroup.
+// All lanes of the block must call this together (LDS staging).
+template <typename T>
+__device__ __forceinline__ void spectral_sums(const ModeGrid& g, double x, double y, bool active,
+                                              cplx<T>* lds, double out[5]) {
+  T px = 0, py = 0, pxx = 0, pxy = 0, pyy = 0;
+  double sr, cr;
+  sincos(g.s * x, &sr, &cr);
+  const T rr = (T)cr, ri = (T)sr;  // exp(1i*s*x)
+  for (int j = 0; j < g.nky; ++j) {
+    const double ky = (g.ky0 + j) * g.s;
+    double s0, c0;
+    sincos(g.kx0 * g.s * x + ky * y, &s0, &c0);
+    T er = (T)c0, ei = (T)s0;
+    T A0 = 0, A1 = 0, B0 = 0, B1 = 0, B2 = 0;
+    for (int i0 = 0; i0 < g.nkx; i0 += kSpecChunk) {
+      const int cnt = min(kSpecChunk, g.nkx - i0);
+      __syncthreads();
+      for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
+        const double2 c = g.C[(size_t)j * g.nkx + i0 + t];
+        lds[t].re = (T)c.x;
+        lds[t].im = (T)c.y;
+      }
+      __syncthreads();
+      if (active) {
+        // this sum has no reference rounding order to reproduce: let FMAs form
+#pragma clang fp contract(fast)
+        T kx = (T)((g.kx0 + i0) * g.s);
+        const T ds = (T)g.s;
+        for (int t = 0; t < cnt; ++t) {
+          const cplx<T> c = lds[t];
+          const T zr = c.re * er - c.im * ei;
+          const T zi = c.re * ei + c.im * er;
+          A0 += zi;
+          A1 += kx * zi;
+          B0 += zr;
+          B1 += kx * zr;
+          B2 += (kx * kx) * zr;
+          const T nr = er * rr - ei * ri;
+          ei = er * ri + ei * rr;
+          er = nr;
+          kx += ds;
+        }
+      }
+    }
+    const T kyT = (T)ky;
+    px -= A1;
+    py -= kyT * A0;
+    pxx -= B2;
+    pxy -= kyT * B1;
+    pyy -= (kyT * kyT) * B0;
+  }
+  out[0] = px;
+  out[1] = py;
+  out[2] = pxx;
+  out[3] = pxy;
+  out[4] = pyy;
+}
+
+// U, grad U (6 x n, same order as swrt_eval) from the five psi derivatives.
+__device__ __forceinline__ void psi_to_flow(const double d[5], double I[6]) {
+  I[0] = -d[1];  // u = -psi_y
+  I[1] = d[0];   // v = psi_x
+  I[2] = -d[3];  // u_x = -psi_xy
+  I[3] = -d[4];  // u_y = -psi_yy
+  I[4] = d[2];   // v_x = psi_xx
+  I[5] = d[3];   // v_y = psi_xy
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kSpecThreads) spectral_eval_kernel(ModeGrid g, const double* x,
+                                                                     const double* y, int64_t n,
+                                                                     double* out) {
+  __shared__ cplx<T> lds[kSpecChunk];
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = p < n;
+  double d[5];
+  spectral_sums<T>(g, active ? x[p] : 0.0, active ? y[p] : 0.0, active, lds, d);
+  if (!active) return;
+  double I[6];
+  psi_to_flow(d, I);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) out[(int64_t)q * n + p] = I[q];
+}
+
+// ode_symplectic.m:13-37 with the exact spectral kick (the scheme of
+// scratch/fourier_interpolate_test.m:73-114): drift, exact U and
+// (grad U)^T k at x1, kick, drift.  State N x 2 column-major.
+template <typename T>
+__global__ void __launch_bounds__(kSpecThreads) spectral_leapfrog_kernel(ModeGrid g, double* xs,
+                                                                         double* ks, int64_t n,
+                                                                         double dt, int nsteps,
+                                                                         double f2, double gH) {
+  __shared__ cplx<T> lds[kSpecChunk];
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = p < n;
+  double x0 = 0, y0 = 0, k0 = 0, l0 = 0;
+  if (active) {
+    x0 = xs[p]; y0 = xs[n + p]; k0 = ks[p]; l0 = ks[n + p];
+  }
+  const double half = dt / 2;
+  for (int s = 0; s < nsteps; ++s) {
+    double w = sqrt(f2 + gH * (k0 * k0 + l0 * l0));
+    const double x1 = x0 + half * (gH * k0 / w);
+    const double y1 = y0 + half * (gH * l0 / w);
+    double d[5], I[6];
+    spectral_sums<T>(g, x1, y1, active, lds, d);
+    psi_to_flow(d, I);
+    const double x2 = x1 + dt * I[0];
+    const double y2 = y1 + dt * I[1];
+    const double k2 = k0 - dt * (I[2] * k0 + I[4] * l0);
+    const double l2 = l0 - dt * (I[3] * k0 + I[5] * l0);
+    w = sqrt(f2 + gH * (k2 * k2 + l2 * l2));
+    x0 = x2 + half * (gH * k2 / w);
+    y0 = y2 + half * (gH * l2 / w);
+    k0 = k2;
+    l0 = l2;
+  }
+  if (active) {
+    xs[p] = x0; xs[n + p] = y0; ks[p] = k0; ks[n + p] = l0;
+  }
+}
+
+}  // namespace swrt

@@ -301,3 +301,51 @@ def grid_U(qk, K_d2, K2, kx_, ky_, shear_strength=0.0, ctx: Context | None = Non
     if qk.ndim == 2:
         return {n: v[0] for n, v in out.items()}
     return {n: np.stack(v, axis=2) for n, v in out.items()}
+
+
+class FourierScheme(RaytracingScheme):
+    """Exact spectral evaluation of the background (no grid, no interpolation):
+    the evaluator of scratch/fourier_interpolate_test.m:92-136, generalised to
+    any dense mode grid, on the GPU (swrt_spectral_*).  Construct from a g2k
+    half-plane streamfunction spectrum or from the scratch test's amp/phase."""
+
+    def __init__(self, C, kx0, ky0, s, precision=64, device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self.precision = precision
+        self.ctx.spectral_set_modes(C, kx0, ky0, s)
+
+    @classmethod
+    def from_halfplane(cls, psik, k_scale=1.0, **kw):
+        psik = np.asarray(psik, dtype=np.complex128)
+        kmax = psik.shape[1] - 1
+        C = 2 * psik
+        C[:kmax, 0] = 0
+        C[kmax, 0] = psik[kmax, 0].real
+        return cls(C, -kmax, 0, k_scale, **kw)
+
+    @classmethod
+    def from_amp_phase(cls, amp, phase, n, **kw):
+        return cls(np.asarray(amp) * np.exp(1j * np.asarray(phase)), -n, -n, 1.0, **kw)
+
+    def streamfunction(self, x, y, t=0.0):  # pragma: no cover - not needed by the integrators
+        raise NotImplementedError
+
+    def _eval(self, x):
+        x, xx, yy = _split_xy(x)
+        return x, self.ctx.spectral_eval(xx, yy, self.precision)
+
+    def U(self, x, t=0.0):
+        x, I = self._eval(x)
+        u = np.zeros_like(x)
+        shp = x[:, 0, ...].shape
+        u[:, 0, ...] = np.reshape(I[0], shp, order="F")
+        u[:, 1, ...] = np.reshape(I[1], shp, order="F")
+        return u
+
+    def grad_U(self, x, t=0.0):
+        _, I = self._eval(x)
+        return {"u_x": I[2], "u_y": I[3], "v_x": I[4], "v_y": I[5]}
+
+    def leapfrog(self, x, k, dt, nsteps, f, gH):
+        """Fused device leapfrog with the exact kick (x, k: N x 2)."""
+        return self.ctx.spectral_leapfrog(x, k, dt, nsteps, f, gH, self.precision)
