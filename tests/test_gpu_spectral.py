@@ -46,7 +46,7 @@ def test_halfplane_spectrum_vs_direct_sum_and_grid(ctx, nx):
     rng = np.random.default_rng(nx)
     psi = np.zeros_like(X)
     for _ in range(30):
-        kx, ky = rng.integers(-nx // 4, nx // 4, 2)
+        kx, ky = rng.integers(-nx // 8, nx // 8, 2)  # <= 0.8 rad/cell: 6-point Lagrange accurate to ~1e-4
         psi += rng.normal() / (1 + kx * kx + ky * ky) * np.cos(kx * X + ky * Y + rng.uniform(0, 6))
     fk = orc.g2k(psi)
     C, kx0, ky0, s = orc.modes_from_halfplane(fk)
