@@ -190,6 +190,18 @@ int swrt_spectral_leapfrog(swrt_ctx* ctx, double* x, double* k, int64_t n, doubl
                            double f, double gH, int precision);
 
 /* ---------------------------------------------------------------------------
+ * Diagnostics (analysis/load_data.m)
+ * ------------------------------------------------------------------------ */
+
+/* Energy-vs-omega input of load_data.m:33-52 for the device-resident packets:
+ * omega = sqrt(f^2 + Cg^2*|k|^2) per packet, histcounts over `edges`
+ * (nbins + 1 increasing values; last bin closed) ADDED to counts_inout (so a
+ * window of frames accumulates), and the ensemble mean omega of this frame
+ * (load_data.m:63; deterministic block-ordered sum). */
+int swrt_omega_histogram(swrt_ctx* ctx, double f, double Cg, const double* edges, int64_t nbins,
+                         int64_t* counts_inout, double* mean_omega_out);
+
+/* ---------------------------------------------------------------------------
  * Runtime helpers
  * ------------------------------------------------------------------------ */
 int swrt_synchronize(swrt_ctx* ctx);

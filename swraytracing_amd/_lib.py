@@ -64,6 +64,7 @@ SIGNATURES = {
     "swrt_spectral_set_modes": (_INT, [_VP, _P, _I, _I, _D, _D, _D]),
     "swrt_spectral_eval": (_INT, [_VP, _P, _P, _I, _INT, _P]),
     "swrt_spectral_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT]),
+    "swrt_omega_histogram": (_INT, [_VP, _D, _D, _P, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_D)]),
     "swrt_synchronize": (_INT, [_VP]),
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
@@ -295,6 +296,20 @@ class Context:
         self._chk(self._L.swrt_spectral_leapfrog(self._h, _p(x), _p(k), x.shape[0], float(dt), int(nsteps),
                                                  float(f), float(gH), int(precision)), "swrt_spectral_leapfrog")
         return x, k
+
+    # ---- diagnostics (load_data.m) -----------------------------------------
+    def omega_histogram(self, f, Cg, edges, counts=None):
+        """Add this frame's omega histcounts to `counts` (int64); returns
+        (counts, mean omega)."""
+        edges = _f64(np.asarray(edges, dtype=np.float64))
+        nb = edges.size - 1
+        counts = np.zeros(nb, dtype=np.int64) if counts is None else counts
+        assert counts.dtype == np.int64 and counts.size == nb and counts.flags["C_CONTIGUOUS"]
+        mean = _D()
+        self._chk(self._L.swrt_omega_histogram(self._h, float(f), float(Cg), _p(edges), nb,
+                                               counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                               ctypes.byref(mean)), "swrt_omega_histogram")
+        return counts, mean.value
 
     # ---- runtime ---------------------------------------------------------
     def synchronize(self):

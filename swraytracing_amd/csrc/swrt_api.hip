@@ -21,6 +21,7 @@
 #include "swrt_tile.hpp"
 #include "swrt_xka.hpp"
 #include "swrt_spectral.hpp"
+#include "swrt_diag.hpp"
 
 using namespace swrt;
 
@@ -1107,6 +1108,46 @@ int swrt_spectral_leapfrog(swrt_ctx* c, double* x, double* k, int64_t n, double 
   HIPCHK(c, hipMemcpyAsync(x, dxp, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(k, dkp, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_omega_histogram(swrt_ctx* c, double f, double Cg, const double* edges, int64_t nbins,
+                         int64_t* counts_inout, double* mean_omega_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (nbins <= 0 || nbins > kMaxHistBins) return fail(c, SWRT_ERR_ARG, "nbins must be 1..4096");
+  if (!edges || !counts_inout) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  for (int64_t i = 0; i < nbins; ++i)
+    if (!(edges[i] < edges[i + 1])) return fail(c, SWRT_ERR_ARG, "edges must increase");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int nblk = 1024;
+  const size_t bytes = sizeof(double) * (nbins + 1) + sizeof(unsigned long long) * nbins +
+                       sizeof(double) * (nblk + 1);
+  int rc;
+  if ((rc = ensure_scratch(c, bytes))) return rc;
+  double* dedges = (double*)c->scratch;
+  unsigned long long* dcounts = (unsigned long long*)(dedges + nbins + 1);
+  double* partial = (double*)(dcounts + nbins);
+  HIPCHK(c, hipMemcpyAsync(dedges, edges, sizeof(double) * (nbins + 1), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(dcounts, 0, sizeof(unsigned long long) * nbins, c->stream));
+  double mean = 0.0;
+  if (c->n > 0) {
+    hipLaunchKernelGGL(omega_hist_kernel, dim3(nblk), dim3(kHistThreads), 0, c->stream, c->dk, c->n, f * f,
+                       Cg * Cg, dedges, (int)nbins, dcounts, partial);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(omega_sum_kernel, dim3(1), dim3(64), 0, c->stream, partial, nblk, partial + nblk);
+    HIPCHK(c, hipGetLastError());
+  }
+  std::vector<unsigned long long> hc(nbins, 0ull);
+  double sum = 0.0;
+  HIPCHK(c, hipMemcpyAsync(hc.data(), dcounts, sizeof(unsigned long long) * nbins, hipMemcpyDeviceToHost, c->stream));
+  if (c->n > 0)
+    HIPCHK(c, hipMemcpyAsync(&sum, partial + nblk, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int64_t i = 0; i < nbins; ++i) counts_inout[i] += (int64_t)hc[i];
+  if (c->n > 0) mean = sum / (double)c->n;
+  if (mean_omega_out) *mean_omega_out = mean;
   return SWRT_OK;
   GUARD_END(c)
 }

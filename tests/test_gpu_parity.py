@@ -465,3 +465,23 @@ def test_step_packet_xka_scalar_api(ctx):
     g = sw.step_packet_xka(P, U, G, H, 1.0, 4.0, dx, dx, 0.02, ctx=ctx)
     o = orc.step_packet_xka(P, U, G, H, 1.0, 4.0, dx, dx, 0.02)
     assert g == o
+
+
+def test_omega_histogram_matches_load_data(ctx):
+    """analysis/load_data.m:33-52,63: omega, histcounts (last bin closed), mean."""
+    rng = np.random.default_rng(31)
+    n = 300_000
+    k = rng.normal(size=(n, 2)) * 5
+    x = rng.uniform(-3, 3, (n, 2))
+    ctx.packets_set(x, k)
+    f, Cg = 3.0, 1.0
+    w = np.sqrt(f ** 2 + Cg ** 2 * (k * k).sum(1))
+    edges = np.linspace(0, w.max(), 300)  # load_data.m:38-39 (bins = 300 edges)
+    counts, mean = ctx.omega_histogram(f, Cg, edges)
+    ref, _ = np.histogram(w, edges)
+    np.testing.assert_array_equal(counts, ref)
+    assert counts.sum() == n  # max sits on the closed last edge
+    assert abs(mean - w.mean()) < 1e-12 * w.mean()
+    # accumulation over frames (load_data.m windows)
+    counts2, _ = ctx.omega_histogram(f, Cg, edges, counts.copy())
+    np.testing.assert_array_equal(counts2, 2 * ref)
