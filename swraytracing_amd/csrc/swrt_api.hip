@@ -106,9 +106,12 @@ struct swrt_ctx {
   int64_t xka_hcap = 0;  // doubles allocated
   // exact spectral evaluator (dense coefficient grid)
   double2* modes = nullptr;
+  int2* mode_rows = nullptr;
   int64_t mode_cap = 0;
+  int64_t rows_cap = 0;
   ModeGrid mg{};
   bool modes_set = false;
+  int64_t mode_active = 0;  // coefficients inside the per-row nonzero spans
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -487,7 +490,8 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->hk) (void)hipFree(c->hk);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->tw) (void)hipFree(c->tw);
-  for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist, (void*)c->modes})
+  for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist, (void*)c->modes,
+                  (void*)c->mode_rows})
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -1037,8 +1041,28 @@ int swrt_spectral_set_modes(swrt_ctx* c, const double* C, int64_t nkx, int64_t n
     HIPCHK(c, hipMalloc(&c->modes, sizeof(double2) * nkx * nky));
     c->mode_cap = nkx * nky;
   }
+  if (nky > c->rows_cap) {
+    if (c->mode_rows) (void)hipFree(c->mode_rows);
+    c->mode_rows = nullptr;
+    c->rows_cap = 0;
+    HIPCHK(c, hipMalloc(&c->mode_rows, sizeof(int2) * nky));
+    c->rows_cap = nky;
+  }
+  // nonzero span of each row (the kernel skips zero head/tail segments)
+  std::vector<int2> rows(nky);
+  for (int64_t j = 0; j < nky; ++j) {
+    int lo = 0, hi = (int)nkx;
+    while (lo < hi && C[2 * (j * nkx + lo)] == 0.0 && C[2 * (j * nkx + lo) + 1] == 0.0) ++lo;
+    while (hi > lo && C[2 * (j * nkx + hi - 1)] == 0.0 && C[2 * (j * nkx + hi - 1) + 1] == 0.0) --hi;
+    rows[j] = make_int2(lo, hi);
+  }
   HIPCHK(c, hipMemcpyAsync(c->modes, C, sizeof(double2) * nkx * nky, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->mode_rows, rows.data(), sizeof(int2) * nky, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  int64_t active = 0;
+  for (auto& r : rows) active += r.y - r.x;
+  c->mode_active = active;
+  c->mg.rows = c->mode_rows;
   c->mg.C = c->modes;
   c->mg.nkx = (int)nkx;
   c->mg.nky = (int)nky;

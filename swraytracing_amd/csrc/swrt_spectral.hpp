@@ -9,9 +9,9 @@
 // field of the scratch test (C = A*exp(1i*phi)).  U = -psi_y, V = psi_x,
 // u_x = -psi_xy, u_y = -psi_yy, v_x = psi_xx, v_y = psi_xy.
 //
-// One lane per packet; the workgroup streams coefficient rows through LDS
-// (every lane reads the same coefficient: broadcast, conflict-free) and each
-// lane walks a row with the phase recurrence e <- e*exp(1i*s*x) (re-seeded
+// One lane per packet; all lanes read the same coefficient at the same time
+// (wave-uniform scalar loads) and each lane walks a row with the phase
+// recurrence e <- e*exp(1i*s*x) (re-seeded
 // with sincos at the start of every row), accumulating the five row sums
 //   A0 = sum Im z, A1 = sum kx Im z, B0 = sum Re z, B1 = sum kx Re z,
 //   B2 = sum kx^2 Re z   (z = C*e)
@@ -27,61 +27,57 @@ namespace swrt {
 
 struct ModeGrid {
   const double2* C;  // nkx x nky column-major (i fastest): row j = fixed ky
+  const int2* rows;  // per row: [first, last+1) of the nonzero coefficients
   int nkx, nky;
   double kx0, ky0, s;
 };
 
 constexpr int kSpecThreads = 256;
-constexpr int kSpecChunk = 512;  // coefficients staged per LDS pass
 
 template <typename T>
 struct cplx {
   T re, im;
 };
 
-// Five derivative sums of psi at (x, y) for the lanes of a workgroup.
-// All lanes of the block must call this together (LDS staging).
+// Five derivative sums of psi at (x, y).  Every lane of a wavefront walks the
+// same coefficient at the same time, so the coefficient loads are
+// wave-uniform (scalar loads through the scalar cache: no LDS staging, no
+// barriers); zero head/tail segments of each row are skipped.
 template <typename T>
-__device__ __forceinline__ void spectral_sums(const ModeGrid& g, double x, double y, bool active,
-                                              cplx<T>* lds, double out[5]) {
+__device__ __forceinline__ void spectral_sums(const ModeGrid& g, double x, double y, double out[5]) {
   T px = 0, py = 0, pxx = 0, pxy = 0, pyy = 0;
   double sr, cr;
   sincos(g.s * x, &sr, &cr);
   const T rr = (T)cr, ri = (T)sr;  // exp(1i*s*x)
   for (int j = 0; j < g.nky; ++j) {
+    const int2 rg = g.rows[j];
+    if (rg.x >= rg.y) continue;
     const double ky = (g.ky0 + j) * g.s;
     double s0, c0;
-    sincos(g.kx0 * g.s * x + ky * y, &s0, &c0);
+    sincos((g.kx0 + rg.x) * g.s * x + ky * y, &s0, &c0);
     T er = (T)c0, ei = (T)s0;
     T A0 = 0, A1 = 0, B0 = 0, B1 = 0, B2 = 0;
-    for (int i0 = 0; i0 < g.nkx; i0 += kSpecChunk) {
-      const int cnt = min(kSpecChunk, g.nkx - i0);
-      __syncthreads();
-      for (int t = threadIdx.x; t < cnt; t += blockDim.x) {
-        const double2 c = g.C[(size_t)j * g.nkx + i0 + t];
-        lds[t].re = (T)c.x;
-        lds[t].im = (T)c.y;
-      }
-      __syncthreads();
-      if (active) {
-        // this sum has no reference rounding order to reproduce: let FMAs form
+    T kx = (T)((g.kx0 + rg.x) * g.s);
+    const T ds = (T)g.s;
+    const double2* row = g.C + (size_t)j * g.nkx;
+    {
+      // this sum has no reference rounding order to reproduce: let FMAs form
 #pragma clang fp contract(fast)
-        T kx = (T)((g.kx0 + i0) * g.s);
-        const T ds = (T)g.s;
-        for (int t = 0; t < cnt; ++t) {
-          const cplx<T> c = lds[t];
-          const T zr = c.re * er - c.im * ei;
-          const T zi = c.re * ei + c.im * er;
-          A0 += zi;
-          A1 += kx * zi;
-          B0 += zr;
-          B1 += kx * zr;
-          B2 += (kx * kx) * zr;
-          const T nr = er * rr - ei * ri;
-          ei = er * ri + ei * rr;
-          er = nr;
-          kx += ds;
-        }
+#pragma unroll 4
+      for (int i = rg.x; i < rg.y; ++i) {
+        const double2 cd = row[i];
+        const T cre = (T)cd.x, cim = (T)cd.y;
+        const T zr = cre * er - cim * ei;
+        const T zi = cre * ei + cim * er;
+        A0 += zi;
+        A1 += kx * zi;
+        B0 += zr;
+        B1 += kx * zr;
+        B2 += (kx * kx) * zr;
+        const T nr = er * rr - ei * ri;
+        ei = er * ri + ei * rr;
+        er = nr;
+        kx += ds;
       }
     }
     const T kyT = (T)ky;
@@ -112,12 +108,10 @@ template <typename T>
 __global__ void __launch_bounds__(kSpecThreads) spectral_eval_kernel(ModeGrid g, const double* x,
                                                                      const double* y, int64_t n,
                                                                      double* out) {
-  __shared__ cplx<T> lds[kSpecChunk];
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = p < n;
+  if (p >= n) return;
   double d[5];
-  spectral_sums<T>(g, active ? x[p] : 0.0, active ? y[p] : 0.0, active, lds, d);
-  if (!active) return;
+  spectral_sums<T>(g, x[p], y[p], d);
   double I[6];
   psi_to_flow(d, I);
 #pragma unroll
@@ -132,20 +126,16 @@ __global__ void __launch_bounds__(kSpecThreads) spectral_leapfrog_kernel(ModeGri
                                                                          double* ks, int64_t n,
                                                                          double dt, int nsteps,
                                                                          double f2, double gH) {
-  __shared__ cplx<T> lds[kSpecChunk];
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = p < n;
-  double x0 = 0, y0 = 0, k0 = 0, l0 = 0;
-  if (active) {
-    x0 = xs[p]; y0 = xs[n + p]; k0 = ks[p]; l0 = ks[n + p];
-  }
+  if (p >= n) return;
+  double x0 = xs[p], y0 = xs[n + p], k0 = ks[p], l0 = ks[n + p];
   const double half = dt / 2;
   for (int s = 0; s < nsteps; ++s) {
     double w = sqrt(f2 + gH * (k0 * k0 + l0 * l0));
     const double x1 = x0 + half * (gH * k0 / w);
     const double y1 = y0 + half * (gH * l0 / w);
     double d[5], I[6];
-    spectral_sums<T>(g, x1, y1, active, lds, d);
+    spectral_sums<T>(g, x1, y1, d);
     psi_to_flow(d, I);
     const double x2 = x1 + dt * I[0];
     const double y2 = y1 + dt * I[1];
@@ -157,9 +147,7 @@ __global__ void __launch_bounds__(kSpecThreads) spectral_leapfrog_kernel(ModeGri
     k0 = k2;
     l0 = l2;
   }
-  if (active) {
-    xs[p] = x0; xs[n + p] = y0; ks[p] = k0; ks[n + p] = l0;
-  }
+  xs[p] = x0; xs[n + p] = y0; ks[p] = k0; ks[n + p] = l0;
 }
 
 }  // namespace swrt

@@ -39,6 +39,12 @@ def main():
     psik[mask] = kk[mask] ** -3.0 * np.exp(2j * np.pi * rng.random(mask.sum()))
     sch = sw.FourierScheme.from_halfplane(psik * 0.05)
     M = (2 * kmax + 1) * (kmax + 1)
+    # coefficients the kernel actually sums (nonzero span of every row)
+    C = 2 * psik * 0.05
+    nz = np.abs(C) > 0
+    spans = [(np.flatnonzero(nz[:, j]).max() - np.flatnonzero(nz[:, j]).min() + 1) if nz[:, j].any() else 0
+             for j in range(C.shape[1])]
+    M_active = int(sum(spans))
     N = args.packets
     L = 2 * np.pi
     x = L * rng.random((N, 2)) - L / 2
@@ -53,14 +59,14 @@ def main():
         xs, ks = sch.leapfrog(x, k, dt, args.steps, 3.0, 1.0)
         t = time.perf_counter() - t0
         rate = N * args.steps / t
-        tf = rate * 16 * M / 1e12
+        tf = rate * 16 * M_active / 1e12
         res[prec] = dict(x=xs, k=ks, rate=rate, tflops=tf, seconds=t)
     err = float(np.abs(res[32]["x"] - res[64]["x"]).max())
     errk = float(np.abs(res[32]["k"] - res[64]["k"]).max() / np.abs(res[64]["k"]).max())
     out = {
         "metric": "packet-steps/sec, exact spectral evaluator (config 5 study)",
         "config": {"workload": "symplectic_full_fourier path, exact Fourier-mode kick", "nx": nx,
-                   "modes": M, "packets": N, "steps": args.steps},
+                   "modes_dense": M, "modes_summed": M_active, "packets": N, "steps": args.steps},
         "fp64": {"value": res[64]["rate"], "unit": "packet-steps/s",
                  "roofline": {"bound": "valu-fp64", "achieved": res[64]["tflops"], "peak": PEAK[64],
                               "unit": "TFLOP/s", "frac": res[64]["tflops"] / PEAK[64]}},
@@ -68,7 +74,7 @@ def main():
                  "roofline": {"bound": "valu-fp32", "achieved": res[32]["tflops"], "peak": PEAK[32],
                               "unit": "TFLOP/s", "frac": res[32]["tflops"] / PEAK[32]},
                  "max_abs_x_err_vs_fp64": err, "max_rel_k_err_vs_fp64": errk},
-        "note": "host-buffer call incl. upload/download; 16 flop/mode accounting",
+        "note": "host-buffer call incl. upload/download; 16 flop per summed mode (zero row ends skipped)",
     }
     print(json.dumps(out))
 
