@@ -43,49 +43,66 @@ struct cplx {
 // same coefficient at the same time, so the coefficient loads are
 // wave-uniform (scalar loads through the scalar cache: no LDS staging, no
 // barriers); zero head/tail segments of each row are skipped.
+constexpr int kSpecChains = 4;  // independent phase recurrences per row (ILP)
+
 template <typename T>
 __device__ __forceinline__ void spectral_sums(const ModeGrid& g, double x, double y, double out[5]) {
   T px = 0, py = 0, pxx = 0, pxy = 0, pyy = 0;
   double sr, cr;
-  sincos(g.s * x, &sr, &cr);
-  const T rr = (T)cr, ri = (T)sr;  // exp(1i*s*x)
+  sincos(kSpecChains * g.s * x, &sr, &cr);
+  const T rr = (T)cr, ri = (T)sr;  // exp(1i*kSpecChains*s*x): stride of one chain
   for (int j = 0; j < g.nky; ++j) {
     const int2 rg = g.rows[j];
     if (rg.x >= rg.y) continue;
     const double ky = (g.ky0 + j) * g.s;
-    double s0, c0;
-    sincos((g.kx0 + rg.x) * g.s * x + ky * y, &s0, &c0);
-    T er = (T)c0, ei = (T)s0;
-    T A0 = 0, A1 = 0, B0 = 0, B1 = 0, B2 = 0;
-    T kx = (T)((g.kx0 + rg.x) * g.s);
-    const T ds = (T)g.s;
+    // chain c walks i = rg.x + c, rg.x + c + kSpecChains, ...
+    T er[kSpecChains], ei[kSpecChains], kx[kSpecChains];
+    T A0[kSpecChains], A1[kSpecChains], B0[kSpecChains], B1[kSpecChains], B2[kSpecChains];
+#pragma unroll
+    for (int c = 0; c < kSpecChains; ++c) {
+      double s0, c0;
+      sincos((g.kx0 + rg.x + c) * g.s * x + ky * y, &s0, &c0);
+      er[c] = (T)c0;
+      ei[c] = (T)s0;
+      kx[c] = (T)((g.kx0 + rg.x + c) * g.s);
+      A0[c] = A1[c] = B0[c] = B1[c] = B2[c] = 0;
+    }
+    const T ds = (T)(kSpecChains * g.s);
     const double2* row = g.C + (size_t)j * g.nkx;
     {
       // this sum has no reference rounding order to reproduce: let FMAs form
 #pragma clang fp contract(fast)
-#pragma unroll 4
-      for (int i = rg.x; i < rg.y; ++i) {
-        const double2 cd = row[i];
-        const T cre = (T)cd.x, cim = (T)cd.y;
-        const T zr = cre * er - cim * ei;
-        const T zi = cre * ei + cim * er;
-        A0 += zi;
-        A1 += kx * zi;
-        B0 += zr;
-        B1 += kx * zr;
-        B2 += (kx * kx) * zr;
-        const T nr = er * rr - ei * ri;
-        ei = er * ri + ei * rr;
-        er = nr;
-        kx += ds;
+      for (int i = rg.x; i < rg.y; i += kSpecChains) {
+#pragma unroll
+        for (int c = 0; c < kSpecChains; ++c) {
+          // past the span end the coefficient is read as 0 (the row stays in bounds)
+          const double2 cd = (i + c < rg.y) ? row[i + c] : make_double2(0.0, 0.0);
+          const T cre = (T)cd.x, cim = (T)cd.y;
+          const T zr = cre * er[c] - cim * ei[c];
+          const T zi = cre * ei[c] + cim * er[c];
+          A0[c] += zi;
+          A1[c] += kx[c] * zi;
+          B0[c] += zr;
+          B1[c] += kx[c] * zr;
+          B2[c] += (kx[c] * kx[c]) * zr;
+          const T nr = er[c] * rr - ei[c] * ri;
+          ei[c] = er[c] * ri + ei[c] * rr;
+          er[c] = nr;
+          kx[c] += ds;
+        }
       }
     }
+    T a0 = 0, a1 = 0, b0 = 0, b1 = 0, b2 = 0;
+#pragma unroll
+    for (int c = 0; c < kSpecChains; ++c) {
+      a0 += A0[c]; a1 += A1[c]; b0 += B0[c]; b1 += B1[c]; b2 += B2[c];
+    }
     const T kyT = (T)ky;
-    px -= A1;
-    py -= kyT * A0;
-    pxx -= B2;
-    pxy -= kyT * B1;
-    pyy -= (kyT * kyT) * B0;
+    px -= a1;
+    py -= kyT * a0;
+    pxx -= b2;
+    pxy -= kyT * b1;
+    pyy -= (kyT * kyT) * b0;
   }
   out[0] = px;
   out[1] = py;
