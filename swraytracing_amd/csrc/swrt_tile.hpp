@@ -157,7 +157,12 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     __syncthreads();
     for (int i = tid; i < nb; i += NT) {
       const int v = kr[i];
+#ifdef SWRT_ABLATE_SORT
+      order[i] = i;
+      (void)v;
+#else
       order[hist[v >> 16] + (v & 0xffff)] = i;
+#endif
     }
     __syncthreads();
 
@@ -177,6 +182,12 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         stencil_at(a.f0, x1, y1, a.bump, sc);
         const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
         double I[kRec], J[kRec];
+#ifdef SWRT_ABLATE_COMPUTE
+        if (true) {
+#pragma unroll
+          for (int q = 0; q < kRec; ++q) { I[q] = sc.wx[q] * 1e-30; J[q] = sc.wy[q] * 1e-30; }
+        } else
+#endif
         if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M) {
           gather6_lds<TWO, W, WN>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
         } else {
