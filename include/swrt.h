@@ -126,7 +126,9 @@ int swrt_set_locality(swrt_ctx* ctx, int64_t rebin_every, int64_t tile);
 /* Packet-kernel variant (same results, bit for bit): 0 = automatic (the
  * LDS-tiled kernel whenever binning is on and nx >= 32), 1 = one lane per
  * packet gathering from the global node array, 2 = LDS-tiled kernel (16x16-
- * cell tiles, field window staged in LDS, in-tile cell sort). */
+ * cell tiles, field window staged in LDS, in-tile cell sort), 3 = persistent
+ * LDS-tiled kernel (one workgroup per CU, next tile's window staged by
+ * LDS-DMA and its packets sorted/prefetched while the current tile runs). */
 int swrt_set_kernel(swrt_ctx* ctx, int variant);
 
 /* Advance the device-resident packets by nsteps leapfrog steps

@@ -19,6 +19,7 @@
 #include "swrt_fft.hpp"
 #include "swrt_kernels.hpp"
 #include "swrt_tile.hpp"
+#include "swrt_persist.hpp"
 #include "swrt_xka.hpp"
 #include "swrt_spectral.hpp"
 #include "swrt_diag.hpp"
@@ -323,7 +324,7 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next)
 
 bool use_tile_kernel(const swrt_ctx* c) {
   if (c->rebin_every <= 0) return false;
-  if (c->kernel == 2) return true;
+  if (c->kernel == 2 || c->kernel == 3) return true;
   return c->kernel == 0 && c->slot[0].nx >= 2 * kTile;
 }
 
@@ -387,12 +388,27 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
     t.next_keys = c->keys;
     t.next_counts = c->bins;
   }
-  if (a.nslots == 2)
+  if (c->kernel == 3) {
+    // persistent: one 1024-lane workgroup per CU walking a contiguous run of tiles
+    int ncu = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
+      ncu = prop.multiProcessorCount;
+    const int tpw = (int)((grid + ncu - 1) / ncu);
+    const unsigned pgrid = (unsigned)((grid + tpw - 1) / tpw);
+    if (a.nslots == 2)
+      hipLaunchKernelGGL((tile_persist_kernel<true, kTile, kMargin, 1024>), dim3(pgrid), dim3(1024), 0,
+                         c->stream, t, tpw);
+    else
+      hipLaunchKernelGGL((tile_persist_kernel<false, kTile, kMargin, 1024>), dim3(pgrid), dim3(1024), 0,
+                         c->stream, t, tpw);
+  } else if (a.nslots == 2) {
     hipLaunchKernelGGL((tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>), dim3(grid),
                        dim3(kTileThreads), 0, c->stream, t);
-  else
+  } else {
     hipLaunchKernelGGL((tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>), dim3(grid),
                        dim3(kTileThreads), 0, c->stream, t);
+  }
   HIPCHK(c, hipGetLastError());
   std::swap(c->dx, c->dx2);
   std::swap(c->dk, c->dk2);
@@ -836,7 +852,7 @@ int swrt_set_timing(swrt_ctx* c, int every) {
 
 int swrt_set_kernel(swrt_ctx* c, int variant) {
   if (!c) return SWRT_ERR_ARG;
-  if (variant < 0 || variant > 2) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0, 1 or 2");
+  if (variant < 0 || variant > 3) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0..3");
   c->kernel = variant;
   c->bin_valid = false;
   c->keys_fresh = false;

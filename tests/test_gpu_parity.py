@@ -367,12 +367,13 @@ def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, til
     np.testing.assert_array_equal(hkg, hko)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("nslots", [1, 2])
 @pytest.mark.parametrize("dt_scale", [1.0, 40.0])
 def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, nslots, dt_scale):
-    """Per-packet (1) and LDS-tiled (2) kernels give the oracle's bits; the
-    large-dt case drives packets out of the LDS window (global fallback)."""
+    """Per-packet (1), LDS-tiled (2) and persistent LDS-tiled (3) kernels give
+    the oracle's bits; the large-dt case drives packets out of the LDS window
+    (global fallback)."""
     c = qg_case
     nx, L = c["nx"], c["L"]
     p0 = _planes(c["flow"])
@@ -396,9 +397,11 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, nslots, dt_
     np.testing.assert_array_equal(hkg, hko)
 
 
-def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib):
+@pytest.mark.parametrize("variant", [2, 3])
+def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant):
     """512^2 two-snapshot field, 2e5 packets, LDS kernel with re-binning every
-    3 steps over 10 steps: random subset bit-identical to the oracle."""
+    3 steps over 10 steps: random subset bit-identical to the oracle (the
+    persistent kernel walks several tiles per workgroup here)."""
     nx, L = 512, 20.0
     rng = np.random.default_rng(2024)
     kmax = nx // 2 - 1
@@ -413,7 +416,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib):
     p1 = ctx.get_field_grid(1, nx)
     N = 200_000
     x, k = orc.initial_packets(N, L, 4.0, 3.0, 1.0, rng)
-    ctx.set_kernel(2)
+    ctx.set_kernel(variant)
     ctx.set_locality(3, 0)
     try:
         ctx.packets_set(x, k)
@@ -427,6 +430,37 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib):
                                        10, 3.0, 1.0)
     np.testing.assert_array_equal(xg[idx], xo)
     np.testing.assert_array_equal(kg[idx], ko)
+
+
+@pytest.mark.parametrize("variant", [2, 3])
+def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
+    """20000 packets packed into a few cells: tiles far above the
+    per-workgroup pipeline depth (the persistent kernel's overflow loop) and
+    one-tile-heavy binning; every packet bit-identical to the oracle."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    p0 = _planes(c["flow"])
+    p1 = _planes({n: np.asarray(v) * 0.9 for n, v in c["flow"].items()})
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    rng = np.random.default_rng(77)
+    N = 20_000
+    dxg = L / nx
+    x = np.stack([rng.random(N) * 3 * dxg + 5.2 * dxg, rng.random(N) * 3 * dxg - 9.7 * dxg], axis=1)
+    th = rng.random(N) * 2 * np.pi
+    k = 3.0 * np.stack([np.cos(th), np.sin(th)], axis=1)
+    ctx.set_kernel(variant)
+    ctx.set_locality(2, 0)
+    try:
+        xg, kg, _, _ = ctx.leapfrog(x, k, c["dt"], 9, c["f"], 1.0, nslots=2, alpha0=0.2, dalpha=0.05,
+                                    bump=orc.BUMP_QG)
+    finally:
+        ctx.set_kernel(0)
+        ctx.set_locality(4, 0)
+    xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.2, 0.05, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, c["dt"], 9,
+                                       c["f"], 1.0)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
 
 
 def _rsw_background(nx, seed=3):
