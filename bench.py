@@ -148,7 +148,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rebin-every", type=int, default=4, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
-    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile, 3 persistent tile")
+    ap.add_argument("--cell-sort", type=int, default=0,
+                    help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
     ap.add_argument("--timing-every", type=int, default=8,
@@ -172,6 +174,7 @@ def main():
     ctx = sw.Context(device)
     ctx.set_locality(args.rebin_every, args.tile)
     ctx.set_kernel(args.kernel)
+    ctx.set_cell_sort(args.cell_sort)
     rng = np.random.default_rng(args.seed + rank)
     w = build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
@@ -236,6 +239,7 @@ def main():
                                f"{args.nx}^2x2 field, {N} packets/GPU, leapfrog",
                    "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
+                   "cell_sort": args.cell_sort,
                    "parallelism": f"packets sharded x{world}, field replicated"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,

@@ -131,6 +131,12 @@ int swrt_set_locality(swrt_ctx* ctx, int64_t rebin_every, int64_t tile);
  * LDS-DMA and its packets sorted/prefetched while the current tile runs). */
 int swrt_set_kernel(swrt_ctx* ctx, int variant);
 
+/* In-tile cell sort of the LDS-tiled kernel (performance only; results are
+ * identical): 0 = sort on the first launch after each re-binning, later
+ * launches read the packets in the cell order the previous launch wrote
+ * (default); 1 = sort on every launch. */
+int swrt_set_cell_sort(swrt_ctx* ctx, int every_launch);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

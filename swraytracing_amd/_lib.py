@@ -54,6 +54,7 @@ SIGNATURES = {
     "swrt_packets_count": (_I, [_VP]),
     "swrt_set_locality": (_INT, [_VP, _I, _I]),
     "swrt_set_kernel": (_INT, [_VP, _INT]),
+    "swrt_set_cell_sort": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
     "swrt_history_get": (_INT, [_VP, _I, _I, _P, _P]),
@@ -224,6 +225,9 @@ class Context:
 
     def set_kernel(self, variant=0):
         self._chk(self._L.swrt_set_kernel(self._h, int(variant)), "swrt_set_kernel")
+
+    def set_cell_sort(self, every_launch=0):
+        self._chk(self._L.swrt_set_cell_sort(self._h, int(every_launch)), "swrt_set_cell_sort")
 
     def advance(self, dt, nsteps, f, gH, nslots=1, alpha0=0.0, dalpha=0.0, bump=1e-13, save_every=0):
         self._chk(self._L.swrt_advance(self._h, float(dt), int(nsteps), float(f), float(gH), int(nslots),

@@ -86,6 +86,8 @@ struct swrt_ctx {
   int64_t steps_since_bin = 0;
   bool bin_valid = false;
   bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
+  int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
+  bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
   double* hx = nullptr;
   double* hk = nullptr;
@@ -368,6 +370,7 @@ int rebin(swrt_ctx* c) {
   std::swap(c->perm, c->perm2);
   c->steps_since_bin = 0;
   c->bin_valid = true;
+  c->cells_sorted = false;
   c->nbins = nbins;
   return SWRT_OK;
 }
@@ -383,6 +386,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   const unsigned grid = (unsigned)(t.ntx * t.ntx);
   t.next_keys = nullptr;
   t.next_counts = nullptr;
+  t.sort_cells = (c->cell_sort == 1 || !c->cells_sorted) ? 1 : 0;
   if (count_next && (int)grid == c->nbins) {
     HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * grid, c->stream));
     t.next_keys = c->keys;
@@ -414,6 +418,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   std::swap(c->dk, c->dk2);
   std::swap(c->perm, c->perm2);
   c->keys_fresh = t.next_keys != nullptr;
+  c->cells_sorted = true;  // written in (the input's or this launch's) cell order
   return SWRT_OK;
 }
 
@@ -850,6 +855,13 @@ int swrt_set_timing(swrt_ctx* c, int every) {
   return SWRT_OK;
 }
 
+int swrt_set_cell_sort(swrt_ctx* c, int every_launch) {
+  if (!c) return SWRT_ERR_ARG;
+  if (every_launch != 0 && every_launch != 1) return fail(c, SWRT_ERR_ARG, "every_launch must be 0 or 1");
+  c->cell_sort = every_launch;
+  return SWRT_OK;
+}
+
 int swrt_set_kernel(swrt_ctx* c, int variant) {
   if (!c) return SWRT_ERR_ARG;
   if (variant < 0 || variant > 3) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0..3");
@@ -1224,5 +1236,22 @@ int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches
   }
   return SWRT_OK;
 }
+
+#ifdef SWRT_PHASE_TIMING
+// diagnostic build only (not in include/swrt.h): copy out / clear the tile
+// kernel's per-workgroup phase stamps (8 u64 per tile).
+int swrt_debug_phases(unsigned long long* out, int ntiles, int clear) {
+  if (hipDeviceSynchronize() != hipSuccess) return SWRT_ERR_HIP;
+  const size_t bytes = (size_t)ntiles * 8 * sizeof(unsigned long long);
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(swrt::swrt_phase_dbg), bytes, 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return SWRT_ERR_HIP;
+  if (clear) {
+    static unsigned long long zeros[16384 * 8];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(swrt::swrt_phase_dbg), zeros, sizeof(zeros), 0, hipMemcpyHostToDevice) != hipSuccess)
+      return SWRT_ERR_HIP;
+  }
+  return SWRT_OK;
+}
+#endif
 
 }  // extern "C"

@@ -23,44 +23,9 @@
 
 namespace swrt {
 
-template <int T, int M>
-struct PersistGeom {
-  static constexpr int W = T + 5 + 2 * M;
-  static constexpr int WN = W * W;
-  static constexpr int WNP = (WN + 63) / 64 * 64;  // whole wavefronts per chunk (DMA lanes)
-};
-
-// Stage tile (ox, oy)'s window for `nch` chunks into buf (chunk-major, WNP
-// nodes per chunk) by LDS-DMA: wave w, chunk c covers nodes e0..e0+63 with
-// destination buf[c*WNP + e0] + lane*16 (lane-linear, as the DMA requires).
-template <bool TWO, int T, int M>
-__device__ __forceinline__ void stage_window_dma(const StepArgs& a, int ox, int oy, double2* buf) {
-  using G = PersistGeom<T, M>;
-  constexpr int NCH = TWO ? 6 : 3;
-  const int nx = a.f0.nx, npad = a.f0.npad;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nwaves = blockDim.x >> 6;
-  constexpr int NJOBS = NCH * (G::WNP / 64);
-  for (int job = wave; job < NJOBS; job += nwaves) {
-    const int c = job / (G::WNP / 64);
-    const int e0 = (job % (G::WNP / 64)) * 64;
-    int e = e0 + lane;
-    if (e >= G::WN) e = G::WN - 1;  // padding lanes re-read a valid node
-    const int wi = e / G::W, wj = e % G::W;
-    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
-    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
-    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec + 2 * (c % 3);
-    const double* base = (c < 3) ? a.f0.nodes : a.f1.nodes;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + src),
-                                     (__attribute__((address_space(3))) void*)(buf + c * G::WNP + e0),
-                                     16, 0, 0);
-  }
-}
-
 template <bool TWO, int T, int M, int NT>
 __global__ void __launch_bounds__(NT, 1) tile_persist_kernel(TileArgs ta, int tiles_per_wg) {
-  using G = PersistGeom<T, M>;
+  using G = WinGeom<T, M>;
   constexpr int W = G::W;
   constexpr int WNP = G::WNP;
   constexpr int NCH = TWO ? 6 : 3;

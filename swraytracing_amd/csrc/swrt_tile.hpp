@@ -7,9 +7,11 @@
 //      two snapshots into LDS (chunk-major: chunk c of node e at
 //      lds[c*WN + e], 16 B each, so lanes reading neighbouring nodes hit
 //      different LDS banks);
-//   2. it counting-sorts the tile's packets by their cell inside the tile
-//      (LDS histogram + scan) so that the 16-lane groups of a ds_read_b128
-//      read equal (broadcast) or adjacent nodes;
+//   2. on the first launch after a re-binning it counting-sorts the tile's
+//      packets by their cell inside the tile (LDS histogram + scan) so that
+//      the 16-lane groups of a ds_read_b128 read equal (broadcast) or
+//      adjacent nodes; later launches find them in that order already (each
+//      launch writes its outputs in the order it processed them);
 //   3. each lane advances one packet: the 36-tap gathers come from LDS, or —
 //      for a packet that drifted beyond the margin since the last re-binning —
 //      from the global node array (same arithmetic, same result);
@@ -34,6 +36,8 @@ struct TileArgs {
   int ntx;               // tiles per side
   int* next_keys;        // non-NULL: write each output packet's tile (next binning) ...
   int* next_counts;      // ... and add it to the per-tile counts (zeroed by the host)
+  int sort_cells;        // 1: counting-sort each tile's packets by cell first; 0: the input
+                         // is already in cell order (written so by the previous launch)
 };
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
@@ -42,6 +46,41 @@ __device__ __forceinline__ int ring_diff(int a, int b, int n) {
   if (d >= n / 2) d -= n;
   if (d < -n / 2) d += n;
   return d;
+}
+
+template <int T, int M>
+struct WinGeom {
+  static constexpr int W = T + 5 + 2 * M;
+  static constexpr int WN = W * W;
+  static constexpr int WNP = (WN + 63) / 64 * 64;  // whole wavefronts per chunk (DMA lanes)
+};
+
+// Stage tile (ox, oy)'s window for `nch` chunks into buf (chunk-major, WNP
+// nodes per chunk) by LDS-DMA: wave w, chunk c covers nodes e0..e0+63 with
+// destination buf[c*WNP + e0] + lane*16 (lane-linear, as the DMA requires).
+template <bool TWO, int T, int M>
+__device__ __forceinline__ void stage_window_dma(const StepArgs& a, int ox, int oy, double2* buf) {
+  using G = WinGeom<T, M>;
+  constexpr int NCH = TWO ? 6 : 3;
+  const int nx = a.f0.nx, npad = a.f0.npad;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwaves = blockDim.x >> 6;
+  constexpr int NJOBS = NCH * (G::WNP / 64);
+  for (int job = wave; job < NJOBS; job += nwaves) {
+    const int c = job / (G::WNP / 64);
+    const int e0 = (job % (G::WNP / 64)) * 64;
+    int e = e0 + lane;
+    if (e >= G::WN) e = G::WN - 1;  // padding lanes re-read a valid node
+    const int wi = e / G::W, wj = e % G::W;
+    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
+    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
+    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec + 2 * (c % 3);
+    const double* base = (c < 3) ? a.f0.nodes : a.f1.nodes;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + src),
+                                     (__attribute__((address_space(3))) void*)(buf + c * G::WNP + e0),
+                                     16, 0, 0);
+  }
 }
 
 template <bool TWO, int W, int WN>
@@ -70,6 +109,20 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
   }
 }
 
+#ifdef SWRT_PHASE_TIMING
+// diagnostic build only: per-workgroup wall-clock stamps (100 MHz) of the
+// phases, read back by swrt_debug_phases; never compiled into the product.
+__device__ unsigned long long swrt_phase_dbg[16384 * 8];
+#define SWRT_STAMP(slot)                                                            \
+  do {                                                                              \
+    if (tid == 0) swrt_phase_dbg[tile * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define SWRT_STAMP(slot) \
+  do {                   \
+  } while (0)
+#endif
+
 #ifndef SWRT_TILE_MIN_WAVES
 #define SWRT_TILE_MIN_WAVES 4
 #endif
@@ -78,10 +131,11 @@ template <bool TWO, int T, int M, int NT>
 __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
   constexpr int WN = W * W;
+  constexpr int WNP = WN;           // nodes per chunk
   constexpr int NCH = TWO ? 6 : 3;  // 16-B chunks per node
   constexpr int NB = T * T + 1;     // in-tile cell bins + "elsewhere"
   constexpr int MAXB = 2 * NT;      // packets sorted per batch
-  __shared__ double2 win[NCH * WN];
+  __shared__ double2 win[NCH * WNP];
   __shared__ int hist[NB];
   __shared__ int kr[MAXB];          // key << 16 | rank
   __shared__ int order[MAXB];
@@ -94,31 +148,49 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   const int nx = a.f0.nx, npad = a.f0.npad;
   const int ox = tx * T, oy = ty * T;  // tile origin (cells)
   if (tid < 9) nbr[tid] = 0;
+  SWRT_STAMP(0);
+#ifdef SWRT_PHASE_TIMING
+  if (tid == 0) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    swrt_phase_dbg[tile * 8 + 7] = ((unsigned long long)xcc << 32) | hw;
+    swrt_phase_dbg[tile * 8 + 6] = (unsigned long long)(ta.starts[tile + 1] - ta.starts[tile]);
+  }
+#endif
 
   // 1. stage the window: node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx
+  //    (register staging: each lane copies whole 48-B records, 3 or 6 loads
+  //    back to back; measured faster than LDS-DMA of the chunk-major image,
+  //    whose 16-B pieces are 48 B apart in HBM)
   for (int e = tid; e < WN; e += NT) {
     const int wi = e / W, wj = e % W;
     int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
     int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
     const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec;
     const double2* s0 = reinterpret_cast<const double2*>(a.f0.nodes + src);
-    win[0 * WN + e] = s0[0];
-    win[1 * WN + e] = s0[1];
-    win[2 * WN + e] = s0[2];
+    win[0 * WNP + e] = s0[0];
+    win[1 * WNP + e] = s0[1];
+    win[2 * WNP + e] = s0[2];
     if constexpr (TWO) {
       const double2* s1 = reinterpret_cast<const double2*>(a.f1.nodes + src);
-      win[3 * WN + e] = s1[0];
-      win[4 * WN + e] = s1[1];
-      win[5 * WN + e] = s1[2];
+      win[3 * WNP + e] = s1[0];
+      win[4 * WNP + e] = s1[1];
+      win[5 * WNP + e] = s1[2];
     }
   }
-
   const int pbeg = ta.starts[tile], pend = ta.starts[tile + 1];
+  if (!ta.sort_cells) {
+    __syncthreads();  // publish the window
+    SWRT_STAMP(1);
+  }
   for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
     const int nb = min(MAXB, pend - b0);
+    if (ta.sort_cells) {
     // 2. in-tile counting sort by the cell of the current position
     for (int h = tid; h < NB; h += NT) hist[h] = 0;
     __syncthreads();  // (also publishes the window on the first batch)
+    if (b0 == pbeg) SWRT_STAMP(1);
     for (int i = tid; i < nb; i += NT) {
       const int64_t p = b0 + i;
       double fa;
@@ -165,10 +237,12 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
 #endif
     }
     __syncthreads();
+    }  // sort_cells
+    if (b0 == pbeg) SWRT_STAMP(2);
 
     // 3. advance the packets in sorted order
     for (int r = tid; r < nb; r += NT) {
-      const int64_t pi = b0 + order[r];
+      const int64_t pi = b0 + (ta.sort_cells ? order[r] : r);
       const int64_t po = b0 + r;
       double x0 = a.x[pi], y0 = a.x[a.n + pi];
       double k0 = a.k[pi], l0 = a.k[a.n + pi];
@@ -189,7 +263,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         } else
 #endif
         if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M) {
-          gather6_lds<TWO, W, WN>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
+          gather6_lds<TWO, W, WNP>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
         } else {
           gather6<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
         }
@@ -241,6 +315,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       }
     }
     __syncthreads();  // LDS sort arrays are reused by the next batch
+    if (b0 == pbeg) SWRT_STAMP(3);
   }
   if (ta.next_keys != nullptr) {
     __syncthreads();
@@ -250,6 +325,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       atomicAdd(&ta.next_counts[gx * n_ + gy], nbr[tid]);
     }
   }
+  SWRT_STAMP(4);
 }
 
 }  // namespace swrt

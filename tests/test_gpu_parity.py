@@ -367,10 +367,10 @@ def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, til
     np.testing.assert_array_equal(hkg, hko)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant,cell_sort", [(1, 0), (2, 0), (2, 1), (3, 0)])
 @pytest.mark.parametrize("nslots", [1, 2])
 @pytest.mark.parametrize("dt_scale", [1.0, 40.0])
-def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, nslots, dt_scale):
+def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, nslots, dt_scale):
     """Per-packet (1), LDS-tiled (2) and persistent LDS-tiled (3) kernels give
     the oracle's bits; the large-dt case drives packets out of the LDS window
     (global fallback)."""
@@ -382,11 +382,13 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, nslots, dt_
     ctx.set_field_grid(1, p1, nx, L, 2 * nx)
     dt = c["dt"] * dt_scale
     ctx.set_kernel(variant)
+    ctx.set_cell_sort(cell_sort)
     ctx.set_locality(5, 0)
     try:
         xg, kg, hxg, hkg = ctx.leapfrog(c["x"], c["k"], dt, 12, c["f"], 1.0, nslots=nslots, alpha0=0.1,
                                         dalpha=0.07, bump=orc.BUMP_QG, save_every=3)
     finally:
+        ctx.set_cell_sort(0)
         ctx.set_kernel(0)
         ctx.set_locality(4, 0)
     xo, ko, hxo, hko = oracle_lib.leapfrog(p0, p1 if nslots == 2 else None, 0.1, 0.07, nx, 2 * nx, L / nx,
@@ -458,6 +460,40 @@ def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
         ctx.set_kernel(0)
         ctx.set_locality(4, 0)
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.2, 0.05, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, c["dt"], 9,
+                                       c["f"], 1.0)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
+
+
+@pytest.mark.parametrize("variant,cell_sort", [(2, 0), (2, 1), (3, 0)])
+def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_sort):
+    """One advance call per step (the bench's pattern): with re-binning every
+    4 steps, 3 of 4 launches read packets in the cell order the previous
+    launch wrote (no in-tile sort); every packet stays bit-identical."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    p0 = _planes(c["flow"])
+    p1 = _planes({n: np.asarray(v) * 1.1 for n, v in c["flow"].items()})
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    rng = np.random.default_rng(5)
+    N = 6000
+    x = (rng.random((N, 2)) - 0.5) * L
+    th = rng.random(N) * 2 * np.pi
+    k = 3.0 * np.stack([np.cos(th), np.sin(th)], axis=1)
+    a0, da, nst = 0.05, 0.09, 11
+    ctx.set_kernel(variant)
+    ctx.set_cell_sort(cell_sort)
+    ctx.set_locality(4, 0)
+    try:
+        ctx.packets_set(x, k)
+        for s in range(nst):
+            ctx.advance(c["dt"] * 3, 1, c["f"], 1.0, nslots=2, alpha0=a0 + s * da, dalpha=da, bump=orc.BUMP_QG)
+        xg, kg = ctx.packets_get()
+    finally:
+        ctx.set_cell_sort(0)
+        ctx.set_kernel(0)
+    xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, a0, da, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, c["dt"] * 3, nst,
                                        c["f"], 1.0)
     np.testing.assert_array_equal(xg, xo)
     np.testing.assert_array_equal(kg, ko)

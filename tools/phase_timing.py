@@ -1,0 +1,102 @@
+"""Diagnostic: per-workgroup phase timeline of the tile kernel.
+
+Needs a -DSWRT_PHASE_TIMING build (tools/sweep builds it as
+build/variants/phase.so) passed through SWRT_LIB_PATH.  Runs the bench
+workload, then for a few single steps reads the per-tile stamps
+(s_memrealtime, 100 MHz) and prints phase shares, per-CU residency and the
+spread of workgroup start times.  Read SHARES, not absolute time: the stamp
+build's barriers-plus-stamps differ from the product kernel."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+import torch  # noqa: F401
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import swraytracing_amd as sw  # noqa: E402
+from swraytracing_amd import _lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nx", type=int, default=512)
+    ap.add_argument("--packets", type=int, default=1_000_000)
+    ap.add_argument("--mode", default="blend")
+    ap.add_argument("--samples", type=int, default=5)
+    args = ap.parse_args()
+    args.world, args.rank, args.seed = 1, 0, 146
+    lib = _lib.load()
+    f = lib.swrt_debug_phases
+    f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.c_int]
+    ctx = sw.Context(0)
+    ctx.set_locality(4, 0)
+    ctx.set_kernel(2)
+    rng = np.random.default_rng(146)
+    w = bench.build_workload(ctx, args, rng)
+    ctx.packets_set(w["x"], w["k"])
+    for _ in range(8):
+        bench.step(ctx, w, 1)
+    ntiles = (args.nx // 16) ** 2
+    buf = np.zeros(ntiles * 8, dtype=np.uint64)
+    ptr = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))
+    res = []
+    for s in range(args.samples):
+        assert f(None, ntiles, 1) == 0
+        bench.step(ctx, w, 1)
+        ctx.synchronize()
+        assert f(ptr, ntiles, 0) == 0
+        d = buf.reshape(ntiles, 8).astype(np.int64)
+        t0 = d[:, 0].min()
+        P = (d[:, :5] - t0) * 10.0 / 1e3  # us
+        stage = P[:, 1] - P[:, 0]
+        sort = P[:, 2] - P[:, 1]
+        comp = P[:, 3] - P[:, 2]
+        tail = P[:, 4] - P[:, 3]
+        life = P[:, 4] - P[:, 0]
+        span = P[:, 4].max()
+        hw = d[:, 7] & 0xFFFFFFFF
+        xcc = d[:, 7] >> 32
+        cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+        ucu = np.unique(cu)
+        per_cu = np.array([np.sum(cu == c) for c in ucu])
+        # busy fraction of each CU: union of its workgroups' lifetimes / span
+        busy = []
+        for c in ucu:
+            iv = sorted(zip(P[cu == c, 0], P[cu == c, 4]))
+            tot, cur_s, cur_e = 0.0, None, None
+            for a_, b_ in iv:
+                if cur_e is None or a_ > cur_e:
+                    if cur_e is not None:
+                        tot += cur_e - cur_s
+                    cur_s, cur_e = a_, b_
+                else:
+                    cur_e = max(cur_e, b_)
+            tot += cur_e - cur_s
+            busy.append(tot / span)
+        res.append(dict(
+            span_us=float(span),
+            wg_life_us_median=float(np.median(life)),
+            share_stage=float(stage.sum() / life.sum()), share_sort=float(sort.sum() / life.sum()),
+            share_compute=float(comp.sum() / life.sum()), share_tail=float(tail.sum() / life.sum()),
+            stage_us_median=float(np.median(stage)), sort_us_median=float(np.median(sort)),
+            compute_us_median=float(np.median(comp)), tail_us_median=float(np.median(tail)),
+            compute_us_p90=float(np.percentile(comp, 90)),
+            start_us_p50=float(np.median(P[:, 0])), start_us_max=float(P[:, 0].max()),
+            end_us_min=float(P[:, 4].min()),
+            cus=int(len(ucu)), wg_per_cu_min=int(per_cu.min()), wg_per_cu_max=int(per_cu.max()),
+            cu_busy_mean=float(np.mean(busy)), cu_busy_min=float(np.min(busy)),
+            packets_per_tile_mean=float(d[:, 6].mean()), packets_per_tile_max=int(d[:, 6].max()),
+            mean_concurrent_wg=float(life.sum() / span),
+        ))
+    print(json.dumps(res[-1], indent=1))
+    print(json.dumps({"span_us_all": [r["span_us"] for r in res]}))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
