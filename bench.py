@@ -115,7 +115,9 @@ def cpu_baseline(ctx, w, target_s):
     n = min(20000, w["x"].shape[0])
     run(n, 1)  # warm-up: OpenMP thread start, page faults
     t = run(n, 4)
-    rate = 4 * n / max(t, 1e-9)
+    s1 = max(4, int(1.0 * 4 / max(t, 1e-9)))  # ~1 s calibration run
+    t = run(n, s1)
+    rate = s1 * n / max(t, 1e-9)
     steps = max(1, int(target_s * rate / n))
     t = run(n, steps)
     return {"value": n * steps / t, "unit": "packet-steps/s", "cores": int(threads), "kind": "port",
