@@ -210,6 +210,58 @@ int swrt_omega_histogram(swrt_ctx* ctx, double f, double Cg, const double* edges
                          int64_t* counts_inout, double* mean_omega_out);
 
 /* ---------------------------------------------------------------------------
+ * QG PDE stepper: the snapshots' producer, device-resident
+ * ------------------------------------------------------------------------ */
+
+/* Parameters of the two drivers' PDEs.  nlayers = 1: qgsw_raytrace.m
+ * (L = 2*pi, integer wavenumbers; update :270-286 with beta, r_drag and the
+ * inertial_ring forcing :216-220; filter :222-230 when filter = 1).
+ * nlayers = 2: qg2layersw_raytrace.m (wavenumbers scaled by 2*pi/L; B
+ * inversion, factor_L with shear, nu*K2^hyper_order + r diffusion and beta
+ * :129-144). */
+typedef struct swrt_qg_params {
+  int nlayers;
+  int filter;
+  double L;
+  double K_d2;
+  double beta;
+  double r_drag;
+  double force_strength;
+  double f;
+  double Cg;
+  double shear;
+  double nu;
+  double hyper_order;
+  double r;
+} swrt_qg_params;
+
+/* Load the initial spectral PV qk (nlayers blocks of the (2kmax+1) x (kmax+1)
+ * g2k half plane, interleaved complex, column-major) and reset the AB3
+ * history (qgsw_raytrace.m:111-112, qg2layersw_raytrace.m:120-121). */
+int swrt_qg_init(swrt_ctx* ctx, const swrt_qg_params* params, int64_t nx, const double* qk_interleaved);
+/* nsteps PDE steps of size dt: AB3 (forward Euler, AB2 for the first two
+ * steps), 1 layer: qgsw_raytrace.m:121-137; 2 layers: qg2layersw_raytrace.m
+ * :167-181 with expLdt/expL2dt recomputed on the device whenever dt changes.
+ * Before each step the previous qk is kept (prev_qk, :122 / :167). */
+int swrt_qg_step(swrt_ctx* ctx, double dt, int64_t nsteps);
+/* U0 = sqrt(max((u + shear)^2 + v^2)) over every layer of grid_U(qk)
+ * (qg2layersw_raytrace.m:156-158; qgsw_raytrace.m:63-65 with shear 0). */
+int swrt_qg_max_speed(swrt_ctx* ctx, double* U0_out);
+/* Copy out qk (same layout as swrt_qg_init), the model time and step count. */
+int swrt_qg_get(swrt_ctx* ctx, double* qk_out, double* t_out, int64_t* steps_out);
+/* q = k2g(qk) per layer: nx x nx x nlayers column-major (pv.bin frames,
+ * qgsw_raytrace.m:167-170). */
+int swrt_qg_get_q(swrt_ctx* ctx, double* q_out);
+/* grid_U of the current (which = 0) or previous (which = 1) qk of one layer
+ * straight into packet field slot `slot` (qgsw_raytrace.m:141-142,
+ * qg2layersw_raytrace.m:187-188: layer 1, u += shear_strength), no host copy.
+ * ny_period as in swrt_set_field_grid (0 = nx). */
+int swrt_qg_snapshot(swrt_ctx* ctx, int slot, int which, int layer, int64_t ny_period);
+/* Exchange two packet field slots (the previous step's "current" snapshot
+ * becomes the next step's "previous" one without recomputing it). */
+int swrt_swap_slots(swrt_ctx* ctx, int a, int b);
+
+/* ---------------------------------------------------------------------------
  * Runtime helpers
  * ------------------------------------------------------------------------ */
 int swrt_synchronize(swrt_ctx* ctx);

@@ -686,3 +686,201 @@ def modes_from_halfplane(fk, k_scale=1.0):
 def modes_from_amp_phase(amp, phase, n):
     """fourier_interpolate_test.m:116-123 field: C = amp .* exp(1i*phase), K, L in -n..n."""
     return np.asarray(amp) * np.exp(1j * np.asarray(phase)), -n, -n, 1.0
+
+
+# ----------------------------------------------------------------------------
+# QG PDE steppers — the step BEFORE the packet path (SURVEY §8f row 1)
+#   1-layer: qg_flow_ray_trace/qgsw_raytrace.m:111-137 (AB3 + filter),
+#            update :270-286, inertial_ring :216-220, filter :222-230
+#   2-layer: qg_flow_ray_trace/qg2layersw_raytrace.m:129-181 (exponential
+#            AB3, adaptive CFL), update :309-323, mmult3 :333-338,
+#            diag_exp :340-343
+# ----------------------------------------------------------------------------
+def inertial_ring(force_strength, K2, f, Cg):
+    """qgsw_raytrace.m:216-220."""
+    omega = np.sqrt(f**2 + Cg**2 * K2)
+    forces = np.zeros(K2.shape)
+    forces[(0.9 * f < omega) & (omega < 1.1 * f)] = force_strength
+    return forces
+
+
+def qg_filter(kx_, ky_, dx):
+    """qgsw_raytrace.m:222-230 (exponential cutoff filter above kc = 0.75 pi)."""
+    Ef = np.ones(kx_.shape)
+    kstar = np.sqrt((kx_ * dx) ** 2 + (ky_ * dx) ** 2)
+    kc = 0.75 * np.pi
+    const = np.log(1e-15) / (0.25 * np.pi) ** 4
+    result = np.exp(const * (kstar - kc) ** 4)
+    sel = kstar >= kc
+    Ef[sel] = result[sel]
+    return Ef
+
+
+def _jacobian_term(psik, qk, kx_, ky_):
+    """J = psix.*qy - psiy.*qx on the grid (update at qgsw_raytrace.m:271-282 /
+    qg2layersw_raytrace.m:311-321), one layer."""
+    psix = k2g(1j * kx_ * psik)
+    psiy = k2g(1j * ky_ * psik)
+    qx = k2g(1j * kx_ * qk)
+    qy = k2g(1j * ky_ * qk)
+    return psix * qy - psiy * qx
+
+
+def qg1_update(qk, K2, K_d2, beta, r_drag, surface_forces, kx_, ky_):
+    """qgsw_raytrace.m:270-286 (including its r_drag*K2 and surface_forces terms
+    exactly as written)."""
+    psik = -qk / (K_d2 + K2)
+    psikx = 1j * kx_ * psik
+    J = _jacobian_term(psik, qk, kx_, ky_)
+    return g2k(J) - beta * psikx + r_drag * K2 + surface_forces
+
+
+class QG1Oracle:
+    """qgsw_raytrace.m:111-137: AB3 (Euler, AB2 start) then the filter."""
+
+    def __init__(self, qk, nx, K_d2, beta=0.0, r_drag=0.1, force_strength=0.1, f=3.0, Cg=1.0,
+                 use_filter=True):
+        self.kx, self.ky, self.K2 = wavenumber_grids(nx)
+        self.nx = nx
+        self.dx = 2 * np.pi / nx
+        self.qk = np.array(qk, dtype=np.complex128)
+        self.K_d2, self.beta, self.r_drag = K_d2, beta, r_drag
+        self.forces = inertial_ring(force_strength, self.K2, f, Cg)
+        self.Ef = qg_filter(self.kx, self.ky, self.dx) if use_filter else np.ones(self.K2.shape)
+        self.Qm = [np.zeros_like(self.qk), np.zeros_like(self.qk)]
+        self.step_no = 0
+        self.t = 0.0
+
+    def step(self, dt):
+        self.step_no += 1
+        Qn = qg1_update(self.qk, self.K2, self.K_d2, self.beta, self.r_drag, self.forces, self.kx, self.ky)
+        if self.step_no == 1:
+            dq = dt * Qn
+        elif self.step_no == 2:
+            dq = dt / 2 * (3 * Qn - self.Qm[0])
+        else:
+            dq = dt / 12 * (23 * Qn - 16 * self.Qm[0] + 5 * self.Qm[1])
+        self.t = self.t + dt
+        self.Qm[1] = self.Qm[0]
+        self.Qm[0] = Qn
+        self.qk = self.qk + dq
+        self.qk = self.Ef * self.qk
+
+
+def mmult3(A, x):
+    """qg2layersw_raytrace.m:333-338: y(:,:,i) = A(i,1).*x(:,:,1) + A(i,2).*x(:,:,2).
+    A: (2, 2, nkx, nky), x: (nkx, nky, 2)."""
+    y = np.zeros(x.shape, dtype=np.complex128)
+    for i in range(2):
+        y[:, :, i] = A[i, 0] * x[:, :, 0] + A[i, 1] * x[:, :, 1]
+    return y
+
+
+def qg2_operators(nx, L, K_d2, beta, shear_strength, nu, alpha, r):
+    """qg2layersw_raytrace.m:129-147: B (PV inversion), factor_L and its
+    eigen-decomposition (pageeig / pageinv)."""
+    kx_, ky_, K2 = wavenumber_grids(nx, L, scale=True)
+    F = K_d2 / 2
+    B = np.zeros((2, 2) + K2.shape)
+    B[0, 0] = -F - K2
+    B[0, 1] = -F
+    B[1, 0] = -F
+    B[1, 1] = -F - K2
+    detB = K2 * (K2 + 2 * F)
+    detB[K2 == 0] = np.inf
+    B = B / detB
+    diffusion_factor = (nu * K2**alpha + r) * K2 - 1j * kx_ * beta
+    diffusion_terms = B * diffusion_factor
+    shear_factor = 1j * kx_ * shear_strength
+    # pagemtimes([-1,0;0,1], eye(2) + 2*F*B)
+    IB = np.zeros((2, 2) + K2.shape)
+    IB[0, 0] = 1 + 2 * F * B[0, 0]
+    IB[0, 1] = 2 * F * B[0, 1]
+    IB[1, 0] = 2 * F * B[1, 0]
+    IB[1, 1] = 1 + 2 * F * B[1, 1]
+    S = np.array([[-1.0, 0.0], [0.0, 1.0]])
+    MF = np.einsum("ij,jk...->ik...", S, IB)
+    factor_L = shear_factor * MF + diffusion_terms
+    Lp = np.moveaxis(factor_L, (0, 1), (-2, -1))  # pages last
+    LD, LV = np.linalg.eig(Lp)
+    LV1 = np.linalg.inv(LV)
+    return dict(kx=kx_, ky=ky_, K2=K2, B=B, factor_L=factor_L, LD=LD, LV=LV, LV1=LV1)
+
+
+def qg2_expL(ops, dt):
+    """LV * diag(exp(dt*LD)) * LV^-1 per wavenumber (qg2layersw_raytrace.m:148,
+    diag_exp :340-343), as (2, 2, nkx, nky)."""
+    E = ops["LV"] * np.exp(dt * ops["LD"])[..., None, :]
+    M = E @ ops["LV1"]
+    return np.moveaxis(M, (-2, -1), (0, 1))
+
+
+def qg2_update(qk, B, kx_, ky_):
+    """qg2layersw_raytrace.m:309-323."""
+    psik = mmult3(B, qk)
+    dq = np.zeros_like(qk)
+    for i in range(2):
+        dq[:, :, i] = g2k(_jacobian_term(psik[:, :, i], qk[:, :, i], kx_, ky_))
+    return dq
+
+
+class QG2Oracle:
+    """qg2layersw_raytrace.m:129-181: exponential AB3 with the adaptive CFL rule
+    of :156-165 (grid_U of both layers, u += shear_strength)."""
+
+    def __init__(self, qk, nx, L, K_d2, beta=0.0, shear_strength=0.5, nu=None, alpha=4, r=0.4,
+                 nutune=0.1, cfl_fraction=0.25):
+        self.nx, self.L = nx, L
+        self.dx = L / nx
+        self.K_d2, self.shear = K_d2, shear_strength
+        self.nu = nutune * self.dx ** (2 * alpha) if nu is None else nu
+        self.ops = qg2_operators(nx, L, K_d2, beta, shear_strength, self.nu, alpha, r)
+        self.qk = np.array(qk, dtype=np.complex128)
+        self.cfl = cfl_fraction
+        self.U0 = self.max_speed()
+        self.dt = cfl_fraction * self.dx / self.U0  # qg2layersw_raytrace.m:78
+        self.exps(self.dt)
+        self.Qm = [np.zeros_like(self.qk), np.zeros_like(self.qk)]
+        self.step_no = 0
+        self.t = 0.0
+
+    def exps(self, dt):
+        self.expLdt = qg2_expL(self.ops, dt)
+        self.expL2dt = qg2_expL(self.ops, 2 * dt)
+
+    def max_speed(self):
+        o = self.ops
+        flow = grid_U(self.qk, self.K_d2, o["K2"], o["kx"], o["ky"], self.shear)
+        return float(np.sqrt((flow["u"] ** 2 + flow["v"] ** 2).max()))
+
+    def cfl_check(self):
+        """qg2layersw_raytrace.m:156-165; returns True when dt changed."""
+        self.U0 = self.max_speed()
+        cond = self.cfl * self.dx / self.U0
+        if cond < self.dt or self.dt < cond / 4:
+            self.dt = self.cfl / 2 * self.dx / self.U0
+            self.exps(self.dt)
+            return True
+        return False
+
+    def step(self, dt=None):
+        """One step; dt=None applies the adaptive CFL rule first (the driver),
+        an explicit dt skips it (fixed-step use)."""
+        if dt is None:
+            self.cfl_check()
+        elif dt != self.dt:
+            self.dt = dt
+            self.exps(dt)
+        dt = self.dt
+        self.step_no += 1
+        Qn = qg2_update(self.qk, self.ops["B"], self.ops["kx"], self.ops["ky"])
+        if self.step_no == 1:
+            dq = dt * Qn
+        elif self.step_no == 2:
+            dq = dt / 2 * (3 * Qn - mmult3(self.expLdt, self.Qm[0]))
+        else:
+            dq = dt / 12 * (23 * Qn - 16 * mmult3(self.expLdt, self.Qm[0]) + 5 * mmult3(self.expL2dt, self.Qm[1]))
+        self.t = self.t + dt
+        self.Qm[1] = self.Qm[0]
+        self.Qm[0] = Qn
+        self.qk = mmult3(self.expLdt, self.qk + dq)

@@ -34,6 +34,13 @@ _INT = ctypes.c_int
 _P = ctypes.POINTER(ctypes.c_double)
 _VP = ctypes.c_void_p
 
+class QGParams(ctypes.Structure):
+    """swrt_qg_params (include/swrt.h)."""
+    _fields_ = [("nlayers", ctypes.c_int), ("filter", ctypes.c_int), ("L", _D), ("K_d2", _D), ("beta", _D),
+                ("r_drag", _D), ("force_strength", _D), ("f", _D), ("Cg", _D), ("shear", _D), ("nu", _D),
+                ("hyper_order", _D), ("r", _D)]
+
+
 # name -> (restype, argtypes).  Kept in the order of include/swrt.h.
 SIGNATURES = {
     "swrt_version": (_INT, []),
@@ -66,6 +73,13 @@ SIGNATURES = {
     "swrt_spectral_eval": (_INT, [_VP, _P, _P, _I, _INT, _P]),
     "swrt_spectral_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT]),
     "swrt_omega_histogram": (_INT, [_VP, _D, _D, _P, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_D)]),
+    "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
+    "swrt_qg_step": (_INT, [_VP, _D, _I]),
+    "swrt_qg_max_speed": (_INT, [_VP, ctypes.POINTER(_D)]),
+    "swrt_qg_get": (_INT, [_VP, _P, ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int64)]),
+    "swrt_qg_get_q": (_INT, [_VP, _P]),
+    "swrt_qg_snapshot": (_INT, [_VP, _INT, _INT, _INT, _I]),
+    "swrt_swap_slots": (_INT, [_VP, _INT, _INT]),
     "swrt_synchronize": (_INT, [_VP]),
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
@@ -314,6 +328,50 @@ class Context:
                                                counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                                                ctypes.byref(mean)), "swrt_omega_histogram")
         return counts, mean.value
+
+    # ---- QG PDE stepper (swrt_qg_*) ---------------------------------------
+    def qg_init(self, params: QGParams, nx, qk):
+        """qk: (2kmax+1, kmax+1) complex, or (2kmax+1, kmax+1, nlayers)."""
+        qk = np.asarray(qk, dtype=np.complex128)
+        if qk.ndim == 2:
+            qk = qk[:, :, None]
+        kmax = nx // 2 - 1
+        assert qk.shape == (2 * kmax + 1, kmax + 1, params.nlayers), qk.shape
+        buf = _f64(np.asfortranarray(qk).ravel(order="F").view(np.float64))
+        self._qg_shape = (2 * kmax + 1, kmax + 1, params.nlayers)
+        self._qg_nx = nx
+        self._chk(self._L.swrt_qg_init(self._h, ctypes.byref(params), nx, _p(buf)), "swrt_qg_init")
+
+    def qg_step(self, dt, nsteps=1):
+        self._chk(self._L.swrt_qg_step(self._h, float(dt), int(nsteps)), "swrt_qg_step")
+
+    def qg_max_speed(self):
+        u = _D()
+        self._chk(self._L.swrt_qg_max_speed(self._h, ctypes.byref(u)), "swrt_qg_max_speed")
+        return u.value
+
+    def qg_get(self):
+        """-> (qk (2kmax+1, kmax+1, nlayers) complex, t, steps)."""
+        out = np.empty(2 * int(np.prod(self._qg_shape)))
+        t = _D()
+        s = ctypes.c_int64()
+        self._chk(self._L.swrt_qg_get(self._h, _p(out), ctypes.byref(t), ctypes.byref(s)), "swrt_qg_get")
+        qk = out.view(np.complex128).reshape(self._qg_shape, order="F")
+        return qk, t.value, s.value
+
+    def qg_get_q(self):
+        """-> q grid (nx, nx, nlayers), column-major per layer (k2g of each layer)."""
+        nx, nl = self._qg_nx, self._qg_shape[2]
+        out = np.empty(nx * nx * nl)
+        self._chk(self._L.swrt_qg_get_q(self._h, _p(out)), "swrt_qg_get_q")
+        return out.reshape((nx, nx, nl), order="F")
+
+    def qg_snapshot(self, slot, which=0, layer=0, ny_period=0):
+        self._chk(self._L.swrt_qg_snapshot(self._h, int(slot), int(which), int(layer), int(ny_period)),
+                  "swrt_qg_snapshot")
+
+    def swap_slots(self, a=0, b=1):
+        self._chk(self._L.swrt_swap_slots(self._h, int(a), int(b)), "swrt_swap_slots")
 
     # ---- runtime ---------------------------------------------------------
     def synchronize(self):

@@ -20,6 +20,7 @@
 #include "swrt_kernels.hpp"
 #include "swrt_tile.hpp"
 #include "swrt_persist.hpp"
+#include "swrt_qg.hpp"
 #include "swrt_xka.hpp"
 #include "swrt_spectral.hpp"
 #include "swrt_diag.hpp"
@@ -51,6 +52,26 @@ struct Slot {
   double L = 0.0;
   bool set = false;
   bool has_psi = false;
+};
+
+// device-resident QG PDE state (swrt_qg.hpp)
+struct QGState {
+  bool init = false;
+  QGDev g{};
+  int64_t nhalf = 0, nn = 0;
+  double2* qk = nullptr;       // nl * nhalf
+  double2* qk_prev = nullptr;  // prev_qk of the last step
+  double2* Qm1 = nullptr;      // Qn_minus(:,:,1) / (:,:,:,1)
+  double2* Qm2 = nullptr;
+  double2* E1 = nullptr;       // expLdt  (2 layers): 4 per wavenumber
+  double2* E2 = nullptr;       // expL2dt
+  double2* Z = nullptr;        // max(2*nl, 3) * nn transform scratch
+  double2* T = nullptr;
+  unsigned long long* dmax = nullptr;
+  double exp_dt = -1.0;        // dt of the current E1/E2
+  int64_t steps = 0;
+  double t = 0.0;
+  bool has_prev = false;
 };
 
 struct Timing {
@@ -115,6 +136,7 @@ struct swrt_ctx {
   ModeGrid mg{};
   bool modes_set = false;
   int64_t mode_active = 0;  // coefficients inside the per-row nonzero spans
+  QGState qg;
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -513,6 +535,9 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->tw) (void)hipFree(c->tw);
   for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist, (void*)c->modes,
                   (void*)c->mode_rows})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->qg.qk, (void*)c->qg.qk_prev, (void*)c->qg.Qm1, (void*)c->qg.Qm2, (void*)c->qg.E1,
+                  (void*)c->qg.E2, (void*)c->qg.Z, (void*)c->qg.T, (void*)c->qg.dmax})
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -1234,6 +1259,206 @@ int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches
     c->timing.folded_ms = 0.0;
     c->timing.folded_n = 0;
   }
+  return SWRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// QG PDE stepper (swrt_qg.hpp)
+// ---------------------------------------------------------------------------
+int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double* qk_in) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!p || !qk_in) return fail(c, SWRT_ERR_ARG, "NULL argument");
+  if (p->nlayers != 1 && p->nlayers != 2) return fail(c, SWRT_ERR_ARG, "nlayers must be 1 or 2");
+  if (nx < 8 || nx > 4096 || !is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two, 8..4096");
+  if (!(p->L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
+  HIPCHK(c, hipSetDevice(c->device));
+  QGState& q = c->qg;
+  for (void* ptr : {(void*)q.qk, (void*)q.qk_prev, (void*)q.Qm1, (void*)q.Qm2, (void*)q.E1, (void*)q.E2,
+                    (void*)q.Z, (void*)q.T, (void*)q.dmax})
+    if (ptr) (void)hipFree(ptr);
+  q = QGState{};
+  const int n = (int)nx, kmax = n / 2 - 1;
+  q.nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
+  q.nn = nx * nx;
+  QGDev& g = q.g;
+  g.n = n;
+  g.nl = p->nlayers;
+  g.kscale = 2.0 * 3.14159265358979323846 / p->L;
+  if (p->nlayers == 1) g.kscale = 1.0;  // qgsw_raytrace.m:13-20: L = 2*pi, integer k
+  g.dx = p->L / (double)n;
+  g.K_d2 = p->K_d2;
+  g.beta = p->beta;
+  g.r_drag = p->r_drag;
+  g.force_strength = p->force_strength;
+  g.f = p->f;
+  g.Cg = p->Cg;
+  g.filter = p->filter;
+  g.shear = p->nlayers == 2 ? p->shear : 0.0;
+  g.nu = p->nu;
+  g.hyper = p->hyper_order;
+  g.r = p->r;
+  const size_t hb = sizeof(double2) * q.nhalf * g.nl;
+  const size_t zb = sizeof(double2) * q.nn * std::max(2 * g.nl, 3);
+  HIPCHK(c, hipMalloc(&q.qk, hb));
+  HIPCHK(c, hipMalloc(&q.qk_prev, hb));
+  HIPCHK(c, hipMalloc(&q.Qm1, hb));
+  HIPCHK(c, hipMalloc(&q.Qm2, hb));
+  HIPCHK(c, hipMalloc(&q.Z, zb));
+  HIPCHK(c, hipMalloc(&q.T, zb));
+  HIPCHK(c, hipMalloc(&q.dmax, sizeof(unsigned long long)));
+  if (g.nl == 2) {
+    HIPCHK(c, hipMalloc(&q.E1, sizeof(double2) * 4 * q.nhalf));
+    HIPCHK(c, hipMalloc(&q.E2, sizeof(double2) * 4 * q.nhalf));
+  }
+  HIPCHK(c, hipMemcpyAsync(q.qk, qk_in, hb, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemsetAsync(q.Qm1, 0, hb, c->stream));
+  HIPCHK(c, hipMemsetAsync(q.Qm2, 0, hb, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  q.init = true;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  QGState& q = c->qg;
+  if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (!(dt > 0) || nsteps < 0) return fail(c, SWRT_ERR_ARG, "dt must be > 0, nsteps >= 0");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  const int n = q.g.n, nl = q.g.nl;
+  if ((rc = ensure_twiddles(c, n))) return rc;
+  const size_t hb = sizeof(double2) * q.nhalf * nl;
+  for (int64_t s = 0; s < nsteps; ++s) {
+    HIPCHK(c, hipMemcpyAsync(q.qk_prev, q.qk, hb, hipMemcpyDeviceToDevice, c->stream));
+    hipLaunchKernelGGL(qg_jac_spectra_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = inverse_2d(c, q.Z, q.T, n, 2 * nl))) return rc;
+    double2* Zj = q.Z;  // J1 + i J2, grid layout (x contiguous)
+    hipLaunchKernelGGL(qg_jacobian_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.T, nl, q.nn, Zj);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = run_fft_pass(c, Zj, n, 1, 0))) return rc;   // along x
+    if ((rc = run_transpose(c, Zj, q.T, n, 1))) return rc;
+    if ((rc = run_fft_pass(c, q.T, n, 1, 0))) return rc;  // along y: [ky + n*kx]
+    if (nl == 2 && dt != q.exp_dt) {
+      hipLaunchKernelGGL(qg2_exp_kernel, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.g, dt, q.E1, q.E2);
+      HIPCHK(c, hipGetLastError());
+      q.exp_dt = dt;
+    }
+    const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
+    hipLaunchKernelGGL(qg_update_kernel, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
+                       abstep, q.E1, q.E2, q.qk, q.Qm1, q.Qm2);
+    HIPCHK(c, hipGetLastError());
+    q.steps += 1;
+    q.t = q.t + dt;
+    q.has_prev = true;
+  }
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_qg_max_speed(swrt_ctx* c, double* U0_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  QGState& q = c->qg;
+  if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (!U0_out) return fail(c, SWRT_ERR_ARG, "NULL output");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  const int n = q.g.n, nl = q.g.nl;
+  if ((rc = ensure_twiddles(c, n))) return rc;
+  hipLaunchKernelGGL(qg_vel_spectra_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = inverse_2d(c, q.Z, q.T, n, nl))) return rc;
+  HIPCHK(c, hipMemsetAsync(q.dmax, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(qg_max_speed2_kernel, dim3(256), dim3(256), 0, c->stream, q.T, q.nn * nl, q.g.shear, q.dmax);
+  HIPCHK(c, hipGetLastError());
+  unsigned long long bits = 0;
+  HIPCHK(c, hipMemcpyAsync(&bits, q.dmax, sizeof(bits), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  double s2;
+  std::memcpy(&s2, &bits, sizeof(s2));
+  *U0_out = std::sqrt(s2);
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_qg_get(swrt_ctx* c, double* qk_out, double* t_out, int64_t* steps_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  QGState& q = c->qg;
+  if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (qk_out)
+    HIPCHK(c, hipMemcpyAsync(qk_out, q.qk, sizeof(double2) * q.nhalf * q.g.nl, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (t_out) *t_out = q.t;
+  if (steps_out) *steps_out = q.steps;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_qg_get_q(swrt_ctx* c, double* q_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  QGState& q = c->qg;
+  if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (!q_out) return fail(c, SWRT_ERR_ARG, "NULL output");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  const int n = q.g.n, nl = q.g.nl;
+  if ((rc = ensure_twiddles(c, n))) return rc;
+  for (int l = 0; l < nl; ++l) {
+    hipLaunchKernelGGL(fulspec_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk + l * q.nhalf, n,
+                       q.Z + l * q.nn);
+    HIPCHK(c, hipGetLastError());
+  }
+  if ((rc = inverse_2d(c, q.Z, q.T, n, nl))) return rc;
+  double* planes = reinterpret_cast<double*>(q.Z);
+  hipLaunchKernelGGL(real_part_kernel, dim3(nblocks(q.nn * nl, 256)), dim3(256), 0, c->stream, q.T, planes,
+                     q.nn * nl);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(q_out, planes, sizeof(double) * q.nn * nl, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_period) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  QGState& q = c->qg;
+  if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (current) or 1 (previous)");
+  if (which == 1 && !q.has_prev) return fail(c, SWRT_ERR_STATE, "no previous qk before the first step");
+  if (layer < 0 || layer >= q.g.nl) return fail(c, SWRT_ERR_ARG, "layer out of range");
+  const int64_t nx = q.g.n;
+  int rc = check_slot_args(c, slot, nx);
+  if (rc) return rc;
+  if (ny_period == 0) ny_period = nx;
+  if (ny_period % nx) return fail(c, SWRT_ERR_ARG, "ny_period must be a multiple of nx");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_slot(c, slot, nx))) return rc;
+  if ((rc = ensure_twiddles(c, (int)nx))) return rc;
+  const double2* src = (which == 0 ? q.qk : q.qk_prev) + layer * q.nhalf;
+  if ((rc = fields_from_halfplane(c, slot, src, (int)nx, 1, q.g.K_d2, q.g.kscale, q.g.shear, 0, q.Z, q.T)))
+    return rc;
+  Slot& s = c->slot[slot];
+  s.L = q.g.dx * (double)nx;
+  s.ny_period = ny_period;
+  s.set = true;
+  c->keys_fresh = false;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_swap_slots(swrt_ctx* c, int a, int b) {
+  if (!c) return SWRT_ERR_ARG;
+  if (a < 0 || a >= SWRT_MAX_SLOTS || b < 0 || b >= SWRT_MAX_SLOTS) return fail(c, SWRT_ERR_ARG, "slot out of range");
+  std::swap(c->slot[a], c->slot[b]);
+  c->keys_fresh = false;
   return SWRT_OK;
 }
 

@@ -1,0 +1,352 @@
+// swrt_qg.hpp — the QG PDE steppers that produce the packets' background
+// snapshots, on the device.
+//
+//   1 layer:  qgsw_raytrace.m:111-137   AB3 (Euler / AB2 start) + filter,
+//             update :270-286, inertial_ring :216-220, filter :222-230.
+//   2 layers: qg2layersw_raytrace.m:129-181  exponential AB3 (expLdt,
+//             expL2dt = LV diag(exp(LD dt)) LV^-1 of factor_L), update
+//             :309-323, mmult3 :333-338; adaptive CFL :156-165 (host logic
+//             over swrt_qg_max_speed).
+//
+// State: qk, its two previous tendencies and the previous qk, each
+// nlayers x (2kmax+1) x (kmax+1) complex (the g2k half plane, column-major,
+// row = kx + kmax fastest), resident in HBM.  One step is
+//   spectra of psi_x + i psi_y and q_x + i q_y per layer (Hermitian
+//   completion = fulspec)  ->  inverse 2-D FFT  ->  J = psi_x q_y - psi_y q_x
+//   (both layers packed J1 + i J2 into one forward transform)  ->  g2k crop
+//   and the AB3 update fused in one pass over the half plane.
+// The Fourier transforms are the Stockham passes of swrt_fft.hpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "swrt_fft.hpp"
+
+namespace swrt {
+
+struct QGDev {
+  int n;          // grid size (power of two)
+  int nl;         // layers: 1 or 2
+  double kscale;  // 2*pi/L (1 for the 1-layer driver's L = 2*pi)
+  double dx;      // L / n
+  double K_d2;
+  double beta;
+  double r_drag;  // 1 layer: the r_drag*K2 term of update (qgsw_raytrace.m:285)
+  double force_strength, f, Cg;  // 1 layer: inertial_ring forcing
+  int filter;     // 1 layer: apply the exponential filter (qgsw_raytrace.m:137)
+  double shear;   // 2 layers: shear_strength (mean-flow terms; grid_U's u offset)
+  double nu, hyper, r;  // 2 layers: (nu*K2^alpha + r)*K2 diffusion factor
+};
+
+struct cd {
+  double x, y;
+};
+__device__ __forceinline__ cd cmk(double x, double y) { return cd{x, y}; }
+__device__ __forceinline__ cd cadd(cd a, cd b) { return cd{a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cd csub(cd a, cd b) { return cd{a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cd cmul(cd a, cd b) { return cd{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x}; }
+__device__ __forceinline__ cd crs(double s, cd a) { return cd{s * a.x, s * a.y}; }  // real * complex
+__device__ __forceinline__ cd cdivr(cd a, double s) { return cd{a.x / s, a.y / s}; }
+__device__ __forceinline__ cd cexp_(cd z) {
+  const double e = exp(z.x);
+  double sn, cs;
+  sincos(z.y, &sn, &cs);
+  return cd{e * cs, e * sn};
+}
+__device__ __forceinline__ cd csqrt_(cd z) {
+  const double r = hypot(z.x, z.y);
+  if (r == 0.0) return cd{0.0, 0.0};
+  if (z.x >= 0.0) {
+    const double t = sqrt(0.5 * (r + z.x));
+    return cd{t, z.y / (2.0 * t)};
+  }
+  const double t = sqrt(0.5 * (r - z.x));
+  return cd{fabs(z.y) / (2.0 * t), z.y >= 0.0 ? t : -t};
+}
+__device__ __forceinline__ cd cdiv(cd a, cd b) {
+  const double d = b.x * b.x + b.y * b.y;
+  return cd{(a.x * b.x + a.y * b.y) / d, (a.y * b.x - a.x * b.y) / d};
+}
+__device__ __forceinline__ cd ld(const double2* p, int64_t i) { const double2 v = p[i]; return cd{v.x, v.y}; }
+__device__ __forceinline__ void st(double2* p, int64_t i, cd v) { p[i] = make_double2(v.x, v.y); }
+// (1i*k).*z as MATLAB evaluates it
+__device__ __forceinline__ cd ik(double k, cd z) { return cd{-(k * z.y), k * z.x}; }
+// pack two real fields' spectra: A + i*B
+__device__ __forceinline__ double2 pack2(cd a, cd b) { return make_double2(a.x - b.y, a.y + b.x); }
+
+// 2-layer PV inversion B = [-F-K2, -F; -F, -F-K2] ./ (K2.*(K2+2F)), B = 0 at K2 = 0
+// (qg2layersw_raytrace.m:129-136).  Returns B11 (= B22) and B12 (= B21).
+__device__ __forceinline__ void qg2_B(double K2, double K_d2, double& b11, double& b12) {
+  const double F = K_d2 / 2;
+  if (K2 == 0.0) { b11 = 0.0; b12 = 0.0; return; }
+  const double det = K2 * (K2 + 2 * F);
+  b11 = (-F - K2) / det;
+  b12 = -F / det;
+}
+
+// Step 1 of update: per full-spectrum index (layout [c + n*r], ky FFT index c
+// contiguous) and layer l, Z[2l] = psi_x + i psi_y, Z[2l+1] = q_x + i q_y with
+// the Hermitian completion of fulspec.m (kx < 0 on ky = 0 and ky < 0 from
+// their conjugate partners; Nyquist row/column zero).
+__global__ void qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+  const int n = g.n;
+  const int64_t nn = (int64_t)n * n;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nn) return;
+  const int c = (int)(idx % n), r = (int)(idx / n);
+  const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int64_t nhalf = (int64_t)nkx * (kmax + 1);
+  const int kx = signed_k(r, n), ky = signed_k(c, n);
+  const bool inband = (kx >= -kmax && kx <= kmax && ky >= -kmax && ky <= kmax);
+  int hx = kx, hy = ky;
+  bool cj = false;
+  if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
+  const int64_t h = inband ? (hx + kmax) + (int64_t)nkx * hy : 0;
+  const double kxs = (double)hx * g.kscale, kys = (double)hy * g.kscale;
+  const double K2 = kxs * kxs + kys * kys;
+  cd q[2], ps[2];
+  for (int l = 0; l < g.nl; ++l) q[l] = inband ? ld(qk, l * nhalf + h) : cmk(0.0, 0.0);
+  if (g.nl == 1) {
+    // psik = -qk./(K_d2 + K2)   (qgsw_raytrace.m:271)
+    const double den = g.K_d2 + K2;
+    ps[0] = cmk(-q[0].x / den, -q[0].y / den);
+  } else {
+    // psik = mmult3(B, qk)      (qg2layersw_raytrace.m:310)
+    double b11, b12;
+    qg2_B(K2, g.K_d2, b11, b12);
+    ps[0] = cadd(crs(b11, q[0]), crs(b12, q[1]));
+    ps[1] = cadd(crs(b12, q[0]), crs(b11, q[1]));
+  }
+  for (int l = 0; l < g.nl; ++l) {
+    cd px = ik(kxs, ps[l]), py = ik(kys, ps[l]), qx = ik(kxs, q[l]), qy = ik(kys, q[l]);
+    if (cj) { px.y = -px.y; py.y = -py.y; qx.y = -qx.y; qy.y = -qy.y; }
+    if (!inband) px = py = qx = qy = cmk(0.0, 0.0);
+    Z[(2 * l) * nn + idx] = pack2(px, py);
+    Z[(2 * l + 1) * nn + idx] = pack2(qx, qy);
+  }
+}
+
+// J = psix.*qy - psiy.*qx per grid point and layer (qgsw_raytrace.m:282);
+// both layers packed into one complex field J1 + i J2 for the forward FFT.
+__global__ void qg_jacobian_kernel(const double2* T, int nl, int64_t nn, double2* Zj) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nn) return;
+  double J[2] = {0.0, 0.0};
+  for (int l = 0; l < nl; ++l) {
+    const double2 P = T[(2 * l) * nn + i], Q = T[(2 * l + 1) * nn + i];
+    J[l] = P.x * Q.y - P.y * Q.x;
+  }
+  Zj[i] = make_double2(J[0], J[1]);
+}
+
+// filter (qgsw_raytrace.m:222-230) at one wavenumber
+__device__ __forceinline__ double qg_filter_at(double kx, double ky, double dx) {
+  const double ks = sqrt((kx * dx) * (kx * dx) + (ky * dx) * (ky * dx));
+  const double kc = 0.75 * 3.14159265358979323846;
+  if (!(ks >= kc)) return 1.0;
+  const double q = 0.25 * 3.14159265358979323846;
+  const double cst = log(1e-15) / (q * q * q * q);
+  const double d = ks - kc;
+  return exp(cst * (d * d * d * d));
+}
+
+// 2-layer factor_L at one wavenumber (qg2layersw_raytrace.m:140-144):
+//   B.*((nu*K2.^alpha + r).*K2 - 1i*kx*beta)
+//   + 1i*kx*shear .* [-1,0;0,1]*(eye(2) + 2F*B)
+__device__ __forceinline__ void qg2_factor_L(const QGDev& g, double kxs, double K2, cd L[4]) {
+  double b11, b12;
+  qg2_B(K2, g.K_d2, b11, b12);
+  const double F = g.K_d2 / 2;
+  const cd dfac = cmk((g.nu * pow(K2, g.hyper) + g.r) * K2, -(kxs * g.beta));
+  const cd sf = cmk(0.0, kxs * g.shear);
+  const double m00 = -(1 + 2 * F * b11), m01 = -(2 * F * b12), m10 = 2 * F * b12, m11 = 1 + 2 * F * b11;
+  L[0] = cadd(crs(m00, sf), crs(b11, dfac));
+  L[1] = cadd(crs(m01, sf), crs(b12, dfac));
+  L[2] = cadd(crs(m10, sf), crs(b12, dfac));
+  L[3] = cadd(crs(m11, sf), crs(b11, dfac));
+}
+
+// exp(t*M) of a 2x2 complex matrix through its eigenvalues s +- d
+// (= LV*diag(exp(t*LD))*LV^-1, qg2layersw_raytrace.m:146-149):
+//   exp(tM) = (e1+e2)/2 I + (e1-e2)/(2d) (M - sI),  e1,2 = exp(t(s +- d)),
+// with the series of exp(ts) sinh(td)/d near a double eigenvalue.
+__device__ __forceinline__ void expm2(const cd M[4], double t, cd E[4]) {
+  const cd s = crs(0.5, cadd(M[0], M[3]));
+  const cd D = crs(0.5, csub(M[0], M[3]));
+  const cd d = csqrt_(cadd(cmul(D, D), cmul(M[1], M[2])));
+  const cd td = crs(t, d);
+  const cd ets = cexp_(crs(t, s));
+  cd A, S;  // A = e^{ts} cosh(td), S = e^{ts} sinh(td)/d
+  if (hypot(td.x, td.y) > 1e-3) {
+    const cd e1 = cexp_(cadd(crs(t, s), td)), e2 = cexp_(csub(crs(t, s), td));
+    A = crs(0.5, cadd(e1, e2));
+    S = cdiv(crs(0.5, csub(e1, e2)), d);
+  } else {
+    const cd z2 = cmul(td, td);
+    // cosh = 1 + z2/2 + z2^2/24, sinh(td)/d = t (1 + z2/6 + z2^2/120)
+    const cd ch = cadd(cadd(cmk(1.0, 0.0), crs(0.5, z2)), crs(1.0 / 24.0, cmul(z2, z2)));
+    const cd sh = crs(t, cadd(cadd(cmk(1.0, 0.0), crs(1.0 / 6.0, z2)), crs(1.0 / 120.0, cmul(z2, z2))));
+    A = cmul(ets, ch);
+    S = cmul(ets, sh);
+  }
+  E[0] = cadd(A, cmul(S, D));
+  E[1] = cmul(S, M[1]);
+  E[2] = cmul(S, M[2]);
+  E[3] = csub(A, cmul(S, D));
+}
+
+// expLdt and expL2dt for every half-plane wavenumber: E[4*idx + (2i+j)].
+__global__ void qg2_exp_kernel(QGDev g, double dt, double2* E1, double2* E2) {
+  const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)nkx * (kmax + 1)) return;
+  const int row = (int)(idx % nkx), col = (int)(idx / nkx);
+  const double kxs = (double)(row - kmax) * g.kscale, kys = (double)col * g.kscale;
+  const double K2 = kxs * kxs + kys * kys;
+  cd L[4], e[4];
+  qg2_factor_L(g, kxs, K2, L);
+  expm2(L, dt, e);
+  for (int q = 0; q < 4; ++q) st(E1, 4 * idx + q, e[q]);
+  expm2(L, 2 * dt, e);
+  for (int q = 0; q < 4; ++q) st(E2, 4 * idx + q, e[q]);
+}
+
+__device__ __forceinline__ void mmul2(const double2* E, int64_t idx, const cd x[2], cd y[2]) {
+  const cd a = ld(E, 4 * idx), b = ld(E, 4 * idx + 1), c = ld(E, 4 * idx + 2), d = ld(E, 4 * idx + 3);
+  y[0] = cadd(cmul(a, x[0]), cmul(b, x[1]));
+  y[1] = cadd(cmul(c, x[0]), cmul(d, x[1]));
+}
+
+// g2k crop of the (packed) forward spectrum, the tendency, and the AB3 update
+// of qk, fused per half-plane wavenumber (both layers together for mmult3).
+//   1 layer:  Qn = g2k(J) - beta*psikx + r_drag*K2 + surface_forces
+//             qk = Ef.*(qk + dq)                       (qgsw_raytrace.m:121-137)
+//   2 layers: Qn = g2k(J);  qk = mmult3(expLdt, qk + dq)   (:168-181)
+//   dq = dt*Qn | dt/2*(3Qn - X1) | dt/12*(23Qn - 16X1 + 5X2), X = Qm (1 layer)
+//   or mmult3(expL(2)dt, Qm) (2 layers); then Qm2 = Qm1, Qm1 = Qn.
+__global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abstep, const double2* E1,
+                                 const double2* E2, double2* qk, double2* Qm1, double2* Qm2) {
+  const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int64_t nhalf = (int64_t)nkx * (kmax + 1);
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nhalf) return;
+  const int row = (int)(idx % nkx), col = (int)(idx / nkx);
+  const int kx = row - kmax, ky = col;
+  const double kxs = (double)kx * g.kscale, kys = (double)ky * g.kscale;
+  const double K2 = kxs * kxs + kys * kys;
+  const double nn = (double)n * (double)n;
+  // packed forward spectrum Z = F1 + i F2 at k and -k (FFT indices)
+  const int r = kx < 0 ? kx + n : kx, c = ky;
+  const int rm = kx > 0 ? n - kx : -kx, cm = ky > 0 ? n - ky : 0;
+  const double2 Fk = Fj[c + (int64_t)n * r], Fm = Fj[cm + (int64_t)n * rm];
+  cd Qn[2];
+  if (g.nl == 1) {
+    // g2k(J) = fftshift(fft2(J))/nx^2 of a real J: the packed imaginary part is 0
+    Qn[0] = cmk(Fk.x / nn, Fk.y / nn);
+  } else {
+    const cd F1 = cmk(0.5 * (Fk.x + Fm.x), 0.5 * (Fk.y - Fm.y));
+    const cd F2 = cmk(0.5 * (Fk.y + Fm.y), -0.5 * (Fk.x - Fm.x));
+    Qn[0] = cdivr(F1, nn);
+    Qn[1] = cdivr(F2, nn);
+  }
+  cd q[2];
+  for (int l = 0; l < g.nl; ++l) q[l] = ld(qk, l * nhalf + idx);
+  if (g.nl == 1) {
+    const double den = g.K_d2 + K2;
+    const cd psik = cmk(-q[0].x / den, -q[0].y / den);
+    const cd psikx = ik(kxs, psik);
+    const double omega = sqrt(g.f * g.f + (g.Cg * g.Cg) * K2);
+    const double force = (0.9 * g.f < omega && omega < 1.1 * g.f) ? g.force_strength : 0.0;
+    Qn[0] = csub(Qn[0], crs(g.beta, psikx));
+    Qn[0].x = Qn[0].x + g.r_drag * K2;
+    Qn[0].x = Qn[0].x + force;
+  }
+  cd X1[2], X2[2], m1[2], m2[2];
+  for (int l = 0; l < g.nl; ++l) {
+    m1[l] = ld(Qm1, l * nhalf + idx);
+    m2[l] = ld(Qm2, l * nhalf + idx);
+  }
+  if (g.nl == 1) {
+    X1[0] = m1[0];
+    X2[0] = m2[0];
+  } else {
+    mmul2(E1, idx, m1, X1);
+    mmul2(E2, idx, m2, X2);
+  }
+  cd dq[2];
+  for (int l = 0; l < g.nl; ++l) {
+    if (abstep == 1) {
+      dq[l] = crs(dt, Qn[l]);
+    } else if (abstep == 2) {
+      dq[l] = crs(dt / 2, csub(crs(3.0, Qn[l]), X1[l]));
+    } else {
+      dq[l] = crs(dt / 12, cadd(csub(crs(23.0, Qn[l]), crs(16.0, X1[l])), crs(5.0, X2[l])));
+    }
+  }
+  cd out[2];
+  if (g.nl == 1) {
+    const double Ef = g.filter ? qg_filter_at(kxs, kys, g.dx) : 1.0;
+    out[0] = crs(Ef, cadd(q[0], dq[0]));
+  } else {
+    cd s[2] = {cadd(q[0], dq[0]), cadd(q[1], dq[1])};
+    mmul2(E1, idx, s, out);
+  }
+  for (int l = 0; l < g.nl; ++l) {
+    st(qk, l * nhalf + idx, out[l]);
+    st(Qm2, l * nhalf + idx, m1[l]);
+    st(Qm1, l * nhalf + idx, Qn[l]);
+  }
+}
+
+// u + i v per layer from grid_U's inversion psik = -qk./(K_d2+K2) (grid_U.m:2-6),
+// for the CFL speed (qg2layersw_raytrace.m:156-158); layout [c + n*r].
+__global__ void qg_vel_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+  const int n = g.n;
+  const int64_t nn = (int64_t)n * n;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nn) return;
+  const int c = (int)(idx % n), r = (int)(idx / n);
+  const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int64_t nhalf = (int64_t)nkx * (kmax + 1);
+  const int kx = signed_k(r, n), ky = signed_k(c, n);
+  const bool inband = (kx >= -kmax && kx <= kmax && ky >= -kmax && ky <= kmax);
+  int hx = kx, hy = ky;
+  bool cj = false;
+  if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
+  const double kxs = (double)hx * g.kscale, kys = (double)hy * g.kscale;
+  const double den = g.K_d2 + (kxs * kxs + kys * kys);
+  for (int l = 0; l < g.nl; ++l) {
+    cd u = cmk(0.0, 0.0), v = cmk(0.0, 0.0);
+    if (inband) {
+      const cd q = ld(qk, l * nhalf + (hx + kmax) + (int64_t)nkx * hy);
+      const cd ps = cmk(-q.x / den, -q.y / den);
+      u = cmk(kys * ps.y, -(kys * ps.x));  // (-1i*ky).*psik
+      v = ik(kxs, ps);
+      if (hx == 0 && hy == 0) { u.y = 0.0; v.y = 0.0; }
+      if (cj) { u.y = -u.y; v.y = -v.y; }
+    }
+    Z[l * nn + idx] = pack2(u, v);
+  }
+}
+
+// max over the grid of (u + shear)^2 + v^2 (all layers) into *out (as the
+// bit pattern of a non-negative double, so integer max == double max).
+__global__ void qg_max_speed2_kernel(const double2* T, int64_t cnt, double shear, unsigned long long* out) {
+  __shared__ double red[256];
+  double m = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * blockDim.x) {
+    const double2 z = T[i];
+    const double u = z.x + shear, v = z.y;
+    const double s2 = u * u + v * v;
+    m = s2 > m ? s2 : m;
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicMax(out, (unsigned long long)__double_as_longlong(red[0]));
+}
+
+}  // namespace swrt

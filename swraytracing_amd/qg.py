@@ -1,0 +1,318 @@
+"""The QG PDE steppers that produce the packets' background snapshots, with
+their state resident on the GPU, and the two reference
+drivers built on them.
+
+* :class:`QGModel` — ``qgsw_raytrace.m:111-137`` (1 layer: AB3 + filter,
+  ``update`` :270-286) and ``qg2layersw_raytrace.m:129-181`` (2 layers:
+  exponential AB3, adaptive CFL :156-165) over ``swrt_qg_*``.
+* :func:`qgsw_raytrace` / :func:`qg2layersw_raytrace` — the drivers
+  (``qgsw_raytrace.m:1-180``, ``qg2layersw_raytrace.m:1-247``): PDE on the
+  device, per PDE step grid_U of (prev_qk, qk) straight into the packet slots
+  and the packets advanced through [t, t+dt] by the fused symplectic kernel
+  (the reference's ``ode23`` is replaced by ``nsub`` leapfrog substeps with the
+  interpolate_U blend), frames written in the reference's
+  ``data/*.bin`` layout (``write_field.m``).
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+
+from ._lib import Context, QGParams
+from .integrate import PacketEnsemble
+from .io import write_field
+from .scheme import BUMP_QG
+
+
+class QGModel:
+    """Device-resident spectral QG model (``swrt_qg_init`` / ``swrt_qg_step``).
+
+    ``qk``: the g2k half plane, (2kmax+1, kmax+1) for one layer or
+    (2kmax+1, kmax+1, 2) for two."""
+
+    def __init__(self, qk, nx, params: QGParams, ctx: Context | None = None, device=0):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self.nx = int(nx)
+        self.params = params
+        self.nlayers = params.nlayers
+        self.L = params.L
+        self.dx = params.L / nx
+        self.ctx.qg_init(params, nx, qk)
+
+    @classmethod
+    def one_layer(cls, qk, nx, f, Cg, beta=0.0, r_drag=0.1, force_strength=0.1, use_filter=True, **kw):
+        """qgsw_raytrace.m:22-27,111-137: L = 2*pi, K_d2 = f/Cg, inertial_ring forcing."""
+        p = QGParams(nlayers=1, filter=1 if use_filter else 0, L=2 * math.pi, K_d2=f / Cg, beta=beta,
+                     r_drag=r_drag, force_strength=force_strength, f=f, Cg=Cg, shear=0.0, nu=0.0,
+                     hyper_order=0.0, r=0.0)
+        return cls(qk, nx, p, **kw)
+
+    @classmethod
+    def two_layer(cls, qk, nx, f, Cg, L=20.0, beta=0.0, shear=0.5, alpha=4, r=0.4, nutune=0.1, **kw):
+        """qg2layersw_raytrace.m:13-34,79,129-147."""
+        dx = L / nx
+        p = QGParams(nlayers=2, filter=0, L=L, K_d2=f / Cg, beta=beta, r_drag=0.0, force_strength=0.0, f=f,
+                     Cg=Cg, shear=shear, nu=nutune * dx ** (2 * alpha), hyper_order=float(alpha), r=r)
+        return cls(qk, nx, p, **kw)
+
+    def step(self, dt, nsteps=1):
+        self.ctx.qg_step(dt, nsteps)
+
+    def max_speed(self):
+        """U0 = sqrt(max(u.^2 + v.^2)) of grid_U(qk) (all layers, u + shear)."""
+        return self.ctx.qg_max_speed()
+
+    def cfl_update(self, dt, cfl_fraction):
+        """qg2layersw_raytrace.m:156-165: returns (dt, U0, changed)."""
+        U0 = self.max_speed()
+        cond = cfl_fraction * self.dx / U0
+        if cond < dt or dt < cond / 4:
+            return cfl_fraction / 2 * self.dx / U0, U0, True
+        return dt, U0, False
+
+    @property
+    def qk(self):
+        return self.ctx.qg_get()[0]
+
+    @property
+    def t(self):
+        return self.ctx.qg_get()[1]
+
+    @property
+    def steps(self):
+        return self.ctx.qg_get()[2]
+
+    def q(self):
+        """k2g(qk) per layer: (nx, nx) or (nx, nx, 2)."""
+        q = self.ctx.qg_get_q()
+        return q[:, :, 0] if self.nlayers == 1 else q
+
+    def snapshot(self, slot, which=0, layer=0, ny_period=0):
+        """grid_U of the current (0) / previous (1) qk into packet slot `slot`."""
+        self.ctx.qg_snapshot(slot, which, layer, ny_period)
+
+
+# ----------------------------------------------------------------------------
+# Drivers
+# ----------------------------------------------------------------------------
+def initial_q(nx, L, a_g, K_d2, k_min, k_max, rng, ndgrid=False):
+    """initial_q (qgsw_raytrace.m:191-214, qg2layersw_raytrace.m:258-281): a
+    random-phase ring k_min < |k| <= k_max normalised to max|U| = a_g, on
+    linspace(-L/2, L/2, nx) (meshgrid for 1 layer, ndgrid for 2).  numpy's
+    generator replaces MATLAB's rng (its stream is not reproducible here)."""
+    xs = np.linspace(-L / 2, L / 2, nx)
+    X, Y = np.meshgrid(xs, xs, indexing="ij" if ndgrid else "xy")
+    q = np.zeros_like(X)
+    U = np.zeros_like(X)
+    V = np.zeros_like(X)
+    phase = 2 * np.pi * rng.random((2 * k_max + 1, 2 * k_max + 1))
+    for k in range(-k_max, k_max + 1):
+        for l in range(-k_max, k_max + 1):
+            if k_min ** 2 < k * k + l * l <= k_max ** 2:
+                wp = k * X + l * Y + phase[k + k_max, l + k_max]
+                U = U - l * np.sin(wp)
+                V = V + k * np.sin(wp)
+                q = q - (K_d2 + k * k + l * l) * np.cos(wp)
+    return a_g / np.sqrt((U ** 2 + V ** 2).max()) * q
+
+
+def _packets(N, L, near_inertial_factor, f, Cg, rng):
+    """qgsw_raytrace.m:54-60."""
+    wf = math.sqrt((near_inertial_factor ** 2 - 1) * f ** 2 / Cg ** 2)
+    i = np.arange(1, N + 1, dtype=np.float64)
+    k = np.stack([wf * np.cos(2 * np.pi * i / N), wf * np.sin(2 * np.pi * i / N)], axis=1)
+    x = L * rng.random((N, 2)) - L / 2
+    return x, k
+
+
+class _Log:
+    def __init__(self, path, verbose):
+        self.f = open(path, "w") if path else None
+        self.verbose = verbose
+
+    def __call__(self, msg):
+        if self.verbose:
+            print(msg, end="")
+        if self.f:
+            self.f.write(msg)
+            self.f.flush()
+
+    def close(self):
+        if self.f:
+            self.f.close()
+
+
+def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
+                  out_dir="data", nsub=4, max_steps=None, seed=146, verbose=False, r_drag=0.1,
+                  ctx: Context | None = None):
+    """qgsw_raytrace.m:1-180 with the PDE and the packets on the GPU.
+
+    Writes ``out_dir``/packet_x.bin, packet_k.bin, packet_time.bin, pv.bin,
+    pv_time.bin (frames appended, write_field.m) and run.log.  ``max_steps``
+    bounds the run (None: the reference's Nsteps = ceil(T/dt)).  ``r_drag``
+    (0.1 in the reference, :25) enters update as the literal `+ r_drag*K2`
+    term of :285, which forces every mode and makes long runs blow up; pass
+    0 to drop it.  Returns a dict of run facts (dt, Nsteps, steps run, frames
+    written, final t)."""
+    ctx = ctx if ctx is not None else Context(0)
+    os.makedirs(out_dir, exist_ok=True)
+    for name in ("packet_x", "packet_k", "packet_time", "pv", "pv_time"):
+        p = os.path.join(out_dir, name + ".bin")
+        if os.path.exists(p):
+            os.remove(p)
+    log = _Log(os.path.join(out_dir, "run.log"), verbose)
+    L = 2 * math.pi
+    dx = L / nx
+    rng = np.random.default_rng(seed)
+    K_d2 = f / Cg
+    T_days = T_Fr_days / f
+    CFL_fraction = 0.05
+    steps_per_save = 50
+    packet_delay = packet_delay_days / f
+    packet_steps_per_save = 5
+    q = initial_q(nx, L, U_g, K_d2, 5, 8, rng)
+    qk = ctx.g2k(q)
+    x, k = _packets(Npackets, L, near_inertial_factor, f, Cg, rng)
+    model = QGModel.one_layer(qk, nx, f, Cg, r_drag=r_drag, ctx=ctx)
+    U0 = model.max_speed()
+    Fr = U0 / Cg
+    T = T_days / Fr ** 2
+    dt = CFL_fraction * dx / U0
+    Nsteps = math.ceil(T / dt)
+    packet_step_start = math.ceil(packet_delay / dt)
+    log(f"Resolution: {nx}x{nx}\n")
+    log(f"Number of packets: {Npackets}\n")
+    log(f"Initial wavenumber radius: {near_inertial_factor * f:f}\n")
+    log(f"Time step: {dt:f}\n")
+    log(f"Simulation time: {T:f}\n")
+    log(f"Spin-up time: {packet_delay:f}\n")
+    log(f"Steps per save: {steps_per_save}\n")
+    log(f"Steps per packet save: {packet_steps_per_save}\n")
+    log(f"Coriolis parameter: {f:f}\n")
+    log(f"Group velocity: {Cg:f}\n")
+    log(f"Background velocity (parameter,computed): ({U_g:f},{U0:f})\n")
+    log(f"Froude Number: {Fr:f}\n")
+    log(f"Deformation wavenumber: {K_d2:f}\n")
+    ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, bump=BUMP_QG, ctx=ctx) \
+        if Npackets > 0 else None
+    t = 0.0
+    frames = 1
+    if ens is not None:
+        ens.write_frame(dt * (packet_step_start - 1), out_dir)
+    write_field(model.q(), os.path.join(out_dir, "pv"))
+    write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+    nrun = Nsteps if max_steps is None else min(Nsteps, int(max_steps))
+    have_cur = False
+    for step in range(1, nrun + 1):
+        model.step(dt)
+        t = t + dt
+        if ens is not None and t > packet_delay:
+            if have_cur:
+                ctx.swap_slots(0, 1)          # last step's grid_U(qk) is this step's grid_U(prev_qk)
+            else:
+                model.snapshot(0, which=1)    # grid_U(prev_qk)
+            model.snapshot(1, which=0)        # grid_U(qk)
+            have_cur = True
+            ens.advance(dt, nsub)
+            if (step - packet_step_start + 1) % packet_steps_per_save == 0:
+                ens.write_frame(t, out_dir)
+                frames += 1
+        else:
+            have_cur = False
+        if step % steps_per_save == 0:
+            write_field(model.q(), os.path.join(out_dir, "pv"))
+            write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+    log.close()
+    return dict(dt=dt, Nsteps=Nsteps, steps=nrun, packet_frames=frames, t=t, U0=U0,
+                packet_step_start=packet_step_start)
+
+
+def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
+                        out_dir="data", nsub=4, max_steps=None, seed=5, verbose=False,
+                        ctx: Context | None = None):
+    """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
+    (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and
+    interpolate's 2*nx y-period).  Same packet outputs as :func:`qgsw_raytrace`;
+    pv.bin holds the initial nx x nx x 2 frame only, as in the reference."""
+    ctx = ctx if ctx is not None else Context(0)
+    os.makedirs(out_dir, exist_ok=True)
+    for name in ("packet_x", "packet_k", "packet_time", "pv", "pv_time"):
+        p = os.path.join(out_dir, name + ".bin")
+        if os.path.exists(p):
+            os.remove(p)
+    log = _Log(os.path.join(out_dir, "run.log"), verbose)
+    L = 20.0
+    dx = L / nx
+    rng = np.random.default_rng(seed)
+    K_d2 = f / Cg
+    shear = 0.5
+    T_Fr = T_Fr_days / f
+    packet_delay_Fr = packet_delay_Fr_days / f
+    CFL_fraction = 0.25
+    steps_per_save = 10
+    packet_delay_steps = packet_delay_Fr / f
+    packet_steps_per_save = 25
+    q1 = initial_q(nx, L, U_g, K_d2, 10, 30, rng, ndgrid=True)
+    qk1 = ctx.g2k(q1)
+    qk2 = ctx.g2k(-q1)
+    qk = np.stack([qk1, qk2], axis=2)
+    x, k = _packets(Npackets, L, near_inertial_factor, f, Cg, rng)
+    model = QGModel.two_layer(qk, nx, f, Cg, L=L, shear=shear, ctx=ctx)
+    U0 = model.max_speed()
+    Fr = U0 / Cg
+    T = T_Fr / Fr ** 2
+    dt = CFL_fraction * dx / U0
+    Nsteps = math.ceil(T / dt)
+    packet_step_start = math.ceil(packet_delay_steps / dt)
+    log(f"Resolution: {nx}x{nx}\n")
+    log(f"Number of packets: {Npackets}\n")
+    log(f"Initial wavenumber radius: {near_inertial_factor * f:f}\n")
+    log(f"Initial time step: {dt:f}\n")
+    log(f"Simulation time: {T:f}\n")
+    log(f"Spin-up time: {packet_delay_steps:f}\n")
+    log(f"Steps per save: {steps_per_save}\n")
+    log(f"Steps per packet save: {packet_steps_per_save}\n")
+    log(f"Coriolis parameter: {f:f}\n")
+    log(f"Group velocity: {Cg:f}\n")
+    log(f"Background velocity (parameter,computed): ({U_g:f},{U0:f})\n")
+    log(f"Froude Number: {Fr:f}\n")
+    log(f"Deformation wavenumber: {K_d2:f}\n")
+    ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=shear, k_scale=2 * math.pi / L, nlayers=2,
+                         bump=BUMP_QG, ctx=ctx) if Npackets > 0 else None
+    t = 0.0
+    frames = 1
+    if ens is not None:
+        ens.write_frame(dt * (packet_step_start - 1), out_dir)
+    write_field(model.q(), os.path.join(out_dir, "pv"))
+    write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+    step = 0
+    have_cur = False
+    dts = []
+    while t <= T and (max_steps is None or step < max_steps):
+        step += 1
+        dt, U0, changed = model.cfl_update(dt, CFL_fraction)
+        if changed:
+            log(f"CFL condition not met, max|u|={U0:f}, new dt={dt:f}\n")
+        dts.append(dt)
+        model.step(dt)
+        t = t + dt
+        if ens is not None and t > packet_delay_steps:
+            if have_cur:
+                ctx.swap_slots(0, 1)
+            else:
+                model.snapshot(0, which=1, layer=0, ny_period=2 * nx)
+            model.snapshot(1, which=0, layer=0, ny_period=2 * nx)
+            have_cur = True
+            ens.advance(dt, nsub)
+            if (step - packet_step_start + 1) % packet_steps_per_save == 0:
+                ens.write_frame(t, out_dir)
+                frames += 1
+        else:
+            have_cur = False
+        # (the reference only plots q every steps_per_save steps here; its
+        # pv.bin writes are commented out, qg2layersw_raytrace.m:211-239)
+    log.close()
+    return dict(dt=dt, dts=dts, Nsteps=Nsteps, steps=step, packet_frames=frames, t=t, U0=U0,
+                packet_step_start=packet_step_start)

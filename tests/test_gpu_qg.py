@@ -1,0 +1,222 @@
+"""GPU parity of the device QG PDE stepper (swrt_qg_*, swraytracing_amd/qg.py)
+against the oracle (QG1Oracle / QG2Oracle, pinned by tests/test_oracle_qg.py).
+
+Tolerance: the GPU FFT rounds differently from numpy's pocketfft, so every
+spectral quantity is compared relative to its max-abs at QG_RTOL.  Over 10-20
+PDE steps the nonlinearity does not amplify round-off beyond that (the flows
+are smooth, CFL-limited, and the comparison horizon short).  Packets driven by
+the device PDE are compared with the oracle pipeline at TRAJ_ATOL.
+"""
+import numpy as np
+import pytest
+
+import swraytracing_amd as sw
+from oracle import swrt_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+QG_RTOL = 1e-11
+TRAJ_ATOL = 1e-9
+
+
+def _rel(a, b):
+    return np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(b).max(), 1e-300)
+
+
+def _one_layer_case(nx=64, seed=146):
+    rng = np.random.default_rng(seed)
+    q = orc.initial_q(nx, 2 * np.pi, 0.2, 3.0, 5, 8, rng)
+    return orc.g2k(q)
+
+
+def _two_layer_case(nx=64, seed=5):
+    rng = np.random.default_rng(seed)
+    # qg2layersw_raytrace.m:261-262 uses 10 < |k| <= 30 at production resolution;
+    # on these small test grids a lower ring keeps the field resolved
+    q1 = orc.initial_q(nx, 20.0, 0.2, 3.0, 1, 3, rng)
+    return np.stack([orc.g2k(q1), orc.g2k(-q1)], axis=2)
+
+
+def test_qg1_steps_match_oracle(ctx):
+    """AB3 + filter + inertial-ring forcing.  r_drag = 0 here: update's
+    `+ r_drag*K2` term (qgsw_raytrace.m:285, reproduced as written) forces
+    every mode by 0.1*K2 and the run blows up within a few steps (both the
+    device and the oracle, identically); it is covered separately below."""
+    nx, f, Cg = 64, 3.0, 1.0
+    qk0 = _one_layer_case(nx)
+    m = sw.QGModel.one_layer(qk0, nx, f, Cg, r_drag=0.0, ctx=ctx)
+    o = orc.QG1Oracle(qk0, nx, f / Cg, r_drag=0.0, force_strength=0.1, f=f, Cg=Cg, use_filter=True)
+    dt = 0.05 * (2 * np.pi / nx) / 0.2
+    for n in range(12):
+        m.step(dt)
+        o.step(dt)
+    qk, t, steps = ctx.qg_get()
+    assert steps == 12 and abs(t - o.t) < 1e-15
+    assert _rel(qk[:, :, 0], o.qk) < QG_RTOL
+
+
+def test_qg1_r_drag_term_as_written(ctx):
+    """The reference's `+ r_drag*K2` (qgsw_raytrace.m:285) on a zero field:
+    one Euler step gives qk = dt*0.1*K2 (filtered), exactly as the oracle."""
+    nx, f, Cg = 32, 3.0, 1.0
+    kmax = nx // 2 - 1
+    qk0 = np.zeros((2 * kmax + 1, kmax + 1), complex)
+    m = sw.QGModel.one_layer(qk0, nx, f, Cg, r_drag=0.1, force_strength=0.0, ctx=ctx)
+    o = orc.QG1Oracle(qk0, nx, f / Cg, r_drag=0.1, force_strength=0.0, f=f, Cg=Cg, use_filter=True)
+    m.step(0.01)
+    o.step(0.01)
+    assert _rel(m.qk[:, :, 0], o.qk) < 1e-14
+
+
+def test_qg1_filter_off_and_forcing_off(ctx):
+    nx, f, Cg = 32, 3.0, 1.0
+    qk0 = _one_layer_case(nx, seed=9)
+    m = sw.QGModel.one_layer(qk0, nx, f, Cg, r_drag=0.0, force_strength=0.0, use_filter=False, ctx=ctx)
+    o = orc.QG1Oracle(qk0, nx, f / Cg, r_drag=0.0, force_strength=0.0, f=f, Cg=Cg, use_filter=False)
+    for _ in range(8):
+        m.step(0.03)
+        o.step(0.03)
+    assert _rel(m.qk[:, :, 0], o.qk) < QG_RTOL
+
+
+def test_qg2_fixed_dt_matches_oracle(ctx):
+    nx, L = 64, 20.0
+    qk0 = _two_layer_case(nx)
+    m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, L=L, ctx=ctx)
+    o = orc.QG2Oracle(qk0, nx, L, 3.0, shear_strength=0.5)
+    dt = o.dt
+    for _ in range(10):
+        m.step(dt)
+        o.step(dt)
+    assert _rel(m.qk, o.qk) < QG_RTOL
+
+
+def test_qg2_single_mode_exponential(ctx):
+    """J = 0 for one wavevector: the device expLdt alone moves qk; compare
+    with the oracle's pageeig exponential (itself checked against expm)."""
+    nx, L = 32, 20.0
+    kmax = nx // 2 - 1
+    qk0 = np.zeros((2 * kmax + 1, kmax + 1, 2), complex)
+    qk0[5 + kmax, 2, :] = [0.3 - 0.1j, 0.2 + 0.4j]
+    m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, L=L, ctx=ctx)
+    o = orc.QG2Oracle(qk0, nx, L, 3.0, shear_strength=0.5)
+    for dt in (0.04, 0.04, 0.07, 0.07, 0.07):  # dt change re-computes the exponentials
+        m.step(dt)
+        o.step(dt)
+    np.testing.assert_allclose(m.qk, o.qk, rtol=1e-12, atol=1e-15)
+
+
+def test_qg2_adaptive_cfl_sequence(ctx):
+    """The driver's CFL rule (qg2layersw_raytrace.m:156-165) on device speeds:
+    same dt sequence and state as the oracle."""
+    nx, L = 64, 20.0
+    qk0 = _two_layer_case(nx, seed=11)
+    m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, L=L, ctx=ctx)
+    o = orc.QG2Oracle(qk0, nx, L, 3.0, shear_strength=0.5)
+    U0 = m.max_speed()
+    assert abs(U0 - o.U0) < 1e-13 * o.U0
+    dt = 0.25 * (L / nx) / U0
+    assert abs(dt - o.dt) < 1e-13 * o.dt
+    # start from a deliberately too-large dt so the rule fires
+    o.dt = dt = 3 * dt
+    o.exps(o.dt)
+    for _ in range(6):
+        dt, U0, _ = m.cfl_update(dt, 0.25)
+        m.step(dt)
+        o.step()
+        assert abs(dt - o.dt) <= 1e-12 * o.dt
+    assert _rel(m.qk, o.qk) < QG_RTOL
+
+
+def test_qg_get_q_is_k2g(ctx):
+    nx = 64
+    qk0 = _two_layer_case(nx)
+    m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, ctx=ctx)
+    q = m.q()
+    for l in range(2):
+        assert _rel(q[:, :, l], orc.k2g(qk0[:, :, l])) < 1e-13
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_qg_snapshot_is_grid_U(ctx, which):
+    """swrt_qg_snapshot == swrt_set_field_qk of the same qk (same device code,
+    bit for bit) and == the oracle grid_U (layer 1, u + shear) to FFT round-off."""
+    nx, L = 64, 20.0
+    qk0 = _two_layer_case(nx)
+    m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, L=L, ctx=ctx)
+    m.step(0.01)
+    src = (m.qk if which == 0 else None)
+    m.snapshot(0, which=which, layer=0, ny_period=2 * nx)
+    got = ctx.get_field_grid(0, nx)
+    if which == 1:
+        src = qk0  # previous qk of the first step is the initial state
+    ctx.set_field_qk(1, src[:, :, 0], nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+    ref = ctx.get_field_grid(1, nx)
+    np.testing.assert_array_equal(got, ref)
+    kx_, ky_, K2 = orc.wavenumber_grids(nx, L, scale=True)
+    flow = orc.grid_U(src[:, :, 0], 3.0, K2, kx_, ky_, 0.5)
+    for i, name in enumerate(orc.FIELD_ORDER):
+        assert _rel(got[i], np.asarray(flow[name]).ravel(order="F")) < 1e-12
+
+
+def test_swap_slots(ctx):
+    nx = 32
+    a = np.random.default_rng(1).random((6, nx * nx))
+    b = np.random.default_rng(2).random((6, nx * nx))
+    ctx.set_field_grid(0, a, nx, 2 * np.pi)
+    ctx.set_field_grid(1, b, nx, 2 * np.pi)
+    ctx.swap_slots(0, 1)
+    np.testing.assert_array_equal(ctx.get_field_grid(0, nx), b)
+    np.testing.assert_array_equal(ctx.get_field_grid(1, nx), a)
+
+
+def test_qgsw_driver_packets_match_oracle_pipeline(ctx, oracle_lib, tmp_path):
+    """qgsw_raytrace on the device (PDE + snapshots + fused packets) against
+    the same pipeline on the CPU oracle: QG1Oracle steps, grid_U of (prev_qk,
+    qk), the C-oracle leapfrog with the blend; 12 PDE steps, all packet-active."""
+    nx, N, nsub = 64, 300, 3
+    f, Cg = 3.0, 1.0
+    res = sw.qgsw_raytrace(nx, N, 4.0, 10.0, 0.0, 0.2, f, Cg, out_dir=str(tmp_path), nsub=nsub,
+                           max_steps=12, seed=146, r_drag=0.0, ctx=ctx)
+    assert res["steps"] == 12
+    xg = sw.read_field(str(tmp_path / "packet_x"), N, 2, 1)
+    kg = sw.read_field(str(tmp_path / "packet_k"), N, 2, 1)
+    tg = sw.read_field(str(tmp_path / "packet_time"))
+    frames = 1 + 12 // 5
+    assert xg.shape == (N, 2, frames) and tg.shape == (1, frames)
+    # oracle pipeline from the same initial state
+    rng = np.random.default_rng(146)
+    L = 2 * np.pi
+    q = sw.qg.initial_q(nx, L, 0.2, f / Cg, 5, 8, rng)
+    x, k = sw.qg._packets(N, L, 4.0, f, Cg, rng)
+    o = orc.QG1Oracle(orc.g2k(q), nx, f / Cg, r_drag=0.0, f=f, Cg=Cg)
+    dt = res["dt"]
+    kx_, ky_, K2 = orc.wavenumber_grids(nx)
+    from tests.test_gpu_parity import _planes
+    for step in range(1, 13):
+        prev = o.qk.copy()
+        o.step(dt)
+        p0 = _planes(orc.grid_U(prev, f / Cg, K2, kx_, ky_))
+        p1 = _planes(orc.grid_U(o.qk, f / Cg, K2, kx_, ky_))
+        x, k, _, _ = oracle_lib.leapfrog(p0, p1, 0.5 / nsub, 1.0 / nsub, nx, nx, L / nx, orc.BUMP_QG, x, k,
+                                         dt / nsub, nsub, f, Cg ** 2)
+    xw = np.mod(x + L / 2, L) - L / 2
+    xs, ks = ctx.packets_get()
+    np.testing.assert_allclose(xs, x, atol=TRAJ_ATOL, rtol=0)
+    np.testing.assert_allclose(ks, k, atol=TRAJ_ATOL, rtol=0)
+    assert np.abs(xg[:, :, -1]).max() <= L / 2 + 1e-12
+    assert np.isfinite(xw).all()
+
+
+def test_qg2layer_driver_runs_and_writes(ctx, tmp_path):
+    nx, N = 64, 500
+    res = sw.qg2layersw_raytrace(nx, N, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(tmp_path), nsub=2,
+                                 max_steps=30, seed=5, ctx=ctx)
+    assert res["steps"] == 30
+    xg = sw.read_field(str(tmp_path / "packet_x"), N, 2, 1)
+    assert xg.shape[-1] == 1 + 30 // 25
+    assert np.isfinite(xg).all()
+    pv = sw.read_field(str(tmp_path / "pv"), nx, nx, 2)
+    assert pv.shape == (nx, nx, 2)
+    log = open(tmp_path / "run.log").read()
+    assert "Resolution: 64x64" in log and "Froude Number" in log
