@@ -272,24 +272,39 @@ int inverse_2d(swrt_ctx* c, double2* Z, double2* out, int n, int nb) {
   return SWRT_OK;
 }
 
-// Shared tail of set_field_psi / set_field_qk: fk half-plane in device memory.
+// Shared tail of set_field_psi / set_field_qk / swrt_qg_snapshot: fk half
+// plane in device memory, read at fk[(kx + kmax)*sx + ky*sy].
 int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int mode, double K_d2,
-                          double kscale, double shear, int with_psi, double2* Z, double2* T) {
+                          double kscale, double shear, int with_psi, double2* Z, double2* T, int sx, int sy) {
   int rc;
   const int64_t nn = (int64_t)n * n;
   const int nb = with_psi ? 4 : 3;
   hipLaunchKernelGGL(spectra_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, dfk, n, mode,
-                     K_d2, kscale, with_psi, Z);
+                     K_d2, kscale, with_psi, Z, sx, sy);
   HIPCHK(c, hipGetLastError());
   if ((rc = inverse_2d(c, Z, T, n, nb))) return rc;
-  // T now holds fields in [r + n*c]; unpair into planes (reuse Z as planes buffer)
-  double* planes = reinterpret_cast<double*>(Z);
+  // T now holds the packed fields in [x + n*y]
   Slot& s = c->slot[slot];
   if (with_psi && !s.psi) HIPCHK(c, hipMalloc(&s.psi, sizeof(double) * nn));
-  hipLaunchKernelGGL(unpair_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, n, with_psi,
-                     planes, with_psi ? s.psi : nullptr);
-  HIPCHK(c, hipGetLastError());
-  if ((rc = pack_slot(c, slot, planes, shear))) return rc;
+  if (n % 16 == 0) {
+    hipLaunchKernelGGL(pack_pairs_kernel, dim3(n / 16, n / 16), dim3(256), 0, c->stream, T, n, (int)s.npad, shear,
+                       s.nodes);
+    HIPCHK(c, hipGetLastError());
+    const int64_t ghosts = 2 * (int64_t)(s.npad - n) * s.npad;
+    hipLaunchKernelGGL(halo_nodes_kernel, dim3(nblocks(ghosts, 256)), dim3(256), 0, c->stream, s.nodes, n,
+                       (int)s.npad);
+    HIPCHK(c, hipGetLastError());
+    if (with_psi) {
+      hipLaunchKernelGGL(psi_plane_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T + 3 * nn, s.psi, nn);
+      HIPCHK(c, hipGetLastError());
+    }
+  } else {  // tiny grids: unpair into planes (reuse Z), then pack
+    double* planes = reinterpret_cast<double*>(Z);
+    hipLaunchKernelGGL(unpair_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, n, with_psi,
+                       planes, with_psi ? s.psi : nullptr);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = pack_slot(c, slot, planes, shear))) return rc;
+  }
   s.has_psi = with_psi != 0;
   return SWRT_OK;
 }
@@ -605,7 +620,7 @@ int swrt_set_field_psi(swrt_ctx* c, int slot, const double* psi_grid, int64_t nx
   if ((rc = run_fft_pass(c, T, n, 1, 0))) return rc;  // along y; T: [c + n*r]
   hipLaunchKernelGGL(crop_half_kernel, dim3(nblocks(nhalf, 256)), dim3(256), 0, c->stream, T, n, fk);
   HIPCHK(c, hipGetLastError());
-  if ((rc = fields_from_halfplane(c, slot, fk, n, 0, 0.0, 1.0, 0.0, 1, Z, T))) return rc;
+  if ((rc = fields_from_halfplane(c, slot, fk, n, 0, 0.0, 1.0, 0.0, 1, Z, T, 1, 2 * (n / 2 - 1) + 1))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   Slot& s = c->slot[slot];
   s.L = L;
@@ -642,7 +657,7 @@ int swrt_set_field_qk(swrt_ctx* c, int slot, const double* qk_interleaved, int64
   double2* fk = (double2*)(base + 2 * zb);
   HIPCHK(c, hipMemcpyAsync(fk, qk_interleaved, sizeof(double2) * nhalf, hipMemcpyHostToDevice,
                            c->stream));
-  if ((rc = fields_from_halfplane(c, slot, fk, n, 1, K_d2, k_scale, shear, 0, Z, T))) return rc;
+  if ((rc = fields_from_halfplane(c, slot, fk, n, 1, K_d2, k_scale, shear, 0, Z, T, 1, 2 * kmax + 1))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   Slot& s = c->slot[slot];
   s.L = L;
@@ -706,7 +721,7 @@ int swrt_k2g(swrt_ctx* c, const double* fk_in, int64_t nx, double* fg_out) {
   double2* fk = (double2*)(base + 2 * zb);
   double* raw = (double*)(base + 2 * zb + sizeof(double2) * nhalf);
   HIPCHK(c, hipMemcpyAsync(fk, fk_in, sizeof(double2) * nhalf, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(fulspec_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, fk, n, Z);
+  hipLaunchKernelGGL(fulspec_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, fk, n, Z, 1, 2 * kmax + 1);
   HIPCHK(c, hipGetLastError());
   if ((rc = inverse_2d(c, Z, T, n, 1))) return rc;
   hipLaunchKernelGGL(real_part_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, raw, nn);
@@ -1311,7 +1326,11 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
     HIPCHK(c, hipMalloc(&q.E1, sizeof(double2) * 4 * q.nhalf));
     HIPCHK(c, hipMalloc(&q.E2, sizeof(double2) * 4 * q.nhalf));
   }
-  HIPCHK(c, hipMemcpyAsync(q.qk, qk_in, hb, hipMemcpyHostToDevice, c->stream));
+  // host column-major (kx fastest) -> device ky-fastest, via qk_prev as staging
+  HIPCHK(c, hipMemcpyAsync(q.qk_prev, qk_in, hb, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(halfplane_relayout_kernel, dim3(nblocks(q.nhalf * g.nl, 256)), dim3(256), 0, c->stream,
+                     q.qk_prev, q.qk, 2 * kmax + 1, kmax + 1, 1, g.nl);
+  HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemsetAsync(q.Qm1, 0, hb, c->stream));
   HIPCHK(c, hipMemsetAsync(q.Qm2, 0, hb, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1330,9 +1349,7 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
   int rc;
   const int n = q.g.n, nl = q.g.nl;
   if ((rc = ensure_twiddles(c, n))) return rc;
-  const size_t hb = sizeof(double2) * q.nhalf * nl;
   for (int64_t s = 0; s < nsteps; ++s) {
-    HIPCHK(c, hipMemcpyAsync(q.qk_prev, q.qk, hb, hipMemcpyDeviceToDevice, c->stream));
     hipLaunchKernelGGL(qg_jac_spectra_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
     HIPCHK(c, hipGetLastError());
     if ((rc = inverse_2d(c, q.Z, q.T, n, 2 * nl))) return rc;
@@ -1348,9 +1365,11 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
       q.exp_dt = dt;
     }
     const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
+    // out of place: the new qk goes to the other buffer, the old one becomes prev_qk
     hipLaunchKernelGGL(qg_update_kernel, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
-                       abstep, q.E1, q.E2, q.qk, q.Qm1, q.Qm2);
+                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
     HIPCHK(c, hipGetLastError());
+    std::swap(q.qk, q.qk_prev);
     q.steps += 1;
     q.t = q.t + dt;
     q.has_prev = true;
@@ -1391,8 +1410,14 @@ int swrt_qg_get(swrt_ctx* c, double* qk_out, double* t_out, int64_t* steps_out) 
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   HIPCHK(c, hipSetDevice(c->device));
-  if (qk_out)
-    HIPCHK(c, hipMemcpyAsync(qk_out, q.qk, sizeof(double2) * q.nhalf * q.g.nl, hipMemcpyDeviceToHost, c->stream));
+  if (qk_out) {
+    const int kmax = q.g.n / 2 - 1;
+    double2* tmp = q.Z;  // relayout to the host's kx-fastest order
+    hipLaunchKernelGGL(halfplane_relayout_kernel, dim3(nblocks(q.nhalf * q.g.nl, 256)), dim3(256), 0, c->stream,
+                       q.qk, tmp, 2 * kmax + 1, kmax + 1, 0, q.g.nl);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(qk_out, tmp, sizeof(double2) * q.nhalf * q.g.nl, hipMemcpyDeviceToHost, c->stream));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if (t_out) *t_out = q.t;
   if (steps_out) *steps_out = q.steps;
@@ -1412,7 +1437,7 @@ int swrt_qg_get_q(swrt_ctx* c, double* q_out) {
   if ((rc = ensure_twiddles(c, n))) return rc;
   for (int l = 0; l < nl; ++l) {
     hipLaunchKernelGGL(fulspec_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk + l * q.nhalf, n,
-                       q.Z + l * q.nn);
+                       q.Z + l * q.nn, n / 2, 1);
     HIPCHK(c, hipGetLastError());
   }
   if ((rc = inverse_2d(c, q.Z, q.T, n, nl))) return rc;
@@ -1443,7 +1468,8 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   if ((rc = ensure_slot(c, slot, nx))) return rc;
   if ((rc = ensure_twiddles(c, (int)nx))) return rc;
   const double2* src = (which == 0 ? q.qk : q.qk_prev) + layer * q.nhalf;
-  if ((rc = fields_from_halfplane(c, slot, src, (int)nx, 1, q.g.K_d2, q.g.kscale, q.g.shear, 0, q.Z, q.T)))
+  if ((rc = fields_from_halfplane(c, slot, src, (int)nx, 1, q.g.K_d2, q.g.kscale, q.g.shear, 0, q.Z, q.T,
+                                  (int)(nx / 2), 1)))
     return rc;
   Slot& s = c->slot[slot];
   s.L = q.g.dx * (double)nx;

@@ -97,13 +97,15 @@ __device__ __forceinline__ double2 mul_mik(double k, double2 z) { return make_do
 // Z2 = v_x + i v_y, and (if with_psi) Z3 = psi.  Output layout [c + n*r]
 // (ky FFT index c contiguous), each Zk an n*n block.
 // mode 0: psik = fk (SpectralScheme path); mode 1: psik = -qk./(K_d2 + K2).
+// The half plane is read at fk[(kx + kmax)*sx + ky*sy]: (1, 2kmax+1) for the
+// host's column-major layout, (kmax+1, 1) for the QG state's ky-fastest one.
 __global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, double kscale,
-                               int with_psi, double2* Z) {
+                               int with_psi, double2* Z, int sx, int sy) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nn = (int64_t)n * n;
   if (idx >= nn) return;
   const int c = (int)(idx % n), r = (int)(idx / n);
-  const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int kmax = n / 2 - 1;
   const int kx = signed_k(r, n), ky = signed_k(c, n);
   double2 z[4];
 #pragma unroll
@@ -114,7 +116,7 @@ __global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, 
     int hx = kx, hy = ky;
     bool cj = false;
     if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
-    double2 q = fk[(hx + kmax) + (int64_t)nkx * hy];
+    double2 q = fk[(int64_t)(hx + kmax) * sx + (int64_t)hy * sy];
     const double kxs = (double)hx * kscale, kys = (double)hy * kscale;
     double2 ps;
     if (mode == 0) {
@@ -165,23 +167,97 @@ __global__ void unpair_kernel(const double2* Z, int n, int with_psi, double* pla
 
 // fulspec.m:10-19 + ifftshift of ONE field: full Hermitian spectrum in layout
 // [c + n*r] (ky FFT index contiguous).  DC keeps its real part only.
-__global__ void fulspec_kernel(const double2* fk, int n, double2* Z) {
+__global__ void fulspec_kernel(const double2* fk, int n, double2* Z, int sx, int sy) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nn = (int64_t)n * n;
   if (idx >= nn) return;
   const int c = (int)(idx % n), r = (int)(idx / n);
-  const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int kmax = n / 2 - 1;
   const int kx = signed_k(r, n), ky = signed_k(c, n);
   double2 z = make_double2(0.0, 0.0);
   if (kx >= -kmax && kx <= kmax && ky >= -kmax && ky <= kmax) {
     int hx = kx, hy = ky;
     bool cj = false;
     if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
-    z = fk[(hx + kmax) + (int64_t)nkx * hy];
+    z = fk[(int64_t)(hx + kmax) * sx + (int64_t)hy * sy];
     if (hx == 0 && hy == 0) z.y = 0.0;
     if (cj) z.y = -z.y;
   }
   Z[idx] = z;
+}
+
+// Fused unpair + pack: the inverse transforms T0 = u + i v, T1 = u_x + i u_y,
+// T2 = v_x + i v_y (layout [x + n*y]) -> interior node records (y fastest,
+// 48 B each) through a 16x16 LDS tile, so both the reads (along x) and the
+// record writes (along y) are contiguous.  u gets `shear` (grid_U.m:11).
+// Ghost nodes are filled by halo_nodes_kernel afterwards.
+__global__ void __launch_bounds__(256) pack_pairs_kernel(const double2* T, int n, int npad, double shear,
+                                                         double* nodes) {
+  __shared__ double2 tile[3][16][17];
+  const int64_t nn = (int64_t)n * n;
+  const int x0 = blockIdx.x * 16, y0 = blockIdx.y * 16;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) tile[k][ty][tx] = T[k * nn + (x0 + tx) + (int64_t)n * (y0 + ty)];
+  __syncthreads();
+  // write: thread (tx, ty) -> node x = x0 + ty, y = y0 + tx
+  const double2 a = tile[0][tx][ty], b = tile[1][tx][ty], c = tile[2][tx][ty];
+  double* dst = nodes + ((int64_t)(x0 + ty + 2) * npad + (y0 + tx + 2)) * 6;
+  dst[0] = a.x + shear;
+  dst[1] = a.y;
+  dst[2] = b.x;
+  dst[3] = b.y;
+  dst[4] = c.x;
+  dst[5] = c.y;
+}
+
+// Periodic ghost records of the padded node array (2 below, 3 above in each
+// direction) copied from their interior images.
+__global__ void halo_nodes_kernel(double* nodes, int nx, int npad) {
+  const int nghost_rows = npad - nx;  // 5 full padded rows/columns
+  const int64_t per = (int64_t)nghost_rows * npad;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= 2 * per) return;
+  int ip, jp;
+  if (idx < per) {  // ghost rows (all columns)
+    const int g = (int)(idx / npad);
+    jp = (int)(idx % npad);
+    ip = g < 2 ? g : nx + g;  // 0,1 and nx+2..nx+4
+  } else {          // ghost columns of the interior rows
+    const int64_t j = idx - per;
+    const int g = (int)(j / npad);
+    ip = (int)(j % npad);
+    jp = g < 2 ? g : nx + g;
+    if (ip < 2 || ip >= nx + 2) return;  // corners done by the row part
+  }
+  int ig = ((ip - 2) % nx + nx) % nx, jg = ((jp - 2) % nx + nx) % nx;
+  if ((ip >= 2 && ip < nx + 2) && (jp >= 2 && jp < nx + 2)) return;
+  const double* src = nodes + ((int64_t)(ig + 2) * npad + (jg + 2)) * 6;
+  double* dst = nodes + ((int64_t)ip * npad + jp) * 6;
+#pragma unroll
+  for (int f = 0; f < 6; ++f) dst[f] = src[f];
+}
+
+// psi plane of the packed transform T3 (layout [x + n*y]).
+__global__ void psi_plane_kernel(const double2* T3, double* psi, int64_t cnt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cnt) psi[i] = T3[i].x;
+}
+
+// Half-plane relayout: kx-fastest (host, column-major) <-> ky-fastest (QG state).
+__global__ void halfplane_relayout_kernel(const double2* in, double2* out, int nkx, int nky, int to_ky_fastest,
+                                          int nlayers) {
+  const int64_t nh = (int64_t)nkx * nky;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nh * nlayers) return;
+  const int64_t l = idx / nh, e = idx % nh;
+  if (to_ky_fastest) {  // e = ky + nky*row (write contiguous)
+    const int ky = (int)(e % nky), row = (int)(e / nky);
+    out[l * nh + e] = in[l * nh + row + (int64_t)nkx * ky];
+  } else {              // e = row + nkx*ky
+    const int row = (int)(e % nkx), ky = (int)(e / nkx);
+    out[l * nh + e] = in[l * nh + ky + (int64_t)nky * row];
+  }
 }
 
 __global__ void real_part_kernel(const double2* Z, double* out, int64_t cnt) {

@@ -9,8 +9,10 @@
 //             over swrt_qg_max_speed).
 //
 // State: qk, its two previous tendencies and the previous qk, each
-// nlayers x (2kmax+1) x (kmax+1) complex (the g2k half plane, column-major,
-// row = kx + kmax fastest), resident in HBM.  One step is
+// nlayers x (2kmax+1) x (kmax+1) complex (the g2k half plane), resident in
+// HBM in ky-fastest order (h = (kx + kmax)*(kmax+1) + ky) so that the passes
+// over the full spectrum (layout [ky + n*kx]) read and write it contiguously;
+// the C ABI converts from/to the host's column-major order.  One step is
 //   spectra of psi_x + i psi_y and q_x + i q_y per layer (Hermitian
 //   completion = fulspec)  ->  inverse 2-D FFT  ->  J = psi_x q_y - psi_y q_x
 //   (both layers packed J1 + i J2 into one forward transform)  ->  g2k crop
@@ -101,7 +103,7 @@ __global__ void qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
   int hx = kx, hy = ky;
   bool cj = false;
   if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
-  const int64_t h = inband ? (hx + kmax) + (int64_t)nkx * hy : 0;
+  const int64_t h = inband ? (int64_t)(hx + kmax) * (kmax + 1) + hy : 0;
   const double kxs = (double)hx * g.kscale, kys = (double)hy * g.kscale;
   const double K2 = kxs * kxs + kys * kys;
   cd q[2], ps[2];
@@ -195,12 +197,13 @@ __device__ __forceinline__ void expm2(const cd M[4], double t, cd E[4]) {
   E[3] = csub(A, cmul(S, D));
 }
 
-// expLdt and expL2dt for every half-plane wavenumber: E[4*idx + (2i+j)].
+// expLdt and expL2dt for every half-plane wavenumber: E[4*idx + (2i+j)]
+// (idx in the ky-fastest state order).
 __global__ void qg2_exp_kernel(QGDev g, double dt, double2* E1, double2* E2) {
   const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)nkx * (kmax + 1)) return;
-  const int row = (int)(idx % nkx), col = (int)(idx / nkx);
+  const int col = (int)(idx % (kmax + 1)), row = (int)(idx / (kmax + 1));
   const double kxs = (double)(row - kmax) * g.kscale, kys = (double)col * g.kscale;
   const double K2 = kxs * kxs + kys * kys;
   cd L[4], e[4];
@@ -225,12 +228,13 @@ __device__ __forceinline__ void mmul2(const double2* E, int64_t idx, const cd x[
 //   dq = dt*Qn | dt/2*(3Qn - X1) | dt/12*(23Qn - 16X1 + 5X2), X = Qm (1 layer)
 //   or mmult3(expL(2)dt, Qm) (2 layers); then Qm2 = Qm1, Qm1 = Qn.
 __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abstep, const double2* E1,
-                                 const double2* E2, double2* qk, double2* Qm1, double2* Qm2) {
+                                 const double2* E2, const double2* qk, double2* qk_out, double2* Qm1,
+                                 double2* Qm2) {
   const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t nhalf = (int64_t)nkx * (kmax + 1);
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nhalf) return;
-  const int row = (int)(idx % nkx), col = (int)(idx / nkx);
+  const int col = (int)(idx % (kmax + 1)), row = (int)(idx / (kmax + 1));
   const int kx = row - kmax, ky = col;
   const double kxs = (double)kx * g.kscale, kys = (double)ky * g.kscale;
   const double K2 = kxs * kxs + kys * kys;
@@ -292,7 +296,7 @@ __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abst
     mmul2(E1, idx, s, out);
   }
   for (int l = 0; l < g.nl; ++l) {
-    st(qk, l * nhalf + idx, out[l]);
+    st(qk_out, l * nhalf + idx, out[l]);
     st(Qm2, l * nhalf + idx, m1[l]);
     st(Qm1, l * nhalf + idx, Qn[l]);
   }
@@ -318,7 +322,7 @@ __global__ void qg_vel_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
   for (int l = 0; l < g.nl; ++l) {
     cd u = cmk(0.0, 0.0), v = cmk(0.0, 0.0);
     if (inband) {
-      const cd q = ld(qk, l * nhalf + (hx + kmax) + (int64_t)nkx * hy);
+      const cd q = ld(qk, l * nhalf + (int64_t)(hx + kmax) * (kmax + 1) + hy);
       const cd ps = cmk(-q.x / den, -q.y / den);
       u = cmk(kys * ps.y, -(kys * ps.x));  // (-1i*ky).*psik
       v = ik(kxs, ps);
