@@ -210,6 +210,27 @@ int swrt_omega_histogram(swrt_ctx* ctx, double f, double Cg, const double* edges
                          int64_t* counts_inout, double* mean_omega_out);
 
 /* ---------------------------------------------------------------------------
+ * ode23 packet integrator (the drivers' integrator)
+ * ------------------------------------------------------------------------ */
+
+/* Device stages of MATLAB's ode23 (Bogacki-Shampine 3(2), FSAL) over the
+ * device-resident packets as ONE 4N-vector ODE (qgsw_raytrace.m:143-150 with
+ * odefun :259-265: dx/dt = U + Cg*k/sqrt(f^2 + Cg^2|k|^2), dk/dt =
+ * -(grad U)^T k, U from interpolate_U(slot 0, slot 1, t/tmax) — nslots = 1
+ * reads slot 0 only).  The step-size controller (a global decision over the
+ * max-norm error) runs on the host; thr = AbsTol/RelTol.
+ * swrt_ode23_f1:     F1 = odefun(t, y);  *rh_raw = max |F1| ./ max(|y|, thr)
+ * swrt_ode23_attempt: stages 2-4 of one trial step of size h ending at tnew
+ *                    (ynew uses h4 = tnew - t); *err_raw = max over all
+ *                    components of |F*E| ./ max(max(|y|, |ynew|), thr)
+ * swrt_ode23_accept: y = ynew, F1 = F4 (FSAL). */
+int swrt_ode23_f1(swrt_ctx* ctx, double t, double tmax, double f, double Cg, int nslots, double thr, double bump,
+                  double* rh_raw_out);
+int swrt_ode23_attempt(swrt_ctx* ctx, double t, double h, double tnew, double tmax, double f, double Cg,
+                       int nslots, double thr, double bump, double* err_raw_out);
+int swrt_ode23_accept(swrt_ctx* ctx);
+
+/* ---------------------------------------------------------------------------
  * QG PDE stepper: the snapshots' producer, device-resident
  * ------------------------------------------------------------------------ */
 

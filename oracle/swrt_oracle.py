@@ -884,3 +884,110 @@ class QG2Oracle:
         self.Qm[1] = self.Qm[0]
         self.Qm[0] = Qn
         self.qk = mmult3(self.expLdt, self.qk + dq)
+
+
+# ----------------------------------------------------------------------------
+# ode23 — the production drivers' packet integrator (qgsw_raytrace.m:143-150,
+# qg2layersw_raytrace.m:189-196).  MATLAB's ode23 is
+# proprietary and not vendored: this restates its published algorithm
+# (Bogacki-Shampine 3(2) pair, FSAL; Shampine & Reichelt, "The MATLAB ODE
+# Suite", SIAM J. Sci. Comput. 18 (1997)) with R2020b's defaults RelTol 1e-3,
+# AbsTol 1e-6, MaxStep 0.1*|tspan|, max-norm error control, the initial-step
+# heuristic and the step-size update rules.  PARITY UNPINNED against MATLAB
+# itself (no reference run or fixture exists); the GPU path is pinned to
+# this restatement.
+# ----------------------------------------------------------------------------
+def raytracing_rhs(flow1, flow2, f, Cg, tmax, h, nyF=None, bump=BUMP_QG):
+    """generate_raytracing_ode / odefun (qgsw_raytrace.m:258-268): y is the 4N
+    column [x(:,1); x(:,2); k(:,1); k(:,2)] (ode_xk2y, :238-244)."""
+    def odefun(t, y):
+        n = y.size // 4
+        x = np.stack([y[0:n], y[n:2 * n]], axis=1)
+        k = np.stack([y[2 * n:3 * n], y[3 * n:4 * n]], axis=1)
+        U, nab = interpolate_U(flow1, flow2, t / tmax, x, h, bump=bump, nyF=nyF)
+        s = np.sqrt(f**2 + Cg**2 * (k[:, 0] * k[:, 0] + k[:, 1] * k[:, 1]))
+        dxdt = U + (Cg * k) / s[:, None]
+        dk1 = -(nab["u_x"] * k[:, 0] + nab["v_x"] * k[:, 1])
+        dk2 = -(nab["u_y"] * k[:, 0] + nab["v_y"] * k[:, 1])
+        return np.concatenate([dxdt[:, 0], dxdt[:, 1], dk1, dk2])
+    return odefun
+
+
+ODE23_A = (0.5, 0.75, 1.0)
+ODE23_B3 = (2.0 / 9.0, 1.0 / 3.0, 4.0 / 9.0)
+ODE23_E = (-5.0 / 72.0, 1.0 / 12.0, 1.0 / 9.0, -1.0 / 8.0)
+
+
+def ode23(odefun, tspan, y0, rtol=1e-3, atol=1e-6, stats=None):
+    """[t, y] = ode23(odefun, [t0 tfinal], y0) restricted to what the drivers
+    use (scalar AbsTol, no events/mass/NonNegative, Refine irrelevant since
+    only y(end) is consumed).  Returns (t_accepted, y_final)."""
+    t0, tfinal = float(tspan[0]), float(tspan[1])
+    tdir = math.copysign(1.0, tfinal - t0)
+    pow_ = 1.0 / 3.0
+    rtol = max(rtol, 100 * np.finfo(float).eps)
+    threshold = atol / rtol
+    htspan = abs(tfinal - t0)
+    hmax = 0.1 * htspan
+    t = t0
+    y = np.array(y0, dtype=np.float64)
+    f1 = odefun(t, y)
+    # initial step (ode23.m: absh = min(hmax, htspan); rh = ...)
+    absh = min(hmax, htspan)
+    rh = np.max(np.abs(f1) / np.maximum(np.abs(y), threshold)) / (0.8 * rtol**pow_)
+    if absh * rh > 1:
+        absh = 1.0 / rh
+    absh = max(absh, 16 * np.spacing(t))
+    ts = [t]
+    done = False
+    nfailed = 0
+    while not done:
+        hmin = 16 * np.spacing(t)
+        absh = min(hmax, max(hmin, absh))
+        h = tdir * absh
+        if 1.1 * absh >= abs(tfinal - t):
+            h = tfinal - t
+            absh = abs(h)
+            done = True
+        nofailed = True
+        while True:
+            y2 = y + f1 * (h * 0.5)
+            f2 = odefun(t + h * ODE23_A[0], y2)
+            y3 = y + f2 * (h * 0.75)
+            f3 = odefun(t + h * ODE23_A[1], y3)
+            tnew = t + h * ODE23_A[2]
+            if done:
+                tnew = tfinal
+            h = tnew - t
+            ynew = y + (((f1 * (h * ODE23_B3[0])) + f2 * (h * ODE23_B3[1])) + f3 * (h * ODE23_B3[2]))
+            f4 = odefun(tnew, ynew)
+            fE = ((f1 * ODE23_E[0] + f2 * ODE23_E[1]) + f3 * ODE23_E[2]) + f4 * ODE23_E[3]
+            err = absh * np.max(np.abs(fE) / np.maximum(np.maximum(np.abs(y), np.abs(ynew)), threshold))
+            if err > rtol:
+                nfailed += 1
+                if absh <= hmin:
+                    raise RuntimeError(f"ode23: step size {absh} below hmin at t={t}")
+                if nofailed:
+                    nofailed = False
+                    absh = max(hmin, absh * max(0.5, 0.8 * (rtol / err) ** pow_))
+                else:
+                    absh = max(hmin, 0.5 * absh)
+                h = tdir * absh
+                done = False
+            else:
+                break
+        t = tnew
+        y = ynew
+        f1 = f4
+        ts.append(t)
+        if done:
+            break
+        if nofailed:
+            temp = 1.25 * (err / rtol) ** pow_
+            if temp > 0.2:
+                absh = absh / temp
+            else:
+                absh = 5.0 * absh
+    if stats is not None:
+        stats.update(steps=len(ts) - 1, failed=nfailed)
+    return np.array(ts), y

@@ -73,6 +73,9 @@ SIGNATURES = {
     "swrt_spectral_eval": (_INT, [_VP, _P, _P, _I, _INT, _P]),
     "swrt_spectral_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT]),
     "swrt_omega_histogram": (_INT, [_VP, _D, _D, _P, _I, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(_D)]),
+    "swrt_ode23_f1": (_INT, [_VP, _D, _D, _D, _D, _INT, _D, _D, ctypes.POINTER(_D)]),
+    "swrt_ode23_attempt": (_INT, [_VP, _D, _D, _D, _D, _D, _D, _INT, _D, _D, ctypes.POINTER(_D)]),
+    "swrt_ode23_accept": (_INT, [_VP]),
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_max_speed": (_INT, [_VP, ctypes.POINTER(_D)]),
@@ -328,6 +331,23 @@ class Context:
                                                counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                                                ctypes.byref(mean)), "swrt_omega_histogram")
         return counts, mean.value
+
+    # ---- ode23 device stages (swrt_ode23_*) --------------------------------
+    def ode23_f1(self, t, tmax, f, Cg, nslots, thr, bump):
+        r = _D()
+        self._chk(self._L.swrt_ode23_f1(self._h, float(t), float(tmax), float(f), float(Cg), int(nslots),
+                                        float(thr), float(bump), ctypes.byref(r)), "swrt_ode23_f1")
+        return r.value
+
+    def ode23_attempt(self, t, h, tnew, tmax, f, Cg, nslots, thr, bump):
+        r = _D()
+        self._chk(self._L.swrt_ode23_attempt(self._h, float(t), float(h), float(tnew), float(tmax), float(f),
+                                             float(Cg), int(nslots), float(thr), float(bump), ctypes.byref(r)),
+                  "swrt_ode23_attempt")
+        return r.value
+
+    def ode23_accept(self):
+        self._chk(self._L.swrt_ode23_accept(self._h), "swrt_ode23_accept")
 
     # ---- QG PDE stepper (swrt_qg_*) ---------------------------------------
     def qg_init(self, params: QGParams, nx, qk):

@@ -21,6 +21,7 @@
 #include "swrt_tile.hpp"
 #include "swrt_persist.hpp"
 #include "swrt_qg.hpp"
+#include "swrt_ode23.hpp"
 #include "swrt_xka.hpp"
 #include "swrt_spectral.hpp"
 #include "swrt_diag.hpp"
@@ -137,6 +138,12 @@ struct swrt_ctx {
   bool modes_set = false;
   int64_t mode_active = 0;  // coefficients inside the per-row nonzero spans
   QGState qg;
+  // ode23 stage buffers (cap-sized, device packet order)
+  double* oF[4] = {nullptr, nullptr, nullptr, nullptr};
+  double* o_ynx = nullptr;
+  double* o_ynk = nullptr;
+  int64_t o_cap = 0;
+  unsigned long long* o_dmax = nullptr;
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -553,6 +560,9 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->qg.qk, (void*)c->qg.qk_prev, (void*)c->qg.Qm1, (void*)c->qg.Qm2, (void*)c->qg.E1,
                   (void*)c->qg.E2, (void*)c->qg.Z, (void*)c->qg.T, (void*)c->qg.dmax})
+    if (p) (void)hipFree(p);
+  for (void* p : {(void*)c->oF[0], (void*)c->oF[1], (void*)c->oF[2], (void*)c->oF[3], (void*)c->o_ynx,
+                  (void*)c->o_ynk, (void*)c->o_dmax})
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->stream);
@@ -1485,6 +1495,122 @@ int swrt_swap_slots(swrt_ctx* c, int a, int b) {
   if (a < 0 || a >= SWRT_MAX_SLOTS || b < 0 || b >= SWRT_MAX_SLOTS) return fail(c, SWRT_ERR_ARG, "slot out of range");
   std::swap(c->slot[a], c->slot[b]);
   c->keys_fresh = false;
+  return SWRT_OK;
+}
+
+// ---------------------------------------------------------------------------
+// ode23 device stages (swrt_ode23.hpp)
+// ---------------------------------------------------------------------------
+namespace {
+int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, double Cg, double thr,
+                  double bump) {
+  if (c->n <= 0 || !c->dx) return fail(c, SWRT_ERR_STATE, "no packets (swrt_packets_set)");
+  if (nslots != 1 && nslots != 2) return fail(c, SWRT_ERR_ARG, "nslots must be 1 or 2");
+  if (!c->slot[0].set || (nslots == 2 && !c->slot[1].set)) return fail(c, SWRT_ERR_STATE, "field slot not set");
+  if (nslots == 2 && c->slot[1].nx != c->slot[0].nx) return fail(c, SWRT_ERR_ARG, "slots differ in nx");
+  if (c->o_cap < c->cap) {
+    for (double*& p : c->oF) { if (p) (void)hipFree(p); p = nullptr; }
+    if (c->o_ynx) (void)hipFree(c->o_ynx);
+    if (c->o_ynk) (void)hipFree(c->o_ynk);
+    c->o_ynx = c->o_ynk = nullptr;
+    c->o_cap = 0;
+    for (double*& p : c->oF) HIPCHK(c, hipMalloc(&p, sizeof(double) * 4 * c->cap));
+    HIPCHK(c, hipMalloc(&c->o_ynx, sizeof(double) * 2 * c->cap));
+    HIPCHK(c, hipMalloc(&c->o_ynk, sizeof(double) * 2 * c->cap));
+    c->o_cap = c->cap;
+  }
+  if (!c->o_dmax) HIPCHK(c, hipMalloc(&c->o_dmax, sizeof(unsigned long long)));
+  a.f0 = view_of(c->slot[0]);
+  a.f1 = nslots == 2 ? view_of(c->slot[1]) : a.f0;
+  a.nslots = nslots;
+  a.n = c->n;
+  a.yx = c->dx;
+  a.yk = c->dk;
+  for (int s = 0; s < 4; ++s) a.F[s] = c->oF[s];
+  a.ynx = c->o_ynx;
+  a.ynk = c->o_ynk;
+  a.tmax = tmax;
+  a.inv_tmax = 0.0;
+  a.f2 = f * f;
+  a.Cg = Cg;
+  a.Cg2 = Cg * Cg;
+  a.thr = thr;
+  a.bump = bump;
+  a.dmax = c->o_dmax;
+  return SWRT_OK;
+}
+
+int read_max(swrt_ctx* c, double* out) {
+  unsigned long long bits = 0;
+  HIPCHK(c, hipMemcpyAsync(&bits, c->o_dmax, sizeof(bits), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  std::memcpy(out, &bits, sizeof(double));
+  return SWRT_OK;
+}
+}  // namespace
+
+int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int nslots, double thr, double bump,
+                  double* rh_raw_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  // one spatial re-binning per ode23 call (the packet order is free: the
+  // error norm is a max over all components)
+  if (c->rebin_every > 0 && c->slot[0].set) {
+    if ((rc = rebin(c))) return rc;
+  }
+  Ode23Args a;
+  if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;
+  a.ts = t;
+  HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(ode23_stage_kernel<1>, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  if (rh_raw_out) return read_max(c, rh_raw_out);
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax, double f, double Cg,
+                       int nslots, double thr, double bump, double* err_raw_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  Ode23Args a;
+  if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;
+  const unsigned grid = nblocks(c->n, 256);
+  // ode23: f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2)
+  a.ts = t + h * 0.5;
+  a.c[0] = h * 0.5;
+  hipLaunchKernelGGL(ode23_stage_kernel<2>, dim3(grid), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  a.ts = t + h * 0.75;
+  a.c[0] = h * 0.75;
+  hipLaunchKernelGGL(ode23_stage_kernel<3>, dim3(grid), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  // h = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew
+  const double h4 = tnew - t;
+  a.ts = tnew;
+  a.c[0] = h4 * (2.0 / 9.0);
+  a.c[1] = h4 * (1.0 / 3.0);
+  a.c[2] = h4 * (4.0 / 9.0);
+  HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(ode23_stage_kernel<4>, dim3(grid), dim3(256), 0, c->stream, a);
+  HIPCHK(c, hipGetLastError());
+  if (err_raw_out) return read_max(c, err_raw_out);
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_ode23_accept(swrt_ctx* c) {
+  if (!c) return SWRT_ERR_ARG;
+  if (!c->o_ynx) return fail(c, SWRT_ERR_STATE, "no ode23 step attempted");
+  std::swap(c->dx, c->o_ynx);
+  std::swap(c->dk, c->o_ynk);
+  std::swap(c->oF[0], c->oF[3]);
+  c->keys_fresh = false;
+  c->cells_sorted = false;
   return SWRT_OK;
 }
 

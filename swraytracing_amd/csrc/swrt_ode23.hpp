@@ -1,0 +1,112 @@
+// swrt_ode23.hpp — device stages of the drivers' ode23 packet integrator
+// (qgsw_raytrace.m:143-150, qg2layersw_raytrace.m:189-196).
+//
+// MATLAB's ode23 (Bogacki-Shampine 3(2), FSAL, max-norm error control)
+// integrates all packets as ONE 4N-vector ODE, so the step size is a global
+// decision; the host controller (swraytracing_amd/integrate.py ode23_packets)
+// keeps that logic, the device does everything per packet:
+//   stage 1:  F1 = odefun(t, y)             + max |F1| / max(|y|, thr)   (initial step)
+//   stage 2:  F2 = odefun(t + h/2, y + F1*(h/2))
+//   stage 3:  F3 = odefun(t + 3h/4, y + F2*(3h/4))
+//   stage 4:  ynew = y + ((F1*(2h/9) + F2*(h/3)) + F3*(4h/9)),  F4 = odefun(tnew, ynew),
+//             max |((F1 E1 + F2 E2) + F3 E3) + F4 E4| / max(max(|y|, |ynew|), thr)
+// odefun (qgsw_raytrace.m:259-265): dx/dt = U + Cg*k./sqrt(f^2 + Cg^2*|k|^2),
+// dk/dt = -[u_x k + v_x l, u_y k + v_y l], U and grad U from interpolate_U at
+// alpha = t/tmax (same stencil code as every packet kernel).  The vectors are
+// SoA over the device-ordered packets: y = {x, y} (2N) and {k, l} (2N).
+// The max-norms leave the kernel as the bit pattern of a non-negative double
+// through atomicMax (order independent, so the result is exact).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "swrt_kernels.hpp"
+
+namespace swrt {
+
+struct Ode23Args {
+  FieldView f0, f1;
+  int nslots;
+  int64_t n;
+  const double* yx;  // x, y   (2N)
+  const double* yk;  // k, l   (2N)
+  double* F[4];      // stage derivatives, 4N each: [dx; dy; dk; dl]
+  double* ynx;       // ynew x, y (stage 4)
+  double* ynk;       // ynew k, l
+  double ts;         // stage time
+  double inv_tmax;   // unused when tmax == 0 (steady)
+  double tmax;
+  double f2, Cg, Cg2;
+  double c[3];       // stage coefficients (already multiplied by h)
+  double thr;        // AbsTol / RelTol
+  double bump;
+  unsigned long long* dmax;
+};
+
+__device__ __forceinline__ void ode_rhs(const Ode23Args& a, const double ys[4], double fo[4]) {
+  const double alpha = a.tmax != 0.0 ? a.ts / a.tmax : 0.0;  // interpolate_U(..., t/tmax, ...)
+  double I[kRec];
+  eval_flow(a.f0, a.f1, a.nslots, alpha, ys[0], ys[1], a.bump, I);
+  const double k1 = ys[2], k2 = ys[3];
+  const double s = sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2));
+  fo[0] = I[0] + (a.Cg * k1) / s;
+  fo[1] = I[1] + (a.Cg * k2) / s;
+  fo[2] = -(I[2] * k1 + I[4] * k2);
+  fo[3] = -(I[3] * k1 + I[5] * k2);
+}
+
+__device__ __forceinline__ void block_max_to(double m, unsigned long long* out) {
+  __shared__ double red[256];
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicMax(out, (unsigned long long)__double_as_longlong(red[0]));
+}
+
+template <int STAGE>
+__global__ void __launch_bounds__(256) ode23_stage_kernel(Ode23Args a) {
+  const int64_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const int64_t n = a.n;
+  double m = 0.0;
+  if (p < n) {
+    const double y[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
+    double ys[4];
+    if constexpr (STAGE == 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ys[c] = y[c];
+    } else if constexpr (STAGE == 2 || STAGE == 3) {
+      const double* Fp = a.F[STAGE - 2];  // F1 for stage 2, F2 for stage 3
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ys[c] = y[c] + Fp[c * n + p] * a.c[0];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        ys[c] = y[c] + (((a.F[0][c * n + p] * a.c[0]) + a.F[1][c * n + p] * a.c[1]) + a.F[2][c * n + p] * a.c[2]);
+      a.ynx[p] = ys[0]; a.ynx[n + p] = ys[1];
+      a.ynk[p] = ys[2]; a.ynk[n + p] = ys[3];
+    }
+    double fo[4];
+    ode_rhs(a, ys, fo);
+    double* Fo = a.F[STAGE - 1];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) Fo[c * n + p] = fo[c];
+    if constexpr (STAGE == 1) {
+      // norm(f0 ./ max(abs(y), threshold), inf)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) m = fmax(m, fabs(fo[c]) / fmax(fabs(y[c]), a.thr));
+    } else if constexpr (STAGE == 4) {
+      constexpr double E1 = -5.0 / 72.0, E2 = 1.0 / 12.0, E3 = 1.0 / 9.0, E4 = -1.0 / 8.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double fe = ((a.F[0][c * n + p] * E1 + a.F[1][c * n + p] * E2) + a.F[2][c * n + p] * E3) + fo[c] * E4;
+        m = fmax(m, fabs(fe) / fmax(fmax(fabs(y[c]), fabs(ys[c])), a.thr));
+      }
+    }
+  }
+  if constexpr (STAGE == 1 || STAGE == 4) block_max_to(m, a.dmax);
+}
+
+}  // namespace swrt

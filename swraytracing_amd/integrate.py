@@ -71,6 +71,78 @@ def ode_symplectic(x0, k0, dt, T, f, gH, scheme):
     return x, k, t
 
 
+def ode23_packets(ctx: Context, tspan, tmax, f, Cg, nslots=2, rtol=1e-3, atol=1e-6, bump=BUMP_QG,
+                  allreduce_max=None, stats=None):
+    """[~, y] = ode23(ray_ode, tspan, y0) for the device-resident packets
+    (qgsw_raytrace.m:143-150, qg2layersw_raytrace.m:189-196): MATLAB ode23's
+    Bogacki-Shampine controller (defaults RelTol 1e-3, AbsTol 1e-6, MaxStep
+    0.1*|tspan|, max-norm error, its initial-step heuristic and step update)
+    on the host, every per-packet stage on the GPU (swrt_ode23_*).  The error
+    norm is global over all packets — with packets sharded over ranks pass
+    ``allreduce_max`` (a callable max-reducing one float over the ranks, e.g.
+    an RCCL all_reduce) so every rank takes the same steps.
+    Parity: bit-identical to oracle ode23 (its restatement; MATLAB itself is
+    unpinned).  Returns the accepted times."""
+    red = allreduce_max or (lambda v: v)
+    t0, tfinal = float(tspan[0]), float(tspan[1])
+    tdir = math.copysign(1.0, tfinal - t0)
+    pw = 1.0 / 3.0
+    rtol = max(rtol, 100 * np.finfo(float).eps)
+    thr = atol / rtol
+    htspan = abs(tfinal - t0)
+    hmax = 0.1 * htspan
+    t = t0
+    rh = red(ctx.ode23_f1(t, tmax, f, Cg, nslots, thr, bump)) / (0.8 * rtol ** pw)
+    absh = min(hmax, htspan)
+    if absh * rh > 1:
+        absh = 1.0 / rh
+    absh = max(absh, 16 * np.spacing(t))
+    ts = [t]
+    done = False
+    nfailed = 0
+    attempts = 0
+    while not done:
+        hmin = 16 * np.spacing(t)
+        absh = min(hmax, max(hmin, absh))
+        h = tdir * absh
+        if 1.1 * absh >= abs(tfinal - t):
+            h = tfinal - t
+            absh = abs(h)
+            done = True
+        nofailed = True
+        while True:
+            tnew = t + h * 1.0
+            if done:
+                tnew = tfinal
+            attempts += 1
+            err = absh * red(ctx.ode23_attempt(t, h, tnew, tmax, f, Cg, nslots, thr, bump))
+            h = tnew - t
+            if err > rtol:
+                nfailed += 1
+                if absh <= hmin:
+                    raise RuntimeError(f"ode23: step size {absh} below hmin at t={t}")
+                if nofailed:
+                    nofailed = False
+                    absh = max(hmin, absh * max(0.5, 0.8 * (rtol / err) ** pw))
+                else:
+                    absh = max(hmin, 0.5 * absh)
+                h = tdir * absh
+                done = False
+            else:
+                break
+        ctx.ode23_accept()
+        t = tnew
+        ts.append(t)
+        if done:
+            break
+        if nofailed:
+            temp = 1.25 * (err / rtol) ** pw
+            absh = absh / temp if temp > 0.2 else 5.0 * absh
+    if stats is not None:
+        stats.update(steps=len(ts) - 1, failed=nfailed, attempts=attempts)
+    return np.array(ts)
+
+
 class PacketEnsemble:
     """Device-resident packets advanced through a sequence of background
     snapshots — the packet branch of qgsw_raytrace.m:140-163 /
@@ -111,6 +183,12 @@ class PacketEnsemble:
         h = dt / nsub
         self.ctx.advance(h, nsub, self.f, self.gH, nslots=2, alpha0=0.5 / nsub, dalpha=1.0 / nsub,
                          bump=self.bump, save_every=save_every)
+
+    def advance_ode23(self, dt, rtol=1e-3, atol=1e-6, allreduce_max=None, stats=None):
+        """The reference drivers' own integrator over [0, dt] with
+        interpolate_U's alpha = t/dt (ode23(ray_ode, [0, dt], y0))."""
+        return ode23_packets(self.ctx, (0.0, dt), dt, self.f, self.Cg, nslots=2, rtol=rtol, atol=atol,
+                             bump=self.bump, allreduce_max=allreduce_max, stats=stats)
 
     def state(self):
         return self.ctx.packets_get()

@@ -1,0 +1,91 @@
+"""GPU ode23 (swrt_ode23_* stages + the host controller ode23_packets) against
+the oracle's restatement of MATLAB ode23 with the drivers' odefun
+(qgsw_raytrace.m:143-150,259-265).  Every stage is the same IEEE-754 op
+sequence as the oracle (same stencil code, correctly rounded sqrt/division,
+-ffp-contract=off) and the error norm is a max, so the step sequence and the
+final state are bit-identical.  (MATLAB's own ode23 is not pinned.)"""
+import numpy as np
+import pytest
+
+import swraytracing_amd as sw
+from oracle import swrt_oracle as orc
+from tests.test_gpu_parity import _planes
+
+pytestmark = pytest.mark.gpu
+
+
+def _y0(x, k):
+    return np.concatenate([x[:, 0], x[:, 1], k[:, 0], k[:, 1]])
+
+
+@pytest.mark.parametrize("rebin", [0, 4])
+def test_ode23_packets_bitexact(ctx, qg_case, rebin):
+    c = qg_case
+    nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    flow1 = c["flow"]
+    flow2 = {n: np.asarray(v) * 1.3 for n, v in flow1.items()}
+    ctx.set_field_grid(0, _planes(flow1), nx, L)
+    ctx.set_field_grid(1, _planes(flow2), nx, L)
+    x, k = c["x"][:200], c["k"][:200]
+    tmax = 40 * c["dt"]  # long enough for several (and some rejected) steps
+    ctx.set_locality(rebin, 0)
+    try:
+        ctx.packets_set(x, k)
+        st = {}
+        ts = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, stats=st)
+        xg, kg = ctx.packets_get()
+    finally:
+        ctx.set_locality(4, 0)
+    rhs = orc.raytracing_rhs(flow1, flow2, f, Cg, tmax, L / nx)
+    so = {}
+    to, yo = orc.ode23(rhs, [0.0, tmax], _y0(x, k), stats=so)
+    n = x.shape[0]
+    np.testing.assert_array_equal(ts, to)
+    assert so["failed"] > 0 and so["steps"] > 10
+    assert st["steps"] == so["steps"] and st["failed"] == so["failed"]
+    np.testing.assert_array_equal(xg[:, 0], yo[:n])
+    np.testing.assert_array_equal(xg[:, 1], yo[n:2 * n])
+    np.testing.assert_array_equal(kg[:, 0], yo[2 * n:3 * n])
+    np.testing.assert_array_equal(kg[:, 1], yo[3 * n:])
+
+
+def test_ode23_rejections_happen_and_match(ctx, qg_case):
+    """A loose start (tiny rtol) forces rejected steps; still bit-identical."""
+    c = qg_case
+    nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    flow1 = c["flow"]
+    flow2 = {n: np.asarray(v) * -0.7 for n, v in flow1.items()}
+    ctx.set_field_grid(0, _planes(flow1), nx, L)
+    ctx.set_field_grid(1, _planes(flow2), nx, L)
+    x, k = c["x"][:64], c["k"][:64] * 4
+    tmax = 60 * c["dt"]
+    ctx.packets_set(x, k)
+    st = {}
+    ts = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, rtol=1e-6, atol=1e-9, stats=st)
+    xg, kg = ctx.packets_get()
+    so = {}
+    to, yo = orc.ode23(orc.raytracing_rhs(flow1, flow2, f, Cg, tmax, L / nx), [0.0, tmax], _y0(x, k),
+                       rtol=1e-6, atol=1e-9, stats=so)
+    np.testing.assert_array_equal(ts, to)
+    assert so["failed"] > 0
+    assert st["failed"] == so["failed"]
+    np.testing.assert_array_equal(np.concatenate([xg[:, 0], xg[:, 1], kg[:, 0], kg[:, 1]]), yo)
+
+
+def test_packet_ensemble_ode23_interval(ctx, qg_case):
+    """PacketEnsemble.advance_ode23 == ode23(ray_ode, [0, dt], y0) with the
+    snapshots in slots 0/1 (the drivers' packet branch)."""
+    c = qg_case
+    nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    ens = sw.PacketEnsemble(c["x"], c["k"], L, f, Cg, nx, c["K_d2"], ctx=ctx)
+    q2 = c["qk"] * np.exp(0.1j)
+    ens.set_snapshots(c["qk"], q2)
+    dt = 25 * c["dt"]
+    ens.advance_ode23(dt)
+    xg, kg = ens.state()
+    p0 = ctx.get_field_grid(0, nx)
+    p1 = ctx.get_field_grid(1, nx)
+    fl = lambda p: {n: p[i].reshape((nx, nx), order="F") for i, n in enumerate(orc.FIELD_ORDER)}
+    to, yo = orc.ode23(orc.raytracing_rhs(fl(p0), fl(p1), f, Cg, dt, L / nx), [0.0, dt], _y0(c["x"], c["k"]))
+    n = c["x"].shape[0]
+    np.testing.assert_array_equal(np.concatenate([xg[:, 0], xg[:, 1], kg[:, 0], kg[:, 1]]), yo)

@@ -129,3 +129,40 @@ def test_qg_oracle_random_field_stays_finite(layers):
         for _ in range(10):
             m.step()
     assert np.isfinite(m.qk).all()
+
+
+# ---------------------------------------------------------------------------
+# ode23 restatement (oracle.ode23; MATLAB's own ode23 is unpinned)
+# ---------------------------------------------------------------------------
+def test_ode23_exponential_decay_within_tolerance():
+    st = {}
+    ts, y = orc.ode23(lambda t, y: -y, [0.0, 1.0], np.array([1.0, 2.0]), stats=st)
+    np.testing.assert_allclose(y, np.exp(-1.0) * np.array([1.0, 2.0]), rtol=1e-4)
+    assert ts[0] == 0.0 and ts[-1] == 1.0
+    assert st["steps"] >= 10  # MaxStep = 0.1*|tspan| bounds every step
+
+
+def test_ode23_constant_rhs_is_exact():
+    """y' = c: every stage combination reproduces c, the error estimate is 0
+    (sum E = 0) and the solution is y0 + t*c up to the additions' round-off."""
+    c = np.array([0.3, -1.2, 2.0])
+    ts, y = orc.ode23(lambda t, y: c.copy(), [0.0, 2.0], np.zeros(3))
+    np.testing.assert_allclose(y, 2.0 * c, rtol=1e-13)
+
+
+def test_ode23_raytracing_rhs_zero_flow_is_linear_drift():
+    """SW_zero_background_raytracing config (U = 0): x(t) = x0 + t*Cg*k/omega(k), k fixed."""
+    nx = 16
+    zero = {n: np.zeros((nx, nx)) for n in orc.FIELD_ORDER}
+    f, Cg = 3.0, 1.0
+    rhs = orc.raytracing_rhs(zero, zero, f, Cg, 1.0, 2 * np.pi / nx)
+    rng = np.random.default_rng(0)
+    x0 = rng.random((20, 2))
+    k0 = rng.normal(size=(20, 2)) * 3
+    y0 = np.concatenate([x0[:, 0], x0[:, 1], k0[:, 0], k0[:, 1]])
+    ts, y = orc.ode23(rhs, [0.0, 0.7], y0)
+    om = np.sqrt(f ** 2 + Cg ** 2 * (k0 ** 2).sum(1))
+    want = x0 + 0.7 * Cg * k0 / om[:, None]
+    np.testing.assert_allclose(y[:20], want[:, 0], rtol=1e-13)
+    np.testing.assert_allclose(y[20:40], want[:, 1], rtol=1e-13)
+    np.testing.assert_array_equal(y[40:], y0[40:])

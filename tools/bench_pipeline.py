@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--packets", type=int, default=1_000_000)
     ap.add_argument("--nsub", type=int, default=4)
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--ode23", action="store_true", help="also time the drivers' ode23 over one PDE interval")
     args = ap.parse_args()
     nx, L, f, Cg = args.nx, 20.0, 3.0, 1.0
     ctx = sw.Context(0)
@@ -71,12 +72,22 @@ def main():
         ens.advance(d, args.nsub)
 
     full = timed(ctx, full_step, r)
+    ode = None
+    if args.ode23:
+        st = {}
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        ens.advance_ode23(state["dt"], stats=st)
+        ctx.synchronize()
+        ode = {"interval_ms": (time.perf_counter() - t0) * 1e3, **st,
+               "rhs_evals": 1 + 3 * st["attempts"]}
     xg, kg = ens.state()
     out = {
         "metric": "driver step time, qg2layersw_raytrace loop on device (PDE + snapshots + packets)",
         "config": {"nx": nx, "layers": 2, "packets": args.packets, "nsub": args.nsub, "steps": r},
         "pde_ms": pde, "cfl_ms": cfl, "snapshot_ms": snap, "packets_ms": pk, "step_ms": full,
         "packet_steps_per_s": args.packets * args.nsub / (full / 1e3),
+        "ode23": ode,
         "finite": bool(np.isfinite(xg).all() and np.isfinite(kg).all()),
     }
     print(json.dumps(out))
