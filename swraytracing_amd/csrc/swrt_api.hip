@@ -1549,6 +1549,30 @@ int read_max(swrt_ctx* c, double* out) {
 }
 }  // namespace
 
+}  // extern "C"
+namespace {
+// one ode23 stage over all packets: the LDS-tiled kernel when the packets are
+// binned by the tile kernel's 16x16-cell tiles, else one lane per packet
+template <int STAGE>
+int ode23_launch(swrt_ctx* c, const Ode23Args& a) {
+  const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  if (use_tile_kernel(c) && c->bin_valid && c->nbins == ntx * ntx) {
+    const int* starts = c->bins + 2 * kMaxBins;
+    if (a.nslots == 2)
+      hipLaunchKernelGGL((tile_ode23_kernel<STAGE, true, kTile, kMargin, kTileThreads>), dim3(ntx * ntx),
+                         dim3(kTileThreads), 0, c->stream, a, starts, ntx);
+    else
+      hipLaunchKernelGGL((tile_ode23_kernel<STAGE, false, kTile, kMargin, kTileThreads>), dim3(ntx * ntx),
+                         dim3(kTileThreads), 0, c->stream, a, starts, ntx);
+  } else {
+    hipLaunchKernelGGL(ode23_stage_kernel<STAGE>, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, a);
+  }
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+}  // namespace
+extern "C" {
+
 int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int nslots, double thr, double bump,
                   double* rh_raw_out) {
   if (!c) return SWRT_ERR_ARG;
@@ -1564,8 +1588,7 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
   if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;
   a.ts = t;
   HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL(ode23_stage_kernel<1>, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
+  if ((rc = ode23_launch<1>(c, a))) return rc;
   if (rh_raw_out) return read_max(c, rh_raw_out);
   return SWRT_OK;
   GUARD_END(c)
@@ -1579,16 +1602,13 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
   int rc;
   Ode23Args a;
   if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;
-  const unsigned grid = nblocks(c->n, 256);
   // ode23: f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2)
   a.ts = t + h * 0.5;
   a.c[0] = h * 0.5;
-  hipLaunchKernelGGL(ode23_stage_kernel<2>, dim3(grid), dim3(256), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
+  if ((rc = ode23_launch<2>(c, a))) return rc;
   a.ts = t + h * 0.75;
   a.c[0] = h * 0.75;
-  hipLaunchKernelGGL(ode23_stage_kernel<3>, dim3(grid), dim3(256), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
+  if ((rc = ode23_launch<3>(c, a))) return rc;
   // h = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew
   const double h4 = tnew - t;
   a.ts = tnew;
@@ -1596,8 +1616,7 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
   a.c[1] = h4 * (1.0 / 3.0);
   a.c[2] = h4 * (4.0 / 9.0);
   HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL(ode23_stage_kernel<4>, dim3(grid), dim3(256), 0, c->stream, a);
-  HIPCHK(c, hipGetLastError());
+  if ((rc = ode23_launch<4>(c, a))) return rc;
   if (err_raw_out) return read_max(c, err_raw_out);
   return SWRT_OK;
   GUARD_END(c)

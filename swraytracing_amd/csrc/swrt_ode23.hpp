@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "swrt_kernels.hpp"
+#include "swrt_tile.hpp"
 
 namespace swrt {
 
@@ -107,6 +108,91 @@ __global__ void __launch_bounds__(256) ode23_stage_kernel(Ode23Args a) {
     }
   }
   if constexpr (STAGE == 1 || STAGE == 4) block_max_to(m, a.dmax);
+}
+
+// The same four stages over spatially binned packets, one workgroup per
+// T x T-cell tile with the field window of both snapshots in LDS
+// (stage_window_regs; the packets move well under the M-cell margin within
+// one PDE interval, a packet outside it takes the global gather).  Same
+// arithmetic as ode23_stage_kernel, so the same bits.
+template <int STAGE, bool TWO, int T, int M, int NT>
+__global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const int* starts, int ntx) {
+  constexpr int W = T + 5 + 2 * M;
+  constexpr int WN = W * W;
+  constexpr int NCH = TWO ? 6 : 3;
+  __shared__ double2 win[NCH * WN];
+  __shared__ double red[NT / 64];
+  const int tile = (int)xcd_block(blockIdx.x, gridDim.x);
+  const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
+  const int nx = a.f0.nx;
+  stage_window_regs<TWO, T, M, NT>(a.f0, a.f1, ox, oy, win);
+  __syncthreads();
+  const int64_t n = a.n;
+  const double alpha = a.tmax != 0.0 ? a.ts / a.tmax : 0.0;
+  double m = 0.0;
+  for (int64_t p = starts[tile] + threadIdx.x; p < starts[tile + 1]; p += NT) {
+    const double y[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
+    double ys[4];
+    if constexpr (STAGE == 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ys[c] = y[c];
+    } else if constexpr (STAGE == 2 || STAGE == 3) {
+      const double* Fp = a.F[STAGE - 2];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ys[c] = y[c] + Fp[c * n + p] * a.c[0];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        ys[c] = y[c] + (((a.F[0][c * n + p] * a.c[0]) + a.F[1][c * n + p] * a.c[1]) + a.F[2][c * n + p] * a.c[2]);
+      a.ynx[p] = ys[0]; a.ynx[n + p] = ys[1];
+      a.ynk[p] = ys[2]; a.ynk[n + p] = ys[3];
+    }
+    // odefun at (ts, ys): interpolate_U from the window (or global memory)
+    Stencil sc;
+    stencil_at(a.f0, ys[0], ys[1], a.bump, sc);
+    const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
+    double I[kRec], J[kRec];
+    if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M)
+      gather6_lds<TWO, W, WN>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
+    else
+      gather6<TWO>(a.f0.nodes, a.f1.nodes, a.f0.npad, sc, I, J);
+    if constexpr (TWO) {
+      const double oma = 1 - alpha;
+#pragma unroll
+      for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
+    }
+    const double k1 = ys[2], k2 = ys[3];
+    const double s = sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2));
+    double fo[4];
+    fo[0] = I[0] + (a.Cg * k1) / s;
+    fo[1] = I[1] + (a.Cg * k2) / s;
+    fo[2] = -(I[2] * k1 + I[4] * k2);
+    fo[3] = -(I[3] * k1 + I[5] * k2);
+    double* Fo = a.F[STAGE - 1];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) Fo[c * n + p] = fo[c];
+    if constexpr (STAGE == 1) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) m = fmax(m, fabs(fo[c]) / fmax(fabs(y[c]), a.thr));
+    } else if constexpr (STAGE == 4) {
+      constexpr double E1 = -5.0 / 72.0, E2 = 1.0 / 12.0, E3 = 1.0 / 9.0, E4 = -1.0 / 8.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double fe = ((a.F[0][c * n + p] * E1 + a.F[1][c * n + p] * E2) + a.F[2][c * n + p] * E3) + fo[c] * E4;
+        m = fmax(m, fabs(fe) / fmax(fmax(fabs(y[c]), fabs(ys[c])), a.thr));
+      }
+    }
+  }
+  if constexpr (STAGE == 1 || STAGE == 4) {
+    for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double b = red[0];
+      for (int w = 1; w < NT / 64; ++w) b = fmax(b, red[w]);
+      atomicMax(a.dmax, (unsigned long long)__double_as_longlong(b));
+    }
+  }
 }
 
 }  // namespace swrt

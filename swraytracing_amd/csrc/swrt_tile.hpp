@@ -109,6 +109,35 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
   }
 }
 
+// Stage tile (ox, oy)'s window into LDS, chunk-major (chunk c of node e at
+// win[c*WN + e]): node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx.
+// Register staging: each lane copies whole 48-B records, 3 or 6 loads back
+// to back (measured faster than LDS-DMA of the chunk-major image, whose 16-B
+// pieces are 48 B apart in HBM).  The caller publishes with a barrier.
+template <bool TWO, int T, int M, int NT>
+__device__ __forceinline__ void stage_window_regs(const FieldView& f0, const FieldView& f1, int ox, int oy,
+                                                  double2* win) {
+  constexpr int W = T + 5 + 2 * M;
+  constexpr int WN = W * W;
+  const int nx = f0.nx, npad = f0.npad;
+  for (int e = threadIdx.x; e < WN; e += NT) {
+    const int wi = e / W, wj = e % W;
+    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
+    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
+    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec;
+    const double2* s0 = reinterpret_cast<const double2*>(f0.nodes + src);
+    win[0 * WN + e] = s0[0];
+    win[1 * WN + e] = s0[1];
+    win[2 * WN + e] = s0[2];
+    if constexpr (TWO) {
+      const double2* s1 = reinterpret_cast<const double2*>(f1.nodes + src);
+      win[3 * WN + e] = s1[0];
+      win[4 * WN + e] = s1[1];
+      win[5 * WN + e] = s1[2];
+    }
+  }
+}
+
 #ifdef SWRT_PHASE_TIMING
 // diagnostic build only: per-workgroup wall-clock stamps (100 MHz) of the
 // phases, read back by swrt_debug_phases; never compiled into the product.
@@ -159,26 +188,8 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   }
 #endif
 
-  // 1. stage the window: node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx
-  //    (register staging: each lane copies whole 48-B records, 3 or 6 loads
-  //    back to back; measured faster than LDS-DMA of the chunk-major image,
-  //    whose 16-B pieces are 48 B apart in HBM)
-  for (int e = tid; e < WN; e += NT) {
-    const int wi = e / W, wj = e % W;
-    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
-    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
-    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec;
-    const double2* s0 = reinterpret_cast<const double2*>(a.f0.nodes + src);
-    win[0 * WNP + e] = s0[0];
-    win[1 * WNP + e] = s0[1];
-    win[2 * WNP + e] = s0[2];
-    if constexpr (TWO) {
-      const double2* s1 = reinterpret_cast<const double2*>(a.f1.nodes + src);
-      win[3 * WNP + e] = s1[0];
-      win[4 * WNP + e] = s1[1];
-      win[5 * WNP + e] = s1[2];
-    }
-  }
+  // 1. stage the window
+  stage_window_regs<TWO, T, M, NT>(a.f0, a.f1, ox, oy, win);
   const int pbeg = ta.starts[tile], pend = ta.starts[tile + 1];
   if (!ta.sort_cells) {
     __syncthreads();  // publish the window
