@@ -15,6 +15,15 @@
 //   FI   = swrt_mex('interpolate', x, y, F, dx, dy, bump)    % interpolate.m
 //   [x, k, hx, hk] = swrt_mex('leapfrog', x0, k0, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every)
 //   fk = swrt_mex('g2k', fg);  fg = swrt_mex('k2g', fk);
+//   swrt_mex('packets_set', x, k);  [x, k] = swrt_mex('packets_get');
+//   swrt_mex('advance', dt, nsteps, f, gH, nslots, alpha0, dalpha, bump)
+//   rh  = swrt_mex('ode23_f1', t, tmax, f, Cg, nslots, thr, bump)          % see ode23_packets_gpu.m
+//   err = swrt_mex('ode23_attempt', t, h, tnew, tmax, f, Cg, nslots, thr, bump)
+//   swrt_mex('ode23_accept')
+//   swrt_mex('qg_init', params_struct, qk)   % qk (2kmax+1) x (kmax+1) [x 2], complex
+//   swrt_mex('qg_step', dt, nsteps);  U0 = swrt_mex('qg_max_speed');
+//   [qk, t, steps] = swrt_mex('qg_get');  q = swrt_mex('qg_get_q');
+//   swrt_mex('qg_snapshot', slot, which, layer, ny_period);  swrt_mex('swap_slots', a, b)
 //   swrt_mex('destroy')
 #include <cstring>
 #include <string>
@@ -153,6 +162,111 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     plhs[0] = mxCreateDoubleMatrix(nx, nx, mxREAL);
     check(swrt_k2g(ctx(), (const double*)mxGetComplexDoubles(prhs[1]), nx, mxGetDoubles(plhs[0])),
           "swrt_k2g");
+    return;
+  }
+  if (!strcmp(cmd, "packets_set")) {  // (x Nx2, k Nx2)
+    check(swrt_packets_set(ctx(), reals(prhs[1], "x"), reals(prhs[2], "k"), (int64_t)mxGetM(prhs[1])),
+          "swrt_packets_set");
+    return;
+  }
+  if (!strcmp(cmd, "packets_get")) {
+    const int64_t n = swrt_packets_count(ctx());
+    plhs[0] = mxCreateDoubleMatrix((mwSize)n, 2, mxREAL);
+    plhs[1] = mxCreateDoubleMatrix((mwSize)n, 2, mxREAL);
+    check(swrt_packets_get(ctx(), mxGetDoubles(plhs[0]), mxGetDoubles(plhs[1])), "swrt_packets_get");
+    return;
+  }
+  if (!strcmp(cmd, "advance")) {  // (dt, nsteps, f, gH, nslots, alpha0, dalpha, bump)
+    check(swrt_advance(ctx(), scalar(prhs[1]), (int64_t)scalar(prhs[2]), scalar(prhs[3]), scalar(prhs[4]),
+                       (int)scalar(prhs[5]), scalar(prhs[6]), scalar(prhs[7]), scalar(prhs[8]), 0),
+          "swrt_advance");
+    return;
+  }
+  if (!strcmp(cmd, "ode23_f1")) {  // (t, tmax, f, Cg, nslots, thr, bump) -> rh_raw
+    double r = 0.0;
+    check(swrt_ode23_f1(ctx(), scalar(prhs[1]), scalar(prhs[2]), scalar(prhs[3]), scalar(prhs[4]),
+                        (int)scalar(prhs[5]), scalar(prhs[6]), scalar(prhs[7]), &r),
+          "swrt_ode23_f1");
+    plhs[0] = mxCreateDoubleScalar(r);
+    return;
+  }
+  if (!strcmp(cmd, "ode23_attempt")) {  // (t, h, tnew, tmax, f, Cg, nslots, thr, bump) -> err_raw
+    double r = 0.0;
+    check(swrt_ode23_attempt(ctx(), scalar(prhs[1]), scalar(prhs[2]), scalar(prhs[3]), scalar(prhs[4]),
+                             scalar(prhs[5]), scalar(prhs[6]), (int)scalar(prhs[7]), scalar(prhs[8]),
+                             scalar(prhs[9]), &r),
+          "swrt_ode23_attempt");
+    plhs[0] = mxCreateDoubleScalar(r);
+    return;
+  }
+  if (!strcmp(cmd, "ode23_accept")) {
+    check(swrt_ode23_accept(ctx()), "swrt_ode23_accept");
+    return;
+  }
+  if (!strcmp(cmd, "qg_init")) {  // (params struct, qk complex (2kmax+1) x (kmax+1) [x nlayers])
+    const mxArray* s = prhs[1];
+    auto fld = [&](const char* name, double dflt) {
+      const mxArray* v = mxGetField(s, 0, name);
+      return v ? mxGetScalar(v) : dflt;
+    };
+    swrt_qg_params p;
+    p.nlayers = (int)fld("nlayers", 1);
+    p.filter = (int)fld("filter", 1);
+    p.L = fld("L", 6.283185307179586);
+    p.K_d2 = fld("K_d2", 1.0);
+    p.beta = fld("beta", 0.0);
+    p.r_drag = fld("r_drag", 0.0);
+    p.force_strength = fld("force_strength", 0.0);
+    p.f = fld("f", 1.0);
+    p.Cg = fld("Cg", 1.0);
+    p.shear = fld("shear", 0.0);
+    p.nu = fld("nu", 0.0);
+    p.hyper_order = fld("hyper_order", 4.0);
+    p.r = fld("r", 0.0);
+    if (!mxIsComplex(prhs[2])) mexErrMsgIdAndTxt("swrt:arg", "qk must be complex");
+    const int64_t nx = (int64_t)mxGetM(prhs[2]) + 1;
+    check(swrt_qg_init(ctx(), &p, nx, (const double*)mxGetComplexDoubles(prhs[2])), "swrt_qg_init");
+    return;
+  }
+  if (!strcmp(cmd, "qg_step")) {  // (dt, nsteps)
+    check(swrt_qg_step(ctx(), scalar(prhs[1]), nrhs > 2 ? (int64_t)scalar(prhs[2]) : 1), "swrt_qg_step");
+    return;
+  }
+  if (!strcmp(cmd, "qg_max_speed")) {
+    double u = 0.0;
+    check(swrt_qg_max_speed(ctx(), &u), "swrt_qg_max_speed");
+    plhs[0] = mxCreateDoubleScalar(u);
+    return;
+  }
+  if (!strcmp(cmd, "qg_get")) {  // -> qk, t, steps (dims as given to qg_init)
+    double t = 0.0;
+    int64_t steps = 0;
+    if (nrhs < 3) mexErrMsgIdAndTxt("swrt:arg", "qg_get needs (nx, nlayers)");
+    const int64_t nx = (int64_t)scalar(prhs[1]);
+    const int nl = (int)scalar(prhs[2]);
+    const mwSize dims[3] = {(mwSize)(nx - 1), (mwSize)(nx / 2), (mwSize)nl};
+    plhs[0] = mxCreateNumericArray(nl > 1 ? 3 : 2, dims, mxDOUBLE_CLASS, mxCOMPLEX);
+    check(swrt_qg_get(ctx(), (double*)mxGetComplexDoubles(plhs[0]), &t, &steps), "swrt_qg_get");
+    if (nlhs > 1) plhs[1] = mxCreateDoubleScalar(t);
+    if (nlhs > 2) plhs[2] = mxCreateDoubleScalar((double)steps);
+    return;
+  }
+  if (!strcmp(cmd, "qg_get_q")) {  // (nx, nlayers) -> q nx x nx [x nlayers]
+    const int64_t nx = (int64_t)scalar(prhs[1]);
+    const int nl = (int)scalar(prhs[2]);
+    const mwSize dims[3] = {(mwSize)nx, (mwSize)nx, (mwSize)nl};
+    plhs[0] = mxCreateNumericArray(nl > 1 ? 3 : 2, dims, mxDOUBLE_CLASS, mxREAL);
+    check(swrt_qg_get_q(ctx(), mxGetDoubles(plhs[0])), "swrt_qg_get_q");
+    return;
+  }
+  if (!strcmp(cmd, "qg_snapshot")) {  // (slot, which, layer, ny_period)
+    check(swrt_qg_snapshot(ctx(), (int)scalar(prhs[1]), (int)scalar(prhs[2]), (int)scalar(prhs[3]),
+                           (int64_t)scalar(prhs[4])),
+          "swrt_qg_snapshot");
+    return;
+  }
+  if (!strcmp(cmd, "swap_slots")) {
+    check(swrt_swap_slots(ctx(), (int)scalar(prhs[1]), (int)scalar(prhs[2])), "swrt_swap_slots");
     return;
   }
   mexErrMsgIdAndTxt("swrt:arg", "unknown command '%s'", cmd);
