@@ -155,7 +155,7 @@ def main():
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
-    ap.add_argument("--timing-every", type=int, default=8,
+    ap.add_argument("--timing-every", type=int, default=5,
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather all trajectories to rank 0 (one all_gather)")

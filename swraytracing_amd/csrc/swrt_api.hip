@@ -235,6 +235,7 @@ FieldView view_of(const Slot& s) {
   v.py = (double)s.ny_period;
   v.inv_px = 1.0 / v.px;
   v.inv_py = 1.0 / v.py;
+  v.inv_dx = 1.0 / v.dx;
   v.pow2x = is_pow2(s.nx);
   v.pow2y = is_pow2(s.ny_period);
   return v;
@@ -388,7 +389,7 @@ int rebin(swrt_ctx* c) {
   const Slot& s = c->slot[0];
   const FieldView v = view_of(s);
   BinGeom g;
-  g.dx = v.dx; g.px = v.px; g.py = v.py; g.inv_px = v.inv_px; g.inv_py = v.inv_py;
+  g.dx = v.dx; g.px = v.px; g.py = v.py; g.inv_px = v.inv_px; g.inv_py = v.inv_py; g.inv_dx = v.inv_dx;
   g.pow2x = v.pow2x; g.pow2y = v.pow2y; g.nx = v.nx;
   g.tile = tile_cells(c, s.nx);
   g.ntx = (int)((s.nx + g.tile - 1) / g.tile);

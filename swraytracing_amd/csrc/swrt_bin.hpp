@@ -16,16 +16,15 @@
 namespace swrt {
 
 struct BinGeom {
-  double dx, px, py, inv_px, inv_py;
+  double dx, px, py, inv_px, inv_py, inv_dx;
   int pow2x, pow2y, nx;
   int tile;     // cells per tile side
   int ntx;      // tiles per side
 };
 
 __device__ __forceinline__ int tile_of(const BinGeom& g, double x, double y) {
-  double a;
-  const int cx = cell_frac(x, g.dx, g.px, g.inv_px, g.pow2x, g.nx, a);
-  const int cy = cell_frac(y, g.dx, g.py, g.inv_py, g.pow2y, g.nx, a);
+  const int cx = fast_cell(x, g.inv_dx, g.nx);
+  const int cy = fast_cell(y, g.inv_dx, g.nx);
   return (cx / g.tile) * g.ntx + (cy / g.tile);
 }
 

@@ -30,6 +30,7 @@ struct FieldView {
   double px, py;        // mod periods of x/dx and y/dy (nx, ny_period)
   double inv_px, inv_py;
   int pow2x, pow2y;     // period is a power of two: a/m == a*(1/m) exactly
+  double inv_dx;        // 1/dx, for locality keys only (never for the arithmetic)
 };
 
 // interpolate.m:21-31 — xl = mod(x/dx, n); i0 = 1 + floor(xl); a = 1 + xl - i0.
@@ -103,6 +104,17 @@ __device__ __forceinline__ void lagrange_w(double a, double bump, double w[kNT])
   w[3] = lagrange_wi<1>(t);
   w[4] = lagrange_wi<2>(t);
   w[5] = lagrange_wi<3>(t);
+}
+
+// Cell index for LOCALITY only (binning keys, in-tile sort keys): floor of
+// x*(1/dx) mod nx — a multiply instead of the correctly rounded division of
+// cell_frac.  A packet classified one cell off near a cell edge is merely
+// sorted or binned next door; every result is computed by cell_frac.
+__device__ __forceinline__ int fast_cell(double x, double inv_dx, int nx) {
+  const double q = floor(x * inv_dx);
+  int c = (q > -1073741824.0 && q < 1073741824.0) ? (int)q : 0;  // NaN/huge -> 0
+  c %= nx;
+  return c < 0 ? c + nx : c;
 }
 
 // Cell and 1-D weights of a point: shared by every field and snapshot of the

@@ -63,9 +63,8 @@ __global__ void __launch_bounds__(NT, 1) tile_persist_kernel(TileArgs ta, int ti
     __syncthreads();
     for (int i = tid; i < nb; i += NT) {
       const int64_t p = b0 + i;
-      double fa;
-      const int ic = cell_frac(a.x[p], a.f0.dx, a.f0.px, a.f0.inv_px, a.f0.pow2x, nx, fa);
-      const int jc = cell_frac(a.x[a.n + p], a.f0.dx, a.f0.py, a.f0.inv_py, a.f0.pow2y, nx, fa);
+      const int ic = fast_cell(a.x[p], a.f0.inv_dx, nx);
+      const int jc = fast_cell(a.x[a.n + p], a.f0.inv_dx, nx);
       const int dx_ = ring_diff(ic, ox, nx), dy_ = ring_diff(jc, oy, nx);
       const int key = (dx_ >= 0 && dx_ < T && dy_ >= 0 && dy_ < T) ? dx_ * T + dy_ : T * T;
       const int r = atomicAdd(&hist[key], 1);
@@ -164,9 +163,8 @@ __global__ void __launch_bounds__(NT, 1) tile_persist_kernel(TileArgs ta, int ti
     ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
     ta.perm_out[po] = orig;
     if (ta.next_keys != nullptr) {
-      double fa;
-      const int ic = cell_frac(x0, a.f0.dx, a.f0.px, a.f0.inv_px, a.f0.pow2x, nx, fa);
-      const int jc = cell_frac(y0, a.f0.dx, a.f0.py, a.f0.inv_py, a.f0.pow2y, nx, fa);
+      const int ic = fast_cell(x0, a.f0.inv_dx, nx);
+      const int jc = fast_cell(y0, a.f0.inv_dx, nx);
       const int ntx_ = ta.ntx;
       const int ntx2 = ic / T, nty2 = jc / T;
       ta.next_keys[po] = ntx2 * ntx_ + nty2;

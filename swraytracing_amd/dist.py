@@ -63,3 +63,10 @@ def max_over_ranks(value: float, backend: str = "gloo", group=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=_device_for(backend))
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
     return float(t.item())
+
+
+def allreduce_max_fn(backend: str = "nccl", group=None):
+    """A callable v -> MAX over ranks of v, for ode23_packets' global error
+    norm when packets are sharded (one 8-byte all_reduce per attempted step,
+    RCCL on "nccl")."""
+    return lambda v: max_over_ranks(v, backend=backend, group=group)

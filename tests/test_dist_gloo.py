@@ -77,3 +77,85 @@ def test_gloo_world2_shard_gather_matches_single_process(n):
     ok, tmax = q.get(timeout=10)
     assert ok
     assert tmax == 1.5
+
+
+class _ShardCtx:
+    """numpy stand-in for the device ode23 stages (swrt_ode23_*) on one shard,
+    with the oracle's odefun — so the sharded controller can run on CPU."""
+
+    def __init__(self, y, rhs):
+        self.y = y.copy()
+        self.rhs = rhs
+        self.n = y.size // 4
+
+    def ode23_f1(self, t, tmax, f, Cg, nslots, thr, bump):
+        self.F1 = self.rhs(t, self.y)
+        return float(np.max(np.abs(self.F1) / np.maximum(np.abs(self.y), thr)))
+
+    def ode23_attempt(self, t, h, tnew, tmax, f, Cg, nslots, thr, bump):
+        y = self.y
+        F2 = self.rhs(t + h * 0.5, y + self.F1 * (h * 0.5))
+        F3 = self.rhs(t + h * 0.75, y + F2 * (h * 0.75))
+        h4 = tnew - t
+        self.ynew = y + (((self.F1 * (h4 * (2.0 / 9.0))) + F2 * (h4 * (1.0 / 3.0))) + F3 * (h4 * (4.0 / 9.0)))
+        self.F4 = self.rhs(tnew, self.ynew)
+        fE = ((self.F1 * (-5.0 / 72.0) + F2 * (1.0 / 12.0)) + F3 * (1.0 / 9.0)) + self.F4 * (-1.0 / 8.0)
+        return float(np.max(np.abs(fE) / np.maximum(np.maximum(np.abs(y), np.abs(self.ynew)), thr)))
+
+    def ode23_accept(self):
+        self.y, self.F1 = self.ynew, self.F4
+
+
+def _ode23_worker(rank, world, port, n, q):
+    import torch.distributed as dist
+
+    from oracle import swrt_oracle as orc
+    from swraytracing_amd.dist import allreduce_max_fn, gather_to_root, shard_range
+    from swraytracing_amd.integrate import ode23_packets
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(7)
+        nx, L, f, Cg = 32, 2 * np.pi, 3.0, 1.0
+        X = np.arange(nx) * L / nx
+        XX, YY = np.meshgrid(X, X, indexing="ij")
+        f1 = orc.spectral_scheme_fields(L, nx, 0.08 * np.cos(2 * XX + YY))
+        f2 = orc.spectral_scheme_fields(L, nx, 0.08 * np.cos(2 * XX + YY + 0.4))
+        for d_ in (f1, f2):
+            d_.pop("psi")
+        x, k = orc.initial_packets(n, L, 4.0, f, Cg, rng)
+        lo, hi = shard_range(n, world, rank)
+        tmax = 0.6
+        rhs = orc.raytracing_rhs(f1, f2, f, Cg, tmax, L / nx)
+        ys = np.concatenate([x[lo:hi, 0], x[lo:hi, 1], k[lo:hi, 0], k[lo:hi, 1]])
+        c = _ShardCtx(ys, rhs)
+        st = {}
+        ts = ode23_packets(c, (0.0, tmax), tmax, f, Cg, allreduce_max=allreduce_max_fn("gloo"), stats=st)
+        m = hi - lo
+        local = np.stack([c.y[:m], c.y[m:2 * m], c.y[2 * m:3 * m], c.y[3 * m:]], axis=1)
+        full = gather_to_root(local, n, world, rank)
+        if rank == 0:
+            y0 = np.concatenate([x[:, 0], x[:, 1], k[:, 0], k[:, 1]])
+            to, yo = orc.ode23(rhs, [0.0, tmax], y0)
+            want = np.stack([yo[:n], yo[n:2 * n], yo[2 * n:3 * n], yo[3 * n:]], axis=1)
+            q.put((bool(np.array_equal(ts, to)), bool(np.array_equal(full, want)), st["steps"]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_ode23_takes_the_global_steps():
+    """ode23's error norm is global: with the packets split over 2 ranks and
+    the per-attempt error max-reduced over them, both ranks take exactly the
+    single-process step sequence and the gathered state is bit-identical."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ode23_worker, args=(r, 2, port, 90, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    same_ts, same_y, steps = q.get(timeout=10)
+    assert same_ts and same_y and steps >= 10
