@@ -108,6 +108,7 @@ struct swrt_ctx {
   int64_t steps_since_bin = 0;
   bool bin_valid = false;
   bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
+  bool counts_zero = false;  // bins' count block is all zero (cleared by the last scan)
   int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -407,6 +408,7 @@ int rebin(swrt_ctx* c) {
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins,
                      c->bins + 2 * kMaxBins);
   HIPCHK(c, hipGetLastError());
+  c->counts_zero = true;
   hipLaunchKernelGGL(bin_scatter_kernel, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream, c->dx,
                      c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2);
   HIPCHK(c, hipGetLastError());
@@ -433,7 +435,8 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   t.next_counts = nullptr;
   t.sort_cells = (c->cell_sort == 1 || !c->cells_sorted) ? 1 : 0;
   if (count_next && (int)grid == c->nbins) {
-    HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * grid, c->stream));
+    if (!c->counts_zero) HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * grid, c->stream));
+    c->counts_zero = false;
     t.next_keys = c->keys;
     t.next_counts = c->bins;
   }

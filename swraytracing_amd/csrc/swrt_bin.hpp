@@ -56,7 +56,9 @@ __global__ void __launch_bounds__(256) bin_count_kernel(BinGeom g, const double*
 }
 
 // Pass 2: exclusive scan of counts -> cursor (single workgroup, nbins <= 16384).
-__global__ void __launch_bounds__(1024) bin_scan_kernel(const int* counts, int nbins, int* cursor,
+// Also clears counts (each thread its own bins, after reading them) so the next
+// fused count in the tile kernel starts from zero without a memset launch.
+__global__ void __launch_bounds__(1024) bin_scan_kernel(int* counts, int nbins, int* cursor,
                                                         int* starts) {
   __shared__ int part[1024];
   const int per = (nbins + 1023) / 1024;
@@ -82,6 +84,7 @@ __global__ void __launch_bounds__(1024) bin_scan_kernel(const int* counts, int n
       cursor[b] = run;
       starts[b] = run;
       run += counts[b];
+      counts[b] = 0;
     }
   }
   if (threadIdx.x == 1023) starts[nbins] = part[1023];
