@@ -151,6 +151,8 @@ def main():
     ap.add_argument("--rebin-every", type=int, default=4, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile, 3 persistent tile")
+    ap.add_argument("--blend-mode", type=int, default=0,
+                    help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -177,6 +179,7 @@ def main():
     ctx.set_locality(args.rebin_every, args.tile)
     ctx.set_kernel(args.kernel)
     ctx.set_cell_sort(args.cell_sort)
+    ctx.set_blend_mode(args.blend_mode)
     rng = np.random.default_rng(args.seed + rank)
     w = build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
@@ -241,7 +244,7 @@ def main():
                                f"{args.nx}^2x2 field, {N} packets/GPU, leapfrog",
                    "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
-                   "cell_sort": args.cell_sort,
+                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode,
                    "parallelism": f"packets sharded x{world}, field replicated"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,

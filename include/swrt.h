@@ -137,6 +137,16 @@ int swrt_set_kernel(swrt_ctx* ctx, int variant);
  * (default); 1 = sort on every launch. */
 int swrt_set_cell_sort(swrt_ctx* ctx, int every_launch);
 
+/* Two-snapshot blend of the LDS-tiled kernel.  0 (default): interpolate each
+ * snapshot, then blend (1-alpha)*U1 + alpha*U2 — interpolate_U.m:19-23 in its
+ * own operation order, bit-identical to the reference arithmetic.  1: blend
+ * the snapshots' node values once per step in the LDS window, then
+ * interpolate once — the same linear function (interpolate_U is linear in
+ * the fields) with a different rounding order: half the gather work, results
+ * agree to ~1e-16 relative per step (tolerance parity, not bits); launches
+ * advance one step each. */
+int swrt_set_blend_mode(swrt_ctx* ctx, int mode);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

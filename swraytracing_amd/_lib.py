@@ -62,6 +62,7 @@ SIGNATURES = {
     "swrt_set_locality": (_INT, [_VP, _I, _I]),
     "swrt_set_kernel": (_INT, [_VP, _INT]),
     "swrt_set_cell_sort": (_INT, [_VP, _INT]),
+    "swrt_set_blend_mode": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
     "swrt_history_get": (_INT, [_VP, _I, _I, _P, _P]),
@@ -242,6 +243,10 @@ class Context:
 
     def set_kernel(self, variant=0):
         self._chk(self._L.swrt_set_kernel(self._h, int(variant)), "swrt_set_kernel")
+
+    def set_blend_mode(self, mode=0):
+        """0: bit-exact interpolate-then-blend; 1: blend in the LDS window (tolerance parity)."""
+        self._chk(self._L.swrt_set_blend_mode(self._h, int(mode)), "swrt_set_blend_mode")
 
     def set_cell_sort(self, every_launch=0):
         self._chk(self._L.swrt_set_cell_sort(self._h, int(every_launch)), "swrt_set_cell_sort")

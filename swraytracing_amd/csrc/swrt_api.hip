@@ -110,6 +110,7 @@ struct swrt_ctx {
   bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
   bool counts_zero = false;  // bins' count block is all zero (cleared by the last scan)
   int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
+  int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
   double* hx = nullptr;
@@ -454,6 +455,9 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
     else
       hipLaunchKernelGGL((tile_persist_kernel<false, kTile, kMargin, 1024>), dim3(pgrid), dim3(1024), 0,
                          c->stream, t, tpw);
+  } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
+    hipLaunchKernelGGL((tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>), dim3(grid),
+                       dim3(kTileThreads), 0, c->stream, t);
   } else if (a.nslots == 2) {
     hipLaunchKernelGGL((tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>), dim3(grid),
                        dim3(kTileThreads), 0, c->stream, t);
@@ -492,6 +496,7 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
   int64_t s0 = 0;
   while (s0 < nsteps) {
     int64_t chunk = std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
+    if (c->blend_mode == 1 && nslots == 2 && use_tile_kernel(c)) chunk = 1;  // alpha fixed per launch
     if (c->rebin_every > 0) {
       if (!c->bin_valid || c->steps_since_bin >= c->rebin_every) {
         int rc = rebin(c);
@@ -906,6 +911,13 @@ int swrt_set_timing(swrt_ctx* c, int every) {
   if (every < 0) return fail(c, SWRT_ERR_ARG, "timing interval must be >= 0");
   c->timing_every = every;
   c->launch_count = 0;
+  return SWRT_OK;
+}
+
+int swrt_set_blend_mode(swrt_ctx* c, int mode) {
+  if (!c) return SWRT_ERR_ARG;
+  if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "blend mode must be 0 or 1");
+  c->blend_mode = mode;
   return SWRT_OK;
 }
 

@@ -173,6 +173,33 @@ __device__ __forceinline__ void interp6(const FieldView& fv, double x, double y,
   gather6<false>(fv.nodes, fv.nodes, fv.npad, s, out, dummy);
 }
 
+// Blend-then-interpolate from global memory (the out-of-window fallback of
+// the blend-in-LDS mode): each node value is (1-alpha)*F1 + alpha*F2 exactly
+// as stage_window_blend forms it, then one stencil sum.
+__device__ __forceinline__ void gather6_blend(const double* nodes0, const double* nodes1, int npad,
+                                              const Stencil& s, double alpha, double o[kRec]) {
+  const double oma = 1 - alpha;
+#pragma unroll
+  for (int f = 0; f < kRec; ++f) o[f] = 0.0;
+  const size_t off = ((size_t)s.ic * npad + s.jc) * kRec;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+    const size_t ro = off + (size_t)i * npad * kRec;
+    const double2* r0 = reinterpret_cast<const double2*>(nodes0 + ro);
+    const double2* r1 = reinterpret_cast<const double2*>(nodes1 + ro);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const double wij = s.wx[i] * s.wy[j];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const double2 u = r0[3 * j + c], v = r1[3 * j + c];
+        o[2 * c] = o[2 * c] + wij * (oma * u.x + alpha * v.x);
+        o[2 * c + 1] = o[2 * c + 1] + wij * (oma * u.y + alpha * v.y);
+      }
+    }
+  }
+}
+
 // interpolate_U.m:19-23 — (1 - alpha)*U1 + alpha*U2, per field.  Both
 // snapshots live on the same grid (checked on the host).
 template <bool TWO>

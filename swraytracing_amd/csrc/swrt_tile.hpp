@@ -160,6 +160,33 @@ __device__ __forceinline__ void stage_window_regs(const FieldView& f0, const Fie
   }
 }
 
+// Blend-then-interpolate staging (swrt_set_blend_mode 1): the window holds
+// (1-alpha)*U1 + alpha*U2 per node and field, 3 chunks.  interpolate_U is
+// linear, so this is the same function as interpolating each snapshot and
+// blending (interpolate_U.m:19-23) with a different rounding order: half the
+// LDS reads and half the gather arithmetic, tolerance parity instead of bits.
+template <int T, int M, int NT>
+__device__ __forceinline__ void stage_window_blend(const FieldView& f0, const FieldView& f1, int ox, int oy,
+                                                   double alpha, double2* win) {
+  constexpr int W = T + 5 + 2 * M;
+  constexpr int WN = W * W;
+  const int nx = f0.nx, npad = f0.npad;
+  const double oma = 1 - alpha;
+  for (int e = threadIdx.x; e < WN; e += NT) {
+    const int wi = e / W, wj = e % W;
+    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
+    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
+    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec;
+    const double2* s0 = reinterpret_cast<const double2*>(f0.nodes + src);
+    const double2* s1 = reinterpret_cast<const double2*>(f1.nodes + src);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const double2 u = s0[c], v = s1[c];
+      win[c * WN + e] = make_double2(oma * u.x + alpha * v.x, oma * u.y + alpha * v.y);
+    }
+  }
+}
+
 #ifdef SWRT_PHASE_TIMING
 // diagnostic build only: per-workgroup wall-clock stamps (100 MHz) of the
 // phases, read back by swrt_debug_phases; never compiled into the product.
@@ -178,12 +205,13 @@ __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 #define SWRT_TILE_MIN_WAVES 4
 #endif
 
-template <bool TWO, int T, int M, int NT>
+template <bool TWO, int T, int M, int NT, bool WBLEND = false>
 __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
   constexpr int WN = W * W;
   constexpr int WNP = WN;           // nodes per chunk
-  constexpr int NCH = TWO ? 6 : 3;  // 16-B chunks per node
+  constexpr bool GTWO = TWO && !WBLEND;  // two snapshots in the LDS window
+  constexpr int NCH = GTWO ? 6 : 3; // 16-B chunks per node
   constexpr int NB = T * T + 1;     // in-tile cell bins + "elsewhere"
   constexpr int MAXB = 2 * NT;      // packets sorted per batch
   __shared__ double2 win[NCH * WNP];
@@ -210,8 +238,11 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   }
 #endif
 
-  // 1. stage the window
-  stage_window_regs<TWO, T, M, NT>(a.f0, a.f1, ox, oy, win);
+  // 1. stage the window (WBLEND: one launch = one step, alpha fixed)
+  if constexpr (WBLEND)
+    stage_window_blend<T, M, NT>(a.f0, a.f1, ox, oy, a.alpha0 + (double)a.s0 * a.dalpha, win);
+  else
+    stage_window_regs<TWO, T, M, NT>(a.f0, a.f1, ox, oy, win);
   const int lane_rank = b128_lane_rank(tid & 63);
   const int pbeg = ta.starts[tile], pend = ta.starts[tile + 1];
   if (!ta.sort_cells) {
@@ -298,16 +329,23 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
           for (int q = 0; q < kRec; ++q) { I[q] = sc.wx[q] * 1e-30; J[q] = sc.wy[q] * 1e-30; }
         } else
 #endif
-        if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M) {
-          gather6_lds<TWO, W, WNP>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
+        const bool inwin = dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M;
+        if constexpr (WBLEND) {
+          if (inwin)
+            gather6_lds<false, W, WNP>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
+          else
+            gather6_blend(a.f0.nodes, a.f1.nodes, npad, sc, a.alpha0 + (double)sg * a.dalpha, I);
         } else {
-          gather6<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
-        }
-        if constexpr (TWO) {
-          const double alpha = a.alpha0 + (double)sg * a.dalpha;
-          const double oma = 1 - alpha;
+          if (inwin)
+            gather6_lds<TWO, W, WNP>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
+          else
+            gather6<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
+          if constexpr (TWO) {
+            const double alpha = a.alpha0 + (double)sg * a.dalpha;
+            const double oma = 1 - alpha;
 #pragma unroll
-          for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
+            for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
+          }
         }
         const double x2 = x1 + a.dt * I[0];
         const double y2 = y1 + a.dt * I[1];

@@ -555,3 +555,35 @@ def test_omega_histogram_matches_load_data(ctx):
     # accumulation over frames (load_data.m windows)
     counts2, _ = ctx.omega_histogram(f, Cg, edges, counts.copy())
     np.testing.assert_array_equal(counts2, 2 * ref)
+
+
+@pytest.mark.parametrize("dt_scale", [1.0, 40.0])
+def test_blend_in_window_mode_tolerance(ctx, oracle_lib, qg_case, dt_scale):
+    """swrt_set_blend_mode(1): the snapshots are blended per node in the LDS
+    window (or on the fly in the global fallback) and interpolated once —
+    interpolate_U is linear, so this is the same function with another
+    rounding order.  Tolerance parity over 12 steps: <= 1e-12 absolute at the
+    driver's dt; dt x 40 (CFL-violating steps that also drive packets out of
+    the window onto the global fallback) amplifies the ulp-level differences
+    through the kick, <= 1e-9 relative.  (The default mode is the bit-exact one.)"""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    p0 = _planes(c["flow"])
+    p1 = _planes({n: np.asarray(v) * 0.8 for n, v in c["flow"].items()})
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    dt = c["dt"] * dt_scale
+    ctx.set_blend_mode(1)
+    ctx.set_locality(4, 0)
+    try:
+        ctx.packets_set(c["x"], c["k"])
+        for s in range(12):
+            ctx.advance(dt, 1, c["f"], 1.0, nslots=2, alpha0=0.1 + s * 0.07, dalpha=0.07, bump=orc.BUMP_QG)
+        xg, kg = ctx.packets_get()
+    finally:
+        ctx.set_blend_mode(0)
+    xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.07, nx, 2 * nx, L / nx, orc.BUMP_QG, c["x"], c["k"], dt, 12,
+                                       c["f"], 1.0)
+    rtol, atol = (1e-12, 1e-12) if dt_scale == 1.0 else (1e-9, 1e-10)
+    np.testing.assert_allclose(xg, xo, rtol=rtol, atol=atol)
+    np.testing.assert_allclose(kg, ko, rtol=rtol, atol=atol)
