@@ -20,6 +20,26 @@ def planes(flow):
     return np.stack([np.asarray(flow[n]).ravel(order="F") for n in orc.FIELD_ORDER])
 
 
+def qg_fixture():
+    nx = 32
+    rng = np.random.default_rng(2718)
+    q = orc.initial_q(nx, 2 * np.pi, 0.2, 3.0, 5, 8, rng)
+    qk1 = orc.g2k(q)
+    m1 = orc.QG1Oracle(qk1, nx, 3.0, r_drag=0.0, force_strength=0.1, f=3.0, Cg=1.0, use_filter=True)
+    dt1 = 0.05 * (2 * np.pi / nx) / 0.2
+    for _ in range(8):
+        m1.step(dt1)
+    q2 = orc.initial_q(nx, 20.0, 0.2, 3.0, 1, 3, rng)
+    qk2 = np.stack([orc.g2k(q2), orc.g2k(-q2)], axis=2)
+    m2 = orc.QG2Oracle(qk2, nx, 20.0, 3.0, shear_strength=0.5)
+    dts = []
+    for _ in range(8):
+        m2.step()
+        dts.append(m2.dt)
+    return dict(nx=nx, qk1_0=qk1, qk1_8=m1.qk, dt1=dt1, qk2_0=qk2, qk2_8=m2.qk, dts2=np.array(dts),
+                L2=20.0, K_d2=3.0, f=3.0, Cg=1.0)
+
+
 def main():
     nx, L, f, Cg = 32, 2 * np.pi, 3.0, 1.0
     rng = np.random.default_rng(146)
@@ -59,7 +79,21 @@ def main():
     np.savez_compressed(os.path.join(HERE, "golden_fields.npz"), psi_in=psi, psi=sf["psi"],
                         planes_psi=planes(sf), qk=qk, K_d2=K_d2, planes_qk=planes(flow),
                         planes_qk_shear=planes(flow1))
-    for fn in ("golden_steady.npz", "golden_blend.npz", "golden_fields.npz"):
+    # QG PDE steppers (qgsw_raytrace.m:111-137 / qg2layersw_raytrace.m:129-181)
+    qg = qg_fixture()
+    np.savez_compressed(os.path.join(HERE, "golden_qg.npz"), **qg)
+    # ode23 over the blend fixture's snapshots (qgsw_raytrace.m:143-150)
+    T = 12 * dt
+    rhs = orc.raytracing_rhs({n: flow1[n] for n in orc.FIELD_ORDER}, {n: flow2[n] for n in orc.FIELD_ORDER},
+                             f, Cg, T, dx, nyF=2 * nx)
+    y0 = np.concatenate([x[:, 0], x[:, 1], k[:, 0], k[:, 1]])
+    st = {}
+    ts, yT = orc.ode23(rhs, [0.0, T], y0, stats=st)
+    np.savez_compressed(os.path.join(HERE, "golden_ode23.npz"), planes0=planes(flow1), planes1=planes(flow2),
+                        nx=nx, ny_period=2 * nx, L=L, f=f, Cg=Cg, tmax=T, x0=x, k0=k, ts=ts, y=yT,
+                        failed=st["failed"])
+    for fn in ("golden_steady.npz", "golden_blend.npz", "golden_fields.npz", "golden_qg.npz",
+               "golden_ode23.npz"):
         print(fn, os.path.getsize(os.path.join(HERE, fn)))
 
 

@@ -89,3 +89,16 @@ def test_packet_ensemble_ode23_interval(ctx, qg_case):
     to, yo = orc.ode23(orc.raytracing_rhs(fl(p0), fl(p1), f, Cg, dt, L / nx), [0.0, dt], _y0(c["x"], c["k"]))
     n = c["x"].shape[0]
     np.testing.assert_array_equal(np.concatenate([xg[:, 0], xg[:, 1], kg[:, 0], kg[:, 1]]), yo)
+
+
+def test_golden_ode23_fixture(ctx):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_ode23.npz"))
+    nx, L = int(g["nx"]), float(g["L"])
+    ctx.set_field_grid(0, g["planes0"], nx, L, int(g["ny_period"]))
+    ctx.set_field_grid(1, g["planes1"], nx, L, int(g["ny_period"]))
+    ctx.packets_set(g["x0"], g["k0"])
+    ts = sw.ode23_packets(ctx, (0.0, float(g["tmax"])), float(g["tmax"]), float(g["f"]), float(g["Cg"]))
+    xg, kg = ctx.packets_get()
+    np.testing.assert_array_equal(ts, g["ts"])
+    np.testing.assert_array_equal(np.concatenate([xg[:, 0], xg[:, 1], kg[:, 0], kg[:, 1]]), g["y"])

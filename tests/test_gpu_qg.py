@@ -220,3 +220,19 @@ def test_qg2layer_driver_runs_and_writes(ctx, tmp_path):
     assert pv.shape == (nx, nx, 2)
     log = open(tmp_path / "run.log").read()
     assert "Resolution: 64x64" in log and "Froude Number" in log
+
+
+def test_golden_qg_fixture(ctx):
+    import os
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_qg.npz"))
+    nx = int(g["nx"])
+    m1 = sw.QGModel.one_layer(g["qk1_0"], nx, 3.0, 1.0, r_drag=0.0, ctx=ctx)
+    m1.step(float(g["dt1"]), 8)
+    assert _rel(m1.qk[:, :, 0], g["qk1_8"]) < QG_RTOL
+    m2 = sw.QGModel.two_layer(g["qk2_0"], nx, 3.0, 1.0, L=float(g["L2"]), ctx=ctx)
+    dt = 0.25 * (float(g["L2"]) / nx) / m2.max_speed()
+    for want in g["dts2"]:
+        dt, _, _ = m2.cfl_update(dt, 0.25)
+        assert abs(dt - want) <= 1e-12 * want
+        m2.step(dt)
+    assert _rel(m2.qk, g["qk2_8"]) < QG_RTOL

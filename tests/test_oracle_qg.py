@@ -166,3 +166,36 @@ def test_ode23_raytracing_rhs_zero_flow_is_linear_drift():
     np.testing.assert_allclose(y[:20], want[:, 0], rtol=1e-13)
     np.testing.assert_allclose(y[20:40], want[:, 1], rtol=1e-13)
     np.testing.assert_array_equal(y[40:], y0[40:])
+
+
+# ---------------------------------------------------------------------------
+# committed fixtures (tests/golden/gen_golden.py) reproduce exactly
+# ---------------------------------------------------------------------------
+def _gold(name):
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", name))
+
+
+def test_golden_qg_fixture_reproduces():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "gen_golden", os.path.join(os.path.dirname(__file__), "golden", "gen_golden.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    fresh = gen.qg_fixture()
+    g = _gold("golden_qg.npz")
+    for key in ("qk1_0", "qk1_8", "qk2_0", "qk2_8", "dts2"):
+        np.testing.assert_array_equal(fresh[key], g[key])
+
+
+def test_golden_ode23_fixture_reproduces():
+    g = _gold("golden_ode23.npz")
+    nx = int(g["nx"])
+    fl = lambda p: {n: p[i].reshape((nx, nx), order="F") for i, n in enumerate(orc.FIELD_ORDER)}
+    rhs = orc.raytracing_rhs(fl(g["planes0"]), fl(g["planes1"]), float(g["f"]), float(g["Cg"]),
+                             float(g["tmax"]), float(g["L"]) / nx, nyF=int(g["ny_period"]))
+    x0, k0 = g["x0"], g["k0"]
+    ts, y = orc.ode23(rhs, [0.0, float(g["tmax"])], np.concatenate([x0[:, 0], x0[:, 1], k0[:, 0], k0[:, 1]]))
+    np.testing.assert_array_equal(ts, g["ts"])
+    np.testing.assert_array_equal(y, g["y"])
