@@ -278,6 +278,12 @@ int swrt_qg_step(swrt_ctx* ctx, double dt, int64_t nsteps);
 /* U0 = sqrt(max((u + shear)^2 + v^2)) over every layer of grid_U(qk)
  * (qg2layersw_raytrace.m:156-158; qgsw_raytrace.m:63-65 with shear 0). */
 int swrt_qg_max_speed(swrt_ctx* ctx, double* U0_out);
+/* The same, split: _async enqueues the speed of the CURRENT qk (read back into
+ * pinned memory behind an event) and returns at once, so the caller can queue
+ * the packet work of this step before _result waits for U0 — the driver's
+ * CFL decision for the next step no longer stalls the GPU. */
+int swrt_qg_max_speed_async(swrt_ctx* ctx);
+int swrt_qg_max_speed_result(swrt_ctx* ctx, double* U0_out);
 /* Copy out qk (same layout as swrt_qg_init), the model time and step count. */
 int swrt_qg_get(swrt_ctx* ctx, double* qk_out, double* t_out, int64_t* steps_out);
 /* q = k2g(qk) per layer: nx x nx x nlayers column-major (pv.bin frames,

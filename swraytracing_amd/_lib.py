@@ -80,6 +80,8 @@ SIGNATURES = {
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_max_speed": (_INT, [_VP, ctypes.POINTER(_D)]),
+    "swrt_qg_max_speed_async": (_INT, [_VP]),
+    "swrt_qg_max_speed_result": (_INT, [_VP, ctypes.POINTER(_D)]),
     "swrt_qg_get": (_INT, [_VP, _P, ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int64)]),
     "swrt_qg_get_q": (_INT, [_VP, _P]),
     "swrt_qg_snapshot": (_INT, [_VP, _INT, _INT, _INT, _I]),
@@ -373,6 +375,14 @@ class Context:
     def qg_max_speed(self):
         u = _D()
         self._chk(self._L.swrt_qg_max_speed(self._h, ctypes.byref(u)), "swrt_qg_max_speed")
+        return u.value
+
+    def qg_max_speed_async(self):
+        self._chk(self._L.swrt_qg_max_speed_async(self._h), "swrt_qg_max_speed_async")
+
+    def qg_max_speed_result(self):
+        u = _D()
+        self._chk(self._L.swrt_qg_max_speed_result(self._h, ctypes.byref(u)), "swrt_qg_max_speed_result")
         return u.value
 
     def qg_get(self):

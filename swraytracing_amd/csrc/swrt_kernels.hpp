@@ -342,7 +342,7 @@ __global__ void pack_nodes_kernel(const double* planes, int nx, int npad, double
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t tot = (int64_t)npad * npad;
   if (idx >= tot) return;
-  const int ip = (int)(idx / npad), jp = (int)(idx % npad);
+  const int ip = (int)idx / npad, jp = (int)idx % npad;
   int ig = ip - kPadLo, jg = jp - kPadLo;
   ig = ((ig % nx) + nx) % nx;
   jg = ((jg % nx) + nx) % nx;
@@ -358,7 +358,7 @@ __global__ void unpack_nodes_kernel(const double* nodes, int nx, int npad, doubl
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t plane = (int64_t)nx * nx;
   if (idx >= plane) return;
-  const int ig = (int)(idx % nx), jg = (int)(idx / nx);
+  const int ig = (int)idx % nx, jg = (int)idx / nx;
   const double* src = nodes + ((int64_t)(ig + kPadLo) * npad + (jg + kPadLo)) * kRec;
 #pragma unroll
   for (int f = 0; f < kRec; ++f) planes[f * plane + idx] = src[f];

@@ -90,12 +90,14 @@ __device__ __forceinline__ void qg2_B(double K2, double K_d2, double& b11, doubl
 // contiguous) and layer l, Z[2l] = psi_x + i psi_y, Z[2l+1] = q_x + i q_y with
 // the Hermitian completion of fulspec.m (kx < 0 on ky = 0 and ky < 0 from
 // their conjugate partners; Nyquist row/column zero).
-__global__ void qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+template <int NL>
+__global__ void __launch_bounds__(256) qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
   const int n = g.n;
   const int64_t nn = (int64_t)n * n;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nn) return;
-  const int c = (int)(idx % n), r = (int)(idx / n);
+  const int sh_ = __ffs(n) - 1;  // n is a power of two
+  const int c = (int)idx & (n - 1), r = (int)idx >> sh_;
   const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t nhalf = (int64_t)nkx * (kmax + 1);
   const int kx = signed_k(r, n), ky = signed_k(c, n);
@@ -107,8 +109,9 @@ __global__ void qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
   const double kxs = (double)hx * g.kscale, kys = (double)hy * g.kscale;
   const double K2 = kxs * kxs + kys * kys;
   cd q[2], ps[2];
-  for (int l = 0; l < g.nl; ++l) q[l] = inband ? ld(qk, l * nhalf + h) : cmk(0.0, 0.0);
-  if (g.nl == 1) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) q[l] = inband ? ld(qk, l * nhalf + h) : cmk(0.0, 0.0);
+  if constexpr (NL == 1) {
     // psik = -qk./(K_d2 + K2)   (qgsw_raytrace.m:271)
     const double den = g.K_d2 + K2;
     ps[0] = cmk(-q[0].x / den, -q[0].y / den);
@@ -119,7 +122,8 @@ __global__ void qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
     ps[0] = cadd(crs(b11, q[0]), crs(b12, q[1]));
     ps[1] = cadd(crs(b12, q[0]), crs(b11, q[1]));
   }
-  for (int l = 0; l < g.nl; ++l) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
     cd px = ik(kxs, ps[l]), py = ik(kys, ps[l]), qx = ik(kxs, q[l]), qy = ik(kys, q[l]);
     if (cj) { px.y = -px.y; py.y = -py.y; qx.y = -qx.y; qy.y = -qy.y; }
     if (!inband) px = py = qx = qy = cmk(0.0, 0.0);
@@ -203,7 +207,8 @@ __global__ void qg2_exp_kernel(QGDev g, double dt, double2* E1, double2* E2) {
   const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (int64_t)nkx * (kmax + 1)) return;
-  const int col = (int)(idx % (kmax + 1)), row = (int)(idx / (kmax + 1));
+  const int shh_ = __ffs(n) - 2;  // kmax + 1 = n/2, a power of two
+  const int col = (int)idx & (kmax), row = (int)idx >> shh_;
   const double kxs = (double)(row - kmax) * g.kscale, kys = (double)col * g.kscale;
   const double K2 = kxs * kxs + kys * kys;
   cd L[4], e[4];
@@ -227,14 +232,16 @@ __device__ __forceinline__ void mmul2(const double2* E, int64_t idx, const cd x[
 //   2 layers: Qn = g2k(J);  qk = mmult3(expLdt, qk + dq)   (:168-181)
 //   dq = dt*Qn | dt/2*(3Qn - X1) | dt/12*(23Qn - 16X1 + 5X2), X = Qm (1 layer)
 //   or mmult3(expL(2)dt, Qm) (2 layers); then Qm2 = Qm1, Qm1 = Qn.
-__global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abstep, const double2* E1,
+template <int NL>
+__global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev g, double dt, int abstep, const double2* E1,
                                  const double2* E2, const double2* qk, double2* qk_out, double2* Qm1,
                                  double2* Qm2) {
   const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t nhalf = (int64_t)nkx * (kmax + 1);
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nhalf) return;
-  const int col = (int)(idx % (kmax + 1)), row = (int)(idx / (kmax + 1));
+  const int shh_ = __ffs(n) - 2;  // kmax + 1 = n/2, a power of two
+  const int col = (int)idx & (kmax), row = (int)idx >> shh_;
   const int kx = row - kmax, ky = col;
   const double kxs = (double)kx * g.kscale, kys = (double)ky * g.kscale;
   const double K2 = kxs * kxs + kys * kys;
@@ -244,7 +251,7 @@ __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abst
   const int rm = kx > 0 ? n - kx : -kx, cm = ky > 0 ? n - ky : 0;
   const double2 Fk = Fj[c + (int64_t)n * r], Fm = Fj[cm + (int64_t)n * rm];
   cd Qn[2];
-  if (g.nl == 1) {
+  if constexpr (NL == 1) {
     // g2k(J) = fftshift(fft2(J))/nx^2 of a real J: the packed imaginary part is 0
     Qn[0] = cmk(Fk.x / nn, Fk.y / nn);
   } else {
@@ -254,8 +261,8 @@ __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abst
     Qn[1] = cdivr(F2, nn);
   }
   cd q[2];
-  for (int l = 0; l < g.nl; ++l) q[l] = ld(qk, l * nhalf + idx);
-  if (g.nl == 1) {
+  _Pragma("unroll") for (int l = 0; l < NL; ++l) q[l] = ld(qk, l * nhalf + idx);
+  if constexpr (NL == 1) {
     const double den = g.K_d2 + K2;
     const cd psik = cmk(-q[0].x / den, -q[0].y / den);
     const cd psikx = ik(kxs, psik);
@@ -266,11 +273,11 @@ __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abst
     Qn[0].x = Qn[0].x + force;
   }
   cd X1[2], X2[2], m1[2], m2[2];
-  for (int l = 0; l < g.nl; ++l) {
+  _Pragma("unroll") for (int l = 0; l < NL; ++l) {
     m1[l] = ld(Qm1, l * nhalf + idx);
     m2[l] = ld(Qm2, l * nhalf + idx);
   }
-  if (g.nl == 1) {
+  if constexpr (NL == 1) {
     X1[0] = m1[0];
     X2[0] = m2[0];
   } else {
@@ -278,7 +285,7 @@ __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abst
     mmul2(E2, idx, m2, X2);
   }
   cd dq[2];
-  for (int l = 0; l < g.nl; ++l) {
+  _Pragma("unroll") for (int l = 0; l < NL; ++l) {
     if (abstep == 1) {
       dq[l] = crs(dt, Qn[l]);
     } else if (abstep == 2) {
@@ -288,14 +295,14 @@ __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abst
     }
   }
   cd out[2];
-  if (g.nl == 1) {
+  if constexpr (NL == 1) {
     const double Ef = g.filter ? qg_filter_at(kxs, kys, g.dx) : 1.0;
     out[0] = crs(Ef, cadd(q[0], dq[0]));
   } else {
     cd s[2] = {cadd(q[0], dq[0]), cadd(q[1], dq[1])};
     mmul2(E1, idx, s, out);
   }
-  for (int l = 0; l < g.nl; ++l) {
+  _Pragma("unroll") for (int l = 0; l < NL; ++l) {
     st(qk_out, l * nhalf + idx, out[l]);
     st(Qm2, l * nhalf + idx, m1[l]);
     st(Qm1, l * nhalf + idx, Qn[l]);
@@ -304,12 +311,14 @@ __global__ void qg_update_kernel(const double2* Fj, QGDev g, double dt, int abst
 
 // u + i v per layer from grid_U's inversion psik = -qk./(K_d2+K2) (grid_U.m:2-6),
 // for the CFL speed (qg2layersw_raytrace.m:156-158); layout [c + n*r].
-__global__ void qg_vel_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+template <int NL>
+__global__ void __launch_bounds__(256) qg_vel_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
   const int n = g.n;
   const int64_t nn = (int64_t)n * n;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nn) return;
-  const int c = (int)(idx % n), r = (int)(idx / n);
+  const int sh_ = __ffs(n) - 1;  // n is a power of two
+  const int c = (int)idx & (n - 1), r = (int)idx >> sh_;
   const int kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t nhalf = (int64_t)nkx * (kmax + 1);
   const int kx = signed_k(r, n), ky = signed_k(c, n);
@@ -319,7 +328,8 @@ __global__ void qg_vel_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
   if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
   const double kxs = (double)hx * g.kscale, kys = (double)hy * g.kscale;
   const double den = g.K_d2 + (kxs * kxs + kys * kys);
-  for (int l = 0; l < g.nl; ++l) {
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
     cd u = cmk(0.0, 0.0), v = cmk(0.0, 0.0);
     if (inband) {
       const cd q = ld(qk, l * nhalf + (int64_t)(hx + kmax) * (kmax + 1) + hy);

@@ -176,7 +176,7 @@ __global__ void pack_xka_kernel(const double* planes, int nx, int npad, double* 
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t tot = (int64_t)npad * npad;
   if (idx >= tot) return;
-  const int ip = (int)(idx / npad), jp = (int)(idx % npad);
+  const int ip = (int)idx / npad, jp = (int)idx % npad;
   const int ig = ((ip - kPadLo) % nx + nx) % nx, jg = ((jp - kPadLo) % nx + nx) % nx;
   const int64_t plane = (int64_t)nx * nx, src = ig + (int64_t)nx * jg;
   double* d = nodes + idx * kXkaRec;

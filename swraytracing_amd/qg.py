@@ -64,13 +64,26 @@ class QGModel:
         """U0 = sqrt(max(u.^2 + v.^2)) of grid_U(qk) (all layers, u + shear)."""
         return self.ctx.qg_max_speed()
 
+    def cfl_rule(self, dt, U0, cfl_fraction):
+        """qg2layersw_raytrace.m:159-165 given U0: returns (dt, changed)."""
+        cond = cfl_fraction * self.dx / U0
+        if cond < dt or dt < cond / 4:
+            return cfl_fraction / 2 * self.dx / U0, True
+        return dt, False
+
     def cfl_update(self, dt, cfl_fraction):
         """qg2layersw_raytrace.m:156-165: returns (dt, U0, changed)."""
         U0 = self.max_speed()
-        cond = cfl_fraction * self.dx / U0
-        if cond < dt or dt < cond / 4:
-            return cfl_fraction / 2 * self.dx / U0, U0, True
-        return dt, U0, False
+        dt, changed = self.cfl_rule(dt, U0, cfl_fraction)
+        return dt, U0, changed
+
+    def max_speed_async(self):
+        """Enqueue U0 of the current qk; collect it with max_speed_result()
+        after queueing other work (the driver queues the packets first)."""
+        self.ctx.qg_max_speed_async()
+
+    def max_speed_result(self):
+        return self.ctx.qg_max_speed_result()
 
     @property
     def qk(self):
@@ -290,14 +303,19 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     step = 0
     have_cur = False
     dts = []
+    # U0 of the current qk is always one step ahead: its read-back is queued
+    # right after the PDE step and collected after the packet work of that
+    # step is queued, so the CFL rule (:156-165, same values, same order)
+    # never idles the GPU
     while t <= T and (max_steps is None or step < max_steps):
         step += 1
-        dt, U0, changed = model.cfl_update(dt, CFL_fraction)
+        dt, changed = model.cfl_rule(dt, U0, CFL_fraction)
         if changed:
             log(f"CFL condition not met, max|u|={U0:f}, new dt={dt:f}\n")
         dts.append(dt)
         model.step(dt)
         t = t + dt
+        model.max_speed_async()
         if ens is not None and t > packet_delay_steps:
             if have_cur:
                 ctx.swap_slots(0, 1)
@@ -311,6 +329,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
                 frames += 1
         else:
             have_cur = False
+        U0 = model.max_speed_result()
         # (the reference only plots q every steps_per_save steps here; its
         # pv.bin writes are commented out, qg2layersw_raytrace.m:211-239)
     log.close()

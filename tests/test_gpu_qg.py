@@ -128,6 +128,18 @@ def test_qg2_adaptive_cfl_sequence(ctx):
     assert _rel(m.qk, o.qk) < QG_RTOL
 
 
+def test_qg_max_speed_async_matches_sync(ctx):
+    nx = 64
+    m = sw.QGModel.two_layer(_two_layer_case(nx), nx, 3.0, 1.0, ctx=ctx)
+    m.step(0.01)
+    u_sync = m.max_speed()
+    m.max_speed_async()
+    ctx.packets_set(np.zeros((4, 2)), np.ones((4, 2)))  # unrelated work queued behind it
+    assert m.max_speed_result() == u_sync
+    with pytest.raises(sw.SwrtError):
+        m.max_speed_result()  # nothing pending
+
+
 def test_qg_get_q_is_k2g(ctx):
     nx = 64
     qk0 = _two_layer_case(nx)

@@ -61,15 +61,19 @@ def main():
     snap = timed(ctx, lambda: model.snapshot(1, which=0, ny_period=2 * nx), r)
     pk = timed(ctx, lambda: ens.advance(dt, args.nsub), r)
 
-    state = {"dt": dt}
+    state = {"dt": dt, "U0": model.max_speed()}
 
     def full_step():
-        d, _, _ = model.cfl_update(state["dt"], 0.25)
+        # the driver's order: CFL rule on the current U0, PDE step, async U0 of
+        # the new qk, snapshot + packets queued, then collect U0
+        d, _ = model.cfl_rule(state["dt"], state["U0"], 0.25)
         state["dt"] = d
         model.step(d)
+        model.max_speed_async()
         ctx.swap_slots(0, 1)
         model.snapshot(1, which=0, ny_period=2 * nx)
         ens.advance(d, args.nsub)
+        state["U0"] = model.max_speed_result()
 
     full = timed(ctx, full_step, r)
     ode = None
