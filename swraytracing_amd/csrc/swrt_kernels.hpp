@@ -173,6 +173,39 @@ __device__ __forceinline__ void interp6(const FieldView& fv, double x, double y,
   gather6<false>(fv.nodes, fv.nodes, fv.npad, s, out, dummy);
 }
 
+// The same sums as gather6 (same per-field order: i outer, j inner) with a
+// scheduling barrier after every tap, so at most one tap's 6 records are in
+// flight: the register-light global fallback of the LDS-tiled kernels, whose
+// hot path then needs no spills.  Rare path; its speed is secondary.
+template <bool TWO>
+__device__ __forceinline__ void gather6_lean(const double* nodes0, const double* nodes1, int npad,
+                                             const Stencil& s, double o0[kRec], double o1[kRec]) {
+#pragma unroll
+  for (int f = 0; f < kRec; ++f) { o0[f] = 0.0; o1[f] = 0.0; }
+  const size_t off = ((size_t)s.ic * npad + s.jc) * kRec;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+    const size_t ro = off + (size_t)i * npad * kRec;
+    const double2* r0 = reinterpret_cast<const double2*>(nodes0 + ro);
+    const double2* r1 = reinterpret_cast<const double2*>(nodes1 + ro);
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const double wij = s.wx[i] * s.wy[j];
+      const double2 a0 = r0[3 * j + 0], a1 = r0[3 * j + 1], a2 = r0[3 * j + 2];
+      o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
+      o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
+      o0[4] = o0[4] + wij * a2.x; o0[5] = o0[5] + wij * a2.y;
+      if constexpr (TWO) {
+        const double2 b0 = r1[3 * j + 0], b1 = r1[3 * j + 1], b2 = r1[3 * j + 2];
+        o1[0] = o1[0] + wij * b0.x; o1[1] = o1[1] + wij * b0.y;
+        o1[2] = o1[2] + wij * b1.x; o1[3] = o1[3] + wij * b1.y;
+        o1[4] = o1[4] + wij * b2.x; o1[5] = o1[5] + wij * b2.y;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 // Blend-then-interpolate from global memory (the out-of-window fallback of
 // the blend-in-LDS mode): each node value is (1-alpha)*F1 + alpha*F2 exactly
 // as stage_window_blend forms it, then one stencil sum.

@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
     if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M)
       gather6_lds<TWO, W, WN>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
     else
-      gather6<TWO>(a.f0.nodes, a.f1.nodes, a.f0.npad, sc, I, J);
+      gather6_lean<TWO>(a.f0.nodes, a.f1.nodes, a.f0.npad, sc, I, J);
     if constexpr (TWO) {
       const double oma = 1 - alpha;
 #pragma unroll

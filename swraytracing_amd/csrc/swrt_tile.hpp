@@ -111,6 +111,26 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
 #pragma unroll
   for (int f = 0; f < kRec; ++f) { o0[f] = 0.0; o1[f] = 0.0; }
   const double2* p = lds + node0;
+#ifdef SWRT_GATHER_SPLIT
+  // one snapshot at a time: 3 (not 6) 16-B reads in flight per tap
+#pragma unroll
+  for (int sn = 0; sn < (TWO ? 2 : 1); ++sn) {
+    double* o = sn == 0 ? o0 : o1;
+    const double2* q = p + 3 * sn * WN;
+#pragma unroll
+    for (int i = 0; i < kNT; ++i) {
+#pragma unroll
+      for (int j = 0; j < kNT; ++j) {
+        const int e = i * W + j;
+        const double wij = s.wx[i] * s.wy[j];
+        const double2 a0 = q[0 * WN + e], a1 = q[1 * WN + e], a2 = q[2 * WN + e];
+        o[0] = o[0] + wij * a0.x; o[1] = o[1] + wij * a0.y;
+        o[2] = o[2] + wij * a1.x; o[3] = o[3] + wij * a1.y;
+        o[4] = o[4] + wij * a2.x; o[5] = o[5] + wij * a2.y;
+      }
+    }
+  }
+#else
 #pragma unroll
   for (int i = 0; i < kNT; ++i) {
 #pragma unroll
@@ -129,6 +149,7 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
       }
     }
   }
+#endif
 }
 
 // Stage tile (ox, oy)'s window into LDS, chunk-major (chunk c of node e at
@@ -339,7 +360,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
           if (inwin)
             gather6_lds<TWO, W, WNP>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
           else
-            gather6<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
+            gather6_lean<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
           if constexpr (TWO) {
             const double alpha = a.alpha0 + (double)sg * a.dalpha;
             const double oma = 1 - alpha;
