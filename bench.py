@@ -125,6 +125,19 @@ def cpu_baseline(ctx, w, target_s):
                       f"(oracle/swrt_oracle.c, OpenMP {threads} threads, {t:.1f} s)"}
 
 
+FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s: 78.6 TFLOP/s counting an FMA as 2
+
+
+def load_valu(config_key):
+    path = os.path.join(ROOT, "profiles", "valu.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get(config_key)
+    except Exception:
+        return None
+
+
 def load_traffic(config_key):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
@@ -226,6 +239,17 @@ def main():
     # fp64 VALU work per packet-step of the exact-order stencil
     key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}"
     traffic = load_traffic(key)
+    valu = load_valu(key)
+    valu_roofline = None
+    if valu is not None and args.blend_mode == 0:
+        # the kernel is fp64-VALU-issue bound (no FMA allowed: bit-exact order):
+        # PMC-measured VALU instructions per launch x 64 lanes / launch time
+        lane_ops = valu["SQ_INSTS_VALU"] * 64.0
+        ach = lane_ops / avg_launch_s
+        valu_roofline = {"bound": "valu-fp64-issue", "achieved": ach, "peak": FP64_LANE_OPS_PEAK,
+                         "unit": "lane-ops/s", "frac": ach / FP64_LANE_OPS_PEAK,
+                         "valu_instructions_per_launch": valu["SQ_INSTS_VALU"],
+                         "source": "profiles/valu.json (rocprofv3 PMC)"}
     out = {
         "metric": "packet-steps/sec @ 512² field, 1e6 packets; 1/2/4/8-GPU scaling",
         "value": value,
@@ -250,6 +274,7 @@ def main():
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_packet_step": B, "avg_launch_ms": avg_launch_s * 1e3,
                      "timed_launches": launches, "timing_every": args.timing_every},
+        "valu_roofline": valu_roofline,
         "finite": finite,
     }
     if gathered is not None:
