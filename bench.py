@@ -95,14 +95,18 @@ def step(ctx, w, sub):
                 bump=sw.BUMP_QG)
 
 
-def cpu_baseline(ctx, w, target_s):
-    """The C oracle (OpenMP) on this host: same fields, same algorithm."""
+def cpu_baseline(ctx, w, target_s, threads=0):
+    """The C oracle (OpenMP) on this host: same fields, same algorithm.
+    threads = 0: all of the process's threads; 1: one core."""
     from oracle import cbind
     cbind.build()
     nx = w["nx"]
     p0 = ctx.get_field_grid(0, nx)
     p1 = ctx.get_field_grid(1, nx) if w["nslots"] == 2 else None
-    threads = cbind.lib().oracle_num_threads()
+    default_threads = cbind.lib().oracle_num_threads()  # OMP_NUM_THREADS (16 on the GPU box)
+    if threads > 0:
+        cbind.lib().oracle_set_threads(threads)
+    nthreads = cbind.lib().oracle_num_threads()
 
     def run(n, steps):
         x = w["x"][:n]
@@ -112,7 +116,7 @@ def cpu_baseline(ctx, w, target_s):
                        w["f"], w["gH"])
         return time.perf_counter() - t0
 
-    n = min(20000, w["x"].shape[0])
+    n = min(20000 if nthreads > 1 else 2000, w["x"].shape[0])
     run(n, 1)  # warm-up: OpenMP thread start, page faults
     t = run(n, 4)
     s1 = max(4, int(1.0 * 4 / max(t, 1e-9)))  # ~1 s calibration run
@@ -120,9 +124,10 @@ def cpu_baseline(ctx, w, target_s):
     rate = s1 * n / max(t, 1e-9)
     steps = max(1, int(target_s * rate / n))
     t = run(n, steps)
-    return {"value": n * steps / t, "unit": "packet-steps/s", "cores": int(threads), "kind": "port",
+    cbind.lib().oracle_set_threads(default_threads)
+    return {"value": n * steps / t, "unit": "packet-steps/s", "cores": int(nthreads), "kind": "port",
             "sample": f"{n} packets x {steps} leapfrog steps of the same {nx}^2 two-snapshot field "
-                      f"(oracle/swrt_oracle.c, OpenMP {threads} threads, {t:.1f} s)"}
+                      f"(oracle/swrt_oracle.c, OpenMP {nthreads} threads, {t:.1f} s)"}
 
 
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s: 78.6 TFLOP/s counting an FMA as 2
@@ -281,6 +286,8 @@ def main():
         out["gathered_finite"] = gathered
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(ctx, w, args.cpu_seconds)
+        # SURVEY §8d also asks for the 1-core figure of the same restatement
+        out["cpu_baseline_1core"] = cpu_baseline(ctx, w, args.cpu_seconds / 3, threads=1)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

@@ -35,6 +35,8 @@ def lib():
                                       _I, _P, _P]
         L.oracle_leapfrog.restype = None
         L.oracle_num_threads.restype = ctypes.c_int
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_set_threads.restype = None
         _lib = L
     return _lib
 

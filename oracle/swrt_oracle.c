@@ -123,6 +123,17 @@ void oracle_leapfrog(const double* fields0, const double* fields1, double alpha0
     }
 }
 
+/* Thread count of the next oracle calls (n <= 0: all processors). */
+void oracle_set_threads(int n) {
+#ifdef _OPENMP
+    extern void omp_set_num_threads(int);
+    extern int omp_get_num_procs(void);
+    omp_set_num_threads(n > 0 ? n : omp_get_num_procs());
+#else
+    (void)n;
+#endif
+}
+
 int oracle_num_threads(void) {
 #ifdef _OPENMP
     extern int omp_get_max_threads(void);
