@@ -4,6 +4,7 @@
 // stream per context, every call synchronous to the host and exception-free
 // across the ABI boundary.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdio>
@@ -152,6 +153,9 @@ struct swrt_ctx {
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
+  // set only around a timed packet launch: the dispatch itself stamps them
+  // (hipExtLaunchKernel), so they bracket the kernel and nothing else
+  hipEvent_t kev0 = nullptr, kev1 = nullptr;
 };
 
 namespace {
@@ -337,7 +341,14 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
 bool use_tile_kernel(const swrt_ctx* c);
 int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next);
 
-// Record a timing event pair around one leapfrog launch.
+// Launch a packet kernel on the context stream; inside a timed launch the
+// start/stop events take the kernel's own begin/end timestamps.
+template <typename F, typename... Args>
+void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
+  hipExtLaunchKernelGGL(kernel, grid, block, 0, c->stream, c->kev0, c->kev1, 0, args...);
+}
+
+// Time every timing_every-th leapfrog launch with a pair of HIP events.
 int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next) {
   const bool timed = c->timing_every > 0 && (c->launch_count++ % c->timing_every) == 0;
   if (!timed) {
@@ -368,21 +379,22 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next)
       c->timing.ev.push_back(ev);
     }
   }
-  hipEvent_t e0 = c->timing.ev[c->timing.used], e1 = c->timing.ev[c->timing.used + 1];
+  c->kev0 = c->timing.ev[c->timing.used];
+  c->kev1 = c->timing.ev[c->timing.used + 1];
   c->timing.used += 2;
-  HIPCHK(c, hipEventRecord(e0, c->stream));
+  int rc = SWRT_OK;
   if (use_tile_kernel(c)) {
-    int rc = tile_launch(c, a, count_next);
-    if (rc) return rc;
+    rc = tile_launch(c, a, count_next);
   } else {
     c->keys_fresh = false;
     if (a.nslots == 2)
-      hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
+      launch_k(c, leapfrog_kernel<true>, dim3(grid), dim3(256), a);
     else
-      hipLaunchKernelGGL(leapfrog_kernel<false>, dim3(grid), dim3(256), 0, c->stream, a);
-    HIPCHK(c, hipGetLastError());
+      launch_k(c, leapfrog_kernel<false>, dim3(grid), dim3(256), a);
   }
-  HIPCHK(c, hipEventRecord(e1, c->stream));
+  c->kev0 = c->kev1 = nullptr;
+  if (rc) return rc;
+  HIPCHK(c, hipGetLastError());
   return SWRT_OK;
 }
 
@@ -465,20 +477,15 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
     const int tpw = (int)((grid + ncu - 1) / ncu);
     const unsigned pgrid = (unsigned)((grid + tpw - 1) / tpw);
     if (a.nslots == 2)
-      hipLaunchKernelGGL((tile_persist_kernel<true, kTile, kMargin, 1024>), dim3(pgrid), dim3(1024), 0,
-                         c->stream, t, tpw);
+      launch_k(c, tile_persist_kernel<true, kTile, kMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
     else
-      hipLaunchKernelGGL((tile_persist_kernel<false, kTile, kMargin, 1024>), dim3(pgrid), dim3(1024), 0,
-                         c->stream, t, tpw);
+      launch_k(c, tile_persist_kernel<false, kTile, kMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
   } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
-    hipLaunchKernelGGL((tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>), dim3(grid),
-                       dim3(kTileThreads), 0, c->stream, t);
+    launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(grid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
-    hipLaunchKernelGGL((tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>), dim3(grid),
-                       dim3(kTileThreads), 0, c->stream, t);
+    launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
   } else {
-    hipLaunchKernelGGL((tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>), dim3(grid),
-                       dim3(kTileThreads), 0, c->stream, t);
+    launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
   }
   HIPCHK(c, hipGetLastError());
   std::swap(c->dx, c->dx2);
