@@ -57,14 +57,27 @@ const char* swrt_last_error(const swrt_ctx* ctx);
  * (SpectralScheme.m:29-35) or a grid_U output struct (grid_U.m:11-17).
  * ny_period: the y-period of interpolate.m's mod (interpolate.m:15,22): nx for
  * a single layer, nlayers*nx for the 2-layer call (qg2layersw_raytrace.m:187-188)
- * where F is nx x nx x 2 and only layer 1 is read.  0 means nx. */
+ * where F is nx x nx x 2 and only layer 1 is read.  0 means nx.
+ * If v_y == -u_x bit for bit at every node (a streamfunction flow stored that
+ * way) the slot is marked divergence-free and the packet kernels carry five
+ * stencil sums instead of six (v_y's is the exact negation of u_x's), with
+ * unchanged results. */
 int swrt_set_field_grid(swrt_ctx* ctx, int slot, const double* fields6, int64_t nx, double L,
                         int64_t ny_period);
+
+/* 1 if slot's v_y is exactly -u_x at every node (always so for fields the
+ * library derives from psi / qk: it stores v_y as -u_x, see
+ * swrt_set_field_psi), 0 if not, < 0 on error. */
+int swrt_field_div_free(swrt_ctx* ctx, int slot);
 
 /* SpectralScheme(L, nx, psi_field) constructor (SpectralScheme.m:6-36):
  * psik = g2k(psi); u = k2g(-i ky psik), v = k2g(i kx psik), gradients by
  * i kx / i ky; integer wavenumbers regardless of L.  FFTs run on the GPU.
- * The filtered psi grid k2g(g2k(psi)) is kept for swrt_get_psi_grid. */
+ * The filtered psi grid k2g(g2k(psi)) is kept for swrt_get_psi_grid.
+ * v_y is stored as -u_x (bit-exact negation): SpectralScheme.m / grid_U.m
+ * transform i ky vk separately, which equals -(i kx uk) up to the FFT's
+ * roundoff (the identity u_x + v_y = 0 of a streamfunction flow); the same
+ * holds for swrt_set_field_qk and swrt_qg_snapshot. */
 int swrt_set_field_psi(swrt_ctx* ctx, int slot, const double* psi_grid, int64_t nx, double L);
 
 /* grid_U(qk, K_d2, K2, kx_, ky_, shear_strength) (grid_U.m:1-18) for one

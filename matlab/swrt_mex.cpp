@@ -24,6 +24,7 @@
 //   swrt_mex('qg_step', dt, nsteps);  U0 = swrt_mex('qg_max_speed');
 //   [qk, t, steps] = swrt_mex('qg_get');  q = swrt_mex('qg_get_q');
 //   swrt_mex('qg_snapshot', slot, which, layer, ny_period);  swrt_mex('swap_slots', a, b)
+//   tf = swrt_mex('field_div_free', slot)   % v_y == -u_x exactly (five-sum kernels)
 //   swrt_mex('destroy')
 #include <cstring>
 #include <string>
@@ -267,6 +268,12 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   }
   if (!strcmp(cmd, "swap_slots")) {
     check(swrt_swap_slots(ctx(), (int)scalar(prhs[1]), (int)scalar(prhs[2])), "swrt_swap_slots");
+    return;
+  }
+  if (!strcmp(cmd, "field_div_free")) {
+    const int rc = swrt_field_div_free(ctx(), (int)scalar(prhs[1]));
+    if (rc < 0) check(rc, "swrt_field_div_free");
+    plhs[0] = mxCreateDoubleScalar(rc == 1 ? 1.0 : 0.0);
     return;
   }
   mexErrMsgIdAndTxt("swrt:arg", "unknown command '%s'", cmd);

@@ -86,6 +86,7 @@ SIGNATURES = {
     "swrt_qg_get_q": (_INT, [_VP, _P]),
     "swrt_qg_snapshot": (_INT, [_VP, _INT, _INT, _INT, _I]),
     "swrt_swap_slots": (_INT, [_VP, _INT, _INT]),
+    "swrt_field_div_free": (_INT, [_VP, _INT]),
     "swrt_synchronize": (_INT, [_VP]),
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
@@ -179,6 +180,14 @@ class Context:
         out = np.empty(6 * nx * nx)
         self._chk(self._L.swrt_get_field_grid(self._h, slot, _p(out)), "swrt_get_field_grid")
         return out.reshape(6, nx * nx)
+
+    def field_div_free(self, slot=0):
+        """True if slot's v_y is exactly -u_x (the packet kernels then carry
+        five stencil sums; results are unchanged)."""
+        rc = self._L.swrt_field_div_free(self._h, int(slot))
+        if rc < 0:
+            self._chk(rc, "swrt_field_div_free")
+        return rc == 1
 
     def get_psi_grid(self, slot, nx):
         out = np.empty(nx * nx)

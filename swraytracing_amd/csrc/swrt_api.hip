@@ -36,13 +36,14 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #define SWRT_TILE 16
 #endif
 #ifndef SWRT_MARGIN
-#define SWRT_MARGIN 2
+#define SWRT_MARGIN 3
 #endif
 #ifndef SWRT_TILE_THREADS
 #define SWRT_TILE_THREADS 512
 #endif
 constexpr int kTile = SWRT_TILE;                // LDS tile kernel: cells per tile side
 constexpr int kMargin = SWRT_MARGIN;            // LDS tile kernel: drift margin (cells)
+constexpr int kPersistMargin = 2;                // variant 3 (experiment): its double-buffered windows need the LDS
 constexpr int kTileThreads = SWRT_TILE_THREADS;
 
 struct Slot {
@@ -54,6 +55,7 @@ struct Slot {
   double L = 0.0;
   bool set = false;
   bool has_psi = false;
+  bool div_free = false;    // every node's v_y is exactly -u_x (five-sum kernels apply)
 };
 
 // device-resident QG PDE state (swrt_qg.hpp)
@@ -102,6 +104,8 @@ struct swrt_ctx {
   double* dk2 = nullptr;
   int* perm2 = nullptr;
   int* keys = nullptr;   // N
+  int* src_idx = nullptr;   // N: source slot of each binned slot (indirect re-binning)
+  bool src_pending = false;  // the next tile launch reads its packets through src_idx
   int* bins = nullptr;   // counts | cursor | starts  (3 * kMaxBins + 1)
   int kernel = 0;        // 0 auto, 1 per-packet global gather, 2 LDS tile kernel
   int nbins = 0;         // bins of the current binning
@@ -335,6 +339,7 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
     if ((rc = pack_slot(c, slot, planes, shear))) return rc;
   }
   s.has_psi = with_psi != 0;
+  s.div_free = true;  // pack_pairs_kernel / unpair_kernel write v_y = -u_x
   return SWRT_OK;
 }
 
@@ -414,7 +419,11 @@ int tile_cells(const swrt_ctx* c, int64_t nx) {
 }
 
 // Counting-sort the packets by spatial tile of slot 0's grid (swrt_bin.hpp).
-int rebin(swrt_ctx* c) {
+// indirect: only build the source index of the binned order (c->src_idx);
+// the tile launch that follows reads through it and writes the packets in
+// binned order (saves moving 36 B per packet twice).  Callers other than the
+// leapfrog loop need the packets moved (indirect = false).
+int rebin(swrt_ctx* c, bool indirect) {
   const Slot& s = c->slot[0];
   const FieldView v = view_of(s);
   BinGeom g;
@@ -437,12 +446,20 @@ int rebin(swrt_ctx* c) {
                      c->bins + 2 * kMaxBins);
   HIPCHK(c, hipGetLastError());
   c->counts_zero = true;
-  hipLaunchKernelGGL(bin_scatter_kernel, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream, c->dx,
-                     c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2);
+  if (indirect) {
+    hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
+                       c->dx, c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2,
+                       c->src_idx);
+  } else {
+    hipLaunchKernelGGL(bin_scatter_kernel<false>, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
+                       c->dx, c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2,
+                       nullptr);
+    std::swap(c->dx, c->dx2);
+    std::swap(c->dk, c->dk2);
+    std::swap(c->perm, c->perm2);
+  }
   HIPCHK(c, hipGetLastError());
-  std::swap(c->dx, c->dx2);
-  std::swap(c->dk, c->dk2);
-  std::swap(c->perm, c->perm2);
+  c->src_pending = indirect;
   c->steps_since_bin = 0;
   c->bin_valid = true;
   c->cells_sorted = false;
@@ -462,6 +479,12 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   t.next_keys = nullptr;
   t.next_counts = nullptr;
   t.sort_cells = (c->cell_sort == 1 || !c->cells_sorted) ? 1 : 0;
+  t.src = nullptr;
+  if (c->src_pending) {  // first launch after an indirect re-binning (always a sort launch)
+    t.src = c->src_idx;
+    t.sort_cells = 1;
+    c->src_pending = false;
+  }
   if (count_next && (int)grid == c->nbins) {
     if (!c->counts_zero) HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * grid, c->stream));
     c->counts_zero = false;
@@ -477,15 +500,23 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
     const int tpw = (int)((grid + ncu - 1) / ncu);
     const unsigned pgrid = (unsigned)((grid + tpw - 1) / tpw);
     if (a.nslots == 2)
-      launch_k(c, tile_persist_kernel<true, kTile, kMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
+      launch_k(c, tile_persist_kernel<true, kTile, kPersistMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
     else
-      launch_k(c, tile_persist_kernel<false, kTile, kMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
+      launch_k(c, tile_persist_kernel<false, kTile, kPersistMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
   } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
     launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(grid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
-    launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
+    if (c->slot[0].div_free && c->slot[1].div_free)
+      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, dim3(grid),
+               dim3(kTileThreads), t);
+    else
+      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
   } else {
-    launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
+    if (c->slot[0].div_free)
+      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true>, dim3(grid),
+               dim3(kTileThreads), t);
+    else
+      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
   }
   HIPCHK(c, hipGetLastError());
   std::swap(c->dx, c->dx2);
@@ -521,7 +552,7 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
     if (c->blend_mode == 1 && nslots == 2 && use_tile_kernel(c)) chunk = 1;  // alpha fixed per launch
     if (c->rebin_every > 0) {
       if (!c->bin_valid || c->steps_since_bin >= c->rebin_every) {
-        int rc = rebin(c);
+        int rc = rebin(c, use_tile_kernel(c) && c->kernel != 3);
         if (rc) return rc;
       }
       chunk = std::min<int64_t>(chunk, c->rebin_every - c->steps_since_bin);
@@ -580,7 +611,7 @@ void swrt_destroy(swrt_ctx* c) {
     if (s.psi) (void)hipFree(s.psi);
   }
   for (void* p : {(void*)c->dx, (void*)c->dk, (void*)c->perm, (void*)c->dx2, (void*)c->dk2,
-                  (void*)c->perm2, (void*)c->keys, (void*)c->bins})
+                  (void*)c->perm2, (void*)c->keys, (void*)c->src_idx, (void*)c->bins})
     if (p) (void)hipFree(p);
   if (c->hx) (void)hipFree(c->hx);
   if (c->hk) (void)hipFree(c->hk);
@@ -619,8 +650,17 @@ int swrt_set_field_grid(swrt_ctx* c, int slot, const double* fields6, int64_t nx
   if ((rc = ensure_scratch(c, bytes))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->scratch, fields6, bytes, hipMemcpyHostToDevice, c->stream));
   if ((rc = pack_slot(c, slot, (const double*)c->scratch, 0.0))) return rc;
+  // host-given fields take the five-sum kernels only if v_y == -u_x bit for bit
+  bool div_free = true;
+  {
+    const int64_t plane = nx * nx;
+    const uint64_t* ux = reinterpret_cast<const uint64_t*>(fields6 + 2 * plane);
+    const uint64_t* vy = reinterpret_cast<const uint64_t*>(fields6 + 5 * plane);
+    for (int64_t i = 0; i < plane && div_free; ++i) div_free = vy[i] == (ux[i] ^ 0x8000000000000000ull);
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   Slot& s = c->slot[slot];
+  s.div_free = div_free;
   s.L = L;
   s.ny_period = ny_period;
   s.has_psi = false;
@@ -775,6 +815,13 @@ int swrt_k2g(swrt_ctx* c, const double* fk_in, int64_t nx, double* fg_out) {
   GUARD_END(c)
 }
 
+int swrt_field_div_free(swrt_ctx* c, int slot) {
+  if (!c) return SWRT_ERR_ARG;
+  if (slot < 0 || slot >= SWRT_MAX_SLOTS || !c->slot[slot].set)
+    return fail(c, SWRT_ERR_STATE, "slot not set");
+  return c->slot[slot].div_free ? 1 : 0;
+}
+
 int swrt_get_field_grid(swrt_ctx* c, int slot, double* out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
@@ -880,7 +927,7 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
   HIPCHK(c, hipSetDevice(c->device));
   if (n > c->cap) {
     for (void** p : {(void**)&c->dx, (void**)&c->dk, (void**)&c->perm, (void**)&c->dx2, (void**)&c->dk2,
-                     (void**)&c->perm2, (void**)&c->keys}) {
+                     (void**)&c->perm2, (void**)&c->keys, (void**)&c->src_idx}) {
       if (*p) (void)hipFree(*p);
       *p = nullptr;
     }
@@ -892,6 +939,7 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
     HIPCHK(c, hipMalloc(&c->perm, sizeof(int) * n));
     HIPCHK(c, hipMalloc(&c->perm2, sizeof(int) * n));
     HIPCHK(c, hipMalloc(&c->keys, sizeof(int) * n));
+    HIPCHK(c, hipMalloc(&c->src_idx, sizeof(int) * n));
     c->cap = n;
   }
   if (!c->bins) HIPCHK(c, hipMalloc(&c->bins, sizeof(int) * (3 * kMaxBins + 1)));
@@ -908,6 +956,7 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
   c->steps_done = 0;
   c->bin_valid = false;
   c->keys_fresh = false;
+  c->src_pending = false;
   c->steps_since_bin = 0;
   return SWRT_OK;
   GUARD_END(c)
@@ -958,6 +1007,7 @@ int swrt_set_kernel(swrt_ctx* c, int variant) {
   c->kernel = variant;
   c->bin_valid = false;
   c->keys_fresh = false;
+  c->src_pending = false;
   return SWRT_OK;
 }
 
@@ -968,6 +1018,7 @@ int swrt_set_locality(swrt_ctx* c, int64_t rebin_every, int64_t tile) {
   c->tile = tile;
   c->bin_valid = false;
   c->keys_fresh = false;
+  c->src_pending = false;
   return SWRT_OK;
 }
 
@@ -1118,6 +1169,8 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   a.npad = (int)(c->xka_nx + kPadTot);
   a.dx = c->xka_dx;
   a.dy = c->xka_dy;
+  a.inv_dx = 1.0 / a.dx;
+  a.inv_dy = 1.0 / a.dy;
   a.px = a.py = (double)c->xka_nx;
   a.inv_px = a.inv_py = 1.0 / (double)c->xka_nx;
   a.pow2x = a.pow2y = is_pow2(c->xka_nx);
@@ -1669,7 +1722,7 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
   // one spatial re-binning per ode23 call (the packet order is free: the
   // error norm is a max over all components)
   if (c->rebin_every > 0 && c->slot[0].set) {
-    if ((rc = rebin(c))) return rc;
+    if ((rc = rebin(c, false))) return rc;
   }
   Ode23Args a;
   if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;

@@ -92,10 +92,14 @@ __global__ void __launch_bounds__(1024) bin_scan_kernel(int* counts, int nbins, 
 
 // Pass 3: scatter.  Each block ranks its packets per bin in LDS, reserves one
 // contiguous range per occupied bin with a single global atomic, then writes.
+// INDEX: write only the source index of every destination slot (src[d] = p,
+// 4 B instead of the 36 B packet): the next tile launch reads its packets
+// through it and writes them in binned order itself.
+template <bool INDEX>
 __global__ void __launch_bounds__(256) bin_scatter_kernel(const double* x, const double* k,
                                                           const int* perm, const int* keys, int64_t n,
                                                           int nbins, int* cursor, double* x2,
-                                                          double* k2, int* perm2) {
+                                                          double* k2, int* perm2, int* src) {
   extern __shared__ int sh[];
   int* cnt = sh;            // nbins
   int* base = sh + nbins;   // nbins
@@ -124,6 +128,10 @@ __global__ void __launch_bounds__(256) bin_scatter_kernel(const double* x, const
     const int64_t p = b0 + (int64_t)q * blockDim.x + threadIdx.x;
     if (p < n) {
       const int64_t d = (int64_t)base[key[q]] + local[q];
+      if constexpr (INDEX) {
+        src[d] = (int)p;
+        continue;
+      }
       x2[d] = x[p];
       x2[n + d] = x[n + p];
       k2[d] = k[p];

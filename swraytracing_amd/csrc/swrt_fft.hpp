@@ -297,7 +297,7 @@ __global__ void unpair_kernel(const double2* Z, int n, int with_psi, double* pla
   planes[2 * nn + idx] = z1.x;
   planes[3 * nn + idx] = z1.y;
   planes[4 * nn + idx] = z2.x;
-  planes[5 * nn + idx] = z2.y;
+  planes[5 * nn + idx] = -z1.x;  // v_y = -u_x exactly (see pack_pairs_kernel)
   if (with_psi) psi[idx] = Z[3 * nn + idx].x;
 }
 
@@ -327,6 +327,10 @@ __global__ void fulspec_kernel(const double2* fk, int n, double2* Z, int sx, int
 // T2 = v_x + i v_y (layout [x + n*y]) -> interior node records (y fastest,
 // 48 B each) through a 16x16 LDS tile, so both the reads (along x) and the
 // record writes (along y) are contiguous.  u gets `shear` (grid_U.m:11).
+// v_y is stored as -u_x, bit for bit: the flow of a streamfunction is
+// divergence-free, and grid_U.m:8-9's separate transform of i ky vk equals
+// -(i kx uk) up to the transform's roundoff.  The exact identity lets the
+// packet kernels carry five stencil sums instead of six (swrt_tile.hpp).
 // Ghost nodes are filled by halo_nodes_kernel afterwards.
 __global__ void __launch_bounds__(256) pack_pairs_kernel(const double2* T, int n, int npad, double shear,
                                                          double* nodes) {
@@ -345,7 +349,7 @@ __global__ void __launch_bounds__(256) pack_pairs_kernel(const double2* T, int n
   dst[2] = b.x;
   dst[3] = b.y;
   dst[4] = c.x;
-  dst[5] = c.y;
+  dst[5] = -b.x;
 }
 
 // Periodic ghost records of the padded node array (2 below, 3 above in each

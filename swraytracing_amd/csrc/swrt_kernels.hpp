@@ -30,15 +30,31 @@ struct FieldView {
   double px, py;        // mod periods of x/dx and y/dy (nx, ny_period)
   double inv_px, inv_py;
   int pow2x, pow2y;     // period is a power of two: a/m == a*(1/m) exactly
-  double inv_dx;        // 1/dx, for locality keys only (never for the arithmetic)
+  double inv_dx;        // RN(1/dx): locality keys, and x/dx via div_rn (correctly rounded)
 };
+
+// a / b correctly rounded (== IEEE a/b) from rb = RN(1/b), in one multiply
+// and two FMAs (Markstein; Handbook of Floating-Point Arithmetic, Thm 4.10):
+// q0 = RN(a*rb) is within 1 ulp of a/b, r = a - b*q0 is exact in an FMA, and
+// RN(q0 + r*rb) is then the correctly rounded quotient.  Outside the normal
+// range the result may differ from IEEE division, which does not matter here:
+// |a/b| < 2^-54 gives the same cell and offset (1 + xl rounds to 1 either
+// way), and an overflowing quotient is NaN instead of Inf, which cell_frac
+// turns into NaN anyway (Inf - Inf).  Checked bit-exact against a/b on 1e9
+// random pairs (a and b over 120 binades each) on the host.
+__device__ __forceinline__ double div_rn(double a, double b, double rb) {
+  const double q0 = a * rb;
+  const double r = __builtin_fma(-q0, b, a);
+  return __builtin_fma(r, rb, q0);
+}
 
 // interpolate.m:21-31 — xl = mod(x/dx, n); i0 = 1 + floor(xl); a = 1 + xl - i0.
 // Returns the 0-based cell reduced mod nx and the fractional offset a.
-__device__ __forceinline__ int cell_frac(double x, double dx, double period, double inv_period,
-                                         int pow2, int nx, double& a) {
-  const double q = x / dx;
-  const double r = pow2 ? q * inv_period : q / period;
+// inv_dx = RN(1/dx) and inv_period = RN(1/period) from the host.
+__device__ __forceinline__ int cell_frac(double x, double dx, double inv_dx, double period,
+                                         double inv_period, int pow2, int nx, double& a) {
+  const double q = div_rn(x, dx, inv_dx);
+  const double r = pow2 ? q * inv_period : div_rn(q, period, inv_period);
   const double xl = q - floor(r) * period;   // MATLAB mod (a - floor(a/m)*m)
   const double fl = floor(xl);
   a = (1.0 + xl) - (1.0 + fl);
@@ -128,8 +144,8 @@ struct Stencil {
 __device__ __forceinline__ void stencil_at(const FieldView& fv, double x, double y, double bump,
                                            Stencil& s) {
   double ax, ay;
-  s.ic = cell_frac(x, fv.dx, fv.px, fv.inv_px, fv.pow2x, fv.nx, ax);
-  s.jc = cell_frac(y, fv.dx, fv.py, fv.inv_py, fv.pow2y, fv.nx, ay);
+  s.ic = cell_frac(x, fv.dx, fv.inv_dx, fv.px, fv.inv_px, fv.pow2x, fv.nx, ax);
+  s.jc = cell_frac(y, fv.dx, fv.inv_dx, fv.py, fv.inv_py, fv.pow2y, fv.nx, ay);
   lagrange_w(ax, bump, s.wx);
   lagrange_w(ay, bump, s.wy);
 }
@@ -137,11 +153,14 @@ __device__ __forceinline__ void stencil_at(const FieldView& fv, double x, double
 // Six-field stencil sums of one or two snapshots:
 //   out[f] = sum_i sum_j (wx_i * wy_j) * F_f[ig, jg]
 // accumulated i-outer / j-inner exactly as interpolate.m:43-49 does per field.
+// The sums start from -0.0, the additive identity (-0 + p == p for every p,
+// so the first add folds away; +0 + p differs from p only in the sign of an
+// all-negative-zero sum, which is numerically equal).
 template <bool TWO>
 __device__ __forceinline__ void gather6(const double* nodes0, const double* nodes1, int npad,
                                         const Stencil& s, double o0[kRec], double o1[kRec]) {
 #pragma unroll
-  for (int f = 0; f < kRec; ++f) { o0[f] = 0.0; o1[f] = 0.0; }
+  for (int f = 0; f < kRec; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
   const size_t off = ((size_t)s.ic * npad + s.jc) * kRec;
 #pragma unroll
   for (int i = 0; i < kNT; ++i) {
@@ -181,7 +200,7 @@ template <bool TWO>
 __device__ __forceinline__ void gather6_lean(const double* nodes0, const double* nodes1, int npad,
                                              const Stencil& s, double o0[kRec], double o1[kRec]) {
 #pragma unroll
-  for (int f = 0; f < kRec; ++f) { o0[f] = 0.0; o1[f] = 0.0; }
+  for (int f = 0; f < kRec; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
   const size_t off = ((size_t)s.ic * npad + s.jc) * kRec;
 #pragma unroll
   for (int i = 0; i < kNT; ++i) {
@@ -213,7 +232,7 @@ __device__ __forceinline__ void gather6_blend(const double* nodes0, const double
                                               const Stencil& s, double alpha, double o[kRec]) {
   const double oma = 1 - alpha;
 #pragma unroll
-  for (int f = 0; f < kRec; ++f) o[f] = 0.0;
+  for (int f = 0; f < kRec; ++f) o[f] = -0.0;
   const size_t off = ((size_t)s.ic * npad + s.jc) * kRec;
 #pragma unroll
   for (int i = 0; i < kNT; ++i) {
@@ -348,8 +367,8 @@ __global__ void __launch_bounds__(256) interp1_kernel(const double* F, int nx, d
   const double px = (double)nx;
   const int pow2x = (nx & (nx - 1)) == 0;
   double ax, ay;
-  const int ic = cell_frac(x[p], dx, px, 1.0 / px, pow2x, nx, ax);
-  const int jc = cell_frac(y[p], dy, pyF, inv_py, pow2y, nx, ay);
+  const int ic = cell_frac(x[p], dx, 1.0 / dx, px, 1.0 / px, pow2x, nx, ax);
+  const int jc = cell_frac(y[p], dy, 1.0 / dy, pyF, inv_py, pow2y, nx, ay);
   double wx[kNT], wy[kNT];
   lagrange_w(ax, bump, wx);
   lagrange_w(ay, bump, wy);

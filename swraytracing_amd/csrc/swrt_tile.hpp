@@ -38,6 +38,8 @@ struct TileArgs {
   int* next_counts;      // ... and add it to the per-tile counts (zeroed by the host)
   int sort_cells;        // 1: counting-sort each tile's packets by cell first; 0: the input
                          // is already in cell order (written so by the previous launch)
+  const int* src;        // non-NULL (sort launches only): binned slot p holds input packet
+                         // src[p] (indirect re-binning); NULL: slot p holds packet p
 };
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
@@ -108,7 +110,7 @@ template <bool TWO, int W, int WN>
 __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const Stencil& s,
                                             double o0[kRec], double o1[kRec]) {
 #pragma unroll
-  for (int f = 0; f < kRec; ++f) { o0[f] = 0.0; o1[f] = 0.0; }
+  for (int f = 0; f < kRec; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
   const double2* p = lds + node0;
 #ifdef SWRT_GATHER_SPLIT
   // one snapshot at a time: 3 (not 6) 16-B reads in flight per tap
@@ -151,12 +153,52 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
 #endif
 }
 
+// gather6_lds for fields with v_y == -u_x bit for bit (Slot::div_free):
+// five sums per snapshot from the V5 window, the same per-field order, and
+// the v_y sum as the exact negation of the u_x sum (negation commutes with
+// rounding), so the results are those of gather6_lds on the same nodes.
+template <bool TWO, int W, int WN>
+__device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const Stencil& s,
+                                            double o0[kRec], double o1[kRec]) {
+#pragma unroll
+  for (int f = 0; f < 5; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
+  const double2* p = lds + node0;
+#pragma unroll
+  for (int i = 0; i < kNT; ++i) {
+#pragma unroll
+    for (int j = 0; j < kNT; ++j) {
+      const int e = i * W + j;
+      const double wij = s.wx[i] * s.wy[j];
+      const double2 a0 = p[0 * WN + e], a1 = p[1 * WN + e];
+      double2 c;
+      if constexpr (TWO)
+        c = p[2 * WN + e];
+      else
+        c.x = reinterpret_cast<const double*>(p + 2 * WN + e)[0];
+      o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
+      o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
+      o0[4] = o0[4] + wij * c.x;
+      if constexpr (TWO) {
+        const double2 b0 = p[3 * WN + e], b1 = p[4 * WN + e];
+        o1[0] = o1[0] + wij * b0.x; o1[1] = o1[1] + wij * b0.y;
+        o1[2] = o1[2] + wij * b1.x; o1[3] = o1[3] + wij * b1.y;
+        o1[4] = o1[4] + wij * c.y;
+      }
+    }
+  }
+  o0[5] = -o0[2];
+  o1[5] = -o1[2];
+}
+
 // Stage tile (ox, oy)'s window into LDS, chunk-major (chunk c of node e at
 // win[c*WN + e]): node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx.
 // Register staging: each lane copies whole 48-B records, 3 or 6 loads back
 // to back (measured faster than LDS-DMA of the chunk-major image, whose 16-B
 // pieces are 48 B apart in HBM).  The caller publishes with a barrier.
-template <bool TWO, int T, int M, int NT, int WS = T + 5 + 2 * M>
+// V5 (fields with v_y == -u_x exactly): 5 chunks for two snapshots —
+// {u,v}0 {ux,uy}0 {vx0,vx1} {u,v}1 {ux,uy}1 — or 3 for one, whose third
+// holds {vx, vy} of which only vx is read.
+template <bool TWO, int T, int M, int NT, int WS = T + 5 + 2 * M, bool V5 = false>
 __device__ __forceinline__ void stage_window_regs(const FieldView& f0, const FieldView& f1, int ox, int oy,
                                                   double2* win) {
   constexpr int W = T + 5 + 2 * M;
@@ -169,14 +211,24 @@ __device__ __forceinline__ void stage_window_regs(const FieldView& f0, const Fie
     const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec;
     const int d = wi * WS + wj;
     const double2* s0 = reinterpret_cast<const double2*>(f0.nodes + src);
-    win[0 * WN + d] = s0[0];
-    win[1 * WN + d] = s0[1];
-    win[2 * WN + d] = s0[2];
-    if constexpr (TWO) {
+    if constexpr (V5 && TWO) {
       const double2* s1 = reinterpret_cast<const double2*>(f1.nodes + src);
-      win[3 * WN + d] = s1[0];
-      win[4 * WN + d] = s1[1];
-      win[5 * WN + d] = s1[2];
+      const double2 a0 = s0[0], a1 = s0[1], a2 = s0[2], b0 = s1[0], b1 = s1[1], b2 = s1[2];
+      win[0 * WN + d] = a0;
+      win[1 * WN + d] = a1;
+      win[2 * WN + d] = make_double2(a2.x, b2.x);
+      win[3 * WN + d] = b0;
+      win[4 * WN + d] = b1;
+    } else {
+      win[0 * WN + d] = s0[0];
+      win[1 * WN + d] = s0[1];
+      win[2 * WN + d] = s0[2];
+      if constexpr (TWO) {
+        const double2* s1 = reinterpret_cast<const double2*>(f1.nodes + src);
+        win[3 * WN + d] = s1[0];
+        win[4 * WN + d] = s1[1];
+        win[5 * WN + d] = s1[2];
+      }
     }
   }
 }
@@ -226,7 +278,7 @@ __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 #define SWRT_TILE_MIN_WAVES 4
 #endif
 
-template <bool TWO, int T, int M, int NT, bool WBLEND = false>
+template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false>
 __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
 #ifdef SWRT_WIN_STRIDE
@@ -239,7 +291,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
 #endif
   constexpr int WNP = W * WS;       // nodes per chunk
   constexpr bool GTWO = TWO && !WBLEND;  // two snapshots in the LDS window
-  constexpr int NCH = GTWO ? 6 : 3; // 16-B chunks per node
+  constexpr int NCH = GTWO ? (V5 ? 5 : 6) : 3;  // 16-B chunks per node
   constexpr int NB = T * T + 1;     // in-tile cell bins + "elsewhere"
   constexpr int MAXB = 2 * NT;      // packets sorted per batch
   __shared__ double2 win[NCH * WNP];
@@ -270,7 +322,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   if constexpr (WBLEND)
     stage_window_blend<T, M, NT, WS>(a.f0, a.f1, ox, oy, a.alpha0 + (double)a.s0 * a.dalpha, win);
   else
-    stage_window_regs<TWO, T, M, NT, WS>(a.f0, a.f1, ox, oy, win);
+    stage_window_regs<TWO, T, M, NT, WS, V5>(a.f0, a.f1, ox, oy, win);
   const int lane_rank = b128_lane_rank(tid & 63);
   const int pbeg = ta.starts[tile], pend = ta.starts[tile + 1];
   if (!ta.sort_cells) {
@@ -285,7 +337,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     __syncthreads();  // (also publishes the window on the first batch)
     if (b0 == pbeg) SWRT_STAMP(1);
     for (int i = tid; i < nb; i += NT) {
-      const int64_t p = b0 + i;
+      const int64_t p = ta.src ? ta.src[b0 + i] : b0 + i;
       const int ic = fast_cell(a.x[p], a.f0.inv_dx, nx);
       const int jc = fast_cell(a.x[a.n + p], a.f0.inv_dx, nx);
       const int dx_ = ring_diff(ic, ox, nx), dy_ = ring_diff(jc, oy, nx);
@@ -333,10 +385,10 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     for (int i = tid; i < nb; i += NT) {
       const int v = kr[i];
 #ifdef SWRT_ABLATE_SORT
-      order[i] = i;
+      order[i] = b0 + i;
       (void)v;
 #else
-      order[hist[v >> 16] + (v & 0xffff)] = i;
+      order[hist[v >> 16] + (v & 0xffff)] = ta.src ? ta.src[b0 + i] : b0 + i;  // input slot
 #endif
     }
     __syncthreads();
@@ -348,7 +400,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     for (int r0 = tid & ~63; r0 < nb; r0 += NT) {
       const int r = r0 + lane_rank;
       if (r >= nb) continue;
-      const int64_t pi = b0 + (ta.sort_cells ? order[r] : r);
+      const int64_t pi = ta.sort_cells ? order[r] : b0 + r;
       const int64_t po = b0 + r;
       double x0 = a.x[pi], y0 = a.x[a.n + pi];
       double k0 = a.k[pi], l0 = a.k[a.n + pi];
@@ -375,10 +427,14 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
           else
             gather6_blend(a.f0.nodes, a.f1.nodes, npad, sc, a.alpha0 + (double)sg * a.dalpha, I);
         } else {
-          if (inwin)
-            gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
-          else
+          if (inwin) {
+            if constexpr (V5)
+              gather5_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+            else
+              gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+          } else {
             gather6_lean<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
+          }
           if constexpr (TWO) {
             const double alpha = a.alpha0 + (double)sg * a.dalpha;
             const double oma = 1 - alpha;
@@ -413,16 +469,16 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         const int ntx2 = ic / T, nty2 = jc / T;
         ta.next_keys[po] = ntx2 * ntx_ + nty2;
         const int ddx = ring_diff(ntx2, tx, ntx_), ddy = ring_diff(nty2, ty, ntx_);
-        int nb_idx = -1;
-        if (ddx >= -1 && ddx <= 1 && ddy >= -1 && ddy <= 1)
-          nb_idx = (ddx + 1) * 3 + (ddy + 1);
-        else
-          atomicAdd(&ta.next_counts[ntx2 * ntx_ + nty2], 1);
-        // wavefront-aggregated LDS counts (same-address LDS atomics serialise)
-#pragma unroll
-        for (int b = 0; b < 9; ++b) {
-          const unsigned long long m = __ballot(nb_idx == b);
-          if (m != 0ull && (tid & 63) == (int)__builtin_ctzll(m)) atomicAdd(&nbr[b], (int)__popcll(m));
+        // Most packets stay in this tile: they cost nothing here, the tile's
+        // own count is (packets in the tile) - (movers), settled at the end.
+        // A mover takes one LDS atomic for a 3x3 neighbour (or one global
+        // atomic beyond) and one on the stayers' correction nbr[4].
+        if (ddx != 0 || ddy != 0) {
+          atomicAdd(&nbr[4], -1);
+          if (ddx >= -1 && ddx <= 1 && ddy >= -1 && ddy <= 1)
+            atomicAdd(&nbr[(ddx + 1) * 3 + (ddy + 1)], 1);
+          else
+            atomicAdd(&ta.next_counts[ntx2 * ntx_ + nty2], 1);
         }
       }
     }
@@ -431,10 +487,11 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   }
   if (ta.next_keys != nullptr) {
     __syncthreads();
-    if (tid < 9 && nbr[tid] != 0) {
+    const int v = tid < 9 ? nbr[tid] + (tid == 4 ? pend - pbeg : 0) : 0;
+    if (v != 0) {
       const int n_ = ta.ntx;
       const int gx = ((tx + tid / 3 - 1) % n_ + n_) % n_, gy = ((ty + tid % 3 - 1) % n_ + n_) % n_;
-      atomicAdd(&ta.next_counts[gx * n_ + gy], nbr[tid]);
+      atomicAdd(&ta.next_counts[gx * n_ + gy], v);
     }
   }
   SWRT_STAMP(4);

@@ -370,16 +370,21 @@ def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, til
 @pytest.mark.parametrize("variant,cell_sort", [(1, 0), (2, 0), (2, 1), (3, 0)])
 @pytest.mark.parametrize("nslots", [1, 2])
 @pytest.mark.parametrize("dt_scale", [1.0, 40.0])
-def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, nslots, dt_scale):
+@pytest.mark.parametrize("div_free", [False, True])
+def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, nslots, dt_scale, div_free):
     """Per-packet (1), LDS-tiled (2) and persistent LDS-tiled (3) kernels give
     the oracle's bits; the large-dt case drives packets out of the LDS window
-    (global fallback)."""
+    (global fallback).  div_free: v_y stored as -u_x, so the tile kernel runs
+    its five-sum window (swrt_field_div_free); the oracle sums all six."""
     c = qg_case
     nx, L = c["nx"], c["L"]
     p0 = _planes(c["flow"])
     p1 = _planes({n: np.asarray(v) * 0.8 for n, v in c["flow"].items()})
+    if div_free:
+        p0[5], p1[5] = -p0[2], -p1[2]
     ctx.set_field_grid(0, p0, nx, L, 2 * nx)
     ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    assert ctx.field_div_free(0) is div_free and ctx.field_div_free(1) is div_free
     dt = c["dt"] * dt_scale
     ctx.set_kernel(variant)
     ctx.set_cell_sort(cell_sort)
@@ -614,3 +619,27 @@ def test_bench_configuration_subset_bitexact(ctx, oracle_lib):
                                            1, w["f"], w["gH"])
     np.testing.assert_array_equal(xg[idx], xo)
     np.testing.assert_array_equal(kg[idx], ko)
+
+
+def test_div_free_detection_and_derived_fields(ctx, qg_case):
+    """Host fields are divergence-free only if v_y == -u_x bit for bit (a
+    one-ulp change at one node turns it off); fields derived on the device
+    from psi / qk store v_y = -u_x, and that v_y agrees with the oracle's
+    separately transformed one within FIELD_RTOL (grid_U.m:9,17)."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    p = _planes(c["flow"])
+    p[5] = -p[2]
+    ctx.set_field_grid(0, p, nx, L)
+    assert ctx.field_div_free(0)
+    p[5, 17] = np.nextafter(p[5, 17], np.inf)
+    ctx.set_field_grid(0, p, nx, L)
+    assert not ctx.field_div_free(0)
+    X, Y = periodic_grid(nx)
+    psi = np.sin(3 * X + Y) + 0.3 * np.cos(X - 5 * Y) + 0.1 * np.sin(7 * Y)
+    ctx.set_field_psi(0, psi, nx, 2 * np.pi)
+    assert ctx.field_div_free(0)
+    g = ctx.get_field_grid(0, nx)
+    np.testing.assert_array_equal(g[5], -g[2])
+    want = orc.spectral_scheme_fields(2 * np.pi, nx, psi)
+    _close_field(g[5], np.asarray(want["vy"]).ravel(order="F"))
