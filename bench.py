@@ -84,7 +84,13 @@ def build_workload(ctx, args, rng):
     i = np.arange(1, N + 1, dtype=np.float64) + args.rank * N
     Ntot = N * args.world
     k = np.stack([wf * np.cos(2 * np.pi * i / Ntot), wf * np.sin(2 * np.pi * i / Ntot)], axis=1)
-    x = L * rng.random((N, 2)) - L / 2
+    if getattr(args, "positions", "uniform") == "stratified":
+        # diagnostic: every 16x16-cell tile gets the same number of packets
+        nt = max(1, nx // 16)
+        t = np.arange(N) % (nt * nt)
+        x = np.stack([(t // nt) * 16 + 16 * rng.random(N), (t % nt) * 16 + 16 * rng.random(N)], axis=1) * (L / nx)
+    else:
+        x = L * rng.random((N, 2)) - L / 2
     return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
                 K_d2=K_d2, ks=ks, shear=shear)
 
@@ -164,6 +170,8 @@ def main():
     ap.add_argument("--substeps", type=int, default=1, help="leapfrog steps per bench step")
     ap.add_argument("--mode", choices=["blend", "steady"], default="blend")
     ap.add_argument("--seed", type=int, default=146)
+    ap.add_argument("--positions", choices=["uniform", "stratified"], default="uniform",
+                    help="initial packet positions (stratified: equal packets per tile, a diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rebin-every", type=int, default=4, help="steps between spatial re-binning (0: off)")
@@ -273,7 +281,7 @@ def main():
                                f"{args.nx}^2x2 field, {N} packets/GPU, leapfrog",
                    "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
-                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode,
+                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "positions": args.positions,
                    "parallelism": f"packets sharded x{world}, field replicated"},
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,

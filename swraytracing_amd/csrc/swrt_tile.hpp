@@ -299,6 +299,9 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   __shared__ int kr[MAXB];          // key << 16 | rank
   __shared__ int order[MAXB];
   __shared__ int nbr[9];            // next-binning counts of the 3x3 neighbour tiles
+#ifdef SWRT_PHASE_TIMING
+  __shared__ int nfall;             // diagnostic: packet-steps that took the global gather
+#endif
 
   const StepArgs& a = ta.s;
   const int tid = threadIdx.x;
@@ -307,6 +310,9 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   const int nx = a.f0.nx, npad = a.f0.npad;
   const int ox = tx * T, oy = ty * T;  // tile origin (cells)
   if (tid < 9) nbr[tid] = 0;
+#ifdef SWRT_PHASE_TIMING
+  if (tid == 0) nfall = 0;
+#endif
   SWRT_STAMP(0);
 #ifdef SWRT_PHASE_TIMING
   if (tid == 0) {
@@ -421,6 +427,9 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         } else
 #endif
         const bool inwin = dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M;
+#ifdef SWRT_PHASE_TIMING
+        if (!inwin) atomicAdd(&nfall, 1);
+#endif
         if constexpr (WBLEND) {
           if (inwin)
             gather6_lds<false, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
@@ -495,6 +504,10 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     }
   }
   SWRT_STAMP(4);
+#ifdef SWRT_PHASE_TIMING
+  __syncthreads();
+  if (tid == 0) swrt_phase_dbg[tile * 8 + 5] = (unsigned long long)nfall;
+#endif
 }
 
 }  // namespace swrt

@@ -92,6 +92,28 @@ def main():
             cu_busy_mean=float(np.mean(busy)), cu_busy_min=float(np.min(busy)),
             packets_per_tile_mean=float(d[:, 6].mean()), packets_per_tile_max=int(d[:, 6].max()),
             mean_concurrent_wg=float(life.sum() / span),
+            # first-round workgroups (start within 2 us) vs the rest
+            compute_us_round1=float(np.median(comp[P[:, 0] < 2.0])) if np.any(P[:, 0] < 2.0) else None,
+            compute_us_later=float(np.median(comp[P[:, 0] >= 2.0])) if np.any(P[:, 0] >= 2.0) else None,
+            stage_us_round1=float(np.median(stage[P[:, 0] < 2.0])) if np.any(P[:, 0] < 2.0) else None,
+            stage_us_later=float(np.median(stage[P[:, 0] >= 2.0])) if np.any(P[:, 0] >= 2.0) else None,
+            n_round1=int(np.sum(P[:, 0] < 2.0)),
+            corr_compute_packets=float(np.corrcoef(comp, d[:, 6])[0, 1]),
+            compute_us_by_packets={f"{lo}-{lo + 64}": float(np.median(comp[(d[:, 6] >= lo) & (d[:, 6] < lo + 64)]))
+                                   for lo in range(832, 1152, 64) if np.any((d[:, 6] >= lo) & (d[:, 6] < lo + 64))},
+            compute_us_deciles=[float(v) for v in np.percentile(comp, np.arange(0, 101, 10))],
+            compute_us_by_xcc={int(x): float(np.median(comp[xcc == x])) for x in np.unique(xcc)},
+            compute_us_round1_by_xcc={int(x): float(np.median(comp[(xcc == x) & (P[:, 0] < 2.0)]))
+                                      for x in np.unique(xcc) if np.any((xcc == x) & (P[:, 0] < 2.0))},
+            slow_share_by_xcc={int(x): float(np.mean(comp[xcc == x] > 24.0)) for x in np.unique(xcc)},
+            slow_share_by_tile_row_band={int(b): float(np.mean(comp[(np.arange(len(comp)) // 32) // 4 == b] > 24.0))
+                                         for b in range(8)},
+            fallback_per_tile_mean=float(d[:, 5].mean()), fallback_per_tile_max=int(d[:, 5].max()),
+            corr_compute_fallback=float(np.corrcoef(comp, d[:, 5])[0, 1]),
+            compute_us_by_fallback={f"{lo}-{hi}": [float(np.median(comp[(d[:, 5] >= lo) & (d[:, 5] < hi)])),
+                                                   int(np.sum((d[:, 5] >= lo) & (d[:, 5] < hi)))]
+                                    for lo, hi in [(0, 1), (1, 5), (5, 20), (20, 50), (50, 100), (100, 100000)]
+                                    if np.any((d[:, 5] >= lo) & (d[:, 5] < hi))},
         ))
     print(json.dumps(res[-1], indent=1))
     print(json.dumps({"span_us_all": [r["span_us"] for r in res]}))
