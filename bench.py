@@ -181,6 +181,8 @@ def main():
                     help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
+    ap.add_argument("--tail-split", type=int, default=-1,
+                    help="tiles per XCD band run as two half-tile workgroups (-1: library default)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
     ap.add_argument("--timing-every", type=int, default=5,
@@ -206,6 +208,8 @@ def main():
     ctx.set_kernel(args.kernel)
     ctx.set_cell_sort(args.cell_sort)
     ctx.set_blend_mode(args.blend_mode)
+    if args.tail_split >= 0:
+        ctx.set_tail_split(args.tail_split)
     rng = np.random.default_rng(args.seed + rank)
     w = build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
@@ -281,10 +285,15 @@ def main():
                                f"{args.nx}^2x2 field, {N} packets/GPU, leapfrog",
                    "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
-                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "positions": args.positions,
+                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "positions": args.positions,
                    "parallelism": f"packets sharded x{world}, field replicated"},
+        # traffic: true HBM bytes per launch (rocprofv3 PMC, profiles/traffic.json), beside the
+        # algorithmic bytes per launch that `achieved` is computed from (taps re-read from LDS)
         "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved_gbs / HBM_PEAK_GBS,
+                     "traffic": traffic["bytes_per_launch"] if traffic else None,
+                     "traffic_detail": traffic, "algorithmic_bytes_per_launch": ps_per_launch * B,
+                     "traffic_gbs": (traffic["bytes_per_launch"] / avg_launch_s / 1e9) if traffic else None,
                      "bytes_per_packet_step": B, "avg_launch_ms": avg_launch_s * 1e3,
                      "timed_launches": launches, "timing_every": args.timing_every},
         "valu_roofline": valu_roofline,

@@ -38,6 +38,9 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #ifndef SWRT_MARGIN
 #define SWRT_MARGIN 3
 #endif
+#ifndef SWRT_TAIL_SPLIT
+#define SWRT_TAIL_SPLIT 16
+#endif
 #ifndef SWRT_TILE_THREADS
 #define SWRT_TILE_THREADS 512
 #endif
@@ -118,6 +121,7 @@ struct swrt_ctx {
   bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
   bool counts_zero = false;  // bins' count block is all zero (cleared by the last scan)
   int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
+  int tail_split = SWRT_TAIL_SPLIT;  // tiles per XCD band run as two half-tile workgroups (swrt_tile.hpp)
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -476,6 +480,10 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   t.starts = c->bins + 2 * kMaxBins;
   t.ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
   const unsigned grid = (unsigned)(t.ntx * t.ntx);
+  // half-tile workgroups at the end of each XCD band (swrt_tile.hpp wg_work)
+  t.split = 0;
+  if (grid % 8 == 0 && c->tail_split > 0) t.split = (int)std::min<unsigned>((unsigned)c->tail_split, grid / 8);
+  const unsigned wgrid = grid + 8u * (unsigned)t.split;
   t.next_keys = nullptr;
   t.next_counts = nullptr;
   t.sort_cells = (c->cell_sort == 1 || !c->cells_sorted) ? 1 : 0;
@@ -499,24 +507,25 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
       ncu = prop.multiProcessorCount;
     const int tpw = (int)((grid + ncu - 1) / ncu);
     const unsigned pgrid = (unsigned)((grid + tpw - 1) / tpw);
+    t.split = 0;  // its own tile walk
     if (a.nslots == 2)
       launch_k(c, tile_persist_kernel<true, kTile, kPersistMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
     else
       launch_k(c, tile_persist_kernel<false, kTile, kPersistMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
   } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
-    launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(grid), dim3(kTileThreads), t);
+    launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(wgrid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
     if (c->slot[0].div_free && c->slot[1].div_free)
-      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, dim3(grid),
+      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
                dim3(kTileThreads), t);
     else
-      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
+      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, dim3(wgrid), dim3(kTileThreads), t);
   } else {
     if (c->slot[0].div_free)
-      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true>, dim3(grid),
+      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
                dim3(kTileThreads), t);
     else
-      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, dim3(grid), dim3(kTileThreads), t);
+      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, dim3(wgrid), dim3(kTileThreads), t);
   }
   HIPCHK(c, hipGetLastError());
   std::swap(c->dx, c->dx2);
@@ -998,6 +1007,13 @@ int swrt_set_cell_sort(swrt_ctx* c, int every_launch) {
   if (!c) return SWRT_ERR_ARG;
   if (every_launch != 0 && every_launch != 1) return fail(c, SWRT_ERR_ARG, "every_launch must be 0 or 1");
   c->cell_sort = every_launch;
+  return SWRT_OK;
+}
+
+int swrt_set_tail_split(swrt_ctx* c, int tiles_per_xcd) {
+  if (!c) return SWRT_ERR_ARG;
+  if (tiles_per_xcd < 0) return fail(c, SWRT_ERR_ARG, "tiles_per_xcd must be >= 0");
+  c->tail_split = tiles_per_xcd;
   return SWRT_OK;
 }
 

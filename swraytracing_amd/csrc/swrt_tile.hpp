@@ -40,7 +40,40 @@ struct TileArgs {
                          // is already in cell order (written so by the previous launch)
   const int* src;        // non-NULL (sort launches only): binned slot p holds input packet
                          // src[p] (indirect re-binning); NULL: slot p holds packet p
+  int split;             // > 0: the last `split` tiles of each XCD's band run as two
+                         // half-tile workgroups (grid = ntiles + 8*split, ntiles % 8 == 0)
 };
+
+// Workgroup -> (tile, packet range).  XCD-aware (xcd_block): XCD x walks one
+// contiguous band of tiles.  With ta.split > 0 each band ends with `split`
+// tiles cut into two workgroups of half the packets each (both stage the
+// whole window): the dispatcher then hands out half-size work items as CUs
+// free up at the end of the launch, which narrows the spread of CU finish
+// times (the launch ends with its slowest CU).
+__device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend) {
+  const int b = (int)blockIdx.x, nb = (int)gridDim.x;
+  int tile, part = -1;
+  if (ta.split > 0) {
+    const int x = b % 8, j = b / 8;
+    const int tpx = nb / 8 - ta.split;  // tiles per XCD band
+    const int whole = tpx - ta.split;
+    if (j < whole) {
+      tile = x * tpx + j;
+    } else {
+      tile = x * tpx + whole + (j - whole) / 2;
+      part = (j - whole) & 1;
+    }
+  } else {
+    tile = (int)xcd_block(b, nb);
+  }
+  pbeg = ta.starts[tile];
+  pend = ta.starts[tile + 1];
+  if (part >= 0) {
+    const int h = (pend - pbeg + 1) / 2;
+    if (part == 0) pend = pbeg + h; else pbeg += h;
+  }
+  return tile;
+}
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
 __device__ __forceinline__ int ring_diff(int a, int b, int n) {
@@ -266,7 +299,7 @@ __device__ __forceinline__ void stage_window_blend(const FieldView& f0, const Fi
 __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 #define SWRT_STAMP(slot)                                                            \
   do {                                                                              \
-    if (tid == 0) swrt_phase_dbg[tile * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+    if (tid == 0) swrt_phase_dbg[blockIdx.x * 8 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #else
 #define SWRT_STAMP(slot) \
@@ -305,7 +338,8 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
 
   const StepArgs& a = ta.s;
   const int tid = threadIdx.x;
-  const int tile = (int)xcd_block(blockIdx.x, gridDim.x);
+  int pbeg, pend;
+  const int tile = wg_work(ta, pbeg, pend);
   const int tx = tile / ta.ntx, ty = tile % ta.ntx;
   const int nx = a.f0.nx, npad = a.f0.npad;
   const int ox = tx * T, oy = ty * T;  // tile origin (cells)
@@ -319,8 +353,8 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    swrt_phase_dbg[tile * 8 + 7] = ((unsigned long long)xcc << 32) | hw;
-    swrt_phase_dbg[tile * 8 + 6] = (unsigned long long)(ta.starts[tile + 1] - ta.starts[tile]);
+    swrt_phase_dbg[blockIdx.x * 8 + 7] = ((unsigned long long)xcc << 32) | hw;
+    swrt_phase_dbg[blockIdx.x * 8 + 6] = (unsigned long long)(pend - pbeg);
   }
 #endif
 
@@ -330,7 +364,6 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   else
     stage_window_regs<TWO, T, M, NT, WS, V5>(a.f0, a.f1, ox, oy, win);
   const int lane_rank = b128_lane_rank(tid & 63);
-  const int pbeg = ta.starts[tile], pend = ta.starts[tile + 1];
   if (!ta.sort_cells) {
     __syncthreads();  // publish the window
     SWRT_STAMP(1);
@@ -506,7 +539,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   SWRT_STAMP(4);
 #ifdef SWRT_PHASE_TIMING
   __syncthreads();
-  if (tid == 0) swrt_phase_dbg[tile * 8 + 5] = (unsigned long long)nfall;
+  if (tid == 0) swrt_phase_dbg[blockIdx.x * 8 + 5] = (unsigned long long)nfall;
 #endif
 }
 

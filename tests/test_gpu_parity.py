@@ -15,6 +15,7 @@ import numpy as np
 import pytest
 
 from oracle import swrt_oracle as orc
+from swraytracing_amd._lib import DEFAULT_TAIL_SPLIT
 from tests.conftest import ROOT, periodic_grid
 
 pytestmark = pytest.mark.gpu
@@ -404,11 +405,13 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, 
     np.testing.assert_array_equal(hkg, hko)
 
 
-@pytest.mark.parametrize("variant", [2, 3])
-def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant):
+@pytest.mark.parametrize("variant,tail_split", [(2, 0), (2, 32), (2, 1000), (3, 0)])
+def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split):
     """512^2 two-snapshot field, 2e5 packets, LDS kernel with re-binning every
     3 steps over 10 steps: random subset bit-identical to the oracle (the
-    persistent kernel walks several tiles per workgroup here)."""
+    persistent kernel walks several tiles per workgroup here; tail_split runs
+    the last tiles of each XCD band — or all of them — as half-tile
+    workgroups)."""
     nx, L = 512, 20.0
     rng = np.random.default_rng(2024)
     kmax = nx // 2 - 1
@@ -425,6 +428,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant):
     x, k = orc.initial_packets(N, L, 4.0, 3.0, 1.0, rng)
     ctx.set_kernel(variant)
     ctx.set_locality(3, 0)
+    ctx.set_tail_split(tail_split)
     try:
         ctx.packets_set(x, k)
         ctx.advance(0.01, 10, 3.0, 1.0, nslots=2, alpha0=0.05, dalpha=0.1, bump=orc.BUMP_QG)
@@ -432,6 +436,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant):
     finally:
         ctx.set_kernel(0)
         ctx.set_locality(4, 0)
+        ctx.set_tail_split(DEFAULT_TAIL_SPLIT)
     idx = np.sort(rng.choice(N, 2000, replace=False))
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.05, 0.1, nx, 2 * nx, L / nx, orc.BUMP_QG, x[idx], k[idx], 0.01,
                                        10, 3.0, 1.0)
@@ -470,8 +475,8 @@ def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
     np.testing.assert_array_equal(kg, ko)
 
 
-@pytest.mark.parametrize("variant,cell_sort", [(2, 0), (2, 1), (3, 0)])
-def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_sort):
+@pytest.mark.parametrize("variant,cell_sort,tail_split", [(2, 0, 0), (2, 1, 0), (3, 0, 0), (2, 0, 1), (2, 1, 2)])
+def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_sort, tail_split):
     """One advance call per step (the bench's pattern): with re-binning every
     4 steps, 3 of 4 launches read packets in the cell order the previous
     launch wrote (no in-tile sort); every packet stays bit-identical."""
@@ -490,6 +495,7 @@ def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_s
     ctx.set_kernel(variant)
     ctx.set_cell_sort(cell_sort)
     ctx.set_locality(4, 0)
+    ctx.set_tail_split(tail_split)
     try:
         ctx.packets_set(x, k)
         for s in range(nst):
@@ -498,6 +504,7 @@ def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_s
     finally:
         ctx.set_cell_sort(0)
         ctx.set_kernel(0)
+        ctx.set_tail_split(DEFAULT_TAIL_SPLIT)
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, a0, da, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, c["dt"] * 3, nst,
                                        c["f"], 1.0)
     np.testing.assert_array_equal(xg, xo)

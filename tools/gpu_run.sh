@@ -19,7 +19,7 @@ step() {  # step <name> <seconds> <cmd...>
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-  step pytest_gpu 900 python -m pytest tests -m gpu -q -x
+  step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 400 python bench.py

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--packets", type=int, default=1_000_000)
     ap.add_argument("--mode", default="blend")
     ap.add_argument("--samples", type=int, default=5)
+    ap.add_argument("--tail-split", type=int, default=-1)
+    ap.add_argument("--dump", default="", help="save every sample's raw stamps (npz) for offline analysis")
     args = ap.parse_args()
     args.world, args.rank, args.seed = 1, 0, 146
     lib = _lib.load()
@@ -36,21 +38,27 @@ def main():
     ctx = sw.Context(0)
     ctx.set_locality(4, 0)
     ctx.set_kernel(2)
+    if args.tail_split >= 0:
+        ctx.set_tail_split(args.tail_split)
     rng = np.random.default_rng(146)
     w = bench.build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
     for _ in range(8):
         bench.step(ctx, w, 1)
     ntiles = (args.nx // 16) ** 2
-    buf = np.zeros(ntiles * 8, dtype=np.uint64)
+    nrows = 2 * ntiles  # workgroups (half-tile workgroups with --tail-split)
+    buf = np.zeros(nrows * 8, dtype=np.uint64)
     ptr = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))
     res = []
+    raw = []
     for s in range(args.samples):
-        assert f(None, ntiles, 1) == 0
+        assert f(None, nrows, 1) == 0
         bench.step(ctx, w, 1)
         ctx.synchronize()
-        assert f(ptr, ntiles, 0) == 0
-        d = buf.reshape(ntiles, 8).astype(np.int64)
+        assert f(ptr, nrows, 0) == 0
+        d = buf.reshape(nrows, 8).astype(np.int64)
+        d = d[d[:, 0] != 0]
+        raw.append(d.copy())
         t0 = d[:, 0].min()
         P = (d[:, :5] - t0) * 10.0 / 1e3  # us
         stage = P[:, 1] - P[:, 0]
@@ -116,6 +124,8 @@ def main():
                                     if np.any((d[:, 5] >= lo) & (d[:, 5] < hi))},
         ))
     print(json.dumps(res[-1], indent=1))
+    if args.dump:
+        np.savez_compressed(args.dump, stamps=np.stack(raw))
     print(json.dumps({"span_us_all": [r["span_us"] for r in res]}))
     ctx.close()
 
