@@ -38,6 +38,9 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #ifndef SWRT_MARGIN
 #define SWRT_MARGIN 3
 #endif
+#ifndef SWRT_SORT_LEAD
+#define SWRT_SORT_LEAD 1
+#endif
 #ifndef SWRT_TAIL_SPLIT
 #define SWRT_TAIL_SPLIT 16
 #endif
@@ -121,6 +124,7 @@ struct swrt_ctx {
   bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
   bool counts_zero = false;  // bins' count block is all zero (cleared by the last scan)
   int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
+  bool sort_lead = SWRT_SORT_LEAD;  // in-tile sort keys lead by the group-velocity drift
   int tail_split = SWRT_TAIL_SPLIT;  // tiles per XCD band run as two half-tile workgroups (swrt_tile.hpp)
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
@@ -488,6 +492,9 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   t.next_counts = nullptr;
   t.sort_cells = (c->cell_sort == 1 || !c->cells_sorted) ? 1 : 0;
   t.src = nullptr;
+  // sort keys lead by half the steps until the next sort (swrt_tile.hpp)
+  t.sort_lead = 0.0;
+  if (c->sort_lead) t.sort_lead = 0.5 * a.dt * (c->cell_sort == 1 ? 1.0 : (double)std::max<int64_t>(1, c->rebin_every));
   if (c->src_pending) {  // first launch after an indirect re-binning (always a sort launch)
     t.src = c->src_idx;
     t.sort_cells = 1;

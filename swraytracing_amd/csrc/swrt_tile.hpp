@@ -40,6 +40,7 @@ struct TileArgs {
                          // is already in cell order (written so by the previous launch)
   const int* src;        // non-NULL (sort launches only): binned slot p holds input packet
                          // src[p] (indirect re-binning); NULL: slot p holds packet p
+  double sort_lead;      // in-tile sort key: position + sort_lead * (group velocity)
   int split;             // > 0: the last `split` tiles of each XCD's band run as two
                          // half-tile workgroups (grid = ntiles + 8*split, ntiles % 8 == 0)
 };
@@ -377,9 +378,25 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     if (b0 == pbeg) SWRT_STAMP(1);
     for (int i = tid; i < nb; i += NT) {
       const int64_t p = ta.src ? ta.src[b0 + i] : b0 + i;
-      const int ic = fast_cell(a.x[p], a.f0.inv_dx, nx);
-      const int jc = fast_cell(a.x[a.n + p], a.f0.inv_dx, nx);
-      const int dx_ = ring_diff(ic, ox, nx), dy_ = ring_diff(jc, oy, nx);
+      // sort key position: the packet drifted by its group velocity to the
+      // middle of the steps this order serves (x0 + sort_lead*gH*k/omega).
+      // Packets of one cell separate at up to 2|cg| (k points every way), so
+      // keys of the launch-start cell go stale within a cycle; the lead
+      // keeps the lane groups compact over the whole cycle (LDS bank-conflict
+      // model, tools/conflict_model.py: 1.40 -> 1.22 LDS cycles per access).
+      // Order only: results do not depend on it.
+      double xs = a.x[p], ys = a.x[a.n + p];
+      if (ta.sort_lead != 0.0) {
+        const double kx = a.k[p], ky = a.k[a.n + p];
+        const double s = ta.sort_lead * a.gH / sqrt(a.f2 + a.gH * (kx * kx + ky * ky));
+        xs += s * kx;
+        ys += s * ky;
+      }
+      const int ic = fast_cell(xs, a.f0.inv_dx, nx);
+      const int jc = fast_cell(ys, a.f0.inv_dx, nx);
+      // cells predicted beyond the tile sort at its edge
+      const int dx_ = min(max(ring_diff(ic, ox, nx), 0), T - 1);
+      const int dy_ = min(max(ring_diff(jc, oy, nx), 0), T - 1);
 #ifndef SWRT_SORT_ROWMAJOR
       // Z-order of the cell within the tile (T = 16): a run of 16 consecutive
       // packets (one ds_read_b128 lane group) stays inside a 2x2 or 4x4 block

@@ -9,3 +9,6 @@ bash tools/sweep.sh "$@" || exit $?
 if [ -f build/variants/phase.so ]; then
   SWRT_LIB_PATH=build/variants/phase.so timeout -k 10 200 python tools/phase_timing.py --samples 12 --dump gpurun_out/phase_raw_exp.npz > gpurun_out/phase_exp.log 2>&1; echo phase rc=$?
 fi
+if [ -n "$PMC_GROUP" ]; then
+  bash tools/pmc_counters.sh "--steps 10 --warmup 2 --no-cpu-baseline" "$PMC_GROUP" > gpurun_out/pmc_exp.log 2>&1; echo pmc rc=$?
+fi
