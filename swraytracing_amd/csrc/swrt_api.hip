@@ -158,6 +158,10 @@ struct swrt_ctx {
   QGState qg;
   // ode23 stage buffers (cap-sized, device packet order)
   double* oF[4] = {nullptr, nullptr, nullptr, nullptr};
+  int* o_order = nullptr;      // ode23 tile kernel: in-tile cell order of the binned slots
+  int64_t o_order_cap = 0;
+  bool o_order_valid = false;  // computed for the current binning
+  int o_order_split = 0;       // ... and launch shape
   double* o_ynx = nullptr;
   double* o_ynk = nullptr;
   int64_t o_cap = 0;
@@ -468,6 +472,7 @@ int rebin(swrt_ctx* c, bool indirect) {
   }
   HIPCHK(c, hipGetLastError());
   c->src_pending = indirect;
+  c->o_order_valid = false;
   c->steps_since_bin = 0;
   c->bin_valid = true;
   c->cells_sorted = false;
@@ -641,6 +646,7 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->qg.hmax) (void)hipHostFree(c->qg.hmax);
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
+  if (c->o_order) (void)hipFree(c->o_order);
   for (void* p : {(void*)c->oF[0], (void*)c->oF[1], (void*)c->oF[2], (void*)c->oF[3], (void*)c->o_ynx,
                   (void*)c->o_ynk, (void*)c->o_dmax})
     if (p) (void)hipFree(p);
@@ -1700,6 +1706,8 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   a.thr = thr;
   a.bump = bump;
   a.dmax = c->o_dmax;
+  a.order = nullptr;
+  a.split = 0;
   return SWRT_OK;
 }
 
@@ -1716,19 +1724,48 @@ int read_max(swrt_ctx* c, double* out) {
 namespace {
 // one ode23 stage over all packets: the LDS-tiled kernel when the packets are
 // binned by the tile kernel's 16x16-cell tiles, else one lane per packet
+template <int STAGE, bool TWO, bool V5>
+void ode23_tile_launch(swrt_ctx* c, const Ode23Args& a, unsigned grid, const int* starts, int ntx) {
+  hipLaunchKernelGGL((tile_ode23_kernel<STAGE, TWO, kTile, kMargin, kTileThreads, V5>), dim3(grid),
+                     dim3(kTileThreads), 0, c->stream, a, starts, ntx);
+}
+
 template <int STAGE>
-int ode23_launch(swrt_ctx* c, const Ode23Args& a) {
+int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
   const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
-  if (use_tile_kernel(c) && c->bin_valid && c->nbins == ntx * ntx) {
+  if (use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx * ntx) {
     const int* starts = c->bins + 2 * kMaxBins;
-    if (a.nslots == 2)
-      hipLaunchKernelGGL((tile_ode23_kernel<STAGE, true, kTile, kMargin, kTileThreads>), dim3(ntx * ntx),
-                         dim3(kTileThreads), 0, c->stream, a, starts, ntx);
-    else
-      hipLaunchKernelGGL((tile_ode23_kernel<STAGE, false, kTile, kMargin, kTileThreads>), dim3(ntx * ntx),
-                         dim3(kTileThreads), 0, c->stream, a, starts, ntx);
+    const unsigned ntiles = (unsigned)(ntx * ntx);
+    Ode23Args a = a0;
+    a.split = (ntiles % 8 == 0 && c->tail_split > 0) ? (int)std::min<unsigned>((unsigned)c->tail_split, ntiles / 8)
+                                                      : 0;
+    const unsigned grid = ntiles + 8u * (unsigned)a.split;
+    // in-tile cell order of this binning, once (swrt_ode23.hpp)
+    if (!c->o_order_valid || c->o_order_split != a.split) {
+      if (c->o_order_cap < c->cap) {
+        if (c->o_order) (void)hipFree(c->o_order);
+        c->o_order = nullptr;
+        HIPCHK(c, hipMalloc(&c->o_order, sizeof(int) * c->cap));
+        c->o_order_cap = c->cap;
+      }
+      const FieldView v = view_of(c->slot[0]);
+      hipLaunchKernelGGL((tile_cell_order_kernel<kTile, kTileThreads>), dim3(grid), dim3(kTileThreads), 0,
+                         c->stream, c->dx, c->n, starts, a.split, ntx, v.inv_dx, v.nx, c->o_order);
+      HIPCHK(c, hipGetLastError());
+      c->o_order_valid = true;
+      c->o_order_split = a.split;
+    }
+    a.order = c->o_order;
+    const bool v5 = c->slot[0].div_free && (a.nslots == 1 || c->slot[1].div_free);
+    if (a.nslots == 2) {
+      if (v5) ode23_tile_launch<STAGE, true, true>(c, a, grid, starts, ntx);
+      else ode23_tile_launch<STAGE, true, false>(c, a, grid, starts, ntx);
+    } else {
+      if (v5) ode23_tile_launch<STAGE, false, true>(c, a, grid, starts, ntx);
+      else ode23_tile_launch<STAGE, false, false>(c, a, grid, starts, ntx);
+    }
   } else {
-    hipLaunchKernelGGL(ode23_stage_kernel<STAGE>, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, a);
+    hipLaunchKernelGGL(ode23_stage_kernel<STAGE>, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, a0);
   }
   HIPCHK(c, hipGetLastError());
   return SWRT_OK;

@@ -42,6 +42,8 @@ struct Ode23Args {
   double thr;        // AbsTol / RelTol
   double bump;
   unsigned long long* dmax;
+  const int* order;  // tile kernel: binned slots in in-tile cell order (NULL: slot order)
+  int split;         // tile kernel: half-tile workgroups at the end of each XCD band
 };
 
 __device__ __forceinline__ void ode_rhs(const Ode23Args& a, const double ys[4], double fo[4]) {
@@ -110,27 +112,103 @@ __global__ void __launch_bounds__(256) ode23_stage_kernel(Ode23Args a) {
   if constexpr (STAGE == 1 || STAGE == 4) block_max_to(m, a.dmax);
 }
 
+// In-tile cell order of the binned packets (one workgroup per tile, once per
+// binning): a counting sort by the Z-order of the packet's cell inside its
+// tile, in batches of up to 2*NT packets, written as slot indices.  The ode23
+// stages then take their packets in that order, so the lanes of one
+// ds_read_b128 group read neighbouring window nodes (as the leapfrog tile
+// kernel's own in-tile sort does).  Order only: results do not depend on it.
+template <int T, int NT>
+__global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, int64_t n, const int* starts,
+                                                             int split, int ntx, double inv_dx, int nx,
+                                                             int* order) {
+  constexpr int NB = T * T;
+  constexpr int MAXB = 2 * NT;
+  __shared__ int hist[NB];
+  __shared__ int kr[MAXB];
+  int pbeg, pend;
+  const int tile = wg_work_range(starts, split, pbeg, pend);
+  const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
+  const int tid = threadIdx.x;
+  for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
+    const int nb = min(MAXB, pend - b0);
+    for (int h = tid; h < NB; h += NT) hist[h] = 0;
+    __syncthreads();
+    for (int i = tid; i < nb; i += NT) {
+      const int64_t p = b0 + i;
+      const int dx_ = min(max(ring_diff(fast_cell(x[p], inv_dx, nx), ox, nx), 0), T - 1);
+      const int dy_ = min(max(ring_diff(fast_cell(x[n + p], inv_dx, nx), oy, nx), 0), T - 1);
+      int key = 0;
+#pragma unroll
+      for (int bit = 0; (1 << bit) < T; ++bit)
+        key |= ((dy_ >> bit) & 1) << (2 * bit) | ((dx_ >> bit) & 1) << (2 * bit + 1);
+      kr[i] = (key << 16) | atomicAdd(&hist[key], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the NB bins by one wavefront
+      constexpr int PER = (NB + 63) / 64;
+      int loc[PER];
+      int sum = 0;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int h = tid * PER + q;
+        loc[q] = h < NB ? hist[h] : 0;
+        sum += loc[q];
+      }
+      int incl = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (tid >= off) incl += v;
+      }
+      int run = incl - sum;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int h = tid * PER + q;
+        if (h < NB) hist[h] = run;
+        run += loc[q];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nb; i += NT) {
+      const int v = kr[i];
+      order[b0 + hist[v >> 16] + (v & 0xffff)] = b0 + i;
+    }
+    __syncthreads();
+  }
+}
+
 // The same four stages over spatially binned packets, one workgroup per
-// T x T-cell tile with the field window of both snapshots in LDS
-// (stage_window_regs; the packets move well under the M-cell margin within
-// one PDE interval, a packet outside it takes the global gather).  Same
-// arithmetic as ode23_stage_kernel, so the same bits.
-template <int STAGE, bool TWO, int T, int M, int NT>
+// T x T-cell tile (half-tile workgroups at the end of each XCD band) with the
+// field window of both snapshots in LDS — the leapfrog tile kernel's window:
+// rows padded to a 12 (mod 16) stride, the five-sum layout for
+// divergence-free slots (V5) — and the packets taken in in-tile cell order
+// (a.order) mapped onto the ds_read_b128 lane groups.  The packets move well
+// under the M-cell margin within one PDE interval; a packet outside it takes
+// the global gather.  Same arithmetic as ode23_stage_kernel, so the same bits.
+template <int STAGE, bool TWO, int T, int M, int NT, bool V5>
 __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const int* starts, int ntx) {
   constexpr int W = T + 5 + 2 * M;
-  constexpr int WN = W * W;
-  constexpr int NCH = TWO ? 6 : 3;
-  __shared__ double2 win[NCH * WN];
+  constexpr int WS = W + ((12 - W % 16) + 16) % 16;  // LDS row stride (nodes)
+  constexpr int WNP = W * WS;
+  constexpr int NCH = TWO ? (V5 ? 5 : 6) : 3;
+  __shared__ double2 win[NCH * WNP];
   __shared__ double red[NT / 64];
-  const int tile = (int)xcd_block(blockIdx.x, gridDim.x);
+  int pbeg, pend;
+  const int tile = wg_work_range(starts, a.split, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int nx = a.f0.nx;
-  stage_window_regs<TWO, T, M, NT>(a.f0, a.f1, ox, oy, win);
+  stage_window_regs<TWO, T, M, NT, WS, V5>(a.f0, a.f1, ox, oy, win);
   __syncthreads();
   const int64_t n = a.n;
   const double alpha = a.tmax != 0.0 ? a.ts / a.tmax : 0.0;
+  const int lane_rank = b128_lane_rank(threadIdx.x & 63);
+  const int cnt = pend - pbeg;
   double m = 0.0;
-  for (int64_t p = starts[tile] + threadIdx.x; p < starts[tile + 1]; p += NT) {
+  for (int r0 = (int)(threadIdx.x & ~63u); r0 < cnt; r0 += NT) {
+    const int r = r0 + lane_rank;
+    if (r >= cnt) continue;
+    const int64_t p = a.order ? a.order[pbeg + r] : pbeg + r;
     const double y[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
     double ys[4];
     if constexpr (STAGE == 1) {
@@ -152,10 +230,14 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
     stencil_at(a.f0, ys[0], ys[1], a.bump, sc);
     const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
     double I[kRec], J[kRec];
-    if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M)
-      gather6_lds<TWO, W, WN>(win, (dx_ + M) * W + (dy_ + M), sc, I, J);
-    else
+    if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M) {
+      if constexpr (V5)
+        gather5_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+      else
+        gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+    } else {
       gather6_lean<TWO>(a.f0.nodes, a.f1.nodes, a.f0.npad, sc, I, J);
+    }
     if constexpr (TWO) {
       const double oma = 1 - alpha;
 #pragma unroll

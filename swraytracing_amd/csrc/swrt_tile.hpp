@@ -51,13 +51,13 @@ struct TileArgs {
 // whole window): the dispatcher then hands out half-size work items as CUs
 // free up at the end of the launch, which narrows the spread of CU finish
 // times (the launch ends with its slowest CU).
-__device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend) {
+__device__ __forceinline__ int wg_work_range(const int* starts, int split, int& pbeg, int& pend) {
   const int b = (int)blockIdx.x, nb = (int)gridDim.x;
   int tile, part = -1;
-  if (ta.split > 0) {
+  if (split > 0) {
     const int x = b % 8, j = b / 8;
-    const int tpx = nb / 8 - ta.split;  // tiles per XCD band
-    const int whole = tpx - ta.split;
+    const int tpx = nb / 8 - split;  // tiles per XCD band
+    const int whole = tpx - split;
     if (j < whole) {
       tile = x * tpx + j;
     } else {
@@ -67,13 +67,17 @@ __device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend)
   } else {
     tile = (int)xcd_block(b, nb);
   }
-  pbeg = ta.starts[tile];
-  pend = ta.starts[tile + 1];
+  pbeg = starts[tile];
+  pend = starts[tile + 1];
   if (part >= 0) {
     const int h = (pend - pbeg + 1) / 2;
     if (part == 0) pend = pbeg + h; else pbeg += h;
   }
   return tile;
+}
+
+__device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend) {
+  return wg_work_range(ta.starts, ta.split, pbeg, pend);
 }
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)

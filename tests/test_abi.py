@@ -57,3 +57,22 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(ImportError):
         L.load()
+
+
+CLI = os.path.join(ROOT, "build", "bin", "swrt_cli")
+
+
+def test_cli_driver_links_the_abi_only():
+    """tools/swrt_cli.cpp (built by __graft_entry__.build()) drives the hot
+    loop through include/swrt.h alone: it links libswrt.so and nothing of
+    torch or Python."""
+    if not os.path.exists(CLI):
+        pytest.skip("swrt_cli not built (run __graft_entry__.build())")
+    out = subprocess.run(["readelf", "-d", CLI], capture_output=True, text=True, check=True).stdout
+    needed = re.findall(r"\(NEEDED\).*\[(.+)\]", out)
+    assert "libswrt.so" in needed
+    assert not any("torch" in n or "python" in n for n in needed)
+    r = subprocess.run([CLI, "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "usage" in r.stdout
+    r = subprocess.run([CLI, "--nx", "48"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2  # argument errors are reported, not run

@@ -650,3 +650,18 @@ def test_div_free_detection_and_derived_fields(ctx, qg_case):
     np.testing.assert_array_equal(g[5], -g[2])
     want = orc.spectral_scheme_fields(2 * np.pi, nx, psi)
     _close_field(g[5], np.asarray(want["vy"]).ravel(order="F"))
+
+
+@pytest.mark.timeout(120)
+def test_cli_driver_runs_the_bench_workload():
+    """The C-ABI command-line driver (no Python in the loop) runs the bench
+    workload at reduced size and reports finite packets and a throughput."""
+    import json
+    import subprocess
+    cli = os.path.join(ROOT, "build", "bin", "swrt_cli")
+    assert os.path.exists(cli), "swrt_cli not built"
+    r = subprocess.run([cli, "--nx", "256", "--packets", "100000", "--steps", "8", "--warmup", "2"],
+                       capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["finite"] is True and d["value"] > 0 and d["steps"] == 8
