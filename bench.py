@@ -6,9 +6,13 @@ shear_strength 0.5, packets advected in layer 1 so interpolate's y-period is
 2*nx), two spectral snapshots (prev_qk, qk) prepared on the GPU by grid_U
 (swrt_set_field_qk), 1e6 packets on the omega0 = 4f ring (f = 3, Cg = 1,
 Ug = 0.2) per GPU.  One bench step = one PDE interval dt = 0.25*dx/U0
-(CFL_fraction of qg2layersw_raytrace.m:31) advanced by `--substeps` fused
-leapfrog steps with the interpolate_U time blend.  Synthetic data: random
-phase ring spectrum 10 < |k| <= 30 (initial_q's ring), normalised so
+(CFL_fraction of qg2layersw_raytrace.m:31) advanced by `--substeps` (5)
+fused leapfrog steps with the interpolate_U time blend, i.e. packet steps
+of 0.05*dx/U0 — the step SURVEY §8d's metric is defined on (qgsw_raytrace.m's
+CFL 0.05, :29,70).  A packet-step is the same work at any dt (drift, 36-tap
+U + grad U of both snapshots, kick, drift); dt only sets how far packets
+move between re-binnings (`--rebin-every` 20 steps here).  Synthetic data:
+random phase ring spectrum 10 < |k| <= 30 (initial_q's ring), normalised so
 max|U| = Ug; a second snapshot with slightly rotated phases.
 
 Multi-GPU: one process per GPU (torch.distributed.run), packets sharded by
@@ -167,14 +171,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nx", type=int, default=512)
     ap.add_argument("--packets", type=int, default=1_000_000, help="packets per GPU (weak scaling)")
-    ap.add_argument("--substeps", type=int, default=1, help="leapfrog steps per bench step")
+    ap.add_argument("--substeps", type=int, default=5,
+                    help="leapfrog steps per bench step (PDE interval 0.25*dx/U0; 5 -> 0.05*dx/U0 per step)")
     ap.add_argument("--mode", choices=["blend", "steady"], default="blend")
     ap.add_argument("--seed", type=int, default=146)
     ap.add_argument("--positions", choices=["uniform", "stratified"], default="uniform",
                     help="initial packet positions (stratified: equal packets per tile, a diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--rebin-every", type=int, default=4, help="steps between spatial re-binning (0: off)")
+    ap.add_argument("--rebin-every", type=int, default=20, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile, 3 persistent tile")
     ap.add_argument("--blend-mode", type=int, default=0,
@@ -251,7 +256,15 @@ def main():
     B = BYTES_BLEND if w["nslots"] == 2 else BYTES_STEADY
     # sampled HIP-event time of the packet kernel; without samples fall back to wall time per step
     avg_launch_s = (kms / 1e3) / launches if launches > 0 else elapsed / args.steps
-    ps_per_launch = N * args.substeps  # one launch advances all local packets by `substeps` steps
+    # packet-steps per launch: a call's substeps run as launches of at most
+    # `rebin_every` steps, cut at the re-binning points (swrt_advance)
+    if args.rebin_every <= 0 or args.rebin_every % args.substeps == 0:
+        steps_per_launch = min(args.substeps, 64)
+    elif args.substeps % args.rebin_every == 0:
+        steps_per_launch = args.rebin_every
+    else:
+        steps_per_launch = min(args.substeps, args.rebin_every)  # approximate (uneven chunks)
+    ps_per_launch = N * steps_per_launch
     achieved_gbs = ps_per_launch * B / avg_launch_s / 1e9
     # fp64 VALU work per packet-step of the exact-order stencil
     key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}"
@@ -267,6 +280,9 @@ def main():
                          "unit": "lane-ops/s", "frac": ach / FP64_LANE_OPS_PEAK,
                          "valu_instructions_per_launch": valu["SQ_INSTS_VALU"],
                          "source": "profiles/valu.json (rocprofv3 PMC)"}
+    workload = ("qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
+                f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, {args.nx}^2x2 field, {N} packets/GPU, "
+                f"leapfrog dt {0.25 / args.substeps:g}*dx/U0 ({args.substeps} per PDE interval)")
     out = {
         "metric": "packet-steps/sec @ 512² field, 1e6 packets; 1/2/4/8-GPU scaling",
         "value": value,
@@ -280,10 +296,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
-        "config": {"workload": "qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
-                               f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, "
-                               f"{args.nx}^2x2 field, {N} packets/GPU, leapfrog",
+        "config": {"workload": workload,
                    "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
+                   "pde_dt": "0.25*dx/U0", "leapfrog_dt": f"{0.25 / args.substeps:g}*dx/U0",
+                   "steps_per_launch": steps_per_launch,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "positions": args.positions,
                    "parallelism": f"packets sharded x{world}, field replicated"},

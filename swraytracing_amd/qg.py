@@ -243,7 +243,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
 
 
 def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
-                        out_dir="data", nsub=4, max_steps=None, seed=5, verbose=False,
+                        out_dir="data", nsub=5, max_steps=None, seed=5, verbose=False,
                         ctx: Context | None = None):
     """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
     (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and

@@ -601,29 +601,34 @@ def test_blend_in_window_mode_tolerance(ctx, oracle_lib, qg_case, dt_scale):
     np.testing.assert_allclose(kg, ko, rtol=rtol, atol=atol)
 
 
-def test_bench_configuration_subset_bitexact(ctx, oracle_lib):
+@pytest.mark.parametrize("substeps,rebin_every,calls", [(5, 20, 10), (1, 4, 12)])
+def test_bench_configuration_subset_bitexact(ctx, oracle_lib, substeps, rebin_every, calls):
     """The headline bench configuration itself (bench.py: 2-layer 512^2 field,
-    L = 20, shear 0.5, two snapshots, 1e6 packets, one advance call per step
-    with re-binning every 4, the default kernel): 12 steps, a random subset of
-    3000 packets bit-identical to the C oracle on the same device-prepared
-    fields."""
+    L = 20, shear 0.5, two snapshots, 1e6 packets, one advance call per PDE
+    interval of `substeps` leapfrog steps — the default 5 steps of
+    0.05*dx/U0 with re-binning every 20, and the single-step 0.25*dx/U0 form
+    with re-binning every 4 — the default kernel): a random subset of 3000
+    packets bit-identical to the C oracle on the same device-prepared fields."""
     import argparse
     import bench
     args = argparse.Namespace(nx=512, packets=1_000_000, world=1, rank=0, seed=146, mode="blend")
-    ctx.set_locality(4, 0)
+    ctx.set_locality(rebin_every, 0)
     ctx.set_kernel(0)
-    w = bench.build_workload(ctx, args, np.random.default_rng(146))
-    ctx.packets_set(w["x"], w["k"])
-    for _ in range(12):
-        bench.step(ctx, w, 1)
-    xg, kg = ctx.packets_get()
-    p0 = ctx.get_field_grid(0, 512)
-    p1 = ctx.get_field_grid(1, 512)
+    try:
+        w = bench.build_workload(ctx, args, np.random.default_rng(146))
+        ctx.packets_set(w["x"], w["k"])
+        for _ in range(calls):
+            bench.step(ctx, w, substeps)
+        xg, kg = ctx.packets_get()
+        p0 = ctx.get_field_grid(0, 512)
+        p1 = ctx.get_field_grid(1, 512)
+    finally:
+        ctx.set_locality(4, 0)
     idx = np.sort(np.random.default_rng(7).choice(args.packets, 3000, replace=False))
     xo, ko = w["x"][idx], w["k"][idx]
-    for _ in range(12):  # bench.step: one leapfrog step, alpha = 0.5
-        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.5, 1.0, 512, 1024, w["L"] / 512, orc.BUMP_QG, xo, ko, w["dt"],
-                                           1, w["f"], w["gH"])
+    for _ in range(calls):  # bench.step: substeps leapfrog steps of dt/substeps, alpha = (s + 1/2)/substeps
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.5 / substeps, 1.0 / substeps, 512, 1024, w["L"] / 512,
+                                           orc.BUMP_QG, xo, ko, w["dt"] / substeps, substeps, w["f"], w["gH"])
     np.testing.assert_array_equal(xg[idx], xo)
     np.testing.assert_array_equal(kg[idx], ko)
 

@@ -36,7 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nx", type=int, default=512)
     ap.add_argument("--packets", type=int, default=1_000_000)
-    ap.add_argument("--nsub", type=int, default=4)
+    ap.add_argument("--nsub", type=int, default=5, help="leapfrog substeps per PDE interval (5: 0.05*dx/U0 each)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ode23", action="store_true", help="also time the drivers' ode23 over one PDE interval")
     args = ap.parse_args()

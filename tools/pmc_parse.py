@@ -39,7 +39,7 @@ def main():
     mode = "steady" if "--mode" in args and args[args.index("--mode") + 1] == "steady" else "blend"
     def arg(name, default):
         return int(args[args.index(name) + 1]) if name in args else default
-    key = f"{mode}_nx{arg('--nx', 512)}_N{arg('--packets', 1000000)}_sub{arg('--substeps', 1)}"
+    key = f"{mode}_nx{arg('--nx', 512)}_N{arg('--packets', 1000000)}_sub{arg('--substeps', 5)}"  # bench.py defaults
     rec = {"bytes_per_launch": corr, "bytes_per_launch_raw": raw, "fetch_kib": f_kib, "write_kib": w_kib,
            "dispatches": len(fetch), "note": "median dispatch; FETCH_SIZE doubled (gfx950 half-count)"}
     path = os.path.join(d, "traffic.json")  # copied into profiles/traffic.json once reviewed

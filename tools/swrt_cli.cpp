@@ -5,12 +5,13 @@
 // Workload = bench.py's (BASELINE.json configs[3]): 2-layer QG background,
 // layer 1 (L = 20, k scaled by 2*pi/L, shear 0.5, y-period 2*nx), two
 // snapshots blended (interpolate_U), packets on the omega0 = 4f ring
-// (f = 3, Cg = 1), dt = 0.25*dx/U0, one leapfrog step per call, re-binning
-// every 4 steps.  Synthetic random-phase ring spectrum 10 < |k| <= 30
+// (f = 3, Cg = 1), one call per PDE interval dt = 0.25*dx/U0 advanced by
+// --substeps (5) leapfrog steps of 0.05*dx/U0, re-binning every --rebin (20)
+// steps.  Synthetic random-phase ring spectrum 10 < |k| <= 30
 // normalised to max|U| = 0.2 (std::mt19937_64, not bench.py's numpy stream).
 //
 //   swrt_cli [--nx 512] [--packets 1000000] [--steps 50] [--warmup 5]
-//            [--device 0] [--substeps 1]
+//            [--device 0] [--substeps 5] [--rebin 20]
 // Prints one JSON line: packet-steps/s (wall clock over the timed steps,
 // synchronised) and the sampled kernel time per launch.
 #include <chrono>
@@ -71,7 +72,7 @@ double max_speed(swrt_ctx* c, int slot, int nx, double shear) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  int nx = 512, device = 0, steps = 50, warmup = 5, substeps = 1;
+  int nx = 512, device = 0, steps = 50, warmup = 5, substeps = 5, rebin = 20;
   long long npk = 1000000;
   for (int i = 1; i < argc; ++i) {
     const std::string a = argv[i];
@@ -85,16 +86,18 @@ int main(int argc, char** argv) {
     else if (a == "--warmup") warmup = std::atoi(next());
     else if (a == "--device") device = std::atoi(next());
     else if (a == "--substeps") substeps = std::atoi(next());
+    else if (a == "--rebin") rebin = std::atoi(next());
     else if (a == "--help" || a == "-h") {
-      std::printf("usage: swrt_cli [--nx N] [--packets P] [--steps K] [--warmup W] [--device D] [--substeps S]\n");
+      std::printf("usage: swrt_cli [--nx N] [--packets P] [--steps K] [--warmup W] [--device D] [--substeps S] "
+                  "[--rebin R]\n");
       return 0;
     } else {
       std::fprintf(stderr, "swrt_cli: unknown option %s\n", a.c_str());
       return 2;
     }
   }
-  if (nx < 32 || (nx & (nx - 1)) != 0 || npk <= 0 || steps <= 0 || substeps <= 0) {
-    std::fprintf(stderr, "swrt_cli: nx must be a power of two >= 32; packets, steps, substeps > 0\n");
+  if (nx < 32 || (nx & (nx - 1)) != 0 || npk <= 0 || steps <= 0 || substeps <= 0 || rebin < 0) {
+    std::fprintf(stderr, "swrt_cli: nx must be a power of two >= 32; packets, steps, substeps > 0; rebin >= 0\n");
     return 2;
   }
   const double L = 20.0, f = 3.0, Cg = 1.0, Ug = 0.2, shear = 0.5, K_d2 = f / Cg;
@@ -137,7 +140,7 @@ int main(int argc, char** argv) {
     k[npk + i] = wf * std::sin(th);
   }
   check(c, swrt_packets_set(c, x.data(), k.data(), npk), "swrt_packets_set");
-  check(c, swrt_set_locality(c, 4, 0), "swrt_set_locality");
+  check(c, swrt_set_locality(c, rebin, 0), "swrt_set_locality");
 
   const double h = dt / substeps;
   auto step = [&]() {
