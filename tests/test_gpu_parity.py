@@ -670,3 +670,49 @@ def test_cli_driver_runs_the_bench_workload():
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["finite"] is True and d["value"] > 0 and d["steps"] == 8
+
+
+@pytest.mark.timeout(120)
+def test_maximum_size_ensemble_subset():
+    """Largest configuration of BASELINE.json (configs[4]'s sizes): a 1024^2
+    two-snapshot field and 1e7 packets through the default LDS tile kernel
+    (4096 tiles, half-tile tail, bench-style calls of 5 substeps, re-binning
+    every 20 over a 40-step run): every packet finite, a random subset of
+    2000 bit-identical to the C oracle on the device-prepared fields."""
+    import swraytracing_amd as sw
+    from oracle import cbind
+    nx, L, N = 1024, 20.0, 10_000_000
+    rng = np.random.default_rng(99)
+    kmax = nx // 2 - 1
+    qk = np.zeros((2 * kmax + 1, kmax + 1), complex)
+    kx = np.arange(-kmax, kmax + 1)[:, None]
+    ky = np.arange(kmax + 1)[None, :]
+    ring = (kx * kx + ky * ky > 100) & (kx * kx + ky * ky <= 900)
+    qk[ring] = np.exp(2j * np.pi * rng.random(ring.sum())) * 0.01
+    ctx = sw.Context(0)
+    try:
+        ctx.set_field_qk(0, qk, nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+        ctx.set_field_qk(1, qk * np.exp(0.03j), nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+        p0 = ctx.get_field_grid(0, nx)
+        p1 = ctx.get_field_grid(1, nx)
+        U0 = float(np.sqrt((p0[0] ** 2 + p0[1] ** 2).max()))
+        dt = 0.25 * (L / nx) / U0
+        x = (rng.random((N, 2)) - 0.5) * L
+        th = rng.random(N) * 2 * np.pi
+        k = np.sqrt(15.0) * 3.0 * np.stack([np.cos(th), np.sin(th)], axis=1)
+        ctx.set_locality(20, 0)
+        ctx.packets_set(x, k)
+        sub, calls = 5, 8
+        for _ in range(calls):
+            ctx.advance(dt / sub, sub, 3.0, 1.0, nslots=2, alpha0=0.5 / sub, dalpha=1.0 / sub, bump=orc.BUMP_QG)
+        xg, kg = ctx.packets_get()
+    finally:
+        ctx.close()
+    assert np.isfinite(xg).all() and np.isfinite(kg).all()
+    idx = np.sort(rng.choice(N, 2000, replace=False))
+    xo, ko = x[idx], k[idx]
+    for _ in range(calls):
+        xo, ko, _, _ = cbind.leapfrog(p0, p1, 0.5 / sub, 1.0 / sub, nx, 2 * nx, L / nx, orc.BUMP_QG, xo, ko,
+                                      dt / sub, sub, 3.0, 1.0)
+    np.testing.assert_array_equal(xg[idx], xo)
+    np.testing.assert_array_equal(kg[idx], ko)

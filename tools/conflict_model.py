@@ -53,6 +53,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nx", type=int, default=512)
     ap.add_argument("--tiles", type=int, default=6, help="side of the block of tiles simulated")
+    ap.add_argument("--cfl", type=float, default=0.05, help="leapfrog dt in units of dx/U0 (bench: 0.05)")
+    ap.add_argument("--cycle", type=int, default=20, help="steps between re-binnings (bench: 20)")
     args = ap.parse_args()
     nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
     rng = np.random.default_rng(146)
@@ -67,7 +69,7 @@ def main():
     p0, p1 = cbind.planes_of(fl1), cbind.planes_of(fl2)
     U0 = math.sqrt(float((np.asarray(fl1["u"]) ** 2 + np.asarray(fl1["v"]) ** 2).max()))
     dx = L / nx
-    dt = 0.25 * dx / U0
+    dt = args.cfl * dx / U0
     N = 1_000_000
     x = L * rng.random((N, 2)) - L / 2
     i = np.arange(1, N + 1)
@@ -79,9 +81,10 @@ def main():
     sel = (cell[:, 0] // T < nt) & (cell[:, 1] // T < nt)
     x, k = x[sel], k[sel]
     n = x.shape[0]
-    _, _, hx, hk = cbind.leapfrog(p0, p1, 0.5, 0.0, nx, 2 * nx, dx, orc.BUMP_QG, x, k, dt, 4, f, 1.0, save_every=1)
-    X = [x] + [hx[j].T for j in range(3)]  # state at the start of launches 0..3
-    K = [k] + [hk[j].T for j in range(3)]
+    R = args.cycle
+    _, _, hx, hk = cbind.leapfrog(p0, p1, 0.5, 0.0, nx, 2 * nx, dx, orc.BUMP_QG, x, k, dt, R, f, 1.0, save_every=1)
+    X = [x] + [hx[j].T for j in range(R - 1)]  # state at the start of steps 0..R-1
+    K = [k] + [hk[j].T for j in range(R - 1)]
     half = 0.5 * dt
 
     def x1(j):
@@ -97,24 +100,18 @@ def main():
     cg0 = K[0] / w0[:, None]
     x1_0 = x1(0)
     U = cbind.eval6(p0, p1, 0.5, nx, 2 * nx, dx, orc.BUMP_QG, x1_0[:, 0], x1_0[:, 1])[:2].T
-    policies = {
-        "x0 (current)": X[0],
-        "x1 of launch 0": x1_0,
-        "x0 + 1.0 dt cg": X[0] + 1.0 * dt * cg0,
-        "x0 + 1.25 dt cg": X[0] + 1.25 * dt * cg0,
-        "x0 + 1.5 dt cg": X[0] + 1.5 * dt * cg0,
-        "x0 + 2 dt cg": X[0] + 2.0 * dt * cg0,
-        "x1 + 1.5 dt (cg + U(x1))": x1_0 + 1.5 * dt * (cg0 + U),
-        "x1 + 1.0 dt (cg + U(x1))": x1_0 + 1.0 * dt * (cg0 + U),
-        "exact x1 each launch (sort every launch)": None,
-    }
+    policies = {"x0 (no lead)": X[0]}
+    for frac in (0.25, 0.4, 0.5, 0.6):
+        policies[f"x0 + {frac:g} R dt cg"] = X[0] + frac * R * dt * cg0
+    policies[f"x1 + 0.5 R dt (cg + U(x1))"] = x1_0 + 0.5 * R * dt * (cg0 + U)
+    policies["exact x1 each step (sort every step)"] = None
     for name, keypos in policies.items():
-        tot = np.zeros(4)
-        base = np.zeros(4)
+        tot = np.zeros(R)
+        base = np.zeros(R)
         for tx in range(nt):
             for ty in range(nt):
                 m = np.where((tile0[:, 0] == tx) & (tile0[:, 1] == ty))[0]
-                for j in range(4):
+                for j in range(R):
                     kp = keypos if keypos is not None else x1(j)
                     c = cells(kp[m])
                     key = zorder(np.clip(c[:, 0] - tx * T, 0, T - 1), np.clip(c[:, 1] - ty * T, 0, T - 1))
@@ -131,8 +128,9 @@ def main():
                             cnt = np.bincount(nd % 16, minlength=16)
                             tot[j] += cnt.max()
                             base[j] += 1
-        print(f"{name:42s} LDS cycles / conflict-free per launch: " + " ".join(f"{t / b:.3f}" for t, b in zip(tot, base))
-              + f"   mean {tot.sum() / base.sum():.3f}")
+        per = tot / base
+        print(f"{name:42s} LDS cycles / conflict-free: first {per[0]:.3f} mid {per[R // 2]:.3f} last {per[-1]:.3f}"
+              f"   mean {tot.sum() / base.sum():.3f}")
 
 
 if __name__ == "__main__":
