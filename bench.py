@@ -188,6 +188,8 @@ def main():
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--tail-split", type=int, default=-1,
                     help="tiles per XCD band run as two half-tile workgroups (-1: library default)")
+    ap.add_argument("--tail-quarters", type=int, default=0,
+                    help="then tiles per XCD band run as four quarter-tile workgroups (with --tail-split)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
     ap.add_argument("--timing-every", type=int, default=5,
@@ -214,7 +216,7 @@ def main():
     ctx.set_cell_sort(args.cell_sort)
     ctx.set_blend_mode(args.blend_mode)
     if args.tail_split >= 0:
-        ctx.set_tail_split(args.tail_split)
+        ctx.set_tail_split(args.tail_split, args.tail_quarters)
     rng = np.random.default_rng(args.seed + rank)
     w = build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
@@ -301,7 +303,7 @@ def main():
                    "pde_dt": "0.25*dx/U0", "leapfrog_dt": f"{0.25 / args.substeps:g}*dx/U0",
                    "steps_per_launch": steps_per_launch,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
-                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "positions": args.positions,
+                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "tail_quarters": args.tail_quarters, "positions": args.positions,
                    "parallelism": f"packets sharded x{world}, field replicated"},
         # traffic: true HBM bytes per launch (rocprofv3 PMC, profiles/traffic.json), beside the
         # algorithmic bytes per launch that `achieved` is computed from (taps re-read from LDS)

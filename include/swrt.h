@@ -150,12 +150,13 @@ int swrt_set_kernel(swrt_ctx* ctx, int variant);
  * (default); 1 = sort on every launch. */
 int swrt_set_cell_sort(swrt_ctx* ctx, int every_launch);
 
-/* Launch shape of the LDS-tiled kernel (performance only; results are
- * identical): the last `tiles_per_xcd` tiles of each XCD's band of tiles run
- * as two workgroups of half the tile's packets each, so the end of a launch
- * is made of smaller work items and the CUs finish closer together.
- * 0 = one workgroup per tile. */
-int swrt_set_tail_split(swrt_ctx* ctx, int tiles_per_xcd);
+/* Launch shape of the LDS-tiled kernels (performance only; results are
+ * identical): each XCD's band of tiles ends with `halves_per_xcd` tiles run
+ * as two workgroups of half the tile's packets and then `quarters_per_xcd`
+ * tiles run as four workgroups of a quarter each, so the end of a launch is
+ * made of smaller work items and the CUs finish closer together.
+ * 0, 0 = one workgroup per tile. */
+int swrt_set_tail_split(swrt_ctx* ctx, int halves_per_xcd, int quarters_per_xcd);
 
 /* Two-snapshot blend of the LDS-tiled kernel.  0 (default): interpolate each
  * snapshot, then blend (1-alpha)*U1 + alpha*U2 — interpolate_U.m:19-23 in its

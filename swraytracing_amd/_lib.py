@@ -26,8 +26,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SWRT_LIB_PATH") or os.path.join(_HERE, "libswrt.so")
 
 SWRT_OK = 0
-# swrt_set_tail_split default of the library build (SWRT_TAIL_SPLIT in swrt_api.hip)
-DEFAULT_TAIL_SPLIT = 16
+# swrt_set_tail_split defaults of the library build (SWRT_TAIL_SPLIT / _QUARTERS in swrt_api.hip)
+DEFAULT_TAIL_SPLIT = (16, 0)
 ERRORS = {1: "SWRT_ERR_ARG", 2: "SWRT_ERR_HIP", 3: "SWRT_ERR_STATE", 4: "SWRT_ERR_ALLOC"}
 
 _D = ctypes.c_double
@@ -64,7 +64,7 @@ SIGNATURES = {
     "swrt_set_locality": (_INT, [_VP, _I, _I]),
     "swrt_set_kernel": (_INT, [_VP, _INT]),
     "swrt_set_cell_sort": (_INT, [_VP, _INT]),
-    "swrt_set_tail_split": (_INT, [_VP, _INT]),
+    "swrt_set_tail_split": (_INT, [_VP, _INT, _INT]),
     "swrt_set_blend_mode": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
@@ -265,9 +265,10 @@ class Context:
     def set_cell_sort(self, every_launch=0):
         self._chk(self._L.swrt_set_cell_sort(self._h, int(every_launch)), "swrt_set_cell_sort")
 
-    def set_tail_split(self, tiles_per_xcd=0):
-        """Half-tile workgroups for the last tiles of each XCD band (launch shape only)."""
-        self._chk(self._L.swrt_set_tail_split(self._h, int(tiles_per_xcd)), "swrt_set_tail_split")
+    def set_tail_split(self, halves_per_xcd=0, quarters_per_xcd=0):
+        """Half- then quarter-tile workgroups for the last tiles of each XCD band (launch shape only)."""
+        self._chk(self._L.swrt_set_tail_split(self._h, int(halves_per_xcd), int(quarters_per_xcd)),
+                  "swrt_set_tail_split")
 
     def advance(self, dt, nsteps, f, gH, nslots=1, alpha0=0.0, dalpha=0.0, bump=1e-13, save_every=0):
         self._chk(self._L.swrt_advance(self._h, float(dt), int(nsteps), float(f), float(gH), int(nslots),

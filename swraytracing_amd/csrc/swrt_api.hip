@@ -41,6 +41,9 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #ifndef SWRT_SORT_LEAD
 #define SWRT_SORT_LEAD 1
 #endif
+#ifndef SWRT_TAIL_QUARTERS
+#define SWRT_TAIL_QUARTERS 0
+#endif
 #ifndef SWRT_TAIL_SPLIT
 #define SWRT_TAIL_SPLIT 16
 #endif
@@ -126,6 +129,7 @@ struct swrt_ctx {
   int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
   bool sort_lead = SWRT_SORT_LEAD;  // in-tile sort keys lead by the group-velocity drift
   int tail_split = SWRT_TAIL_SPLIT;  // tiles per XCD band run as two half-tile workgroups (swrt_tile.hpp)
+  int tail_quarters = SWRT_TAIL_QUARTERS;  // ... then as four quarter-tile workgroups
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -415,6 +419,19 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next)
   return SWRT_OK;
 }
 
+// Tail shape of a tile launch over `ntiles` tiles (swrt_tile.hpp
+// wg_work_range): the split code and the extra workgroups it adds.
+int launch_shape(const swrt_ctx* c, unsigned ntiles, unsigned* extra) {
+  *extra = 0;
+  if (ntiles % 8 != 0 || (c->tail_split <= 0 && c->tail_quarters <= 0)) return 0;
+  const unsigned tpx = ntiles / 8;
+  const unsigned h = std::min<unsigned>((unsigned)std::max(c->tail_split, 0), tpx);
+  const unsigned q = std::min<unsigned>((unsigned)std::max(c->tail_quarters, 0), tpx - h);
+  if (h + q == 0) return 0;
+  *extra = 8u * (h + 3u * q);
+  return (int)(h | (q << 16));
+}
+
 bool use_tile_kernel(const swrt_ctx* c) {
   if (c->rebin_every <= 0) return false;
   if (c->kernel == 2 || c->kernel == 3) return true;
@@ -490,16 +507,16 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   t.ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
   const unsigned grid = (unsigned)(t.ntx * t.ntx);
   // half-tile workgroups at the end of each XCD band (swrt_tile.hpp wg_work)
-  t.split = 0;
-  if (grid % 8 == 0 && c->tail_split > 0) t.split = (int)std::min<unsigned>((unsigned)c->tail_split, grid / 8);
-  const unsigned wgrid = grid + 8u * (unsigned)t.split;
+  unsigned extra = 0;
+  t.split = launch_shape(c, grid, &extra);
+  const unsigned wgrid = grid + extra;
   t.next_keys = nullptr;
   t.next_counts = nullptr;
   t.sort_cells = (c->cell_sort == 1 || !c->cells_sorted) ? 1 : 0;
   t.src = nullptr;
   // sort keys lead by half the steps until the next sort (swrt_tile.hpp)
   t.sort_lead = 0.0;
-  if (c->sort_lead) t.sort_lead = 0.5 * a.dt * (c->cell_sort == 1 ? 1.0 : (double)std::max<int64_t>(1, c->rebin_every));
+  if (c->sort_lead) t.sort_lead = 0.5 * a.dt * (c->cell_sort == 1 ? (double)a.nsteps : (double)std::max<int64_t>(1, c->rebin_every));
   if (c->src_pending) {  // first launch after an indirect re-binning (always a sort launch)
     t.src = c->src_idx;
     t.sort_cells = 1;
@@ -1023,10 +1040,12 @@ int swrt_set_cell_sort(swrt_ctx* c, int every_launch) {
   return SWRT_OK;
 }
 
-int swrt_set_tail_split(swrt_ctx* c, int tiles_per_xcd) {
+int swrt_set_tail_split(swrt_ctx* c, int halves_per_xcd, int quarters_per_xcd) {
   if (!c) return SWRT_ERR_ARG;
-  if (tiles_per_xcd < 0) return fail(c, SWRT_ERR_ARG, "tiles_per_xcd must be >= 0");
-  c->tail_split = tiles_per_xcd;
+  if (halves_per_xcd < 0 || quarters_per_xcd < 0) return fail(c, SWRT_ERR_ARG, "tail split counts must be >= 0");
+  if (halves_per_xcd > 0xffff || quarters_per_xcd > 0x7fff) return fail(c, SWRT_ERR_ARG, "tail split counts too large");
+  c->tail_split = halves_per_xcd;
+  c->tail_quarters = quarters_per_xcd;
   return SWRT_OK;
 }
 
@@ -1737,9 +1756,9 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
     const int* starts = c->bins + 2 * kMaxBins;
     const unsigned ntiles = (unsigned)(ntx * ntx);
     Ode23Args a = a0;
-    a.split = (ntiles % 8 == 0 && c->tail_split > 0) ? (int)std::min<unsigned>((unsigned)c->tail_split, ntiles / 8)
-                                                      : 0;
-    const unsigned grid = ntiles + 8u * (unsigned)a.split;
+    unsigned extra = 0;
+    a.split = launch_shape(c, ntiles, &extra);
+    const unsigned grid = ntiles + extra;
     // in-tile cell order of this binning, once (swrt_ode23.hpp)
     if (!c->o_order_valid || c->o_order_split != a.split) {
       if (c->o_order_cap < c->cap) {

@@ -41,37 +41,45 @@ struct TileArgs {
   const int* src;        // non-NULL (sort launches only): binned slot p holds input packet
                          // src[p] (indirect re-binning); NULL: slot p holds packet p
   double sort_lead;      // in-tile sort key: position + sort_lead * (group velocity)
-  int split;             // > 0: the last `split` tiles of each XCD's band run as two
-                         // half-tile workgroups (grid = ntiles + 8*split, ntiles % 8 == 0)
+  int split;             // launch shape (wg_work_range): halves | quarters << 16 per XCD band
 };
 
 // Workgroup -> (tile, packet range).  XCD-aware (xcd_block): XCD x walks one
-// contiguous band of tiles.  With ta.split > 0 each band ends with `split`
-// tiles cut into two workgroups of half the packets each (both stage the
-// whole window): the dispatcher then hands out half-size work items as CUs
-// free up at the end of the launch, which narrows the spread of CU finish
-// times (the launch ends with its slowest CU).
+// contiguous band of tiles.  `split` = h | q << 16 (ntiles % 8 == 0): each
+// band ends with h tiles run as two half-tile workgroups and then q tiles run
+// as four quarter-tile workgroups (each stages the whole window), so the
+// dispatcher hands out ever smaller work items as CUs free up at the end of
+// the launch, which narrows the spread of CU finish times (the launch ends
+// with its slowest CU).  grid = ntiles + 8*(h + 3q).
 __device__ __forceinline__ int wg_work_range(const int* starts, int split, int& pbeg, int& pend) {
   const int b = (int)blockIdx.x, nb = (int)gridDim.x;
-  int tile, part = -1;
+  int tile, part = 0, nparts = 1;
   if (split > 0) {
+    const int h = split & 0xffff, q = split >> 16;
     const int x = b % 8, j = b / 8;
-    const int tpx = nb / 8 - split;  // tiles per XCD band
-    const int whole = tpx - split;
+    const int tpx = nb / 8 - h - 3 * q;  // tiles per XCD band
+    const int whole = tpx - h - q;
     if (j < whole) {
       tile = x * tpx + j;
-    } else {
+    } else if (j < whole + 2 * h) {
       tile = x * tpx + whole + (j - whole) / 2;
       part = (j - whole) & 1;
+      nparts = 2;
+    } else {
+      const int jj = j - whole - 2 * h;
+      tile = x * tpx + whole + h + jj / 4;
+      part = jj & 3;
+      nparts = 4;
     }
   } else {
     tile = (int)xcd_block(b, nb);
   }
   pbeg = starts[tile];
   pend = starts[tile + 1];
-  if (part >= 0) {
-    const int h = (pend - pbeg + 1) / 2;
-    if (part == 0) pend = pbeg + h; else pbeg += h;
+  if (nparts > 1) {
+    const int cnt = pend - pbeg;
+    pend = pbeg + (int)((int64_t)cnt * (part + 1) / nparts);
+    pbeg = pbeg + (int)((int64_t)cnt * part / nparts);
   }
   return tile;
 }
@@ -467,6 +475,22 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       const int orig = a.perm[pi];
       for (int st = 0; st < a.nsteps; ++st) {
         const int64_t sg = a.s0 + st;
+#ifdef SWRT_FAIR_PRIO
+        {
+          // fair share between co-resident workgroups: a wave's issue
+          // priority falls as it works through its packets, so the workgroup
+          // that started later (the SQ otherwise issues oldest first) catches
+          // up and a CU's last workgroups end together
+          const int it = (b0 - pbeg) / NT + (r0 - (tid & ~63)) / NT;
+          const int niter = max(1, (pend - pbeg - (tid & ~63) + NT - 1) / NT);
+          int bucket = min(3, (4 * (it * a.nsteps + st)) / (niter * a.nsteps));
+          bucket = __builtin_amdgcn_readfirstlane(bucket);
+          if (bucket == 0) __builtin_amdgcn_s_setprio(3);
+          else if (bucket == 1) __builtin_amdgcn_s_setprio(2);
+          else if (bucket == 2) __builtin_amdgcn_s_setprio(1);
+          else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
         const double x1 = x0 + a.half * (a.gH * k0 / w);
         const double y1 = y0 + a.half * (a.gH * l0 / w);

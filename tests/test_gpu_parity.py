@@ -405,7 +405,8 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, 
     np.testing.assert_array_equal(hkg, hko)
 
 
-@pytest.mark.parametrize("variant,tail_split", [(2, 0), (2, 32), (2, 1000), (3, 0)])
+@pytest.mark.parametrize("variant,tail_split", [(2, (0, 0)), (2, (32, 0)), (2, (1000, 0)), (2, (16, 16)),
+                                                (2, (0, 1000)), (3, (0, 0))])
 def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split):
     """512^2 two-snapshot field, 2e5 packets, LDS kernel with re-binning every
     3 steps over 10 steps: random subset bit-identical to the oracle (the
@@ -428,7 +429,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split)
     x, k = orc.initial_packets(N, L, 4.0, 3.0, 1.0, rng)
     ctx.set_kernel(variant)
     ctx.set_locality(3, 0)
-    ctx.set_tail_split(tail_split)
+    ctx.set_tail_split(*tail_split)
     try:
         ctx.packets_set(x, k)
         ctx.advance(0.01, 10, 3.0, 1.0, nslots=2, alpha0=0.05, dalpha=0.1, bump=orc.BUMP_QG)
@@ -436,7 +437,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split)
     finally:
         ctx.set_kernel(0)
         ctx.set_locality(4, 0)
-        ctx.set_tail_split(DEFAULT_TAIL_SPLIT)
+        ctx.set_tail_split(*DEFAULT_TAIL_SPLIT)
     idx = np.sort(rng.choice(N, 2000, replace=False))
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.05, 0.1, nx, 2 * nx, L / nx, orc.BUMP_QG, x[idx], k[idx], 0.01,
                                        10, 3.0, 1.0)
@@ -475,7 +476,8 @@ def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
     np.testing.assert_array_equal(kg, ko)
 
 
-@pytest.mark.parametrize("variant,cell_sort,tail_split", [(2, 0, 0), (2, 1, 0), (3, 0, 0), (2, 0, 1), (2, 1, 2)])
+@pytest.mark.parametrize("variant,cell_sort,tail_split", [(2, 0, (0, 0)), (2, 1, (0, 0)), (3, 0, (0, 0)),
+                                                          (2, 0, (1, 0)), (2, 1, (2, 0)), (2, 0, (1, 1))])
 def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_sort, tail_split):
     """One advance call per step (the bench's pattern): with re-binning every
     4 steps, 3 of 4 launches read packets in the cell order the previous
@@ -495,7 +497,7 @@ def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_s
     ctx.set_kernel(variant)
     ctx.set_cell_sort(cell_sort)
     ctx.set_locality(4, 0)
-    ctx.set_tail_split(tail_split)
+    ctx.set_tail_split(*tail_split)
     try:
         ctx.packets_set(x, k)
         for s in range(nst):
@@ -504,7 +506,7 @@ def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_s
     finally:
         ctx.set_cell_sort(0)
         ctx.set_kernel(0)
-        ctx.set_tail_split(DEFAULT_TAIL_SPLIT)
+        ctx.set_tail_split(*DEFAULT_TAIL_SPLIT)
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, a0, da, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, c["dt"] * 3, nst,
                                        c["f"], 1.0)
     np.testing.assert_array_equal(xg, xo)

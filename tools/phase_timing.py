@@ -29,6 +29,9 @@ def main():
     ap.add_argument("--mode", default="blend")
     ap.add_argument("--samples", type=int, default=5)
     ap.add_argument("--tail-split", type=int, default=-1)
+    ap.add_argument("--tail-quarters", type=int, default=0)
+    ap.add_argument("--substeps", type=int, default=5)
+    ap.add_argument("--rebin-every", type=int, default=20)
     ap.add_argument("--dump", default="", help="save every sample's raw stamps (npz) for offline analysis")
     args = ap.parse_args()
     args.world, args.rank, args.seed = 1, 0, 146
@@ -36,24 +39,24 @@ def main():
     f = lib.swrt_debug_phases
     f.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, ctypes.c_int]
     ctx = sw.Context(0)
-    ctx.set_locality(4, 0)
+    ctx.set_locality(args.rebin_every, 0)
     ctx.set_kernel(2)
     if args.tail_split >= 0:
-        ctx.set_tail_split(args.tail_split)
+        ctx.set_tail_split(args.tail_split, args.tail_quarters)
     rng = np.random.default_rng(146)
     w = bench.build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
     for _ in range(8):
-        bench.step(ctx, w, 1)
+        bench.step(ctx, w, args.substeps)
     ntiles = (args.nx // 16) ** 2
-    nrows = 2 * ntiles  # workgroups (half-tile workgroups with --tail-split)
+    nrows = 4 * ntiles  # workgroups (half/quarter-tile workgroups with --tail-split)
     buf = np.zeros(nrows * 8, dtype=np.uint64)
     ptr = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))
     res = []
     raw = []
     for s in range(args.samples):
         assert f(None, nrows, 1) == 0
-        bench.step(ctx, w, 1)
+        bench.step(ctx, w, args.substeps)
         ctx.synchronize()
         assert f(ptr, nrows, 0) == 0
         d = buf.reshape(nrows, 8).astype(np.int64)
