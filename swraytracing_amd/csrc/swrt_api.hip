@@ -148,6 +148,10 @@ struct swrt_ctx {
   int64_t xka_nx = 0;
   double xka_dx = 0.0, xka_dy = 0.0;
   double* xka_state = nullptr;  // 5n
+  double* xka_state2 = nullptr; // 5n: the state in binned order
+  int* xka_keys = nullptr;      // n
+  int* xka_src = nullptr;       // n: binned slot -> packet
+  int* xka_bins = nullptr;      // counts | cursor | starts of the xka binning
   int64_t xka_cap = 0;
   double* xka_hist = nullptr;
   int64_t xka_hcap = 0;  // doubles allocated
@@ -655,6 +659,8 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->hk) (void)hipFree(c->hk);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->tw) (void)hipFree(c->tw);
+  for (void* p : {(void*)c->xka_state2, (void*)c->xka_keys, (void*)c->xka_src, (void*)c->xka_bins})
+    if (p) (void)hipFree(p);
   for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist, (void*)c->modes,
                   (void*)c->mode_rows})
     if (p) (void)hipFree(p);
@@ -1196,12 +1202,18 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
     return fail(c, SWRT_ERR_ARG, "nsteps must be a multiple of save_every");
   HIPCHK(c, hipSetDevice(c->device));
   if (n > c->xka_cap) {
-    if (c->xka_state) (void)hipFree(c->xka_state);
-    c->xka_state = nullptr;
+    for (void** p : {(void**)&c->xka_state, (void**)&c->xka_state2, (void**)&c->xka_keys, (void**)&c->xka_src}) {
+      if (*p) (void)hipFree(*p);
+      *p = nullptr;
+    }
     c->xka_cap = 0;
     HIPCHK(c, hipMalloc(&c->xka_state, sizeof(double) * 5 * n));
+    HIPCHK(c, hipMalloc(&c->xka_state2, sizeof(double) * 5 * n));
+    HIPCHK(c, hipMalloc(&c->xka_keys, sizeof(int) * n));
+    HIPCHK(c, hipMalloc(&c->xka_src, sizeof(int) * n));
     c->xka_cap = n;
   }
+  if (!c->xka_bins) HIPCHK(c, hipMalloc(&c->xka_bins, sizeof(int) * (3 * kMaxBins + 1)));
   const int64_t frames = (hist5 && save_every > 0) ? nsteps / save_every : 0;
   if (frames * 5 * n > c->xka_hcap) {
     if (c->xka_hist) (void)hipFree(c->xka_hist);
@@ -1231,10 +1243,42 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   a.n = n;
   a.save_every = save_every > 0 ? save_every : 1;
   a.hist = frames ? c->xka_hist : nullptr;
+  a.perm = nullptr;
+  // larger ensembles: step the packets in spatially binned order (8 x 8-cell
+  // tiles, counting sort by index), so a wave gathers from a few nodes
+  const bool binned = n >= 4096 && c->rebin_every > 0;
+  if (binned) {
+    BinGeom g;
+    g.dx = a.dx; g.px = a.px; g.py = a.py; g.inv_px = a.inv_px; g.inv_py = a.inv_py; g.inv_dx = a.inv_dx;
+    g.pow2x = a.pow2x; g.pow2y = a.pow2y; g.nx = a.nx;
+    g.tile = 8;
+    while ((a.nx + g.tile - 1) / g.tile > 64) g.tile *= 2;
+    g.ntx = (a.nx + g.tile - 1) / g.tile;
+    const int nbins = g.ntx * g.ntx;
+    const unsigned bgrid = nblocks(n, 256 * kBinPerThread);
+    HIPCHK(c, hipMemsetAsync(c->xka_bins, 0, sizeof(int) * nbins, c->stream));
+    hipLaunchKernelGGL(bin_count_kernel, dim3(bgrid), dim3(256), sizeof(int) * nbins, c->stream, g, c->xka_state,
+                       n, nbins, c->xka_keys, c->xka_bins);
+    hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->xka_bins, nbins,
+                       c->xka_bins + kMaxBins, c->xka_bins + 2 * kMaxBins);
+    hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3(bgrid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
+                       c->xka_state, c->xka_state, nullptr, c->xka_keys, n, nbins, c->xka_bins + kMaxBins,
+                       nullptr, nullptr, nullptr, c->xka_src);
+    hipLaunchKernelGGL(xka_gather_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, c->xka_state,
+                       c->xka_src, n, c->xka_state2);
+    HIPCHK(c, hipGetLastError());
+    a.st = c->xka_state2;
+    a.perm = c->xka_src;
+  }
   for (int64_t s0 = 0; s0 < nsteps; s0 += kMaxStepsPerLaunch) {
     a.nsteps = (int)std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
     a.frame0 = s0 / a.save_every;
     hipLaunchKernelGGL(xka_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, a);
+    HIPCHK(c, hipGetLastError());
+  }
+  if (binned) {
+    hipLaunchKernelGGL(xka_scatter_back_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, c->xka_state2,
+                       c->xka_src, n, c->xka_state);
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipMemcpyAsync(state5, c->xka_state, sizeof(double) * 5 * n, hipMemcpyDeviceToHost, c->stream));

@@ -32,6 +32,7 @@ struct XkaArgs {
   int64_t save_every;
   double* hist;        // frames of 5 x n (NULL: none)
   int64_t frame0;
+  const int* perm;     // binned slot -> caller's packet index (history frames); NULL: identity
 };
 
 struct XkaStencil {
@@ -165,10 +166,32 @@ __global__ void __launch_bounds__(256) xka_kernel(XkaArgs a) {
     l = Ln;
     if (a.hist != nullptr && ((s + 1) % a.save_every) == 0) {
       double* h = a.hist + (a.frame0 + (s + 1) / a.save_every - 1) * 5 * n;
-      h[p] = x; h[n + p] = y; h[2 * n + p] = k; h[3 * n + p] = l; h[4 * n + p] = ac;
+      const int64_t o = a.perm ? a.perm[p] : p;  // frames in the caller's packet order
+      h[o] = x; h[n + o] = y; h[2 * n + o] = k; h[3 * n + o] = l; h[4 * n + o] = ac;
     }
   }
   a.st[p] = x; a.st[n + p] = y; a.st[2 * n + p] = k; a.st[3 * n + p] = l; a.st[4 * n + p] = ac;
+}
+
+// Spatial order for the xka lanes (swrt_xka_step): the 5 x n state gathered
+// into binned order (src from bin_scatter_kernel<true>), and scattered back.
+// Neighbouring lanes then read the same few node records, which the L1/L2
+// serve: the gathers dominate the unbinned kernel.  Order only: every packet
+// is stepped by the same operations whatever its lane.
+__global__ void xka_gather_kernel(const double* st, const int* src, int64_t n, double* out) {
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  const int64_t p = src[d];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) out[q * n + d] = st[q * n + p];
+}
+
+__global__ void xka_scatter_back_kernel(const double* st, const int* src, int64_t n, double* out) {
+  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n) return;
+  const int64_t p = src[d];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) out[q * n + p] = st[q * n + d];
 }
 
 // 7 column-major planes (u, v, u_x, u_y, v_x, v_y, H) -> padded 8-double node records.

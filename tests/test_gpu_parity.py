@@ -540,6 +540,36 @@ def test_step_packet_xka_bitexact(ctx, nx):
                 assert hist[n][i, j] == P[n], (i, j, n, hist[n][i, j], P[n])
 
 
+def test_step_packet_xka_binned_order_is_invisible(ctx):
+    """Ensembles >= 4096 packets are stepped in spatially binned order
+    (swrt_xka_step): final states and every history frame are bit-identical
+    to the unbinned lane order (itself pinned to the literal oracle above),
+    and the first packets match the oracle directly."""
+    import swraytracing_amd as sw
+    nx = 64
+    U, G, H = _rsw_background(nx)
+    dx = 2 * np.pi / nx
+    rng = np.random.default_rng(11)
+    npk, steps, dt, C0, f = 6000, 6, 0.3 * dx, 1.0, 4.0
+    P0 = {"x": rng.uniform(0, 2 * np.pi, npk), "y": rng.uniform(-7, 7, npk),
+          "k": 40 * np.cos(np.arange(npk)), "l": 40 * np.sin(np.arange(npk)), "a": np.ones(npk)}
+    ctx.set_locality(4, 0)
+    binned = sw.raytrace_xka(P0, U, G, H, C0, f, dx, dx, dt, steps, ctx=ctx)
+    ctx.set_locality(0, 0)
+    try:
+        plain = sw.raytrace_xka(P0, U, G, H, C0, f, dx, dx, dt, steps, ctx=ctx)
+    finally:
+        ctx.set_locality(4, 0)
+    for n in "xykla":
+        np.testing.assert_array_equal(binned[n], plain[n])
+    for i in range(3):
+        P = {n: float(P0[n][i]) for n in "xykla"}
+        for j in range(1, steps):
+            P = orc.step_packet_xka(P, U, G, H, C0, f, dx, dx, dt)
+            for n in "xykla":
+                assert binned[n][i, j] == P[n]
+
+
 def test_step_packet_xka_scalar_api(ctx):
     import swraytracing_amd as sw
     nx = 32
