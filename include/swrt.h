@@ -296,6 +296,11 @@ int swrt_qg_init(swrt_ctx* ctx, const swrt_qg_params* params, int64_t nx, const 
  * :167-181 with expLdt/expL2dt recomputed on the device whenever dt changes.
  * Before each step the previous qk is kept (prev_qk, :122 / :167). */
 int swrt_qg_step(swrt_ctx* ctx, double dt, int64_t nsteps);
+/* 1: steady AB3 steps are replayed from hipGraphs of the step's 9 launches
+ * (one per qk buffer parity and dt; re-captured when dt changes).  0
+ * (default): plain launches, measured faster on ROCm 7 (73.5 vs 67.5 us per
+ * 512^2 two-layer step).  Performance only: results are identical. */
+int swrt_qg_set_graphs(swrt_ctx* ctx, int on);
 /* U0 = sqrt(max((u + shear)^2 + v^2)) over every layer of grid_U(qk)
  * (qg2layersw_raytrace.m:156-158; qgsw_raytrace.m:63-65 with shear 0). */
 int swrt_qg_max_speed(swrt_ctx* ctx, double* U0_out);

@@ -82,6 +82,7 @@ SIGNATURES = {
     "swrt_ode23_accept": (_INT, [_VP]),
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
+    "swrt_qg_set_graphs": (_INT, [_VP, _INT]),
     "swrt_qg_max_speed": (_INT, [_VP, ctypes.POINTER(_D)]),
     "swrt_qg_max_speed_async": (_INT, [_VP]),
     "swrt_qg_max_speed_result": (_INT, [_VP, ctypes.POINTER(_D)]),
@@ -388,6 +389,10 @@ class Context:
 
     def qg_step(self, dt, nsteps=1):
         self._chk(self._L.swrt_qg_step(self._h, float(dt), int(nsteps)), "swrt_qg_step")
+
+    def qg_set_graphs(self, on=False):
+        """hipGraph replay of steady AB3 steps (swrt_qg_set_graphs); results identical."""
+        self._chk(self._L.swrt_qg_set_graphs(self._h, int(bool(on))), "swrt_qg_set_graphs")
 
     def qg_max_speed(self):
         u = _D()

@@ -41,6 +41,9 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #ifndef SWRT_SORT_LEAD
 #define SWRT_SORT_LEAD 1
 #endif
+#ifndef SWRT_QG_GRAPHS
+#define SWRT_QG_GRAPHS 0
+#endif
 #ifndef SWRT_TAIL_QUARTERS
 #define SWRT_TAIL_QUARTERS 0
 #endif
@@ -85,10 +88,24 @@ struct QGState {
   hipEvent_t ev = nullptr;     // recorded after that copy
   bool speed_pending = false;
   double exp_dt = -1.0;        // dt of the current E1/E2
+  // replayable AB3 steps (hipGraph), one per qk buffer parity, for one dt
+  hipGraphExec_t gexec[2] = {nullptr, nullptr};
+  const double2* gqk[2] = {nullptr, nullptr};
+  double gdt[2] = {0.0, 0.0};
+  const double2* gtw[2] = {nullptr, nullptr};  // twiddles baked into each graph
   int64_t steps = 0;
   double t = 0.0;
   bool has_prev = false;
 };
+
+static void qg_drop_graphs(QGState& q) {
+  for (int i = 0; i < 2; ++i) {
+    if (q.gexec[i]) (void)hipGraphExecDestroy(q.gexec[i]);
+    q.gexec[i] = nullptr;
+    q.gqk[i] = nullptr;
+  }
+}
+
 
 struct Timing {
   std::vector<hipEvent_t> ev;  // pairs
@@ -130,6 +147,7 @@ struct swrt_ctx {
   bool sort_lead = SWRT_SORT_LEAD;  // in-tile sort keys lead by the group-velocity drift
   int tail_split = SWRT_TAIL_SPLIT;  // tiles per XCD band run as two half-tile workgroups (swrt_tile.hpp)
   int tail_quarters = SWRT_TAIL_QUARTERS;  // ... then as four quarter-tile workgroups
+  bool qg_graphs = SWRT_QG_GRAPHS;         // replay steady QG steps as hipGraphs
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -669,6 +687,7 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->qg.hmax) (void)hipHostFree(c->qg.hmax);
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
+  qg_drop_graphs(c->qg);
   if (c->o_order) (void)hipFree(c->o_order);
   for (void* p : {(void*)c->oF[0], (void*)c->oF[1], (void*)c->oF[2], (void*)c->oF[3], (void*)c->o_ynx,
                   (void*)c->o_ynk, (void*)c->o_dmax})
@@ -1043,6 +1062,13 @@ int swrt_set_cell_sort(swrt_ctx* c, int every_launch) {
   if (!c) return SWRT_ERR_ARG;
   if (every_launch != 0 && every_launch != 1) return fail(c, SWRT_ERR_ARG, "every_launch must be 0 or 1");
   c->cell_sort = every_launch;
+  return SWRT_OK;
+}
+
+int swrt_qg_set_graphs(swrt_ctx* c, int on) {
+  if (!c) return SWRT_ERR_ARG;
+  if (on != 0 && on != 1) return fail(c, SWRT_ERR_ARG, "on must be 0 or 1");
+  c->qg_graphs = on != 0;
   return SWRT_OK;
 }
 
@@ -1489,6 +1515,7 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
     if (ptr) (void)hipFree(ptr);
   if (q.hmax) (void)hipHostFree(q.hmax);
   if (q.ev) (void)hipEventDestroy(q.ev);
+  qg_drop_graphs(q);
   q = QGState{};
   const int n = (int)nx, kmax = n / 2 - 1;
   q.nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
@@ -1538,6 +1565,72 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
   GUARD_END(c)
 }
 
+namespace {
+// The kernel sequence of one QG step (update of qgsw_raytrace.m:270-286 /
+// qg2layersw_raytrace.m:309-323 + the AB3 step): spectra -> inverse 2-D FFT ->
+// Jacobian -> forward 2-D FFT -> fused g2k crop + AB3 update into qk_prev.
+int qg_step_launches(swrt_ctx* c, double dt, int abstep) {
+  QGState& q = c->qg;
+  const int n = q.g.n, nl = q.g.nl;
+  int rc;
+  if (nl == 2)
+    hipLaunchKernelGGL(qg_jac_spectra_kernel<2>, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
+  else
+    hipLaunchKernelGGL(qg_jac_spectra_kernel<1>, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = inverse_2d(c, q.Z, q.T, n, 2 * nl))) return rc;
+  double2* Zj = q.Z;  // J1 + i J2, grid layout (x contiguous)
+  hipLaunchKernelGGL(qg_jacobian_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.T, nl, q.nn, Zj);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = run_fft_pass(c, Zj, n, 1, 0))) return rc;   // along x
+  if ((rc = run_transpose(c, Zj, q.T, n, 1))) return rc;
+  if ((rc = run_fft_pass(c, q.T, n, 1, 0))) return rc;  // along y: [ky + n*kx]
+  // out of place: the new qk goes to the other buffer, the old one becomes prev_qk
+  if (nl == 2)
+    hipLaunchKernelGGL(qg_update_kernel<2>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
+                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+  else
+    hipLaunchKernelGGL(qg_update_kernel<1>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
+                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+
+// Steady AB3 steps replay a captured graph of the launch sequence (kernel
+// arguments are baked in: one graph per qk buffer parity and dt; the drivers'
+// dt changes only when the CFL rule fires).  Measured slower than the plain
+// launches on ROCm 7 at 512^2 (73.5 vs 67.5 us per step), so
+// off by default (swrt_qg_set_graphs).
+int qg_step_graphed(swrt_ctx* c, double dt) {
+  QGState& q = c->qg;
+  int g = -1;
+  for (int i = 0; i < 2; ++i)
+    if (q.gexec[i] && q.gqk[i] == q.qk && q.gdt[i] == dt && q.gtw[i] == c->tw) g = i;
+  if (g < 0) {
+    g = (q.gexec[0] && q.gqk[0] != q.qk && q.gdt[0] == dt && q.gtw[0] == c->tw) ? 1 : 0;  // keep the other parity
+    if (q.gexec[g]) (void)hipGraphExecDestroy(q.gexec[g]);
+    q.gexec[g] = nullptr;
+    hipGraph_t graph = nullptr;
+    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    const int rc = qg_step_launches(c, dt, 3);
+    const hipError_t e = hipStreamEndCapture(c->stream, &graph);
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    HIPCHK(c, e);
+    const hipError_t ei = hipGraphInstantiate(&q.gexec[g], graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    HIPCHK(c, ei);
+    q.gqk[g] = q.qk;
+    q.gdt[g] = dt;
+    q.gtw[g] = c->tw;
+  }
+  HIPCHK(c, hipGraphLaunch(q.gexec[g], c->stream));
+  return SWRT_OK;
+}
+}  // namespace
+
 int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
@@ -1549,32 +1642,17 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
   const int n = q.g.n, nl = q.g.nl;
   if ((rc = ensure_twiddles(c, n))) return rc;
   for (int64_t s = 0; s < nsteps; ++s) {
-    if (nl == 2)
-      hipLaunchKernelGGL(qg_jac_spectra_kernel<2>, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
-    else
-      hipLaunchKernelGGL(qg_jac_spectra_kernel<1>, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
-    HIPCHK(c, hipGetLastError());
-    if ((rc = inverse_2d(c, q.Z, q.T, n, 2 * nl))) return rc;
-    double2* Zj = q.Z;  // J1 + i J2, grid layout (x contiguous)
-    hipLaunchKernelGGL(qg_jacobian_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.T, nl, q.nn, Zj);
-    HIPCHK(c, hipGetLastError());
-    if ((rc = run_fft_pass(c, Zj, n, 1, 0))) return rc;   // along x
-    if ((rc = run_transpose(c, Zj, q.T, n, 1))) return rc;
-    if ((rc = run_fft_pass(c, q.T, n, 1, 0))) return rc;  // along y: [ky + n*kx]
     if (nl == 2 && dt != q.exp_dt) {
       hipLaunchKernelGGL(qg2_exp_kernel, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.g, dt, q.E1, q.E2);
       HIPCHK(c, hipGetLastError());
       q.exp_dt = dt;
     }
     const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
-    // out of place: the new qk goes to the other buffer, the old one becomes prev_qk
-    if (nl == 2)
-      hipLaunchKernelGGL(qg_update_kernel<2>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
-                         abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+    if (abstep == 3 && c->qg_graphs)
+      rc = qg_step_graphed(c, dt);
     else
-      hipLaunchKernelGGL(qg_update_kernel<1>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
-                         abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
-    HIPCHK(c, hipGetLastError());
+      rc = qg_step_launches(c, dt, abstep);
+    if (rc) return rc;
     std::swap(q.qk, q.qk_prev);
     q.steps += 1;
     q.t = q.t + dt;

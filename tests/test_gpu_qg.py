@@ -248,3 +248,37 @@ def test_golden_qg_fixture(ctx):
         assert abs(dt - want) <= 1e-12 * want
         m2.step(dt)
     assert _rel(m2.qk, g["qk2_8"]) < QG_RTOL
+
+
+@pytest.mark.parametrize("layers", [1, 2])
+def test_qg_graph_replay_bit_identical(ctx, layers):
+    """Steady AB3 steps replayed from hipGraphs (swrt_qg_set_graphs) give the
+    same bits as plain launches, across dt changes (graph re-capture, both qk
+    buffer parities) and a field call at another size between steps (the FFT
+    twiddles are rebuilt under the graph)."""
+    nx = 64
+    dt0 = 0.05 * (2 * np.pi / nx) / 0.2 if layers == 1 else 0.25 * (20.0 / nx) / 0.3
+    dts = [dt0] * 5 + [0.8 * dt0] * 4 + [dt0] * 3 + [0.8 * dt0] * 2
+    other = np.zeros((2 * 15 + 1, 16), complex)
+    other[20, 3] = 0.01
+
+    def run(on):
+        ctx.qg_set_graphs(on)
+        if layers == 1:
+            m = sw.QGModel.one_layer(_one_layer_case(nx), nx, 3.0, 1.0, r_drag=0.0, ctx=ctx)
+        else:
+            m = sw.QGModel.two_layer(_two_layer_case(nx, seed=11), nx, 3.0, 1.0, L=20.0, ctx=ctx)
+        for i, dt in enumerate(dts):
+            m.step(dt)
+            if i == 7:
+                ctx.set_field_qk(0, other, 32, 20.0, 3.0, 0.0, 2 * np.pi / 20.0, 64)
+        qk, t, steps = ctx.qg_get()
+        return qk, t, steps
+
+    try:
+        a = run(True)
+        b = run(False)
+    finally:
+        ctx.qg_set_graphs(False)
+    assert a[2] == b[2] == len(dts) and a[1] == b[1]
+    assert np.array_equal(np.ascontiguousarray(a[0]).view(np.uint64), np.ascontiguousarray(b[0]).view(np.uint64))

@@ -39,9 +39,11 @@ def main():
     ap.add_argument("--nsub", type=int, default=5, help="leapfrog substeps per PDE interval (5: 0.05*dx/U0 each)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ode23", action="store_true", help="also time the drivers' ode23 over one PDE interval")
+    ap.add_argument("--qg-graphs", action="store_true", help="hipGraph replay of the QG step (A/B; default off)")
     args = ap.parse_args()
     nx, L, f, Cg = args.nx, 20.0, 3.0, 1.0
     ctx = sw.Context(0)
+    ctx.qg_set_graphs(args.qg_graphs)
     rng = np.random.default_rng(5)
     q1 = initial_q(nx, L, 0.2, f / Cg, 10, 30, rng, ndgrid=True)
     qk = np.stack([ctx.g2k(q1), ctx.g2k(-q1)], axis=2)
@@ -50,7 +52,8 @@ def main():
     ens = sw.PacketEnsemble(x, k, L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * math.pi / L, nlayers=2, ctx=ctx)
     U0 = model.max_speed()
     dt = 0.25 * (L / nx) / U0
-    model.step(dt)
+    for _ in range(4):  # past the AB1/AB2 start-up; captures both replay graphs
+        model.step(dt)
     model.snapshot(0, which=1, ny_period=2 * nx)
     model.snapshot(1, which=0, ny_period=2 * nx)
     ens.advance(dt, args.nsub)  # warm-up of every kernel
@@ -93,7 +96,8 @@ def main():
     xg, kg = ens.state()
     out = {
         "metric": "driver step time, qg2layersw_raytrace loop on device (PDE + snapshots + packets)",
-        "config": {"nx": nx, "layers": 2, "packets": args.packets, "nsub": args.nsub, "steps": r},
+        "config": {"nx": nx, "layers": 2, "packets": args.packets, "nsub": args.nsub, "steps": r,
+                   "qg_graphs": args.qg_graphs},
         "pde_ms": pde, "cfl_ms": cfl, "snapshot_ms": snap, "packets_ms": pk, "step_ms": full,
         "packet_steps_per_s": args.packets * args.nsub / (full / 1e3),
         "ode23": ode,
