@@ -301,6 +301,14 @@ int swrt_qg_step(swrt_ctx* ctx, double dt, int64_t nsteps);
  * (default): plain launches, measured faster on ROCm 7 (73.5 vs 67.5 us per
  * 512^2 two-layer step).  Performance only: results are identical. */
 int swrt_qg_set_graphs(swrt_ctx* ctx, int on);
+/* 1 (default): the swrt_qg_* calls run on a second HIP stream of the
+ * context, so the next PDE step, its CFL speed and snapshot overlap the
+ * packet launch that reads the previous snapshots.  Slot reads and writes
+ * are ordered across the two streams with events; a swrt_qg_snapshot into a
+ * slot whose buffer a queued packet launch still reads writes a spare buffer
+ * instead (renaming), so it never waits for that launch.  0: one stream.
+ * Results are identical; swrt_synchronize waits for both streams. */
+int swrt_qg_set_stream(swrt_ctx* ctx, int separate);
 /* U0 = sqrt(max((u + shear)^2 + v^2)) over every layer of grid_U(qk)
  * (qg2layersw_raytrace.m:156-158; qgsw_raytrace.m:63-65 with shear 0). */
 int swrt_qg_max_speed(swrt_ctx* ctx, double* U0_out);

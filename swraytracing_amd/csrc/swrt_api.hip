@@ -68,6 +68,10 @@ struct Slot {
   bool set = false;
   bool has_psi = false;
   bool div_free = false;    // every node's v_y is exactly -u_x (five-sum kernels apply)
+  // cross-stream order (they travel with the buffers through swaps and renames):
+  hipEvent_t uev = nullptr;  // last context-stream use (packet kernels, field writes)
+  hipEvent_t wev = nullptr;  // last QG-stream write (swrt_qg_snapshot)
+  bool upend = false, wpend = false;
 };
 
 // device-resident QG PDE state (swrt_qg.hpp)
@@ -122,6 +126,13 @@ struct swrt_ctx {
   hipStream_t stream = nullptr;
   std::string err;
   Slot slot[SWRT_MAX_SLOTS];
+  // The QG PDE (swrt_qg_*) runs on its own stream so the next PDE step, its
+  // CFL speed and snapshot overlap the packet launch reading the previous
+  // snapshots.  A snapshot into a slot whose buffer a queued packet launch
+  // still reads is renamed to `spare` instead of waiting for it.
+  hipStream_t qstream = nullptr;
+  bool qg_sep = true;
+  Slot spare;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
   double* dk = nullptr;  // 2N
@@ -201,6 +212,37 @@ struct swrt_ctx {
 };
 
 namespace {
+// Run a swrt_qg_* call on the QG stream: every helper launches on c->stream.
+struct OnQGStream {
+  swrt_ctx* c;
+  hipStream_t saved;
+  explicit OnQGStream(swrt_ctx* c_) : c(c_), saved(c_->stream) {
+    if (c->qg_sep) c->stream = c->qstream;
+  }
+  ~OnQGStream() { c->stream = saved; }
+};
+
+// A context-stream call that reads or writes the field slots: wait for the
+// QG-stream snapshots written into them, then mark them used by this call.
+struct SlotUse {
+  swrt_ctx* c;
+  explicit SlotUse(swrt_ctx* c_) : c(c_) {
+    if (!c->qg_sep) return;
+    for (Slot& s : c->slot)
+      if (s.wpend) {
+        (void)hipStreamWaitEvent(c->stream, s.wev, 0);
+        s.wpend = false;
+      }
+  }
+  ~SlotUse() {
+    if (!c->qg_sep) return;
+    for (Slot& s : c->slot)
+      if (s.nodes && hipEventRecord(s.uev, c->stream) == hipSuccess) s.upend = true;
+  }
+};
+}  // namespace
+
+namespace {
 
 int fail(swrt_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -238,7 +280,10 @@ int ensure_scratch(swrt_ctx* c, size_t bytes) {
 
 int ensure_twiddles(swrt_ctx* c, int n) {
   if (c->tw_n == n) return SWRT_OK;
-  if (c->tw) (void)hipFree(c->tw);
+  if (c->tw) {
+    HIPCHK(c, hipDeviceSynchronize());  // the other stream may still read them
+    (void)hipFree(c->tw);
+  }
   c->tw = nullptr;
   std::vector<double2> h(n / 2);
   for (int k = 0; k < n / 2; ++k) {
@@ -258,6 +303,7 @@ int ensure_slot(swrt_ctx* c, int slot, int64_t nx) {
   Slot& s = c->slot[slot];
   const int64_t npad = nx + kPadTot;
   if (s.nodes && s.nx == nx) return SWRT_OK;
+  if (s.nodes) HIPCHK(c, hipDeviceSynchronize());  // a queued launch on either stream may read it
   if (s.nodes) (void)hipFree(s.nodes);
   if (s.psi) (void)hipFree(s.psi);
   s.nodes = nullptr;
@@ -658,6 +704,23 @@ int swrt_create(int device, swrt_ctx** out) {
     delete c;
     return SWRT_ERR_HIP;
   }
+  // the QG stream at the highest priority: its short dependent kernels are
+  // dispatched ahead of the waiting workgroups of a packet launch
+  int prio_least = 0, prio_greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+  const char* qp = std::getenv("SWRT_QG_PRIO");
+  const int prio = (qp && std::atoi(qp) == 0) ? prio_least : prio_greatest;
+  bool ok = hipStreamCreateWithPriority(&c->qstream, hipStreamNonBlocking, prio) == hipSuccess;
+  Slot* all[SWRT_MAX_SLOTS + 1];
+  for (int i = 0; i < SWRT_MAX_SLOTS; ++i) all[i] = &c->slot[i];
+  all[SWRT_MAX_SLOTS] = &c->spare;
+  for (Slot* s : all)
+    ok = ok && hipEventCreateWithFlags(&s->uev, hipEventDisableTiming) == hipSuccess &&
+         hipEventCreateWithFlags(&s->wev, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    swrt_destroy(c);
+    return SWRT_ERR_HIP;
+  }
   *out = c;
   return SWRT_OK;
 }
@@ -666,10 +729,15 @@ void swrt_destroy(swrt_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  for (auto& s : c->slot) {
+  if (c->qstream) (void)hipStreamSynchronize(c->qstream);
+  auto free_slot = [](Slot& s) {
     if (s.nodes) (void)hipFree(s.nodes);
     if (s.psi) (void)hipFree(s.psi);
-  }
+    if (s.uev) (void)hipEventDestroy(s.uev);
+    if (s.wev) (void)hipEventDestroy(s.wev);
+  };
+  for (auto& s : c->slot) free_slot(s);
+  free_slot(c->spare);
   for (void* p : {(void*)c->dx, (void*)c->dk, (void*)c->perm, (void*)c->dx2, (void*)c->dk2,
                   (void*)c->perm2, (void*)c->keys, (void*)c->src_idx, (void*)c->bins})
     if (p) (void)hipFree(p);
@@ -693,7 +761,8 @@ void swrt_destroy(swrt_ctx* c) {
                   (void*)c->o_ynk, (void*)c->o_dmax})
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(c->stream);
+  if (c->qstream) (void)hipStreamDestroy(c->qstream);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
@@ -704,6 +773,7 @@ int swrt_set_field_grid(swrt_ctx* c, int slot, const double* fields6, int64_t nx
   int rc = check_slot_args(c, slot, nx);
   if (rc) return rc;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   if (!fields6) return fail(c, SWRT_ERR_ARG, "fields6 is NULL");
   if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
   if (ny_period == 0) ny_period = nx;
@@ -738,6 +808,7 @@ int swrt_set_field_psi(swrt_ctx* c, int slot, const double* psi_grid, int64_t nx
   int rc = check_slot_args(c, slot, nx);
   if (rc) return rc;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   if (!psi_grid) return fail(c, SWRT_ERR_ARG, "psi_grid is NULL");
   if (!is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two for the GPU FFT");
   if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
@@ -783,6 +854,7 @@ int swrt_set_field_qk(swrt_ctx* c, int slot, const double* qk_interleaved, int64
   int rc = check_slot_args(c, slot, nx);
   if (rc) return rc;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   if (!qk_interleaved) return fail(c, SWRT_ERR_ARG, "qk is NULL");
   if (!is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two for the GPU FFT");
   if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
@@ -889,6 +961,7 @@ int swrt_field_div_free(swrt_ctx* c, int slot) {
 int swrt_get_field_grid(swrt_ctx* c, int slot, double* out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   if (slot < 0 || slot >= SWRT_MAX_SLOTS || !c->slot[slot].set)
     return fail(c, SWRT_ERR_STATE, "slot not set");
   if (!out) return fail(c, SWRT_ERR_ARG, "out is NULL");
@@ -909,6 +982,7 @@ int swrt_get_field_grid(swrt_ctx* c, int slot, double* out) {
 int swrt_get_psi_grid(swrt_ctx* c, int slot, double* out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   if (slot < 0 || slot >= SWRT_MAX_SLOTS || !c->slot[slot].set || !c->slot[slot].has_psi)
     return fail(c, SWRT_ERR_STATE, "slot has no psi grid (use swrt_set_field_psi)");
   if (!out) return fail(c, SWRT_ERR_ARG, "out is NULL");
@@ -955,6 +1029,7 @@ int swrt_eval(swrt_ctx* c, const double* x, const double* y, int64_t n, int nslo
               double bump, double* out6) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   if (n < 0) return fail(c, SWRT_ERR_ARG, "n < 0");
   if (n == 0) return SWRT_OK;
   if (!x || !y || !out6) return fail(c, SWRT_ERR_ARG, "NULL buffer");
@@ -1108,6 +1183,7 @@ int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, in
                  double alpha0, double dalpha, double bump, int64_t save_every) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   if (nsteps < 0) return fail(c, SWRT_ERR_ARG, "nsteps < 0");
   if (nslots != 1 && nslots != 2) return fail(c, SWRT_ERR_ARG, "nslots must be 1 or 2");
   if (save_every < 0) return fail(c, SWRT_ERR_ARG, "save_every < 0");
@@ -1469,6 +1545,16 @@ int swrt_synchronize(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->qstream));
+  return SWRT_OK;
+}
+
+int swrt_qg_set_stream(swrt_ctx* c, int separate) {
+  if (!c) return SWRT_ERR_ARG;
+  if (separate != 0 && separate != 1) return fail(c, SWRT_ERR_ARG, "separate must be 0 or 1");
+  int rc = swrt_synchronize(c);
+  if (rc) return rc;
+  c->qg_sep = separate != 0;
   return SWRT_OK;
 }
 
@@ -1504,6 +1590,7 @@ int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches
 int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double* qk_in) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   if (!p || !qk_in) return fail(c, SWRT_ERR_ARG, "NULL argument");
   if (p->nlayers != 1 && p->nlayers != 2) return fail(c, SWRT_ERR_ARG, "nlayers must be 1 or 2");
   if (nx < 8 || nx > 4096 || !is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two, 8..4096");
@@ -1634,6 +1721,7 @@ int qg_step_graphed(swrt_ctx* c, double dt) {
 int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   if (!(dt > 0) || nsteps < 0) return fail(c, SWRT_ERR_ARG, "dt must be > 0, nsteps >= 0");
@@ -1696,6 +1784,7 @@ int qg_speed_wait(swrt_ctx* c, double* U0_out) {
 int swrt_qg_max_speed(swrt_ctx* c, double* U0_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   if (!U0_out) return fail(c, SWRT_ERR_ARG, "NULL output");
@@ -1709,6 +1798,7 @@ int swrt_qg_max_speed(swrt_ctx* c, double* U0_out) {
 int swrt_qg_max_speed_async(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   if (!c->qg.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   HIPCHK(c, hipSetDevice(c->device));
   return qg_speed_launch(c);
@@ -1718,6 +1808,7 @@ int swrt_qg_max_speed_async(swrt_ctx* c) {
 int swrt_qg_max_speed_result(swrt_ctx* c, double* U0_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   if (!c->qg.speed_pending) return fail(c, SWRT_ERR_STATE, "no swrt_qg_max_speed_async pending");
   if (!U0_out) return fail(c, SWRT_ERR_ARG, "NULL output");
   return qg_speed_wait(c, U0_out);
@@ -1727,6 +1818,7 @@ int swrt_qg_max_speed_result(swrt_ctx* c, double* U0_out) {
 int swrt_qg_get(swrt_ctx* c, double* qk_out, double* t_out, int64_t* steps_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1748,6 +1840,7 @@ int swrt_qg_get(swrt_ctx* c, double* qk_out, double* t_out, int64_t* steps_out) 
 int swrt_qg_get_q(swrt_ctx* c, double* q_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   if (!q_out) return fail(c, SWRT_ERR_ARG, "NULL output");
@@ -1774,6 +1867,7 @@ int swrt_qg_get_q(swrt_ctx* c, double* q_out) {
 int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_period) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (current) or 1 (previous)");
@@ -1785,6 +1879,15 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   if (ny_period == 0) ny_period = nx;
   if (ny_period % nx) return fail(c, SWRT_ERR_ARG, "ny_period must be a multiple of nx");
   HIPCHK(c, hipSetDevice(c->device));
+  if (c->qg_sep) {
+    // rename a buffer still read by a queued packet launch, else wait for its last use
+    if (c->slot[slot].upend) {
+      const hipError_t e = hipEventQuery(c->slot[slot].uev);
+      (void)hipGetLastError();  // hipErrorNotReady is a status, not an error
+      if (e == hipErrorNotReady) std::swap(c->slot[slot], c->spare);
+    }
+    if (c->slot[slot].upend) HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot[slot].uev, 0));
+  }
   if ((rc = ensure_slot(c, slot, nx))) return rc;
   if ((rc = ensure_twiddles(c, (int)nx))) return rc;
   const double2* src = (which == 0 ? q.qk : q.qk_prev) + layer * q.nhalf;
@@ -1795,6 +1898,10 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   s.L = q.g.dx * (double)nx;
   s.ny_period = ny_period;
   s.set = true;
+  if (c->qg_sep) {
+    HIPCHK(c, hipEventRecord(s.wev, c->stream));
+    s.wpend = true;
+  }
   c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
@@ -1918,6 +2025,7 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
                   double* rh_raw_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   // one spatial re-binning per ode23 call (the packet order is free: the
@@ -1939,6 +2047,7 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
                        int nslots, double thr, double bump, double* err_raw_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  SlotUse slot_use(c);
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   Ode23Args a;

@@ -282,3 +282,23 @@ def test_qg_graph_replay_bit_identical(ctx, layers):
         ctx.qg_set_graphs(False)
     assert a[2] == b[2] == len(dts) and a[1] == b[1]
     assert np.array_equal(np.ascontiguousarray(a[0]).view(np.uint64), np.ascontiguousarray(b[0]).view(np.uint64))
+
+
+def test_qg_stream_overlap_bit_identical(ctx, tmp_path):
+    """The QG PDE on its own stream (swrt_qg_set_stream, default) with
+    snapshot renaming gives the same packets, frames and PV as one stream."""
+    nx, N = 128, 200_000  # packet launches long enough that snapshots meet in-flight reads
+
+    def run(separate, d):
+        ctx.qg_set_stream(separate)
+        d.mkdir()
+        sw.qg2layersw_raytrace(nx, N, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=2, max_steps=30,
+                               seed=5, ctx=ctx)
+        return [open(d / name, "rb").read() for name in ("packet_x.bin", "packet_k.bin", "pv.bin")]
+
+    try:
+        a = run(True, tmp_path / "two")
+        b = run(False, tmp_path / "one")
+    finally:
+        ctx.qg_set_stream(True)
+    assert all(len(u) > 0 and u == v for u, v in zip(a, b))
