@@ -309,6 +309,13 @@ int swrt_qg_set_graphs(swrt_ctx* ctx, int on);
  * instead (renaming), so it never waits for that launch.  0: one stream.
  * Results are identical; swrt_synchronize waits for both streams. */
 int swrt_qg_set_stream(swrt_ctx* ctx, int separate);
+/* 1 (default): the transforms every consumer of a new qk needs — the next
+ * step's Jacobian, the CFL speed (swrt_qg_max_speed*) and layer 0's grid_U
+ * for swrt_qg_snapshot(which 0, layer 0) — come from ONE batched inverse
+ * 2-D FFT of the current qk, computed once on first use.  0: each call runs
+ * its own transforms.  The same spectra and per-vector FFTs either way:
+ * results are bit-identical. */
+int swrt_qg_set_fused(swrt_ctx* ctx, int on);
 /* U0 = sqrt(max((u + shear)^2 + v^2)) over every layer of grid_U(qk)
  * (qg2layersw_raytrace.m:156-158; qgsw_raytrace.m:63-65 with shear 0). */
 int swrt_qg_max_speed(swrt_ctx* ctx, double* U0_out);

@@ -84,6 +84,7 @@ SIGNATURES = {
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_set_graphs": (_INT, [_VP, _INT]),
     "swrt_qg_set_stream": (_INT, [_VP, _INT]),
+    "swrt_qg_set_fused": (_INT, [_VP, _INT]),
     "swrt_qg_max_speed": (_INT, [_VP, ctypes.POINTER(_D)]),
     "swrt_qg_max_speed_async": (_INT, [_VP]),
     "swrt_qg_max_speed_result": (_INT, [_VP, ctypes.POINTER(_D)]),
@@ -398,6 +399,10 @@ class Context:
     def qg_set_stream(self, separate=True):
         """QG PDE on its own stream, overlapping the packet launches (swrt_qg_set_stream)."""
         self._chk(self._L.swrt_qg_set_stream(self._h, int(bool(separate))), "swrt_qg_set_stream")
+
+    def qg_set_fused(self, on=True):
+        """One batched transform per qk for the step, CFL speed and snapshot (swrt_qg_set_fused)."""
+        self._chk(self._L.swrt_qg_set_fused(self._h, int(bool(on))), "swrt_qg_set_fused")
 
     def qg_max_speed(self):
         u = _D()

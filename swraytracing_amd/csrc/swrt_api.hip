@@ -91,6 +91,13 @@ struct QGState {
   double* hmax = nullptr;      // pinned host copy of dmax (async CFL read-back)
   hipEvent_t ev = nullptr;     // recorded after that copy
   bool speed_pending = false;
+  // fused mode: the post-step transforms of the current qk — the next step's
+  // Jacobian spectrum (PT[0, nn) after its forward FFT), the CFL speed
+  // (dmax) and layer 0's grid_U (the snapshot) — from ONE batched inverse
+  // 2-D FFT, computed once per qk on first use
+  double2* PZ = nullptr;
+  double2* PT = nullptr;
+  bool post_valid = false;
   double exp_dt = -1.0;        // dt of the current E1/E2
   // replayable AB3 steps (hipGraph), one per qk buffer parity, for one dt
   hipGraphExec_t gexec[2] = {nullptr, nullptr};
@@ -132,6 +139,7 @@ struct swrt_ctx {
   // still reads is renamed to `spare` instead of waiting for it.
   hipStream_t qstream = nullptr;
   bool qg_sep = true;
+  bool qg_fused = true;  // swrt_qg_set_fused
   Slot spare;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
@@ -751,7 +759,8 @@ void swrt_destroy(swrt_ctx* c) {
                   (void*)c->mode_rows})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->qg.qk, (void*)c->qg.qk_prev, (void*)c->qg.Qm1, (void*)c->qg.Qm2, (void*)c->qg.E1,
-                  (void*)c->qg.E2, (void*)c->qg.Z, (void*)c->qg.T, (void*)c->qg.dmax})
+                  (void*)c->qg.E2, (void*)c->qg.Z, (void*)c->qg.T, (void*)c->qg.dmax, (void*)c->qg.PZ,
+                  (void*)c->qg.PT})
     if (p) (void)hipFree(p);
   if (c->qg.hmax) (void)hipHostFree(c->qg.hmax);
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
@@ -1549,6 +1558,16 @@ int swrt_synchronize(swrt_ctx* c) {
   return SWRT_OK;
 }
 
+int swrt_qg_set_fused(swrt_ctx* c, int on) {
+  if (!c) return SWRT_ERR_ARG;
+  if (on != 0 && on != 1) return fail(c, SWRT_ERR_ARG, "on must be 0 or 1");
+  int rc = swrt_synchronize(c);
+  if (rc) return rc;
+  c->qg_fused = on != 0;
+  c->qg.post_valid = false;
+  return SWRT_OK;
+}
+
 int swrt_qg_set_stream(swrt_ctx* c, int separate) {
   if (!c) return SWRT_ERR_ARG;
   if (separate != 0 && separate != 1) return fail(c, SWRT_ERR_ARG, "separate must be 0 or 1");
@@ -1598,7 +1617,7 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
   HIPCHK(c, hipSetDevice(c->device));
   QGState& q = c->qg;
   for (void* ptr : {(void*)q.qk, (void*)q.qk_prev, (void*)q.Qm1, (void*)q.Qm2, (void*)q.E1, (void*)q.E2,
-                    (void*)q.Z, (void*)q.T, (void*)q.dmax})
+                    (void*)q.Z, (void*)q.T, (void*)q.dmax, (void*)q.PZ, (void*)q.PT})
     if (ptr) (void)hipFree(ptr);
   if (q.hmax) (void)hipHostFree(q.hmax);
   if (q.ev) (void)hipEventDestroy(q.ev);
@@ -1653,6 +1672,21 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
 }
 
 namespace {
+// fused g2k crop + AB3 update from the forward-transformed Jacobian F into
+// qk_prev (out of place: the new qk goes to the other buffer, the old one
+// becomes prev_qk)
+int qg_update_launch(swrt_ctx* c, double dt, int abstep, const double2* F) {
+  QGState& q = c->qg;
+  if (q.g.nl == 2)
+    hipLaunchKernelGGL(qg_update_kernel<2>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, F, q.g, dt,
+                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+  else
+    hipLaunchKernelGGL(qg_update_kernel<1>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, F, q.g, dt,
+                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+
 // The kernel sequence of one QG step (update of qgsw_raytrace.m:270-286 /
 // qg2layersw_raytrace.m:309-323 + the AB3 step): spectra -> inverse 2-D FFT ->
 // Jacobian -> forward 2-D FFT -> fused g2k crop + AB3 update into qk_prev.
@@ -1672,14 +1706,50 @@ int qg_step_launches(swrt_ctx* c, double dt, int abstep) {
   if ((rc = run_fft_pass(c, Zj, n, 1, 0))) return rc;   // along x
   if ((rc = run_transpose(c, Zj, q.T, n, 1))) return rc;
   if ((rc = run_fft_pass(c, q.T, n, 1, 0))) return rc;  // along y: [ky + n*kx]
-  // out of place: the new qk goes to the other buffer, the old one becomes prev_qk
-  if (nl == 2)
-    hipLaunchKernelGGL(qg_update_kernel<2>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
-                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
-  else
-    hipLaunchKernelGGL(qg_update_kernel<1>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, q.T, q.g, dt,
-                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+  return qg_update_launch(c, dt, abstep, q.T);
+}
+
+// Post-step transforms of the current qk (fused mode), see QGState::PZ.
+// Every transform is the one the unfused calls make (same spectra kernels,
+// same per-vector FFT), so results are bit-identical to them.
+int qg_post(swrt_ctx* c) {
+  QGState& q = c->qg;
+  if (q.post_valid) return SWRT_OK;
+  const int n = q.g.n, nl = q.g.nl;
+  const int nb = 2 * nl + (nl - 1) + 3;  // Jacobian inputs | layer-1 u+iv | layer-0 grid_U (u+iv first)
+  if (!q.PZ) {
+    HIPCHK(c, hipMalloc(&q.PZ, sizeof(double2) * nb * q.nn));
+    HIPCHK(c, hipMalloc(&q.PT, sizeof(double2) * nb * q.nn));
+  }
+  int rc;
+  if ((rc = ensure_twiddles(c, n))) return rc;
+  const dim3 grid((unsigned)nblocks(q.nn, 256)), block(256);
+  double2* uv = q.PZ + 2 * nl * q.nn;
+  if (nl == 2) {
+    hipLaunchKernelGGL(qg_jac_spectra_kernel<2>, grid, block, 0, c->stream, q.qk, q.g, q.PZ);
+    hipLaunchKernelGGL(qg_vel_spectra_kernel<1>, grid, block, 0, c->stream, (const double2*)(q.qk + q.nhalf), q.g,
+                       uv);
+  } else {
+    hipLaunchKernelGGL(qg_jac_spectra_kernel<1>, grid, block, 0, c->stream, q.qk, q.g, q.PZ);
+  }
   HIPCHK(c, hipGetLastError());
+  // swrt_qg_snapshot(which 0, layer 0)'s spectra: grid_U.m inversion, ky-fastest half plane
+  hipLaunchKernelGGL(spectra_kernel, grid, block, 0, c->stream, (const double2*)q.qk, n, 1, q.g.K_d2, q.g.kscale, 0,
+                     uv + (nl - 1) * q.nn, n / 2, 1);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
+  // CFL speed over every layer's u + i v (layer 1, then layer 0: contiguous)
+  HIPCHK(c, hipMemsetAsync(q.dmax, 0, sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(qg_max_speed2_kernel, dim3(256), dim3(256), 0, c->stream, (const double2*)(q.PT + 2 * nl * q.nn),
+                     q.nn * nl, q.g.shear, q.dmax);
+  HIPCHK(c, hipGetLastError());
+  // Jacobian -> forward 2-D FFT; the spectrum lands in PT[0, nn) (psi_x of layer 0 is dead)
+  hipLaunchKernelGGL(qg_jacobian_kernel, grid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = run_fft_pass(c, q.PZ, n, 1, 0))) return rc;
+  if ((rc = run_transpose(c, q.PZ, q.PT, n, 1))) return rc;
+  if ((rc = run_fft_pass(c, q.PT, n, 1, 0))) return rc;
+  q.post_valid = true;
   return SWRT_OK;
 }
 
@@ -1736,11 +1806,16 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
       q.exp_dt = dt;
     }
     const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
-    if (abstep == 3 && c->qg_graphs)
+    if (c->qg_fused) {
+      if ((rc = qg_post(c))) return rc;
+      rc = qg_update_launch(c, dt, abstep, q.PT);
+    } else if (abstep == 3 && c->qg_graphs) {
       rc = qg_step_graphed(c, dt);
-    else
+    } else {
       rc = qg_step_launches(c, dt, abstep);
+    }
     if (rc) return rc;
+    q.post_valid = false;
     std::swap(q.qk, q.qk_prev);
     q.steps += 1;
     q.t = q.t + dt;
@@ -1756,6 +1831,13 @@ int qg_speed_launch(swrt_ctx* c) {
   QGState& q = c->qg;
   int rc;
   const int n = q.g.n, nl = q.g.nl;
+  if (c->qg_fused) {  // the speed comes with the post-step transforms
+    if ((rc = qg_post(c))) return rc;
+    HIPCHK(c, hipMemcpyAsync(q.hmax, q.dmax, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipEventRecord(q.ev, c->stream));
+    q.speed_pending = true;
+    return SWRT_OK;
+  }
   if ((rc = ensure_twiddles(c, n))) return rc;
   if (nl == 2)
     hipLaunchKernelGGL(qg_vel_spectra_kernel<2>, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
@@ -1763,6 +1845,7 @@ int qg_speed_launch(swrt_ctx* c) {
     hipLaunchKernelGGL(qg_vel_spectra_kernel<1>, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
   HIPCHK(c, hipGetLastError());
   if ((rc = inverse_2d(c, q.Z, q.T, n, nl))) return rc;
+  q.post_valid = false;  // dmax is overwritten
   HIPCHK(c, hipMemsetAsync(q.dmax, 0, sizeof(unsigned long long), c->stream));
   hipLaunchKernelGGL(qg_max_speed2_kernel, dim3(256), dim3(256), 0, c->stream, q.T, q.nn * nl, q.g.shear, q.dmax);
   HIPCHK(c, hipGetLastError());
@@ -1890,11 +1973,26 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   }
   if ((rc = ensure_slot(c, slot, nx))) return rc;
   if ((rc = ensure_twiddles(c, (int)nx))) return rc;
-  const double2* src = (which == 0 ? q.qk : q.qk_prev) + layer * q.nhalf;
-  if ((rc = fields_from_halfplane(c, slot, src, (int)nx, 1, q.g.K_d2, q.g.kscale, q.g.shear, 0, q.Z, q.T,
-                                  (int)(nx / 2), 1)))
-    return rc;
   Slot& s = c->slot[slot];
+  if (c->qg_fused && which == 0 && layer == 0 && nx % 16 == 0) {
+    // layer 0's grid_U of the current qk is part of the post-step transforms
+    if ((rc = qg_post(c))) return rc;
+    const double2* T = q.PT + (3 * q.g.nl - 1) * q.nn;
+    hipLaunchKernelGGL(pack_pairs_kernel, dim3(nx / 16, nx / 16), dim3(256), 0, c->stream, T, (int)nx, (int)s.npad,
+                       q.g.shear, s.nodes);
+    HIPCHK(c, hipGetLastError());
+    const int64_t ghosts = 2 * (int64_t)(s.npad - nx) * s.npad;
+    hipLaunchKernelGGL(halo_nodes_kernel, dim3(nblocks(ghosts, 256)), dim3(256), 0, c->stream, s.nodes, (int)nx,
+                       (int)s.npad);
+    HIPCHK(c, hipGetLastError());
+    s.has_psi = false;
+    s.div_free = true;
+  } else {
+    const double2* src = (which == 0 ? q.qk : q.qk_prev) + layer * q.nhalf;
+    if ((rc = fields_from_halfplane(c, slot, src, (int)nx, 1, q.g.K_d2, q.g.kscale, q.g.shear, 0, q.Z, q.T,
+                                    (int)(nx / 2), 1)))
+      return rc;
+  }
   s.L = q.g.dx * (double)nx;
   s.ny_period = ny_period;
   s.set = true;

@@ -264,6 +264,7 @@ def test_qg_graph_replay_bit_identical(ctx, layers):
 
     def run(on):
         ctx.qg_set_graphs(on)
+        ctx.qg_set_fused(False)  # graphs replay the unfused step
         if layers == 1:
             m = sw.QGModel.one_layer(_one_layer_case(nx), nx, 3.0, 1.0, r_drag=0.0, ctx=ctx)
         else:
@@ -280,25 +281,62 @@ def test_qg_graph_replay_bit_identical(ctx, layers):
         b = run(False)
     finally:
         ctx.qg_set_graphs(False)
+        ctx.qg_set_fused(True)
     assert a[2] == b[2] == len(dts) and a[1] == b[1]
     assert np.array_equal(np.ascontiguousarray(a[0]).view(np.uint64), np.ascontiguousarray(b[0]).view(np.uint64))
 
 
-def test_qg_stream_overlap_bit_identical(ctx, tmp_path):
-    """The QG PDE on its own stream (swrt_qg_set_stream, default) with
-    snapshot renaming gives the same packets, frames and PV as one stream."""
-    nx, N = 128, 200_000  # packet launches long enough that snapshots meet in-flight reads
-
-    def run(separate, d):
-        ctx.qg_set_stream(separate)
-        d.mkdir()
-        sw.qg2layersw_raytrace(nx, N, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=2, max_steps=30,
+def _driver_files(ctx, d, layers, separate, fused):
+    ctx.qg_set_stream(separate)
+    ctx.qg_set_fused(fused)
+    d.mkdir()
+    if layers == 2:
+        sw.qg2layersw_raytrace(128, 200_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=2, max_steps=30,
                                seed=5, ctx=ctx)
-        return [open(d / name, "rb").read() for name in ("packet_x.bin", "packet_k.bin", "pv.bin")]
+    else:
+        sw.qgsw_raytrace(64, 50_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=2, max_steps=12,
+                         seed=146, r_drag=0.0, ctx=ctx)
+    return [open(d / name, "rb").read() for name in ("packet_x.bin", "packet_k.bin", "pv.bin", "packet_time.bin")]
 
+
+@pytest.mark.parametrize("layers", [1, 2])
+def test_qg_stream_overlap_and_fusion_bit_identical(ctx, tmp_path, layers):
+    """The QG PDE on its own stream with snapshot renaming
+    (swrt_qg_set_stream) and the fused post-step transforms
+    (swrt_qg_set_fused), both defaults, give the same packets, frames, PV and
+    frame times (the CFL dt sequence) as one stream without fusion.  The
+    2-layer case has packet launches long enough that snapshots meet
+    in-flight reads."""
     try:
-        a = run(True, tmp_path / "two")
-        b = run(False, tmp_path / "one")
+        ref = _driver_files(ctx, tmp_path / "plain", layers, False, False)
+        for sep, fused in [(True, True), (True, False), (False, True)]:
+            got = _driver_files(ctx, tmp_path / f"s{int(sep)}f{int(fused)}", layers, sep, fused)
+            assert all(len(u) > 0 and u == v for u, v in zip(got, ref)), (sep, fused)
     finally:
         ctx.qg_set_stream(True)
-    assert all(len(u) > 0 and u == v for u, v in zip(a, b))
+        ctx.qg_set_fused(True)
+
+
+def test_qg_fused_speed_and_snapshot_match_unfused(ctx):
+    """U0 and the layer-0 snapshot of the current qk from the post-step
+    transforms equal the separate calls' bit for bit (2 layers, AB3 steps)."""
+    nx = 64
+    out = {}
+    try:
+        for fused in (False, True):
+            ctx.qg_set_fused(fused)
+            m = sw.QGModel.two_layer(_two_layer_case(nx, seed=11), nx, 3.0, 1.0, L=20.0, ctx=ctx)
+            dt = 0.25 * (20.0 / nx) / m.max_speed()
+            for _ in range(4):
+                m.step(dt)
+            U0 = m.max_speed()
+            m.snapshot(0, which=0, ny_period=2 * nx)
+            m.step(dt)
+            m.snapshot(1, which=0, ny_period=2 * nx)
+            out[fused] = (U0, m.max_speed(), ctx.get_field_grid(0, nx), ctx.get_field_grid(1, nx), m.qk)
+    finally:
+        ctx.qg_set_fused(True)
+    a, b = out[False], out[True]
+    assert a[0] == b[0] and a[1] == b[1]
+    for u, v in zip(a[2:], b[2:]):
+        assert np.array_equal(np.ascontiguousarray(u).view(np.uint64), np.ascontiguousarray(v).view(np.uint64))
