@@ -79,6 +79,12 @@ def build_workload(ctx, args, rng):
     ctx.set_field_qk(0, qk1, nx, L, K_d2, shear, ks, 2 * nx)
     if nslots == 2:
         ctx.set_field_qk(1, qk2, nx, L, K_d2, shear, ks, 2 * nx)
+        # --intervals K: the later snapshots of K consecutive PDE intervals, each
+        # a further small phase rotation of the previous one
+        qk = qk2
+        for s in range(2, getattr(args, "intervals", 1) + 1):
+            qk = qk * np.exp(1j * rng2.normal(0, 0.05, qk.shape))
+            ctx.set_field_qk(s, qk, nx, L, K_d2, shear, ks, 2 * nx)
     p = ctx.get_field_grid(0, nx)
     U0 = math.sqrt(float((p[0] ** 2 + p[1] ** 2).max()))
     dt = 0.25 * (L / nx) / U0  # qg2layersw_raytrace.m:31,78
@@ -96,11 +102,17 @@ def build_workload(ctx, args, rng):
     else:
         x = L * rng.random((N, 2)) - L / 2
     return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
-                K_d2=K_d2, ks=ks, shear=shear)
+                K_d2=K_d2, ks=ks, shear=shear, intervals=getattr(args, "intervals", 1) if nslots == 2 else 1)
 
 
 def step(ctx, w, sub):
+    """One bench step: `intervals` PDE intervals of `sub` leapfrog steps
+    (interval i blends snapshots i, i+1; one call, swrt_advance_intervals)."""
     h = w["dt"] / sub
+    if w.get("intervals", 1) > 1:
+        ctx.advance_intervals([h] * w["intervals"], sub, w["f"], w["gH"], alpha0=0.5 / sub, dalpha=1.0 / sub,
+                              bump=sw.BUMP_QG)
+        return
     ctx.advance(h, sub, w["f"], w["gH"], nslots=w["nslots"], alpha0=0.5 / sub, dalpha=1.0 / sub,
                 bump=sw.BUMP_QG)
 
@@ -173,6 +185,8 @@ def main():
     ap.add_argument("--packets", type=int, default=1_000_000, help="packets per GPU (weak scaling)")
     ap.add_argument("--substeps", type=int, default=5,
                     help="leapfrog steps per bench step (PDE interval 0.25*dx/U0; 5 -> 0.05*dx/U0 per step)")
+    ap.add_argument("--intervals", type=int, default=1,
+                    help="PDE intervals per bench step, one call (swrt_advance_intervals; up to 4 per launch)")
     ap.add_argument("--mode", choices=["blend", "steady"], default="blend")
     ap.add_argument("--seed", type=int, default=146)
     ap.add_argument("--positions", choices=["uniform", "stratified"], default="uniform",
@@ -253,14 +267,18 @@ def main():
         gathered = None if full is None else bool(np.isfinite(full).all() and full.shape[0] == args.packets * world)
 
     N = args.packets
-    total_ps = N * world * args.substeps * args.steps
+    ivs = w["intervals"]
+    total_ps = N * world * args.substeps * ivs * args.steps
     value = total_ps / elapsed
     B = BYTES_BLEND if w["nslots"] == 2 else BYTES_STEADY
     # sampled HIP-event time of the packet kernel; without samples fall back to wall time per step
     avg_launch_s = (kms / 1e3) / launches if launches > 0 else elapsed / args.steps
     # packet-steps per launch: a call's substeps run as launches of at most
     # `rebin_every` steps, cut at the re-binning points (swrt_advance)
-    if args.rebin_every <= 0 or args.rebin_every % args.substeps == 0:
+    if ivs > 1 and args.rebin_every > 0 and args.rebin_every % args.substeps == 0 and args.kernel in (0, 2):
+        # whole intervals per launch, up to 4, never across a re-binning
+        steps_per_launch = args.substeps * min(ivs, 4, args.rebin_every // args.substeps)
+    elif args.rebin_every <= 0 or args.rebin_every % args.substeps == 0:
         steps_per_launch = min(args.substeps, 64)
     elif args.substeps % args.rebin_every == 0:
         steps_per_launch = args.rebin_every
@@ -269,7 +287,7 @@ def main():
     ps_per_launch = N * steps_per_launch
     achieved_gbs = ps_per_launch * B / avg_launch_s / 1e9
     # fp64 VALU work per packet-step of the exact-order stencil
-    key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}"
+    key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}" + (f"_iv{ivs}" if ivs > 1 else "")
     traffic = load_traffic(key)
     valu = load_valu(key)
     valu_roofline = None
@@ -284,7 +302,8 @@ def main():
                          "source": "profiles/valu.json (rocprofv3 PMC)"}
     workload = ("qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
                 f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, {args.nx}^2x2 field, {N} packets/GPU, "
-                f"leapfrog dt {0.25 / args.substeps:g}*dx/U0 ({args.substeps} per PDE interval)")
+                f"leapfrog dt {0.25 / args.substeps:g}*dx/U0 ({args.substeps} per PDE interval)"
+                + (f", {ivs} PDE intervals per call" if ivs > 1 else ""))
     out = {
         "metric": "packet-steps/sec @ 512² field, 1e6 packets; 1/2/4/8-GPU scaling",
         "value": value,
@@ -292,7 +311,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": elapsed / args.steps * 1e3,  # one step = `intervals` PDE intervals
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -301,7 +320,7 @@ def main():
         "config": {"workload": workload,
                    "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
                    "pde_dt": "0.25*dx/U0", "leapfrog_dt": f"{0.25 / args.substeps:g}*dx/U0",
-                   "steps_per_launch": steps_per_launch,
+                   "steps_per_launch": steps_per_launch, "intervals_per_step": ivs,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "tail_quarters": args.tail_quarters, "positions": args.positions,
                    "parallelism": f"packets sharded x{world}, field replicated"},

@@ -36,7 +36,8 @@ extern "C" {
 #define SWRT_ERR_STATE 3 /* call out of order (e.g. field not set) */
 #define SWRT_ERR_ALLOC 4 /* allocation failure */
 
-#define SWRT_MAX_SLOTS 2 /* snapshot slots: 0 = flow1 / steady, 1 = flow2 */
+#define SWRT_MAX_SLOTS 5 /* snapshot slots: 0 = flow1 / steady, 1 = flow2; 2..4 the later
+                            snapshots of swrt_advance_intervals */
 
 typedef struct swrt_ctx swrt_ctx;
 
@@ -177,6 +178,21 @@ int swrt_set_blend_mode(swrt_ctx* ctx, int mode);
  * buffer, see swrt_history_*). */
 int swrt_advance(swrt_ctx* ctx, double dt, int64_t nsteps, double f, double gH, int nslots,
                  double alpha0, double dalpha, double bump, int64_t save_every);
+
+/* nintervals consecutive PDE intervals in one call: interval i advances the
+ * packets nsub leapfrog steps of size dts[i], blending slots i and i+1 with
+ * alpha = alpha0 + s*dalpha (s = step within the interval) — exactly
+ * nintervals swrt_advance(dts[i], nsub, ..., nslots 2) calls with slots
+ * (i, i+1) moved to (0, 1) in turn, bit for bit.  Slots 0..nintervals must
+ * be set on one grid; nintervals <= SWRT_MAX_SLOTS - 1; save_every (0 = no
+ * history) divides nsub.  With the LDS-tiled kernel and re-binning every
+ * multiple of nsub steps, up to 4 intervals run in ONE launch (each
+ * workgroup re-stages its window between them), so the launch's tail and the
+ * in-tile sort are paid once per 4 intervals instead of once per interval.
+ * (The drivers' packet branch over several PDE steps: qgsw_raytrace.m:140-151,
+ * qg2layersw_raytrace.m:185-197 with the snapshots of the PDE run ahead.) */
+int swrt_advance_intervals(swrt_ctx* ctx, int nintervals, const double* dts, int64_t nsub, double f, double gH,
+                           double alpha0, double dalpha, double bump, int64_t save_every);
 
 /* History frames recorded by swrt_advance since the last swrt_history_reset. */
 int64_t swrt_history_frames(const swrt_ctx* ctx);

@@ -67,6 +67,7 @@ SIGNATURES = {
     "swrt_set_tail_split": (_INT, [_VP, _INT, _INT]),
     "swrt_set_blend_mode": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
+    "swrt_advance_intervals": (_INT, [_VP, _INT, _VP, _I, _D, _D, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
     "swrt_history_get": (_INT, [_VP, _I, _I, _P, _P]),
     "swrt_history_reset": (_INT, [_VP]),
@@ -277,6 +278,14 @@ class Context:
         self._chk(self._L.swrt_advance(self._h, float(dt), int(nsteps), float(f), float(gH), int(nslots),
                                        float(alpha0), float(dalpha), float(bump), int(save_every)),
                   "swrt_advance")
+
+    def advance_intervals(self, dts, nsub, f, gH, alpha0=0.0, dalpha=0.0, bump=1e-13, save_every=0):
+        """len(dts) PDE intervals of nsub steps, interval i blending slots i, i+1
+        (swrt_advance_intervals)."""
+        d = np.ascontiguousarray(dts, dtype=np.float64)
+        self._chk(self._L.swrt_advance_intervals(self._h, int(d.size), _p(d), int(nsub), float(f), float(gH),
+                                                 float(alpha0), float(dalpha), float(bump), int(save_every)),
+                  "swrt_advance_intervals")
 
     def history(self, first=0, count=None):
         n = self._L.swrt_packets_count(self._h)

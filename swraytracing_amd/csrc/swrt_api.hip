@@ -436,7 +436,14 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
 }
 
 bool use_tile_kernel(const swrt_ctx* c);
-int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next);
+// the intervals of one multi-interval tile launch (swrt_advance_intervals)
+struct IvLaunch {
+  int nint;
+  FieldView views[kMaxIntervals + 1];
+  double dts[kMaxIntervals];
+  bool div_free;
+};
+int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch* iv = nullptr);
 
 // Launch a packet kernel on the context stream; inside a timed launch the
 // start/stop events take the kernel's own begin/end timestamps.
@@ -446,10 +453,10 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
 }
 
 // Time every timing_every-th leapfrog launch with a pair of HIP events.
-int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next) {
+int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next, const IvLaunch* iv = nullptr) {
   const bool timed = c->timing_every > 0 && (c->launch_count++ % c->timing_every) == 0;
   if (!timed) {
-    if (use_tile_kernel(c)) return tile_launch(c, a, count_next);
+    if (use_tile_kernel(c)) return tile_launch(c, a, count_next, iv);
     c->keys_fresh = false;
     if (a.nslots == 2)
       hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
@@ -481,7 +488,7 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next)
   c->timing.used += 2;
   int rc = SWRT_OK;
   if (use_tile_kernel(c)) {
-    rc = tile_launch(c, a, count_next);
+    rc = tile_launch(c, a, count_next, iv);
   } else {
     c->keys_fresh = false;
     if (a.nslots == 2)
@@ -573,14 +580,20 @@ int rebin(swrt_ctx* c, bool indirect) {
   return SWRT_OK;
 }
 
-int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
+int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch* iv) {
   TileArgs t;
   t.s = a;
+  t.ivmode = iv != nullptr;
+  t.nint = iv ? iv->nint : 1;
+  if (iv) {
+    for (int i = 0; i <= iv->nint; ++i) t.ivn[i] = iv->views[i].nodes;
+    for (int i = 0; i < iv->nint; ++i) t.ivdt[i] = iv->dts[i];
+  }
   t.x_out = c->dx2;
   t.k_out = c->dk2;
   t.perm_out = c->perm2;
   t.starts = c->bins + 2 * kMaxBins;
-  t.ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  t.ntx = (int)((a.f0.nx + kTile - 1) / kTile);
   const unsigned grid = (unsigned)(t.ntx * t.ntx);
   // half-tile workgroups at the end of each XCD band (swrt_tile.hpp wg_work)
   unsigned extra = 0;
@@ -620,7 +633,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
   } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
     launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(wgrid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
-    if (c->slot[0].div_free && c->slot[1].div_free)
+    if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free))
       launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
                dim3(kTileThreads), t);
     else
@@ -642,10 +655,10 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next) {
 }
 
 int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int nslots,
-                double alpha0, double dalpha, double bump, int64_t save_every) {
+                double alpha0, double dalpha, double bump, int64_t save_every, int sa = 0) {
   StepArgs a;
-  a.f0 = view_of(c->slot[0]);
-  a.f1 = nslots == 2 ? view_of(c->slot[1]) : a.f0;
+  a.f0 = view_of(c->slot[sa]);
+  a.f1 = nslots == 2 ? view_of(c->slot[sa + 1]) : a.f0;
   a.nslots = nslots;
   a.n = c->n;
   a.dt = dt;
@@ -683,6 +696,93 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
     c->steps_since_bin += chunk;
     s0 += chunk;
   }
+  return SWRT_OK;
+}
+
+// nint PDE intervals of nsub steps each, interval i blending slots i, i+1 at
+// step size hs[i]: whole intervals per tile launch (up to kMaxIntervals, never
+// across a re-binning), else one interval at a time through run_advance.
+int run_advance_intervals(swrt_ctx* c, int nint, const double* hs, int64_t nsub, double f, double gH,
+                          double alpha0, double dalpha, double bump, int64_t save_every) {
+  const bool fused = use_tile_kernel(c) && c->kernel != 3 && c->blend_mode == 0 && c->rebin_every > 0 &&
+                     c->rebin_every % nsub == 0 && nsub <= kMaxStepsPerLaunch;
+  const int64_t fpi = save_every > 0 ? nsub / save_every : 0;  // frames per interval
+  int i0 = 0;
+  while (i0 < nint) {
+    int k = 0;
+    if (fused) {
+      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every) {
+        int rc = rebin(c, true);
+        if (rc) return rc;
+      }
+      k = (int)std::min<int64_t>({(int64_t)(nint - i0), (c->rebin_every - c->steps_since_bin) / nsub,
+                                  (int64_t)kMaxIntervals});
+    }
+    if (k < 1) {  // one interval on its own (it may straddle a re-binning)
+      int rc = run_advance(c, hs[i0], nsub, f, gH, 2, alpha0, dalpha, bump, save_every, i0);
+      if (rc) return rc;
+      c->hframes += fpi;
+      i0 += 1;
+      continue;
+    }
+    IvLaunch iv;
+    iv.nint = k;
+    iv.div_free = true;
+    for (int i = 0; i <= k; ++i) {
+      iv.views[i] = view_of(c->slot[i0 + i]);
+      iv.div_free = iv.div_free && c->slot[i0 + i].div_free;
+    }
+    for (int i = 0; i < k; ++i) iv.dts[i] = hs[i0 + i];
+    StepArgs a;
+    a.f0 = iv.views[0];
+    a.f1 = iv.views[1];
+    a.nslots = 2;
+    a.n = c->n;
+    a.dt = hs[i0];
+    a.half = hs[i0] / 2;
+    a.f2 = f * f;
+    a.gH = gH;
+    a.alpha0 = alpha0;
+    a.dalpha = dalpha;
+    a.bump = bump;
+    a.save_every = save_every > 0 ? save_every : 1;
+    a.hist_x = save_every > 0 ? c->hx : nullptr;
+    a.hist_k = save_every > 0 ? c->hk : nullptr;
+    a.frame0 = c->hframes;
+    a.x = c->dx;
+    a.k = c->dk;
+    a.perm = c->perm;
+    a.s0 = 0;
+    a.nsteps = (int)nsub;
+    const bool count_next = c->steps_since_bin + k * nsub >= c->rebin_every;
+    int rc = timed_launch(c, a, nblocks(c->n, 256), count_next, &iv);
+    if (rc) return rc;
+    c->steps_since_bin += k * nsub;
+    c->hframes += k * fpi;
+    i0 += k;
+  }
+  return SWRT_OK;
+}
+
+// grow the history frames (keeps the existing ones)
+int ensure_history(swrt_ctx* c, int64_t new_frames) {
+  if (new_frames <= 0 || c->hframes + new_frames <= c->hcap) return SWRT_OK;
+  const int64_t ncap = std::max<int64_t>(c->hframes + new_frames, 2 * c->hcap);
+  double *nx_ = nullptr, *nk_ = nullptr;
+  HIPCHK(c, hipMalloc(&nx_, sizeof(double) * 2 * c->n * ncap));
+  HIPCHK(c, hipMalloc(&nk_, sizeof(double) * 2 * c->n * ncap));
+  if (c->hframes > 0) {
+    HIPCHK(c, hipMemcpyAsync(nx_, c->hx, sizeof(double) * 2 * c->n * c->hframes, hipMemcpyDeviceToDevice,
+                             c->stream));
+    HIPCHK(c, hipMemcpyAsync(nk_, c->hk, sizeof(double) * 2 * c->n * c->hframes, hipMemcpyDeviceToDevice,
+                             c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  if (c->hx) (void)hipFree(c->hx);
+  if (c->hk) (void)hipFree(c->hk);
+  c->hx = nx_;
+  c->hk = nk_;
+  c->hcap = ncap;
   return SWRT_OK;
 }
 
@@ -1206,29 +1306,43 @@ int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, in
   int64_t new_frames = save_every > 0 ? nsteps / save_every : 0;
   if (save_every > 0 && nsteps % save_every)
     return fail(c, SWRT_ERR_ARG, "nsteps must be a multiple of save_every");
-  if (new_frames > 0 && c->hframes + new_frames > c->hcap) {
-    // grow (keeps existing frames)
-    const int64_t ncap = std::max<int64_t>(c->hframes + new_frames, 2 * c->hcap);
-    double *nx_ = nullptr, *nk_ = nullptr;
-    HIPCHK(c, hipMalloc(&nx_, sizeof(double) * 2 * c->n * ncap));
-    HIPCHK(c, hipMalloc(&nk_, sizeof(double) * 2 * c->n * ncap));
-    if (c->hframes > 0) {
-      HIPCHK(c, hipMemcpyAsync(nx_, c->hx, sizeof(double) * 2 * c->n * c->hframes,
-                               hipMemcpyDeviceToDevice, c->stream));
-      HIPCHK(c, hipMemcpyAsync(nk_, c->hk, sizeof(double) * 2 * c->n * c->hframes,
-                               hipMemcpyDeviceToDevice, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-    }
-    if (c->hx) (void)hipFree(c->hx);
-    if (c->hk) (void)hipFree(c->hk);
-    c->hx = nx_;
-    c->hk = nk_;
-    c->hcap = ncap;
-  }
-  int rc = run_advance(c, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every);
+  int rc = ensure_history(c, new_frames);
+  if (rc) return rc;
+  rc = run_advance(c, dt, nsteps, f, gH, nslots, alpha0, dalpha, bump, save_every);
   if (rc) return rc;
   c->hframes += new_frames;
   c->steps_done += nsteps;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_advance_intervals(swrt_ctx* c, int nintervals, const double* dts, int64_t nsub, double f, double gH,
+                           double alpha0, double dalpha, double bump, int64_t save_every) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  SlotUse slot_use(c);
+  if (nintervals < 1 || nintervals > SWRT_MAX_SLOTS - 1)
+    return fail(c, SWRT_ERR_ARG, "nintervals must be 1..SWRT_MAX_SLOTS-1");
+  if (!dts) return fail(c, SWRT_ERR_ARG, "dts is NULL");
+  if (nsub < 1) return fail(c, SWRT_ERR_ARG, "nsub must be >= 1");
+  if (save_every < 0 || (save_every > 0 && nsub % save_every))
+    return fail(c, SWRT_ERR_ARG, "save_every must divide nsub");
+  for (int s = 0; s <= nintervals; ++s) {
+    const Slot& sl = c->slot[s];
+    if (!sl.set) return fail(c, SWRT_ERR_STATE, "field slot not set");
+    if (sl.nx != c->slot[0].nx || sl.L != c->slot[0].L || sl.ny_period != c->slot[0].ny_period)
+      return fail(c, SWRT_ERR_ARG, "slots have different grids");
+  }
+  for (int i = 0; i < nintervals; ++i)
+    if (!(dts[i] > 0) || !std::isfinite(dts[i])) return fail(c, SWRT_ERR_ARG, "dts must be finite and > 0");
+  if (c->n == 0) return SWRT_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  const int64_t new_frames = save_every > 0 ? nintervals * (nsub / save_every) : 0;
+  int rc = ensure_history(c, new_frames);
+  if (rc) return rc;
+  rc = run_advance_intervals(c, nintervals, dts, nsub, f, gH, alpha0, dalpha, bump, save_every);
+  if (rc) return rc;
+  c->steps_done += nintervals * nsub;
   return SWRT_OK;
   GUARD_END(c)
 }

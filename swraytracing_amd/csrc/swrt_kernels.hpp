@@ -277,6 +277,8 @@ __device__ __forceinline__ void eval_flow(const FieldView& f0, const FieldView& 
     eval_flow_t<false>(f0, f1, alpha, x, y, bump, I);
 }
 
+constexpr int kMaxIntervals = 4;  // PDE intervals per multi-interval launch
+
 struct StepArgs {
   FieldView f0, f1;
   int nslots;

@@ -42,7 +42,35 @@ struct TileArgs {
                          // src[p] (indirect re-binning); NULL: slot p holds packet p
   double sort_lead;      // in-tile sort key: position + sort_lead * (group velocity)
   int split;             // launch shape (wg_work_range): halves | quarters << 16 per XCD band
+  // Multi-interval launch (ivmode, swrt_advance_intervals): nint consecutive
+  // PDE intervals of s.nsteps steps each; interval i blends snapshots iv[i]
+  // and iv[i+1] with alpha = alpha0 + st*dalpha (st = step within the
+  // interval) at step size ivdt[i].  A workgroup owns its tile's packets for
+  // the whole launch: it re-stages the window between intervals and the
+  // later intervals read the previous one's output in place.
+  // All snapshots share s.f0's grid; only their node arrays differ.
+  int ivmode;
+  int nint;
+  const double* ivn[kMaxIntervals + 1];
+  double ivdt[kMaxIntervals];
 };
+
+// Interval views by constant-index selects: a runtime index into the
+// by-value kernel argument would copy the whole argument to scratch.
+__device__ __forceinline__ const double* iv_nodes(const TileArgs& ta, int i) {
+  const double* p = ta.ivn[0];
+#pragma unroll
+  for (int j = 1; j <= kMaxIntervals; ++j)
+    if (i == j) p = ta.ivn[j];
+  return p;
+}
+__device__ __forceinline__ double iv_dt(const TileArgs& ta, int i) {
+  double d = ta.ivdt[0];
+#pragma unroll
+  for (int j = 1; j < kMaxIntervals; ++j)
+    if (i == j) d = ta.ivdt[j];
+  return d;
+}
 
 // Workgroup -> (tile, packet range).  XCD-aware (xcd_block): XCD x walks one
 // contiguous band of tiles.  `split` = h | q << 16 (ntiles % 8 == 0): each
@@ -371,25 +399,47 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   }
 #endif
 
+  const int lane_rank = b128_lane_rank(tid & 63);
+  const int nint = ta.ivmode ? ta.nint : 1;
+  for (int ivl = 0; ivl < nint; ++ivl) {
+  // interval ivl of a multi-interval launch (TileArgs::ivmode): its snapshot
+  // pair and step size; the later intervals take the previous one's output
+  // in place, already in cell order
+  FieldView fa = a.f0, fb = a.f1;
+  if (ta.ivmode) {
+    fa.nodes = iv_nodes(ta, ivl);
+    fb.nodes = iv_nodes(ta, ivl + 1);
+  }
+  const double dt = ta.ivmode ? iv_dt(ta, ivl) : a.dt;
+  const double half = ta.ivmode ? 0.5 * dt : a.half;
+  const bool first = ivl == 0;
+  const double* xin = first ? a.x : ta.x_out;
+  const double* kin = first ? a.k : ta.k_out;
+  const int* pin = first ? a.perm : ta.perm_out;
+  const int sortc = first ? ta.sort_cells : 0;
+  const int* srcp = first ? ta.src : nullptr;
+  int* nkeys = ivl == nint - 1 ? ta.next_keys : nullptr;
+  const int64_t sbase = a.s0 + (int64_t)ivl * a.nsteps;
+  if (!first) __syncthreads();  // every wave is done with the previous window
+
   // 1. stage the window (WBLEND: one launch = one step, alpha fixed)
   if constexpr (WBLEND)
     stage_window_blend<T, M, NT, WS>(a.f0, a.f1, ox, oy, a.alpha0 + (double)a.s0 * a.dalpha, win);
   else
-    stage_window_regs<TWO, T, M, NT, WS, V5>(a.f0, a.f1, ox, oy, win);
-  const int lane_rank = b128_lane_rank(tid & 63);
-  if (!ta.sort_cells) {
+    stage_window_regs<TWO, T, M, NT, WS, V5>(fa, fb, ox, oy, win);
+  if (!sortc) {
     __syncthreads();  // publish the window
     SWRT_STAMP(1);
   }
   for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
     const int nb = min(MAXB, pend - b0);
-    if (ta.sort_cells) {
+    if (sortc) {
     // 2. in-tile counting sort by the cell of the current position
     for (int h = tid; h < NB; h += NT) hist[h] = 0;
     __syncthreads();  // (also publishes the window on the first batch)
     if (b0 == pbeg) SWRT_STAMP(1);
     for (int i = tid; i < nb; i += NT) {
-      const int64_t p = ta.src ? ta.src[b0 + i] : b0 + i;
+      const int64_t p = srcp ? srcp[b0 + i] : b0 + i;
       // sort key position: the packet drifted by its group velocity to the
       // middle of the steps this order serves (x0 + sort_lead*gH*k/omega).
       // Packets of one cell separate at up to 2|cg| (k points every way), so
@@ -397,9 +447,9 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       // keeps the lane groups compact over the whole cycle (LDS bank-conflict
       // model, tools/conflict_model.py: 1.40 -> 1.22 LDS cycles per access).
       // Order only: results do not depend on it.
-      double xs = a.x[p], ys = a.x[a.n + p];
+      double xs = xin[p], ys = xin[a.n + p];
       if (ta.sort_lead != 0.0) {
-        const double kx = a.k[p], ky = a.k[a.n + p];
+        const double kx = kin[p], ky = kin[a.n + p];
         const double s = ta.sort_lead * a.gH / sqrt(a.f2 + a.gH * (kx * kx + ky * ky));
         xs += s * kx;
         ys += s * ky;
@@ -456,7 +506,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       order[i] = b0 + i;
       (void)v;
 #else
-      order[hist[v >> 16] + (v & 0xffff)] = ta.src ? ta.src[b0 + i] : b0 + i;  // input slot
+      order[hist[v >> 16] + (v & 0xffff)] = srcp ? srcp[b0 + i] : b0 + i;  // input slot
 #endif
     }
     __syncthreads();
@@ -468,13 +518,14 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     for (int r0 = tid & ~63; r0 < nb; r0 += NT) {
       const int r = r0 + lane_rank;
       if (r >= nb) continue;
-      const int64_t pi = ta.sort_cells ? order[r] : b0 + r;
+      const int64_t pi = sortc ? order[r] : b0 + r;
       const int64_t po = b0 + r;
-      double x0 = a.x[pi], y0 = a.x[a.n + pi];
-      double k0 = a.k[pi], l0 = a.k[a.n + pi];
-      const int orig = a.perm[pi];
+      double x0 = xin[pi], y0 = xin[a.n + pi];
+      double k0 = kin[pi], l0 = kin[a.n + pi];
+      const int orig = pin[pi];
       for (int st = 0; st < a.nsteps; ++st) {
-        const int64_t sg = a.s0 + st;
+        const int64_t sg = sbase + st;
+        const double alpha = a.alpha0 + (double)(ta.ivmode ? (int64_t)st : sg) * a.dalpha;
 #ifdef SWRT_FAIR_PRIO
         {
           // fair share between co-resident workgroups: a wave's issue
@@ -492,8 +543,8 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         }
 #endif
         double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
-        const double x1 = x0 + a.half * (a.gH * k0 / w);
-        const double y1 = y0 + a.half * (a.gH * l0 / w);
+        const double x1 = x0 + half * (a.gH * k0 / w);
+        const double y1 = y0 + half * (a.gH * l0 / w);
         Stencil sc;
         stencil_at(a.f0, x1, y1, a.bump, sc);
         const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
@@ -512,7 +563,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
           if (inwin)
             gather6_lds<false, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
           else
-            gather6_blend(a.f0.nodes, a.f1.nodes, npad, sc, a.alpha0 + (double)sg * a.dalpha, I);
+            gather6_blend(a.f0.nodes, a.f1.nodes, npad, sc, alpha, I);
         } else {
           if (inwin) {
             if constexpr (V5)
@@ -520,22 +571,21 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
             else
               gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
           } else {
-            gather6_lean<TWO>(a.f0.nodes, a.f1.nodes, npad, sc, I, J);
+            gather6_lean<TWO>(fa.nodes, fb.nodes, npad, sc, I, J);
           }
           if constexpr (TWO) {
-            const double alpha = a.alpha0 + (double)sg * a.dalpha;
             const double oma = 1 - alpha;
 #pragma unroll
             for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
           }
         }
-        const double x2 = x1 + a.dt * I[0];
-        const double y2 = y1 + a.dt * I[1];
-        const double k2 = k0 - a.dt * (I[2] * k0 + I[4] * l0);
-        const double l2 = l0 - a.dt * (I[3] * k0 + I[5] * l0);
+        const double x2 = x1 + dt * I[0];
+        const double y2 = y1 + dt * I[1];
+        const double k2 = k0 - dt * (I[2] * k0 + I[4] * l0);
+        const double l2 = l0 - dt * (I[3] * k0 + I[5] * l0);
         w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
-        x0 = x2 + a.half * (a.gH * k2 / w);
-        y0 = y2 + a.half * (a.gH * l2 / w);
+        x0 = x2 + half * (a.gH * k2 / w);
+        y0 = y2 + half * (a.gH * l2 / w);
         k0 = k2;
         l0 = l2;
         if (a.hist_x != nullptr && ((sg + 1) % a.save_every) == 0) {
@@ -549,12 +599,12 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       ta.x_out[po] = x0; ta.x_out[a.n + po] = y0;
       ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
       ta.perm_out[po] = orig;
-      if (ta.next_keys != nullptr) {  // fused histogram for the next re-binning
+      if (nkeys != nullptr) {  // fused histogram for the next re-binning
         const int ic = fast_cell(x0, a.f0.inv_dx, nx);
         const int jc = fast_cell(y0, a.f0.inv_dx, nx);
         const int ntx_ = ta.ntx;
         const int ntx2 = ic / T, nty2 = jc / T;
-        ta.next_keys[po] = ntx2 * ntx_ + nty2;
+        nkeys[po] = ntx2 * ntx_ + nty2;
         const int ddx = ring_diff(ntx2, tx, ntx_), ddy = ring_diff(nty2, ty, ntx_);
         // Most packets stay in this tile: they cost nothing here, the tile's
         // own count is (packets in the tile) - (movers), settled at the end.
@@ -572,6 +622,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     __syncthreads();  // LDS sort arrays are reused by the next batch
     if (b0 == pbeg) SWRT_STAMP(3);
   }
+  }  // intervals
   if (ta.next_keys != nullptr) {
     __syncthreads();
     const int v = tid < 9 ? nbr[tid] + (tid == 4 ? pend - pbeg : 0) : 0;

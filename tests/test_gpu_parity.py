@@ -290,7 +290,7 @@ def test_edge_cases(ctx, qg_case):
     with pytest.raises(sw.SwrtError):
         ctx.advance(0.01, 1, 3.0, 1.0, nslots=3)
     with pytest.raises(sw.SwrtError):
-        ctx.set_field_grid(2, _planes(c["flow"]), nx, L)
+        ctx.set_field_grid(5, _planes(c["flow"]), nx, L)  # SWRT_MAX_SLOTS = 5
     fresh = sw.Context(0)
     fresh.packets_set(x1, k1)
     with pytest.raises(sw.SwrtError):
