@@ -136,11 +136,13 @@ struct swrt_ctx {
   // The QG PDE (swrt_qg_*) runs on its own stream so the next PDE step, its
   // CFL speed and snapshot overlap the packet launch reading the previous
   // snapshots.  A snapshot into a slot whose buffer a queued packet launch
-  // still reads is renamed to `spare` instead of waiting for it.
+  // still reads takes an idle buffer from `spares` instead (renaming): a
+  // multi-interval launch reads up to 5 snapshots while the PDE writes the
+  // next group's.
   hipStream_t qstream = nullptr;
   bool qg_sep = true;
   bool qg_fused = true;  // swrt_qg_set_fused
-  Slot spare;
+  std::vector<Slot> spares;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
   double* dk = nullptr;  // 2N
@@ -220,6 +222,15 @@ struct swrt_ctx {
 };
 
 namespace {
+constexpr size_t kMaxSpares = 8;  // renamed snapshot buffers per context
+
+// the work recorded in `ev` has not finished yet
+bool event_pending(hipEvent_t ev) {
+  const hipError_t e = hipEventQuery(ev);
+  (void)hipGetLastError();  // hipErrorNotReady is a status, not an error
+  return e == hipErrorNotReady;
+}
+
 // Run a swrt_qg_* call on the QG stream: every helper launches on c->stream.
 struct OnQGStream {
   swrt_ctx* c;
@@ -819,10 +830,7 @@ int swrt_create(int device, swrt_ctx** out) {
   const char* qp = std::getenv("SWRT_QG_PRIO");
   const int prio = (qp && std::atoi(qp) == 0) ? prio_least : prio_greatest;
   bool ok = hipStreamCreateWithPriority(&c->qstream, hipStreamNonBlocking, prio) == hipSuccess;
-  Slot* all[SWRT_MAX_SLOTS + 1];
-  for (int i = 0; i < SWRT_MAX_SLOTS; ++i) all[i] = &c->slot[i];
-  all[SWRT_MAX_SLOTS] = &c->spare;
-  for (Slot* s : all)
+  for (Slot* s = c->slot; s != c->slot + SWRT_MAX_SLOTS; ++s)
     ok = ok && hipEventCreateWithFlags(&s->uev, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s->wev, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
@@ -845,7 +853,7 @@ void swrt_destroy(swrt_ctx* c) {
     if (s.wev) (void)hipEventDestroy(s.wev);
   };
   for (auto& s : c->slot) free_slot(s);
-  free_slot(c->spare);
+  for (auto& s : c->spares) free_slot(s);
   for (void* p : {(void*)c->dx, (void*)c->dk, (void*)c->perm, (void*)c->dx2, (void*)c->dk2,
                   (void*)c->perm2, (void*)c->keys, (void*)c->src_idx, (void*)c->bins})
     if (p) (void)hipFree(p);
@@ -2078,10 +2086,18 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   HIPCHK(c, hipSetDevice(c->device));
   if (c->qg_sep) {
     // rename a buffer still read by a queued packet launch, else wait for its last use
-    if (c->slot[slot].upend) {
-      const hipError_t e = hipEventQuery(c->slot[slot].uev);
-      (void)hipGetLastError();  // hipErrorNotReady is a status, not an error
-      if (e == hipErrorNotReady) std::swap(c->slot[slot], c->spare);
+    if (c->slot[slot].upend && event_pending(c->slot[slot].uev)) {
+      int pick = -1;
+      for (size_t i = 0; i < c->spares.size() && pick < 0; ++i)
+        if (!c->spares[i].upend || !event_pending(c->spares[i].uev)) pick = (int)i;
+      if (pick < 0 && c->spares.size() < kMaxSpares) {
+        Slot sp;
+        HIPCHK(c, hipEventCreateWithFlags(&sp.uev, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&sp.wev, hipEventDisableTiming));
+        c->spares.push_back(sp);
+        pick = (int)c->spares.size() - 1;
+      }
+      if (pick >= 0) std::swap(c->slot[slot], c->spares[pick]);  // else wait for the slot's own reader
     }
     if (c->slot[slot].upend) HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot[slot].uev, 0));
   }

@@ -190,6 +190,16 @@ class PacketEnsemble:
         self.ctx.advance(h, nsub, self.f, self.gH, nslots=2, alpha0=0.5 / nsub, dalpha=1.0 / nsub,
                          bump=self.bump, save_every=save_every)
 
+    def advance_intervals(self, dts, nsub=1, save_every=0):
+        """len(dts) consecutive PDE intervals in one call, interval i between
+        the snapshots in slots i and i+1 (swrt_advance_intervals): the same
+        bits as one advance() per interval with the pair moved to slots 0, 1."""
+        if self._rebin != 4 * nsub:
+            self._rebin = 4 * nsub
+            self.ctx.set_locality(self._rebin, 0)
+        self.ctx.advance_intervals([dt / nsub for dt in dts], nsub, self.f, self.gH, alpha0=0.5 / nsub,
+                                   dalpha=1.0 / nsub, bump=self.bump, save_every=save_every)
+
     def advance_ode23(self, dt, rtol=1e-3, atol=1e-6, allreduce_max=None, stats=None):
         """The reference drivers' own integrator over [0, dt] with
         interpolate_U's alpha = t/dt (ode23(ray_ode, [0, dt], y0))."""

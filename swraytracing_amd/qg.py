@@ -157,9 +157,34 @@ class _Log:
             self.f.close()
 
 
+class _IntervalGroup:
+    """Packet intervals deferred until `k` PDE steps have their end snapshots
+    (slots 1..k; slot 0 holds the group's start), then advanced in one
+    swrt_advance_intervals call — the same bits as one advance per step.  The
+    PDE runs up to k steps ahead of the packets; a frame write flushes."""
+
+    def __init__(self, ctx, ens, k, nsub):
+        self.ctx, self.ens, self.k, self.nsub = ctx, ens, max(1, min(int(k), 4)), nsub
+        self.dts = []
+
+    def next_slot(self):
+        return len(self.dts) + 1
+
+    def add(self, dt):
+        self.dts.append(dt)
+        if len(self.dts) == self.k:
+            self.flush()
+
+    def flush(self):
+        if self.dts:
+            self.ens.advance_intervals(self.dts, self.nsub)
+            self.ctx.swap_slots(0, len(self.dts))  # the last end snapshot starts the next group
+            self.dts = []
+
+
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
                   out_dir="data", nsub=4, max_steps=None, seed=146, verbose=False, r_drag=0.1,
-                  ctx: Context | None = None):
+                  packet_intervals=1, ctx: Context | None = None):
     """qgsw_raytrace.m:1-180 with the PDE and the packets on the GPU.
 
     Writes ``out_dir``/packet_x.bin, packet_k.bin, packet_time.bin, pv.bin,
@@ -167,7 +192,10 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     bounds the run (None: the reference's Nsteps = ceil(T/dt)).  ``r_drag``
     (0.1 in the reference, :25) enters update as the literal `+ r_drag*K2`
     term of :285, which forces every mode and makes long runs blow up; pass
-    0 to drop it.  Returns a dict of run facts (dt, Nsteps, steps run, frames
+    0 to drop it.  ``packet_intervals`` (1..4): PDE steps whose packet
+    intervals go to the device in one call (results identical for any
+    value; 1 is faster end to end here: the PDE chain's latency, not the
+    packet launch, bounds a driver step).  Returns a dict of run facts (dt, Nsteps, steps run, frames
     written, final t)."""
     ctx = ctx if ctx is not None else Context(0)
     os.makedirs(out_dir, exist_ok=True)
@@ -218,18 +246,18 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
     nrun = Nsteps if max_steps is None else min(Nsteps, int(max_steps))
     have_cur = False
+    group = _IntervalGroup(ctx, ens, packet_intervals, nsub) if ens is not None else None
     for step in range(1, nrun + 1):
         model.step(dt)
         t = t + dt
         if ens is not None and t > packet_delay:
-            if have_cur:
-                ctx.swap_slots(0, 1)          # last step's grid_U(qk) is this step's grid_U(prev_qk)
-            else:
-                model.snapshot(0, which=1)    # grid_U(prev_qk)
-            model.snapshot(1, which=0)        # grid_U(qk)
+            if not have_cur:
+                model.snapshot(0, which=1)    # grid_U(prev_qk); later groups start from the last grid_U(qk)
+            model.snapshot(group.next_slot(), which=0)  # grid_U(qk)
             have_cur = True
-            ens.advance(dt, nsub)
+            group.add(dt)
             if (step - packet_step_start + 1) % packet_steps_per_save == 0:
+                group.flush()
                 ens.write_frame(t, out_dir)
                 frames += 1
         else:
@@ -237,6 +265,8 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
         if step % steps_per_save == 0:
             write_field(model.q(), os.path.join(out_dir, "pv"))
             write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+    if group is not None:
+        group.flush()
     log.close()
     return dict(dt=dt, Nsteps=Nsteps, steps=nrun, packet_frames=frames, t=t, U0=U0,
                 packet_step_start=packet_step_start)
@@ -244,11 +274,12 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
 
 def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
                         out_dir="data", nsub=5, max_steps=None, seed=5, verbose=False,
-                        ctx: Context | None = None):
+                        packet_intervals=1, ctx: Context | None = None):
     """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
     (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and
     interpolate's 2*nx y-period).  Same packet outputs as :func:`qgsw_raytrace`;
-    pv.bin holds the initial nx x nx x 2 frame only, as in the reference."""
+    pv.bin holds the initial nx x nx x 2 frame only, as in the reference.
+    ``packet_intervals``: as in :func:`qgsw_raytrace`."""
     ctx = ctx if ctx is not None else Context(0)
     os.makedirs(out_dir, exist_ok=True)
     for name in ("packet_x", "packet_k", "packet_time", "pv", "pv_time"):
@@ -303,6 +334,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     step = 0
     have_cur = False
     dts = []
+    group = _IntervalGroup(ctx, ens, packet_intervals, nsub) if ens is not None else None
     # U0 of the current qk is always one step ahead: its read-back is queued
     # right after the PDE step and collected after the packet work of that
     # step is queued, so the CFL rule (:156-165, same values, same order)
@@ -317,14 +349,13 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
         t = t + dt
         model.max_speed_async()
         if ens is not None and t > packet_delay_steps:
-            if have_cur:
-                ctx.swap_slots(0, 1)
-            else:
+            if not have_cur:
                 model.snapshot(0, which=1, layer=0, ny_period=2 * nx)
-            model.snapshot(1, which=0, layer=0, ny_period=2 * nx)
+            model.snapshot(group.next_slot(), which=0, layer=0, ny_period=2 * nx)
             have_cur = True
-            ens.advance(dt, nsub)
+            group.add(dt)
             if (step - packet_step_start + 1) % packet_steps_per_save == 0:
+                group.flush()
                 ens.write_frame(t, out_dir)
                 frames += 1
         else:
@@ -332,6 +363,8 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
         U0 = model.max_speed_result()
         # (the reference only plots q every steps_per_save steps here; its
         # pv.bin writes are commented out, qg2layersw_raytrace.m:211-239)
+    if group is not None:
+        group.flush()
     log.close()
     return dict(dt=dt, dts=dts, Nsteps=Nsteps, steps=step, packet_frames=frames, t=t, U0=U0,
                 packet_step_start=packet_step_start)

@@ -286,32 +286,34 @@ def test_qg_graph_replay_bit_identical(ctx, layers):
     assert np.array_equal(np.ascontiguousarray(a[0]).view(np.uint64), np.ascontiguousarray(b[0]).view(np.uint64))
 
 
-def _driver_files(ctx, d, layers, separate, fused):
+def _driver_files(ctx, d, layers, separate, fused, intervals):
     ctx.qg_set_stream(separate)
     ctx.qg_set_fused(fused)
     d.mkdir()
     if layers == 2:
         sw.qg2layersw_raytrace(128, 200_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=2, max_steps=30,
-                               seed=5, ctx=ctx)
+                               seed=5, packet_intervals=intervals, ctx=ctx)
     else:
         sw.qgsw_raytrace(64, 50_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=2, max_steps=12,
-                         seed=146, r_drag=0.0, ctx=ctx)
+                         seed=146, r_drag=0.0, packet_intervals=intervals, ctx=ctx)
     return [open(d / name, "rb").read() for name in ("packet_x.bin", "packet_k.bin", "pv.bin", "packet_time.bin")]
 
 
 @pytest.mark.parametrize("layers", [1, 2])
 def test_qg_stream_overlap_and_fusion_bit_identical(ctx, tmp_path, layers):
     """The QG PDE on its own stream with snapshot renaming
-    (swrt_qg_set_stream) and the fused post-step transforms
-    (swrt_qg_set_fused), both defaults, give the same packets, frames, PV and
-    frame times (the CFL dt sequence) as one stream without fusion.  The
-    2-layer case has packet launches long enough that snapshots meet
-    in-flight reads."""
+    (swrt_qg_set_stream), the fused post-step transforms (swrt_qg_set_fused)
+    and packet intervals grouped 4 per call (PDE run ahead,
+    swrt_advance_intervals) — all defaults — give the same packets, frames,
+    PV and frame times (the CFL dt sequence) as one stream without fusion,
+    one interval per call.  The 2-layer case has packet launches long enough
+    that snapshots meet in-flight reads; frames every 5 (1-layer) and 25
+    (2-layer) steps cut groups short."""
     try:
-        ref = _driver_files(ctx, tmp_path / "plain", layers, False, False)
-        for sep, fused in [(True, True), (True, False), (False, True)]:
-            got = _driver_files(ctx, tmp_path / f"s{int(sep)}f{int(fused)}", layers, sep, fused)
-            assert all(len(u) > 0 and u == v for u, v in zip(got, ref)), (sep, fused)
+        ref = _driver_files(ctx, tmp_path / "plain", layers, False, False, 1)
+        for sep, fused, iv in [(True, True, 4), (True, False, 1), (False, True, 4), (True, True, 3)]:
+            got = _driver_files(ctx, tmp_path / f"s{int(sep)}f{int(fused)}i{iv}", layers, sep, fused, iv)
+            assert all(len(u) > 0 and u == v for u, v in zip(got, ref)), (sep, fused, iv)
     finally:
         ctx.qg_set_stream(True)
         ctx.qg_set_fused(True)

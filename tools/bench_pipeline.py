@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--qg-graphs", action="store_true", help="hipGraph replay of the QG step (A/B; default off)")
     ap.add_argument("--one-stream", action="store_true", help="QG PDE on the packet stream (A/B)")
     ap.add_argument("--no-fused", action="store_true", help="separate transforms per QG call (A/B)")
+    ap.add_argument("--intervals", type=int, default=1, help="PDE steps whose packet intervals go in one call")
     args = ap.parse_args()
     nx, L, f, Cg = args.nx, 20.0, 3.0, 1.0
     ctx = sw.Context(0)
@@ -70,6 +71,11 @@ def main():
 
     state = {"dt": dt, "U0": model.max_speed()}
 
+    # the driver's packet branch (qg.py): packet intervals grouped --intervals
+    # per call, the PDE running ahead; slot 0 = the current qk's snapshot
+    group = sw.qg._IntervalGroup(ctx, ens, args.intervals, args.nsub)
+    ctx.swap_slots(0, 1)
+
     def full_step():
         # the driver's order: CFL rule on the current U0, PDE step, async U0 of
         # the new qk, snapshot + packets queued, then collect U0
@@ -77,12 +83,12 @@ def main():
         state["dt"] = d
         model.step(d)
         model.max_speed_async()
-        ctx.swap_slots(0, 1)
-        model.snapshot(1, which=0, ny_period=2 * nx)
-        ens.advance(d, args.nsub)
+        model.snapshot(group.next_slot(), which=0, ny_period=2 * nx)
+        group.add(d)
         state["U0"] = model.max_speed_result()
 
     full = timed(ctx, full_step, r)
+    group.flush()
     ode = None
     if args.ode23:
         # one warm-up interval (first-use allocations), then the mean of 5
@@ -102,7 +108,8 @@ def main():
         "metric": "driver step time, qg2layersw_raytrace loop on device (PDE + snapshots + packets)",
         "config": {"nx": nx, "layers": 2, "packets": args.packets, "nsub": args.nsub, "steps": r,
                    "qg_graphs": args.qg_graphs, "qg_stream": not args.one_stream,
-                   "qg_fused": not args.no_fused},
+                   "qg_fused": not args.no_fused,
+                   "packet_intervals": args.intervals},
         "pde_ms": pde, "cfl_ms": cfl, "snapshot_ms": snap, "packets_ms": pk, "step_ms": full,
         "packet_steps_per_s": args.packets * args.nsub / (full / 1e3),
         "ode23": ode,
