@@ -2240,6 +2240,16 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
       if (v5) ode23_tile_launch<STAGE, false, true>(c, a, grid, starts, ntx);
       else ode23_tile_launch<STAGE, false, false>(c, a, grid, starts, ntx);
     }
+  } else if constexpr (STAGE == 0) {  // one lane per packet: the three stage launches
+    const dim3 grid(nblocks(c->n, 256)), block(256);
+    Ode23Args b = a0;
+    hipLaunchKernelGGL(ode23_stage_kernel<2>, grid, block, 0, c->stream, b);
+    b.ts = a0.ts3;
+    b.c[0] = a0.c3;
+    hipLaunchKernelGGL(ode23_stage_kernel<3>, grid, block, 0, c->stream, b);
+    b.ts = a0.ts4;
+    for (int i = 0; i < 3; ++i) b.c[i] = a0.c4[i];
+    hipLaunchKernelGGL(ode23_stage_kernel<4>, grid, block, 0, c->stream, b);
   } else {
     hipLaunchKernelGGL(ode23_stage_kernel<STAGE>, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, a0);
   }
@@ -2280,21 +2290,20 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
   int rc;
   Ode23Args a;
   if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;
-  // ode23: f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2)
+  // ode23: f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2);
+  // h = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew — one launch (stage 0:
+  // the tile kernel runs the three stages per packet, registers between them)
   a.ts = t + h * 0.5;
   a.c[0] = h * 0.5;
-  if ((rc = ode23_launch<2>(c, a))) return rc;
-  a.ts = t + h * 0.75;
-  a.c[0] = h * 0.75;
-  if ((rc = ode23_launch<3>(c, a))) return rc;
-  // h = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew
+  a.ts3 = t + h * 0.75;
+  a.c3 = h * 0.75;
   const double h4 = tnew - t;
-  a.ts = tnew;
-  a.c[0] = h4 * (2.0 / 9.0);
-  a.c[1] = h4 * (1.0 / 3.0);
-  a.c[2] = h4 * (4.0 / 9.0);
+  a.ts4 = tnew;
+  a.c4[0] = h4 * (2.0 / 9.0);
+  a.c4[1] = h4 * (1.0 / 3.0);
+  a.c4[2] = h4 * (4.0 / 9.0);
   HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, sizeof(unsigned long long), c->stream));
-  if ((rc = ode23_launch<4>(c, a))) return rc;
+  if ((rc = ode23_launch<0>(c, a))) return rc;
   if (err_raw_out) return read_max(c, err_raw_out);
   return SWRT_OK;
   GUARD_END(c)

@@ -39,6 +39,10 @@ struct Ode23Args {
   double tmax;
   double f2, Cg, Cg2;
   double c[3];       // stage coefficients (already multiplied by h)
+  // STAGE 0 (tile kernel): stages 2, 3 and 4 of one attempt fused per packet;
+  // ts / c[0] are stage 2's, these stages 3 and 4's
+  double ts3, ts4, c3;
+  double c4[3];
   double thr;        // AbsTol / RelTol
   double bump;
   unsigned long long* dmax;
@@ -186,6 +190,39 @@ __global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, in
 // (a.order) mapped onto the ds_read_b128 lane groups.  The packets move well
 // under the M-cell margin within one PDE interval; a packet outside it takes
 // the global gather.  Same arithmetic as ode23_stage_kernel, so the same bits.
+// interpolate_U's alpha = t/tmax at stage time ts
+__device__ __forceinline__ double alpha_of(const Ode23Args& a, double ts) { return a.tmax != 0.0 ? ts / a.tmax : 0.0; }
+
+// odefun at ys from the tile's LDS window (or global memory outside it)
+template <bool TWO, int T, int M, int WS, int WNP, bool V5>
+__device__ __forceinline__ void tile_rhs(const Ode23Args& a, const double2* win, int ox, int oy, int nx,
+                                         double alpha, const double ys[4], double fo[4]) {
+  // odefun at (ts, ys): interpolate_U from the window (or global memory)
+  Stencil sc;
+  stencil_at(a.f0, ys[0], ys[1], a.bump, sc);
+  const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
+  double I[kRec], J[kRec];
+  if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M) {
+    if constexpr (V5)
+      gather5_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+    else
+      gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+  } else {
+    gather6_lean<TWO>(a.f0.nodes, a.f1.nodes, a.f0.npad, sc, I, J);
+  }
+  if constexpr (TWO) {
+    const double oma = 1 - alpha;
+#pragma unroll
+    for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
+  }
+  const double k1 = ys[2], k2 = ys[3];
+  const double s = sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2));
+  fo[0] = I[0] + (a.Cg * k1) / s;
+  fo[1] = I[1] + (a.Cg * k2) / s;
+  fo[2] = -(I[2] * k1 + I[4] * k2);
+  fo[3] = -(I[3] * k1 + I[5] * k2);
+}
+
 template <int STAGE, bool TWO, int T, int M, int NT, bool V5>
 __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const int* starts, int ntx) {
   constexpr int W = T + 5 + 2 * M;
@@ -218,38 +255,52 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
       const double* Fp = a.F[STAGE - 2];
 #pragma unroll
       for (int c = 0; c < 4; ++c) ys[c] = y[c] + Fp[c * n + p] * a.c[0];
-    } else {
+    } else if constexpr (STAGE == 4) {
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         ys[c] = y[c] + (((a.F[0][c * n + p] * a.c[0]) + a.F[1][c * n + p] * a.c[1]) + a.F[2][c * n + p] * a.c[2]);
       a.ynx[p] = ys[0]; a.ynx[n + p] = ys[1];
       a.ynk[p] = ys[2]; a.ynk[n + p] = ys[3];
     }
-    // odefun at (ts, ys): interpolate_U from the window (or global memory)
-    Stencil sc;
-    stencil_at(a.f0, ys[0], ys[1], a.bump, sc);
-    const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
-    double I[kRec], J[kRec];
-    if (dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M) {
-      if constexpr (V5)
-        gather5_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
-      else
-        gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
-    } else {
-      gather6_lean<TWO>(a.f0.nodes, a.f1.nodes, a.f0.npad, sc, I, J);
-    }
-    if constexpr (TWO) {
-      const double oma = 1 - alpha;
-#pragma unroll
-      for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
-    }
-    const double k1 = ys[2], k2 = ys[3];
-    const double s = sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2));
     double fo[4];
-    fo[0] = I[0] + (a.Cg * k1) / s;
-    fo[1] = I[1] + (a.Cg * k2) / s;
-    fo[2] = -(I[2] * k1 + I[4] * k2);
-    fo[3] = -(I[3] * k1 + I[5] * k2);
+    if constexpr (STAGE == 0) {
+      // stages 2, 3, 4 of the attempt in one pass (a rolled loop: one copy of
+      // the gather, so registers stay at the single-stage count); the stage
+      // derivatives go to memory as in the separate stages and are re-read
+      // where those read them: same bits
+#pragma unroll 1
+      for (int sg = 0; sg < 3; ++sg) {
+        double ts;
+        if (sg == 0) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ys[c] = y[c] + a.F[0][c * n + p] * a.c[0];
+          ts = a.ts;
+        } else if (sg == 1) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ys[c] = y[c] + fo[c] * a.c3;
+          ts = a.ts3;
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            ys[c] = y[c] + (((a.F[0][c * n + p] * a.c4[0]) + a.F[1][c * n + p] * a.c4[1]) + fo[c] * a.c4[2]);
+          a.ynx[p] = ys[0]; a.ynx[n + p] = ys[1];
+          a.ynk[p] = ys[2]; a.ynk[n + p] = ys[3];
+          ts = a.ts4;
+        }
+        tile_rhs<TWO, T, M, WS, WNP, V5>(a, win, ox, oy, nx, alpha_of(a, ts), ys, fo);
+        double* Fo = sg == 0 ? a.F[1] : (sg == 1 ? a.F[2] : a.F[3]);  // no runtime index into the argument
+#pragma unroll
+        for (int c = 0; c < 4; ++c) Fo[c * n + p] = fo[c];
+      }
+      constexpr double E1 = -5.0 / 72.0, E2 = 1.0 / 12.0, E3 = 1.0 / 9.0, E4 = -1.0 / 8.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const double fe = ((a.F[0][c * n + p] * E1 + a.F[1][c * n + p] * E2) + a.F[2][c * n + p] * E3) + fo[c] * E4;
+        m = fmax(m, fabs(fe) / fmax(fmax(fabs(y[c]), fabs(ys[c])), a.thr));
+      }
+      continue;
+    }
+    tile_rhs<TWO, T, M, WS, WNP, V5>(a, win, ox, oy, nx, alpha, ys, fo);
     double* Fo = a.F[STAGE - 1];
 #pragma unroll
     for (int c = 0; c < 4; ++c) Fo[c * n + p] = fo[c];
@@ -265,7 +316,7 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
       }
     }
   }
-  if constexpr (STAGE == 1 || STAGE == 4) {
+  if constexpr (STAGE == 0 || STAGE == 1 || STAGE == 4) {
     for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
