@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--one-stream", action="store_true", help="QG PDE on the packet stream (A/B)")
     ap.add_argument("--no-fused", action="store_true", help="separate transforms per QG call (A/B)")
     ap.add_argument("--intervals", type=int, default=1, help="PDE steps whose packet intervals go in one call")
+    ap.add_argument("--fixed-dt", action="store_true",
+                    help="no CFL rule / U0 read-back per step (the 1-layer driver's loop, qgsw_raytrace.m)")
     args = ap.parse_args()
     nx, L, f, Cg = args.nx, 20.0, 3.0, 1.0
     ctx = sw.Context(0)
@@ -79,6 +81,12 @@ def main():
     def full_step():
         # the driver's order: CFL rule on the current U0, PDE step, async U0 of
         # the new qk, snapshot + packets queued, then collect U0
+        if args.fixed_dt:
+            d = state["dt"]
+            model.step(d)
+            model.snapshot(group.next_slot(), which=0, ny_period=2 * nx)
+            group.add(d)
+            return
         d, _ = model.cfl_rule(state["dt"], state["U0"], 0.25)
         state["dt"] = d
         model.step(d)
@@ -109,7 +117,7 @@ def main():
         "config": {"nx": nx, "layers": 2, "packets": args.packets, "nsub": args.nsub, "steps": r,
                    "qg_graphs": args.qg_graphs, "qg_stream": not args.one_stream,
                    "qg_fused": not args.no_fused,
-                   "packet_intervals": args.intervals},
+                   "packet_intervals": args.intervals, "fixed_dt": args.fixed_dt},
         "pde_ms": pde, "cfl_ms": cfl, "snapshot_ms": snap, "packets_ms": pk, "step_ms": full,
         "packet_steps_per_s": args.packets * args.nsub / (full / 1e3),
         "ode23": ode,
