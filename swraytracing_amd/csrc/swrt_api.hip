@@ -1846,27 +1846,21 @@ int qg_post(swrt_ctx* c) {
   int rc;
   if ((rc = ensure_twiddles(c, n))) return rc;
   const dim3 grid((unsigned)nblocks(q.nn, 256)), block(256);
+  // Jacobian inputs | layer-1 u+iv | swrt_qg_snapshot(which 0, layer 0)'s
+  // grid_U spectra (grid_U.m inversion, ky-fastest half plane) — one launch
   double2* uv = q.PZ + 2 * nl * q.nn;
-  if (nl == 2) {
-    hipLaunchKernelGGL(qg_jac_spectra_kernel<2>, grid, block, 0, c->stream, q.qk, q.g, q.PZ);
-    hipLaunchKernelGGL(qg_vel_spectra_kernel<1>, grid, block, 0, c->stream, (const double2*)(q.qk + q.nhalf), q.g,
-                       uv);
-  } else {
-    hipLaunchKernelGGL(qg_jac_spectra_kernel<1>, grid, block, 0, c->stream, q.qk, q.g, q.PZ);
-  }
-  HIPCHK(c, hipGetLastError());
-  // swrt_qg_snapshot(which 0, layer 0)'s spectra: grid_U.m inversion, ky-fastest half plane
-  hipLaunchKernelGGL(spectra_kernel, grid, block, 0, c->stream, (const double2*)q.qk, n, 1, q.g.K_d2, q.g.kscale, 0,
-                     uv + (nl - 1) * q.nn, n / 2, 1);
+  if (nl == 2)
+    hipLaunchKernelGGL(qg_post_spectra_kernel<2>, grid, block, 0, c->stream, (const double2*)q.qk, q.g, q.nhalf,
+                       q.PZ, uv, uv + q.nn, q.dmax);
+  else
+    hipLaunchKernelGGL(qg_post_spectra_kernel<1>, grid, block, 0, c->stream, (const double2*)q.qk, q.g, q.nhalf,
+                       q.PZ, uv, uv, q.dmax);
   HIPCHK(c, hipGetLastError());
   if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
-  // CFL speed over every layer's u + i v (layer 1, then layer 0: contiguous)
-  HIPCHK(c, hipMemsetAsync(q.dmax, 0, sizeof(unsigned long long), c->stream));
-  hipLaunchKernelGGL(qg_max_speed2_kernel, dim3(256), dim3(256), 0, c->stream, (const double2*)(q.PT + 2 * nl * q.nn),
-                     q.nn * nl, q.g.shear, q.dmax);
-  HIPCHK(c, hipGetLastError());
-  // Jacobian -> forward 2-D FFT; the spectrum lands in PT[0, nn) (psi_x of layer 0 is dead)
-  hipLaunchKernelGGL(qg_jacobian_kernel, grid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ);
+  // Jacobian and the CFL speed over every layer's u + i v (layer 1, then
+  // layer 0: contiguous); the spectrum of J then lands in PT[0, nn)
+  hipLaunchKernelGGL(qg_jacobian_max_kernel, grid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ,
+                     (const double2*)(q.PT + 2 * nl * q.nn), q.g.shear, q.dmax);
   HIPCHK(c, hipGetLastError());
   if ((rc = run_fft_pass(c, q.PZ, n, 1, 0))) return rc;
   if ((rc = run_transpose(c, q.PZ, q.PT, n, 1))) return rc;

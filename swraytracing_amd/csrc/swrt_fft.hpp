@@ -234,9 +234,8 @@ __device__ __forceinline__ double2 mul_mik(double k, double2 z) { return make_do
 // mode 0: psik = fk (SpectralScheme path); mode 1: psik = -qk./(K_d2 + K2).
 // The half plane is read at fk[(kx + kmax)*sx + ky*sy]: (1, 2kmax+1) for the
 // host's column-major layout, (kmax+1, 1) for the QG state's ky-fastest one.
-__global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, double kscale,
+__device__ __forceinline__ void spectra_at(int64_t idx, const double2* fk, int n, int mode, double K_d2, double kscale,
                                int with_psi, double2* Z, int sx, int sy) {
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nn = (int64_t)n * n;
   if (idx >= nn) return;
   const int sh_ = __ffs(n) - 1;  // n is a power of two
@@ -283,6 +282,12 @@ __global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, 
   Z[nn + idx] = z[1];
   Z[2 * nn + idx] = z[2];
   if (with_psi) Z[3 * nn + idx] = z[3];
+}
+
+__global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, double kscale,
+                               int with_psi, double2* Z, int sx, int sy) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  spectra_at(idx, fk, n, mode, K_d2, kscale, with_psi, Z, sx, sy);
 }
 
 // After the inverse 2-D transform Z is in layout [r + n*c] (x contiguous):

@@ -91,10 +91,9 @@ __device__ __forceinline__ void qg2_B(double K2, double K_d2, double& b11, doubl
 // the Hermitian completion of fulspec.m (kx < 0 on ky = 0 and ky < 0 from
 // their conjugate partners; Nyquist row/column zero).
 template <int NL>
-__global__ void __launch_bounds__(256) qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+__device__ __forceinline__ void qg_jac_spectra_at(int64_t idx, const double2* qk, QGDev g, double2* Z) {
   const int n = g.n;
   const int64_t nn = (int64_t)n * n;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nn) return;
   const int sh_ = __ffs(n) - 1;  // n is a power of two
   const int c = (int)idx & (n - 1), r = (int)idx >> sh_;
@@ -130,6 +129,12 @@ __global__ void __launch_bounds__(256) qg_jac_spectra_kernel(const double2* qk, 
     Z[(2 * l) * nn + idx] = pack2(px, py);
     Z[(2 * l + 1) * nn + idx] = pack2(qx, qy);
   }
+}
+
+template <int NL>
+__global__ void __launch_bounds__(256) qg_jac_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  qg_jac_spectra_at<NL>(idx, qk, g, Z);
 }
 
 // J = psix.*qy - psiy.*qx per grid point and layer (qgsw_raytrace.m:282);
@@ -312,10 +317,9 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
 // u + i v per layer from grid_U's inversion psik = -qk./(K_d2+K2) (grid_U.m:2-6),
 // for the CFL speed (qg2layersw_raytrace.m:156-158); layout [c + n*r].
 template <int NL>
-__global__ void __launch_bounds__(256) qg_vel_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+__device__ __forceinline__ void qg_vel_spectra_at(int64_t idx, const double2* qk, QGDev g, double2* Z) {
   const int n = g.n;
   const int64_t nn = (int64_t)n * n;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= nn) return;
   const int sh_ = __ffs(n) - 1;  // n is a power of two
   const int c = (int)idx & (n - 1), r = (int)idx >> sh_;
@@ -343,6 +347,12 @@ __global__ void __launch_bounds__(256) qg_vel_spectra_kernel(const double2* qk, 
   }
 }
 
+template <int NL>
+__global__ void __launch_bounds__(256) qg_vel_spectra_kernel(const double2* qk, QGDev g, double2* Z) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  qg_vel_spectra_at<NL>(idx, qk, g, Z);
+}
+
 // max over the grid of (u + shear)^2 + v^2 (all layers) into *out (as the
 // bit pattern of a non-negative double, so integer max == double max).
 __global__ void qg_max_speed2_kernel(const double2* T, int64_t cnt, double shear, unsigned long long* out) {
@@ -361,6 +371,52 @@ __global__ void qg_max_speed2_kernel(const double2* T, int64_t cnt, double shear
     __syncthreads();
   }
   if (threadIdx.x == 0) atomicMax(out, (unsigned long long)__double_as_longlong(red[0]));
+}
+
+// Fused mode (swrt_api.hip qg_post): the post-step spectra of one qk in ONE
+// launch — the Jacobian inputs, layer 1's u+iv and layer 0's grid_U, by the
+// three kernels' own element functions (same values) — which also clears
+// the CFL max for qg_jacobian_max_kernel.
+template <int NL>
+__global__ void __launch_bounds__(256) qg_post_spectra_kernel(const double2* qk, QGDev g, int64_t nhalf,
+                                                              double2* Zjac, double2* Zuv1, double2* Zsnap,
+                                                              unsigned long long* dmax) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx == 0) *dmax = 0ull;
+  qg_jac_spectra_at<NL>(idx, qk, g, Zjac);
+  if constexpr (NL == 2) qg_vel_spectra_at<1>(idx, qk + nhalf, g, Zuv1);
+  spectra_at(idx, qk, g.n, 1, g.K_d2, g.kscale, 0, Zsnap, g.n / 2, 1);
+}
+
+// qg_jacobian_kernel + qg_max_speed2_kernel over the same grid points:
+// J1 + i J2, and max (u + shear)^2 + v^2 over the nl u+iv planes at `uv`.
+__global__ void __launch_bounds__(256) qg_jacobian_max_kernel(const double2* T, int nl, int64_t nn, double2* Zj,
+                                                              const double2* uv, double shear,
+                                                              unsigned long long* dmax) {
+  __shared__ double red[256];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double m = 0.0;
+  if (i < nn) {
+    double J[2] = {0.0, 0.0};
+    for (int l = 0; l < nl; ++l) {
+      const double2 P = T[(2 * l) * nn + i], Q = T[(2 * l + 1) * nn + i];
+      J[l] = P.x * Q.y - P.y * Q.x;
+    }
+    Zj[i] = make_double2(J[0], J[1]);
+    for (int l = 0; l < nl; ++l) {
+      const double2 z = uv[l * nn + i];
+      const double u = z.x + shear, v = z.y;
+      const double s2 = u * u + v * v;
+      m = s2 > m ? s2 : m;
+    }
+  }
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) atomicMax(dmax, (unsigned long long)__double_as_longlong(red[0]));
 }
 
 }  // namespace swrt
