@@ -55,6 +55,21 @@ struct TileArgs {
   double ivdt[kMaxIntervals];
 };
 
+// Packet-state stores of the tile kernel.  SWRT_WT_STORES: write-through
+// (`sc1`, agent-scope relaxed atomic stores) so the launch ends with no dirty
+// L2 lines of its 36 MB of output to write back before the next launch.
+#ifndef SWRT_WT_STORES
+#define SWRT_WT_STORES 0
+#endif
+template <typename V>
+__device__ __forceinline__ void st_out(V* p, V v) {
+#if SWRT_WT_STORES
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+
 // Interval views by constant-index selects: a runtime index into the
 // by-value kernel argument would copy the whole argument to scratch.
 __device__ __forceinline__ const double* iv_nodes(const TileArgs& ta, int i) {
@@ -596,9 +611,9 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
           hk[orig] = k0; hk[a.n + orig] = l0;
         }
       }
-      ta.x_out[po] = x0; ta.x_out[a.n + po] = y0;
-      ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
-      ta.perm_out[po] = orig;
+      st_out(&ta.x_out[po], x0); st_out(&ta.x_out[a.n + po], y0);
+      st_out(&ta.k_out[po], k0); st_out(&ta.k_out[a.n + po], l0);
+      st_out(&ta.perm_out[po], orig);
       if (nkeys != nullptr) {  // fused histogram for the next re-binning
         const int ic = fast_cell(x0, a.f0.inv_dx, nx);
         const int jc = fast_cell(y0, a.f0.inv_dx, nx);
