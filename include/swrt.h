@@ -216,6 +216,21 @@ int swrt_leapfrog(swrt_ctx* ctx, double* x, double* k, int64_t n, double dt, int
  * order U.u, U.v, GradU.u_x, GradU.u_y, GradU.v_x, GradU.v_y, H. */
 int swrt_xka_set_fields(swrt_ctx* ctx, const double* fields7, int64_t nx, double dx, double dy);
 
+/* The same background built on the GPU from an RSW state, as
+ * ray_trace_sw/raytrace_sw.m:16-52 does: state3 = S(:,:,1:3) = [u v eta]
+ * (nx x nx x 3 column-major, :12), g2k of each (:26-28), the geostrophic
+ * projection etagk = (f*etak - zetak).*f./(f^2 + gH0*K2) with gH0 = Cg^2
+ * (:22-31), ug/vg and their i*k gradients (:34-41), seven k2g and
+ * H = 1 + etag (:44-52).  Integer wavenumbers (L = 2*pi, :84); L sets
+ * dx = dy = L/nx.  nx a power of two. */
+int swrt_xka_set_rsw(swrt_ctx* ctx, const double* state3, int64_t nx, double f, double Cg, double L);
+
+/* Download the current xka background as the seven planes of
+ * swrt_xka_set_fields (U.u, U.v, GradU.u_x, u_y, v_x, v_y, H); nx x nx each
+ * with nx = swrt_xka_grid(ctx). */
+int swrt_xka_get_fields(swrt_ctx* ctx, double* fields7_out);
+int64_t swrt_xka_grid(const swrt_ctx* ctx);
+
 /* nsteps of Pout = step_packet_xka(P, ...) for n packets (step_packet_xka.m:
  * 38-91 with cg_sw.m:15-32 evaluated per stencil tap; interpolate of
  * ray_trace_sw, bump 1e-13).  state5 (in/out): n x 5 column-major

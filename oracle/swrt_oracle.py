@@ -632,6 +632,34 @@ def step_packet_xka(P, U, GradU, H, C0, f, dx, dy, dt):
     return out
 
 
+def rsw_background(S, f, Cg):
+    """ray_trace_sw/raytrace_sw.m:16-52: geostrophic part of an RSW state.
+
+    S: nx x nx x 3 grid state [u v eta] (raytrace_sw.m:12).  Integer
+    wavenumbers (L = 2*pi, :84).  Returns dict(U={u, v}, GradU={u_x, u_y,
+    v_x, v_y}, H = 1 + eta_g, etag), the inputs of step_packet_xka."""
+    S = np.asarray(S, dtype=np.float64)
+    nx = S.shape[0]
+    kx_, ky_, K2_ = wavenumber_grids(nx)  # :16-18
+    gH0 = Cg ** 2  # :22
+    sig2_ = f ** 2 + gH0 * K2_  # :25
+    uk = g2k(S[:, :, 0])  # :26-28
+    vk = g2k(S[:, :, 1])
+    etak = g2k(S[:, :, 2])
+    zetak = 1j * (kx_ * vk - ky_ * uk)  # :29
+    etagk = (f * etak - zetak) * f / sig2_  # :30
+    ugk = (-1j * ky_) * (gH0 / f * etagk)  # :34
+    vgk = (1j * kx_) * (gH0 / f * etagk)  # :35
+    ugxk = (1j * kx_) * ugk  # :38-41
+    ugyk = (1j * ky_) * ugk
+    vgxk = (1j * kx_) * vgk
+    vgyk = (1j * ky_) * vgk
+    etag = k2g(etagk)  # :44-52
+    return dict(U={"u": k2g(ugk), "v": k2g(vgk)},
+                GradU={"u_x": k2g(ugxk), "u_y": k2g(ugyk), "v_x": k2g(vgxk), "v_y": k2g(vgyk)},
+                H=1 + etag, etag=etag)
+
+
 def childress_soward(nx, U0=0.1, km=4.0, a=0.25, L=2 * math.pi):
     """ray_trace_sw/raytrace.m:30-37 analytic cellular flow on the grid
     x = (0:nx-1)*dx (raytrace.m:26-28): returns U, GradU dicts."""

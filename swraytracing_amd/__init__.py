@@ -6,14 +6,16 @@ CDNA4 kernels behind the C ABI in include/swrt.h, with the reference's
 MATLAB call surface mirrored in Python.
 """
 from ._lib import Context, SwrtError, load
-from .integrate import PacketEnsemble, ode23_packets, ode_symplectic, raytrace_xka, step_packet_xka
+from .integrate import (PacketEnsemble, ode23_packets, ode_symplectic, raytrace_sw, raytrace_xka, rsw_background,
+                        step_packet_xka)
 from .io import read_field, write_field
 from .qg import QGModel, qg2layersw_raytrace, qgsw_raytrace
 from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, FourierScheme, RaytracingScheme, SnapshotPairScheme,
                      SpectralScheme, g2k, grid_U, interpolate, interpolate_U, k2g)
 
 __all__ = [
-    "Context", "SwrtError", "load", "PacketEnsemble", "ode23_packets", "ode_symplectic", "raytrace_xka", "step_packet_xka",
+    "Context", "SwrtError", "load", "PacketEnsemble", "ode23_packets", "ode_symplectic", "raytrace_sw", "raytrace_xka",
+    "rsw_background", "step_packet_xka",
     "read_field", "write_field", "QGModel", "qgsw_raytrace", "qg2layersw_raytrace",
     "BUMP_QG", "BUMP_SW", "DifferenceScheme", "FourierScheme", "RaytracingScheme", "SnapshotPairScheme",
     "SpectralScheme", "g2k", "grid_U", "interpolate", "interpolate_U", "k2g",

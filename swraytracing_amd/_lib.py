@@ -73,6 +73,9 @@ SIGNATURES = {
     "swrt_history_reset": (_INT, [_VP]),
     "swrt_leapfrog": (_INT, [_VP, _P, _P, _I, _D, _I, _D, _D, _INT, _D, _D, _D, _I, _P, _P]),
     "swrt_xka_set_fields": (_INT, [_VP, _P, _I, _D, _D]),
+    "swrt_xka_set_rsw": (_INT, [_VP, _P, _I, _D, _D, _D]),
+    "swrt_xka_get_fields": (_INT, [_VP, _P]),
+    "swrt_xka_grid": (_I, [_VP]),
     "swrt_xka_step": (_INT, [_VP, _P, _I, _D, _D, _D, _I, _I, _P]),
     "swrt_spectral_set_modes": (_INT, [_VP, _P, _I, _I, _D, _D, _D]),
     "swrt_spectral_eval": (_INT, [_VP, _P, _P, _I, _INT, _P]),
@@ -320,6 +323,24 @@ class Context:
                                 (U["u"], U["v"], GradU["u_x"], GradU["u_y"], GradU["v_x"], GradU["v_y"], H)]))
         self._chk(self._L.swrt_xka_set_fields(self._h, _p(planes), nx, float(dx), float(dy)),
                   "swrt_xka_set_fields")
+
+    def xka_set_rsw(self, S, f, Cg, L=2 * np.pi):
+        """Background from an RSW state S = [u v eta] (nx x nx x 3), built on
+        the GPU as ray_trace_sw/raytrace_sw.m:16-52 does."""
+        S = np.asarray(S, dtype=np.float64)
+        if S.ndim != 3 or S.shape[2] != 3 or S.shape[0] != S.shape[1]:
+            raise ValueError("S must be nx x nx x 3")
+        st = _f64(np.stack([S[:, :, i].ravel(order="F") for i in range(3)]))
+        self._chk(self._L.swrt_xka_set_rsw(self._h, _p(st), S.shape[0], float(f), float(Cg), float(L)),
+                  "swrt_xka_set_rsw")
+
+    def xka_get_fields(self):
+        """The current background as (U, GradU, H) dicts/planes (nx x nx)."""
+        nx = int(self._L.swrt_xka_grid(self._h))
+        out = np.empty((7, nx * nx))
+        self._chk(self._L.swrt_xka_get_fields(self._h, _p(out)), "swrt_xka_get_fields")
+        p = [out[i].reshape((nx, nx), order="F") for i in range(7)]
+        return ({"u": p[0], "v": p[1]}, {"u_x": p[2], "u_y": p[3], "v_x": p[4], "v_y": p[5]}, p[6])
 
     def xka_step(self, state, C0, f, dt, nsteps, save_every=0):
         """state: n x 5 [x y k l a]; returns (new state, history frames n x 5 or None)."""

@@ -24,6 +24,7 @@
 #include "swrt_qg.hpp"
 #include "swrt_ode23.hpp"
 #include "swrt_xka.hpp"
+#include "swrt_rsw.hpp"
 #include "swrt_spectral.hpp"
 #include "swrt_diag.hpp"
 
@@ -1395,13 +1396,11 @@ int swrt_leapfrog(swrt_ctx* c, double* x, double* k, int64_t n, double dt, int64
   return SWRT_OK;
 }
 
-int swrt_xka_set_fields(swrt_ctx* c, const double* fields7, int64_t nx, double dx, double dy) {
-  if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
-  if (!fields7) return fail(c, SWRT_ERR_ARG, "fields7 is NULL");
-  if (nx < 6 || nx > 8192) return fail(c, SWRT_ERR_ARG, "nx out of range");
-  if (!(dx > 0) || !(dy > 0)) return fail(c, SWRT_ERR_ARG, "dx, dy must be > 0");
-  HIPCHK(c, hipSetDevice(c->device));
+}  // extern "C"
+
+namespace {
+// (Re)allocate the xka node array for an nx grid.
+int xka_nodes_for(swrt_ctx* c, int64_t nx) {
   const int64_t npad = nx + kPadTot;
   if (c->xka_nx != nx) {
     if (c->xka_nodes) (void)hipFree(c->xka_nodes);
@@ -1410,18 +1409,100 @@ int swrt_xka_set_fields(swrt_ctx* c, const double* fields7, int64_t nx, double d
     HIPCHK(c, hipMalloc(&c->xka_nodes, sizeof(double) * kXkaRec * npad * npad));
     c->xka_nx = nx;
   }
+  return SWRT_OK;
+}
+
+// 7 device planes -> padded node records
+int xka_pack(swrt_ctx* c, const double* dplanes, int64_t nx) {
+  const int64_t npad = nx + kPadTot;
+  hipLaunchKernelGGL(pack_xka_kernel, dim3(nblocks(npad * npad, 256)), dim3(256), 0, c->stream, dplanes, (int)nx,
+                     (int)npad, c->xka_nodes);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int swrt_xka_set_fields(swrt_ctx* c, const double* fields7, int64_t nx, double dx, double dy) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!fields7) return fail(c, SWRT_ERR_ARG, "fields7 is NULL");
+  if (nx < 6 || nx > 8192) return fail(c, SWRT_ERR_ARG, "nx out of range");
+  if (!(dx > 0) || !(dy > 0)) return fail(c, SWRT_ERR_ARG, "dx, dy must be > 0");
+  HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  if ((rc = xka_nodes_for(c, nx))) return rc;
   if ((rc = ensure_scratch(c, sizeof(double) * 7 * nx * nx))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->scratch, fields7, sizeof(double) * 7 * nx * nx, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(pack_xka_kernel, dim3(nblocks(npad * npad, 256)), dim3(256), 0, c->stream,
-                     (const double*)c->scratch, (int)nx, (int)npad, c->xka_nodes);
-  HIPCHK(c, hipGetLastError());
+  if ((rc = xka_pack(c, (const double*)c->scratch, nx))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->xka_dx = dx;
   c->xka_dy = dy;
   return SWRT_OK;
   GUARD_END(c)
 }
+
+int swrt_xka_set_rsw(swrt_ctx* c, const double* state3, int64_t nx, double f, double Cg, double L) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!state3) return fail(c, SWRT_ERR_ARG, "state3 is NULL");
+  if (nx < 8 || nx > 4096 || !is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two, 8..4096");
+  if (!(f != 0.0) || !std::isfinite(f) || !std::isfinite(Cg) || !(L > 0))
+    return fail(c, SWRT_ERR_ARG, "f must be nonzero and finite, L > 0");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_twiddles(c, (int)nx))) return rc;
+  if ((rc = xka_nodes_for(c, nx))) return rc;
+  const int n = (int)nx;
+  const int64_t nn = nx * nx;
+  const size_t zb = sizeof(double2) * nn;
+  // Z: 4 spectra | T: 4 transforms | planes: 7 real (the 3 state planes first)
+  if ((rc = ensure_scratch(c, 8 * zb + sizeof(double) * 7 * nn))) return rc;
+  char* base = (char*)c->scratch;
+  double2* Z = (double2*)base;
+  double2* T = (double2*)(base + 4 * zb);
+  double* planes = (double*)(base + 8 * zb);
+  HIPCHK(c, hipMemcpyAsync(planes, state3, sizeof(double) * 3 * nn, hipMemcpyHostToDevice, c->stream));
+  // g2k.m:8 fft2 of u, v, eta (raytrace_sw.m:26-28)
+  hipLaunchKernelGGL(real_to_complex_kernel, dim3(nblocks(3 * nn, 256)), dim3(256), 0, c->stream, planes, Z, 3 * nn);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = run_fft_pass(c, Z, n, 3, 0))) return rc;
+  if ((rc = run_transpose(c, Z, T, n, 3))) return rc;
+  if ((rc = run_fft_pass(c, T, n, 3, 0))) return rc;
+  // projection + gradients + fulspec (raytrace_sw.m:25-41), then 4 inverse transforms
+  hipLaunchKernelGGL(rsw_spectra_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, n, f, Cg * Cg, Z);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = inverse_2d(c, Z, T, n, 4))) return rc;
+  hipLaunchKernelGGL(rsw_unpack_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, nn, planes);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = xka_pack(c, planes, nx))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->xka_dx = L / (double)nx;
+  c->xka_dy = L / (double)nx;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_xka_get_fields(swrt_ctx* c, double* fields7_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (!fields7_out) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  if (!c->xka_nodes) return fail(c, SWRT_ERR_STATE, "call swrt_xka_set_fields or swrt_xka_set_rsw first");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int64_t nx = c->xka_nx, nn = nx * nx;
+  int rc;
+  if ((rc = ensure_scratch(c, sizeof(double) * 7 * nn))) return rc;
+  hipLaunchKernelGGL(unpack_xka_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, c->xka_nodes, (int)nx,
+                     (int)(nx + kPadTot), (double*)c->scratch);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipMemcpyAsync(fields7_out, c->scratch, sizeof(double) * 7 * nn, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int64_t swrt_xka_grid(const swrt_ctx* c) { return c ? c->xka_nx : -1; }
 
 int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, double dt, int64_t nsteps,
                   int64_t save_every, double* hist5) {

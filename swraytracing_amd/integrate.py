@@ -245,6 +245,33 @@ def raytrace_xka(P0, U, GradU, H, C0, f, dx, dy, dt, nsteps, ctx: Context | None
     from .scheme import default_context
     ctx = ctx or default_context()
     ctx.xka_set_fields(U, GradU, H, dx, dy)
+    return _trace_xka(ctx, P0, C0, f, dt, nsteps)
+
+
+def rsw_background(S, f, Cg, L=2 * np.pi, ctx: Context | None = None):
+    """U, GradU, H of ray_trace_sw/raytrace_sw.m:16-52 from an RSW state
+    S = [u v eta] (nx x nx x 3): the geostrophic projection and its seven
+    k2g run on the GPU, and the result stays there as the xka background
+    (the next raytrace_sw / step_packet_xka call on ctx uses it without a
+    re-upload).  Returns host copies (U dict, GradU dict, H)."""
+    from .scheme import default_context
+    ctx = ctx or default_context()
+    ctx.xka_set_rsw(S, f, Cg, L)
+    return ctx.xka_get_fields()
+
+
+def raytrace_sw(S, f, Cg, P0, dt, nsteps, L=2 * np.pi, ctx: Context | None = None):
+    """ray_trace_sw/raytrace_sw.m end to end on the GPU: the background of
+    :16-52 from S = [u v eta], then the packet loop of :124-130 with
+    step_packet_xka(P, U, GradU, H, C0 = Cg, f, dx, dx, dt) (:22-23, 130).
+    Returns the (np, nsteps) dict of raytrace_xka."""
+    from .scheme import default_context
+    ctx = ctx or default_context()
+    ctx.xka_set_rsw(S, f, Cg, L)
+    return _trace_xka(ctx, P0, Cg, f, dt, nsteps)
+
+
+def _trace_xka(ctx, P0, C0, f, dt, nsteps):
     names = ("x", "y", "k", "l", "a")
     st = np.stack([np.atleast_1d(np.asarray(P0[n], dtype=np.float64)) for n in names], axis=1)
     npk = st.shape[0]
