@@ -195,7 +195,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rebin-every", type=int, default=20, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
-    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile, 3 persistent tile")
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
     ap.add_argument("--blend-mode", type=int, default=0,
                     help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
     ap.add_argument("--cell-sort", type=int, default=0,
@@ -204,6 +204,8 @@ def main():
                     help="tiles per XCD band run as two half-tile workgroups (-1: library default)")
     ap.add_argument("--tail-quarters", type=int, default=0,
                     help="then tiles per XCD band run as four quarter-tile workgroups (with --tail-split)")
+    ap.add_argument("--tile-order", type=int, default=-1,
+                    help="LDS-tiled launches: 1 longest tiles first per XCD band, 0 spatial (-1: library default)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
     ap.add_argument("--timing-every", type=int, default=5,
@@ -231,6 +233,8 @@ def main():
     ctx.set_blend_mode(args.blend_mode)
     if args.tail_split >= 0:
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
+    if args.tile_order >= 0:
+        ctx.set_tile_order(args.tile_order)
     rng = np.random.default_rng(args.seed + rank)
     w = build_workload(ctx, args, rng)
     ctx.packets_set(w["x"], w["k"])
@@ -322,7 +326,7 @@ def main():
                    "pde_dt": "0.25*dx/U0", "leapfrog_dt": f"{0.25 / args.substeps:g}*dx/U0",
                    "steps_per_launch": steps_per_launch, "intervals_per_step": ivs,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
-                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "tail_quarters": args.tail_quarters, "positions": args.positions,
+                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
                    "parallelism": f"packets sharded x{world}, field replicated"},
         # traffic: true HBM bytes per launch (rocprofv3 PMC, profiles/traffic.json), beside the
         # algorithmic bytes per launch that `achieved` is computed from (taps re-read from LDS)

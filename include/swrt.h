@@ -140,9 +140,7 @@ int swrt_set_locality(swrt_ctx* ctx, int64_t rebin_every, int64_t tile);
 /* Packet-kernel variant (same results, bit for bit): 0 = automatic (the
  * LDS-tiled kernel whenever binning is on and nx >= 32), 1 = one lane per
  * packet gathering from the global node array, 2 = LDS-tiled kernel (16x16-
- * cell tiles, field window staged in LDS, in-tile cell sort), 3 = persistent
- * LDS-tiled kernel (one workgroup per CU, next tile's window staged by
- * LDS-DMA and its packets sorted/prefetched while the current tile runs). */
+ * cell tiles, field window staged in LDS, in-tile cell sort). */
 int swrt_set_kernel(swrt_ctx* ctx, int variant);
 
 /* In-tile cell sort of the LDS-tiled kernel (performance only; results are
@@ -158,6 +156,13 @@ int swrt_set_cell_sort(swrt_ctx* ctx, int every_launch);
  * made of smaller work items and the CUs finish closer together.
  * 0, 0 = one workgroup per tile. */
 int swrt_set_tail_split(swrt_ctx* ctx, int halves_per_xcd, int quarters_per_xcd);
+
+/* Tile order of the LDS-tiled kernels (performance only; results are
+ * identical): 1 (default) = each XCD band's tiles longest first (by the
+ * rounds of 512 packets their workgroup runs, spatial order among equals),
+ * so the long tiles start first and the launch ends with short ones;
+ * 0 = spatial order.  Takes effect at the next re-binning (forced). */
+int swrt_set_tile_order(swrt_ctx* ctx, int longest_first);
 
 /* Two-snapshot blend of the LDS-tiled kernel.  0 (default): interpolate each
  * snapshot, then blend (1-alpha)*U1 + alpha*U2 — interpolate_U.m:19-23 in its

@@ -62,6 +62,7 @@ SIGNATURES = {
     "swrt_packets_get": (_INT, [_VP, _P, _P]),
     "swrt_packets_count": (_I, [_VP]),
     "swrt_set_locality": (_INT, [_VP, _I, _I]),
+    "swrt_set_tile_order": (_INT, [_VP, _INT]),
     "swrt_set_kernel": (_INT, [_VP, _INT]),
     "swrt_set_cell_sort": (_INT, [_VP, _INT]),
     "swrt_set_tail_split": (_INT, [_VP, _INT, _INT]),
@@ -261,6 +262,11 @@ class Context:
 
     def set_locality(self, rebin_every=4, tile=0):
         self._chk(self._L.swrt_set_locality(self._h, int(rebin_every), int(tile)), "swrt_set_locality")
+
+    def set_tile_order(self, longest_first=1):
+        """swrt_set_tile_order: LDS-tiled launches take each XCD band's tiles
+        longest first (1, default) or in spatial order (0); same results."""
+        self._chk(self._L.swrt_set_tile_order(self._h, int(longest_first)), "swrt_set_tile_order")
 
     def set_kernel(self, variant=0):
         self._chk(self._L.swrt_set_kernel(self._h, int(variant)), "swrt_set_kernel")

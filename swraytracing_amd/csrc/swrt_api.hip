@@ -20,7 +20,6 @@
 #include "swrt_fft.hpp"
 #include "swrt_kernels.hpp"
 #include "swrt_tile.hpp"
-#include "swrt_persist.hpp"
 #include "swrt_qg.hpp"
 #include "swrt_ode23.hpp"
 #include "swrt_xka.hpp"
@@ -45,6 +44,9 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #ifndef SWRT_QG_GRAPHS
 #define SWRT_QG_GRAPHS 0
 #endif
+#ifndef SWRT_TILE_ORDER
+#define SWRT_TILE_ORDER 1
+#endif
 #ifndef SWRT_TAIL_QUARTERS
 #define SWRT_TAIL_QUARTERS 0
 #endif
@@ -56,7 +58,6 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #endif
 constexpr int kTile = SWRT_TILE;                // LDS tile kernel: cells per tile side
 constexpr int kMargin = SWRT_MARGIN;            // LDS tile kernel: drift margin (cells)
-constexpr int kPersistMargin = 2;                // variant 3 (experiment): its double-buffered windows need the LDS
 constexpr int kTileThreads = SWRT_TILE_THREADS;
 
 struct Slot {
@@ -154,7 +155,7 @@ struct swrt_ctx {
   int* keys = nullptr;   // N
   int* src_idx = nullptr;   // N: source slot of each binned slot (indirect re-binning)
   bool src_pending = false;  // the next tile launch reads its packets through src_idx
-  int* bins = nullptr;   // counts | cursor | starts  (3 * kMaxBins + 1)
+  int* bins = nullptr;   // counts | cursor | starts (kMaxBins + 1) | tile order  (4 * kMaxBins + 1)
   int kernel = 0;        // 0 auto, 1 per-packet global gather, 2 LDS tile kernel
   int nbins = 0;         // bins of the current binning
   int64_t n = 0;
@@ -169,6 +170,7 @@ struct swrt_ctx {
   bool sort_lead = SWRT_SORT_LEAD;  // in-tile sort keys lead by the group-velocity drift
   int tail_split = SWRT_TAIL_SPLIT;  // tiles per XCD band run as two half-tile workgroups (swrt_tile.hpp)
   int tail_quarters = SWRT_TAIL_QUARTERS;  // ... then as four quarter-tile workgroups
+  bool tile_order = SWRT_TILE_ORDER;  // LDS-tiled launches take each XCD band's tiles longest first
   bool qg_graphs = SWRT_QG_GRAPHS;         // replay steady QG steps as hipGraphs
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
@@ -353,8 +355,6 @@ FieldView view_of(const Slot& s) {
   v.inv_px = 1.0 / v.px;
   v.inv_py = 1.0 / v.py;
   v.inv_dx = 1.0 / v.dx;
-  v.pow2x = is_pow2(s.nx);
-  v.pow2y = is_pow2(s.ny_period);
   return v;
 }
 
@@ -374,20 +374,10 @@ int run_fft_pass(swrt_ctx* c, double2* Z, int n, int nb, int inverse) {
   int logn = 0;
   while ((1 << logn) < n) ++logn;
   const int64_t nvec = (int64_t)n * nb;
-#ifndef SWRT_FFT_RADIX8
-  // radix-2 Stockham, 256 lanes per vector (measured faster than the radix-8
-  // register variant below at 512: 8.8 vs 9.7 us per 4-transform pass)
+  // radix-2 Stockham, 256 lanes per vector (measured faster than a radix-8
+  // register variant at 512: 8.8 vs 9.7 us per 4-transform pass)
   const size_t lds = sizeof(double2) * 2 * n;
   hipLaunchKernelGGL(fft_vec_kernel, dim3((unsigned)nvec), dim3(256), lds, c->stream, Z, n, logn, c->tw, inverse);
-#else
-  // mixed-radix Stockham: n/8 lanes per vector, 256- (or n/8-) lane blocks
-  const int tpv = n / 8;
-  const int block = tpv > 256 ? tpv : 256;
-  const int vpb = block / tpv;
-  const size_t lds = sizeof(double2) * 8 * block;
-  hipLaunchKernelGGL(fft8_kernel, dim3((unsigned)((nvec + vpb - 1) / vpb)), dim3(block), lds, c->stream, Z, n, logn,
-                     (int)nvec, c->tw, inverse);
-#endif
   HIPCHK(c, hipGetLastError());
   return SWRT_OK;
 }
@@ -527,9 +517,13 @@ int launch_shape(const swrt_ctx* c, unsigned ntiles, unsigned* extra) {
   return (int)(h | (q << 16));
 }
 
+// Longest-first tile order of the LDS-tiled launches, written by every
+// re-binning's scan (bin_scan_kernel) beside the tile starts.
+int* tile_order_of(swrt_ctx* c) { return c->bins + 3 * kMaxBins + 1; }
+
 bool use_tile_kernel(const swrt_ctx* c) {
   if (c->rebin_every <= 0) return false;
-  if (c->kernel == 2 || c->kernel == 3) return true;
+  if (c->kernel == 2) return true;
   return c->kernel == 0 && c->slot[0].nx >= 2 * kTile;
 }
 
@@ -552,7 +546,7 @@ int rebin(swrt_ctx* c, bool indirect) {
   const FieldView v = view_of(s);
   BinGeom g;
   g.dx = v.dx; g.px = v.px; g.py = v.py; g.inv_px = v.inv_px; g.inv_py = v.inv_py; g.inv_dx = v.inv_dx;
-  g.pow2x = v.pow2x; g.pow2y = v.pow2y; g.nx = v.nx;
+  g.nx = v.nx;
   g.tile = tile_cells(c, s.nx);
   g.ntx = (int)((s.nx + g.tile - 1) / g.tile);
   const int nbins = g.ntx * g.ntx;
@@ -567,7 +561,7 @@ int rebin(swrt_ctx* c, bool indirect) {
   }
   c->keys_fresh = false;
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins,
-                     c->bins + 2 * kMaxBins);
+                     c->bins + 2 * kMaxBins, c->tile_order ? tile_order_of(c) : nullptr, kTileThreads);
   HIPCHK(c, hipGetLastError());
   c->counts_zero = true;
   if (indirect) {
@@ -605,6 +599,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   t.k_out = c->dk2;
   t.perm_out = c->perm2;
   t.starts = c->bins + 2 * kMaxBins;
+  t.order = c->tile_order ? tile_order_of(c) : nullptr;
   t.ntx = (int)((a.f0.nx + kTile - 1) / kTile);
   const unsigned grid = (unsigned)(t.ntx * t.ntx);
   // half-tile workgroups at the end of each XCD band (swrt_tile.hpp wg_work)
@@ -629,20 +624,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     t.next_keys = c->keys;
     t.next_counts = c->bins;
   }
-  if (c->kernel == 3) {
-    // persistent: one 1024-lane workgroup per CU walking a contiguous run of tiles
-    int ncu = 256;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, c->device) == hipSuccess && prop.multiProcessorCount > 0)
-      ncu = prop.multiProcessorCount;
-    const int tpw = (int)((grid + ncu - 1) / ncu);
-    const unsigned pgrid = (unsigned)((grid + tpw - 1) / tpw);
-    t.split = 0;  // its own tile walk
-    if (a.nslots == 2)
-      launch_k(c, tile_persist_kernel<true, kTile, kPersistMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
-    else
-      launch_k(c, tile_persist_kernel<false, kTile, kPersistMargin, 1024>, dim3(pgrid), dim3(1024), t, tpw);
-  } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
+  if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
     launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(wgrid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
     if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free))
@@ -691,7 +673,7 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
     if (c->blend_mode == 1 && nslots == 2 && use_tile_kernel(c)) chunk = 1;  // alpha fixed per launch
     if (c->rebin_every > 0) {
       if (!c->bin_valid || c->steps_since_bin >= c->rebin_every) {
-        int rc = rebin(c, use_tile_kernel(c) && c->kernel != 3);
+        int rc = rebin(c, use_tile_kernel(c));
         if (rc) return rc;
       }
       chunk = std::min<int64_t>(chunk, c->rebin_every - c->steps_since_bin);
@@ -716,7 +698,7 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
 // across a re-binning), else one interval at a time through run_advance.
 int run_advance_intervals(swrt_ctx* c, int nint, const double* hs, int64_t nsub, double f, double gH,
                           double alpha0, double dalpha, double bump, int64_t save_every) {
-  const bool fused = use_tile_kernel(c) && c->kernel != 3 && c->blend_mode == 0 && c->rebin_every > 0 &&
+  const bool fused = use_tile_kernel(c) && c->blend_mode == 0 && c->rebin_every > 0 &&
                      c->rebin_every % nsub == 0 && nsub <= kMaxStepsPerLaunch;
   const int64_t fpi = save_every > 0 ? nsub / save_every : 0;  // frames per interval
   int i0 = 0;
@@ -1135,7 +1117,7 @@ int swrt_interpolate(swrt_ctx* c, const double* F, int64_t nx, int64_t nyF, doub
   HIPCHK(c, hipMemcpyAsync(dyp, y, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
   const double py = (double)nyF;
   hipLaunchKernelGGL(interp1_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, dF, (int)nx, py,
-                     1.0 / py, (int)is_pow2(nyF), dx, dy, bump, dxp, dyp, n, dout);
+                     1.0 / py, dx, dy, bump, dxp, dyp, n, dout);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1199,7 +1181,7 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
     HIPCHK(c, hipMalloc(&c->src_idx, sizeof(int) * n));
     c->cap = n;
   }
-  if (!c->bins) HIPCHK(c, hipMalloc(&c->bins, sizeof(int) * (3 * kMaxBins + 1)));
+  if (!c->bins) HIPCHK(c, hipMalloc(&c->bins, sizeof(int) * (4 * kMaxBins + 1)));
   c->n = n;
   if (n > 0) {
     HIPCHK(c, hipMemcpyAsync(c->dx, x, sizeof(double) * 2 * n, hipMemcpyHostToDevice, c->stream));
@@ -1274,9 +1256,17 @@ int swrt_set_tail_split(swrt_ctx* c, int halves_per_xcd, int quarters_per_xcd) {
   return SWRT_OK;
 }
 
+int swrt_set_tile_order(swrt_ctx* c, int longest_first) {
+  if (!c) return SWRT_ERR_ARG;
+  if (longest_first != 0 && longest_first != 1) return fail(c, SWRT_ERR_ARG, "tile order must be 0 or 1");
+  c->tile_order = longest_first != 0;
+  c->bin_valid = false;  // the next launch re-bins, which writes the order
+  return SWRT_OK;
+}
+
 int swrt_set_kernel(swrt_ctx* c, int variant) {
   if (!c) return SWRT_ERR_ARG;
-  if (variant < 0 || variant > 3) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0..3");
+  if (variant < 0 || variant > 2) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0..2");
   c->kernel = variant;
   c->bin_valid = false;
   c->keys_fresh = false;
@@ -1547,7 +1537,6 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   a.inv_dy = 1.0 / a.dy;
   a.px = a.py = (double)c->xka_nx;
   a.inv_px = a.inv_py = 1.0 / (double)c->xka_nx;
-  a.pow2x = a.pow2y = is_pow2(c->xka_nx);
   a.C0sq = C0 * C0;
   a.f = f;
   a.f2 = f * f;
@@ -1564,7 +1553,7 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   if (binned) {
     BinGeom g;
     g.dx = a.dx; g.px = a.px; g.py = a.py; g.inv_px = a.inv_px; g.inv_py = a.inv_py; g.inv_dx = a.inv_dx;
-    g.pow2x = a.pow2x; g.pow2y = a.pow2y; g.nx = a.nx;
+    g.nx = a.nx;
     g.tile = 8;
     while ((a.nx + g.tile - 1) / g.tile > 64) g.tile *= 2;
     g.ntx = (a.nx + g.tile - 1) / g.tile;

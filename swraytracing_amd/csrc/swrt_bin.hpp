@@ -17,7 +17,7 @@ namespace swrt {
 
 struct BinGeom {
   double dx, px, py, inv_px, inv_py, inv_dx;
-  int pow2x, pow2y, nx;
+  int nx;
   int tile;     // cells per tile side
   int ntx;      // tiles per side
 };
@@ -55,11 +55,20 @@ __global__ void __launch_bounds__(256) bin_count_kernel(BinGeom g, const double*
   }
 }
 
+constexpr int kOrderBuckets = 16;  // workgroup rounds told apart by the tile order
+
 // Pass 2: exclusive scan of counts -> cursor (single workgroup, nbins <= 16384).
 // Also clears counts (each thread its own bins, after reading them) so the next
 // fused count in the tile kernel starts from zero without a memset launch.
+// order != NULL (nbins % 8 == 0): the tile order of the LDS-tiled launches
+// (tile_order_of).  Each of the 8 XCD bands of nbins/8 consecutive tiles is
+// listed longest first — by the rounds ceil(count / lanes) its workgroup of
+// `lanes` threads runs (one packet per lane per round), spatial order within
+// a round count — so a band's long tiles start first and its tail is made of
+// the short ones (longest-processing-time-first list scheduling).  A stable
+// counting sort per band by one wavefront (ballots).
 __global__ void __launch_bounds__(1024) bin_scan_kernel(int* counts, int nbins, int* cursor,
-                                                        int* starts) {
+                                                        int* starts, int* order = nullptr, int lanes = 512) {
   __shared__ int part[1024];
   const int per = (nbins + 1023) / 1024;
   const int b0 = threadIdx.x * per;
@@ -88,6 +97,42 @@ __global__ void __launch_bounds__(1024) bin_scan_kernel(int* counts, int nbins, 
     }
   }
   if (threadIdx.x == 1023) starts[nbins] = part[1023];
+  if (order == nullptr) return;
+  __syncthreads();  // every start written (workgroup scope)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (nbins % 8 != 0) {
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) order[b] = b;
+    return;
+  }
+  if (wave >= 8) return;
+  const int tpx = nbins / 8, base = wave * tpx;
+  const uint64_t below = (1ull << lane) - 1;
+  int cnt[kOrderBuckets];
+#pragma unroll
+  for (int v = 0; v < kOrderBuckets; ++v) cnt[v] = 0;
+  for (int c0 = 0; c0 < tpx; c0 += 64) {
+    const int i = c0 + lane;
+    const int r = i < tpx ? min((starts[base + i + 1] - starts[base + i] + lanes - 1) / lanes, kOrderBuckets - 1) : -1;
+#pragma unroll
+    for (int v = 0; v < kOrderBuckets; ++v) cnt[v] += __popcll(__ballot(r == v));
+  }
+  int acc = 0;
+#pragma unroll
+  for (int v = kOrderBuckets - 1; v >= 0; --v) {  // longest first
+    const int c = cnt[v];
+    cnt[v] = acc;
+    acc += c;
+  }
+  for (int c0 = 0; c0 < tpx; c0 += 64) {
+    const int i = c0 + lane;
+    const int r = i < tpx ? min((starts[base + i + 1] - starts[base + i] + lanes - 1) / lanes, kOrderBuckets - 1) : -1;
+#pragma unroll
+    for (int v = 0; v < kOrderBuckets; ++v) {
+      const uint64_t m = __ballot(r == v);
+      if (r == v) order[base + cnt[v] + __popcll(m & below)] = base + i;
+      cnt[v] += __popcll(m);
+    }
+  }
 }
 
 // Pass 3: scatter.  Each block ranks its packets per bin in LDS, reserves one

@@ -47,140 +47,6 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(double2* data, int n, int 
   for (int i = threadIdx.x; i < n; i += blockDim.x) v[i] = xa[i];
 }
 
-// ---------------------------------------------------------------------------
-// Mixed-radix (8, then 4/2) Stockham pass: the production 1-D batched FFT.
-// n/8 lanes per vector, each holding 8 points per stage, so a 512-point
-// transform is 3 radix-8 stages (3 LDS exchanges) instead of 9 radix-2 ones.
-// Stage (R, Ls): butterfly j < n/R reads x[j + t*n/R] * w^(t*k) (k = j mod
-// Ls, w = exp(-+2 pi i/(Ls*R))), does an R-point DFT and writes
-// y[(j - k)*R + k + t*Ls].  Reads of a stage all complete before its writes
-// (barrier), so one LDS buffer per vector suffices.  Twiddles come from the
-// exp(-2 pi i m/n) table (m < n/2; the second half by symmetry).
-__device__ __forceinline__ double2 c_add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ double2 c_sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ double2 c_mul(double2 a, double2 w) {
-  return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
-}
-// a * (-i) forward, a * (+i) inverse
-__device__ __forceinline__ double2 c_mi(double2 a, bool inv) {
-  return inv ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
-}
-
-__device__ __forceinline__ void dft2(double2& a, double2& b) {
-  const double2 t = a;
-  a = c_add(t, b);
-  b = c_sub(t, b);
-}
-
-__device__ __forceinline__ void dft4(double2& a0, double2& a1, double2& a2, double2& a3, bool inv) {
-  const double2 s02 = c_add(a0, a2), d02 = c_sub(a0, a2);
-  const double2 s13 = c_add(a1, a3), d13 = c_mi(c_sub(a1, a3), inv);
-  a0 = c_add(s02, s13);
-  a2 = c_sub(s02, s13);
-  a1 = c_add(d02, d13);
-  a3 = c_sub(d02, d13);
-}
-
-__device__ __forceinline__ void dft8(double2 v[8], bool inv) {
-  double2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
-  double2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
-  dft4(e0, e1, e2, e3, inv);
-  dft4(o0, o1, o2, o3, inv);
-  constexpr double c = 0.70710678118654752440;
-  // W8^1, W8^2, W8^3 (conjugated for the inverse)
-  o1 = inv ? make_double2(c * (o1.x - o1.y), c * (o1.x + o1.y)) : make_double2(c * (o1.x + o1.y), c * (o1.y - o1.x));
-  o2 = c_mi(o2, inv);
-  o3 = inv ? make_double2(-c * (o3.x + o3.y), c * (o3.x - o3.y)) : make_double2(c * (o3.y - o3.x), -c * (o3.x + o3.y));
-  v[0] = c_add(e0, o0); v[4] = c_sub(e0, o0);
-  v[1] = c_add(e1, o1); v[5] = c_sub(e1, o1);
-  v[2] = c_add(e2, o2); v[6] = c_sub(e2, o2);
-  v[3] = c_add(e3, o3); v[7] = c_sub(e3, o3);
-}
-
-__device__ __forceinline__ double2 tw_at(const double2* tw, int m, int n, bool inv) {
-  double2 w = m < (n >> 1) ? tw[m] : make_double2(-tw[m - (n >> 1)].x, -tw[m - (n >> 1)].y);
-  if (inv) w.y = -w.y;
-  return w;
-}
-
-// One Stockham stage split into its read, compute and write phases so the
-// first stage can read straight from global memory and the last (radix-8)
-// stage write straight back (both coalesced: lane jt touches jt + m*(n/8)).
-template <int R>
-__device__ __forceinline__ void st_read(const double2* src, int n, int jt, int tpv, double2 v[8]) {
-  constexpr int B = 8 / R;
-  const int Ns = n / R;
-#pragma unroll
-  for (int u = 0; u < B; ++u)
-#pragma unroll
-    for (int t = 0; t < R; ++t) v[u * R + t] = src[jt + u * tpv + t * Ns];
-}
-
-template <int R>
-__device__ __forceinline__ void st_compute_write(double2* dst, int n, int Ls, int jt, int tpv, const double2* tw,
-                                                 bool inv, double2 v[8]) {
-  constexpr int B = 8 / R;
-#pragma unroll
-  for (int u = 0; u < B; ++u) {
-    const int j = jt + u * tpv;
-    const int k = j & (Ls - 1);
-    double2* w = v + u * R;
-    if (Ls > 1) {
-      const int step = n / (Ls * R);
-#pragma unroll
-      for (int t = 1; t < R; ++t) w[t] = c_mul(w[t], tw_at(tw, t * k * step, n, inv));
-    }
-    if constexpr (R == 2) dft2(w[0], w[1]);
-    if constexpr (R == 4) dft4(w[0], w[1], w[2], w[3], inv);
-    if constexpr (R == 8) dft8(w, inv);
-    const int d = (j - k) * R + k;
-#pragma unroll
-    for (int t = 0; t < R; ++t) dst[d + t * Ls] = w[t];
-  }
-}
-
-// Batched length-n complex FFT over contiguous vectors data[b*n + i], n a
-// power of two >= 8; blockDim.x = max(256, n/8), (blockDim/(n/8)) vectors per
-// block, dynamic LDS = blockDim * 8 * 16 B.  Radix 2 or 4 first (n not a
-// power of 8), then radix 8; LDS only between stages.
-__global__ void __launch_bounds__(512) fft8_kernel(double2* data, int n, int logn, int nvec, const double2* tw,
-                                                   int inverse) {
-  extern __shared__ double2 sbuf8[];
-  const int tpv = n >> 3;
-  const int vpb = blockDim.x / tpv;
-  const int lv = threadIdx.x / tpv, jt = threadIdx.x % tpv;
-  const int64_t vec = (int64_t)blockIdx.x * vpb + lv;
-  const bool live = vec < nvec;
-  double2* buf = sbuf8 + (size_t)lv * n;
-  double2* g = data + (live ? vec : 0) * n;
-  const bool inv = inverse != 0;
-  const int rem = logn % 3, n8 = logn / 3;
-  const int nst = n8 + (rem ? 1 : 0);
-  double2 v[8];
-  int Ls = 1;
-  for (int s = 0; s < nst; ++s) {
-    const int R = (s == 0 && rem == 1) ? 2 : ((s == 0 && rem == 2) ? 4 : 8);
-    const bool last = s == nst - 1;
-    if (s > 0) __syncthreads();  // previous stage's writes visible
-    if (s == 0) {
-      if (live) {
-        if (R == 2) st_read<2>(g, n, jt, tpv, v);
-        else if (R == 4) st_read<4>(g, n, jt, tpv, v);
-        else st_read<8>(g, n, jt, tpv, v);
-      }
-    } else {
-      st_read<8>(buf, n, jt, tpv, v);
-      __syncthreads();  // every lane has read before the buffer is overwritten
-    }
-    double2* dst = last ? g : buf;
-    if (live || !last) {
-      if (R == 2) st_compute_write<2>(dst, n, Ls, jt, tpv, tw, inv, v);
-      else if (R == 4) st_compute_write<4>(dst, n, Ls, jt, tpv, tw, inv, v);
-      else st_compute_write<8>(dst, n, Ls, jt, tpv, tw, inv, v);
-    }
-    Ls *= R;
-  }
-}
 
 // out[c + n*r] = in[r + n*c] for batch of nb n x n complex matrices.
 __global__ void transpose_kernel(const double2* in, double2* out, int n) {

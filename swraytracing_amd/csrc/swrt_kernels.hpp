@@ -29,7 +29,6 @@ struct FieldView {
   double dx;            // L / nx (interpolate.m dx = dy = h)
   double px, py;        // mod periods of x/dx and y/dy (nx, ny_period)
   double inv_px, inv_py;
-  int pow2x, pow2y;     // period is a power of two: a/m == a*(1/m) exactly
   double inv_dx;        // RN(1/dx): locality keys, and x/dx via div_rn (correctly rounded)
 };
 
@@ -51,17 +50,25 @@ __device__ __forceinline__ double div_rn(double a, double b, double rb) {
 // interpolate.m:21-31 — xl = mod(x/dx, n); i0 = 1 + floor(xl); a = 1 + xl - i0.
 // Returns the 0-based cell reduced mod nx and the fractional offset a.
 // inv_dx = RN(1/dx) and inv_period = RN(1/period) from the host.
+// q/period is div_rn for every period: for a power of two inv_period is
+// exact, q0 = q*inv_period is already the quotient and the correction adds
+// r = 0 (a zero of either sign gives the same cell and offset), so no
+// per-lane select between a plain multiply and div_rn is needed.
 __device__ __forceinline__ int cell_frac(double x, double dx, double inv_dx, double period,
-                                         double inv_period, int pow2, int nx, double& a) {
+                                         double inv_period, int nx, double& a) {
   const double q = div_rn(x, dx, inv_dx);
-  const double r = pow2 ? q * inv_period : div_rn(q, period, inv_period);
+  const double r = div_rn(q, period, inv_period);
   const double xl = q - floor(r) * period;   // MATLAB mod (a - floor(a/m)*m)
   const double fl = floor(xl);
   a = (1.0 + xl) - (1.0 + fl);
   // NaN/Inf positions: keep the index in range (the result is NaN anyway).
   int c = (fl >= 0.0 && fl <= period) ? (int)fl : 0;
-  c = c % nx;  // i0 may equal the period after round-up of mod, and the
-               // 2-layer y-period is 2*nx (interpolate.m:45-46 wrap by nx)
+  // c mod nx: i0 may equal the period after round-up of mod, and the 2-layer
+  // y-period is 2*nx (interpolate.m:45-46 wrap by nx).  c <= period, so one
+  // conditional subtract covers periods up to 2*nx; wider generic grids take
+  // the (rare, divergent) integer remainder.
+  if (c >= nx) c -= nx;
+  if (c >= nx) c %= nx;
   return c;
 }
 
@@ -144,8 +151,8 @@ struct Stencil {
 __device__ __forceinline__ void stencil_at(const FieldView& fv, double x, double y, double bump,
                                            Stencil& s) {
   double ax, ay;
-  s.ic = cell_frac(x, fv.dx, fv.inv_dx, fv.px, fv.inv_px, fv.pow2x, fv.nx, ax);
-  s.jc = cell_frac(y, fv.dx, fv.inv_dx, fv.py, fv.inv_py, fv.pow2y, fv.nx, ay);
+  s.ic = cell_frac(x, fv.dx, fv.inv_dx, fv.px, fv.inv_px, fv.nx, ax);
+  s.jc = cell_frac(y, fv.dx, fv.inv_dx, fv.py, fv.inv_py, fv.nx, ay);
   lagrange_w(ax, bump, s.wx);
   lagrange_w(ay, bump, s.wy);
 }
@@ -314,12 +321,19 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
   if (p >= a.n) return;
   double x0 = a.x[p], y0 = a.x[a.n + p];
   double k0 = a.k[p], l0 = a.k[a.n + p];
+  // phi1(x0, k0, dt/2): x + (dt/2) * (gH*k/omega(k))   (ode_symplectic.m:10-16).
+  // The drift after a kick and the drift that opens the next step use the
+  // same k, so the increment is computed once per step (same bits).
+  double hcx, hcy;
+  {
+    const double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
+    hcx = a.half * (a.gH * k0 / w);
+    hcy = a.half * (a.gH * l0 / w);
+  }
   for (int s = 0; s < a.nsteps; ++s) {
     const int64_t sg = a.s0 + s;
-    // phi1(x0, k0, dt/2): x + (dt/2) * (gH*k/omega(k))   (ode_symplectic.m:10-16)
-    double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
-    const double x1 = x0 + a.half * (a.gH * k0 / w);
-    const double y1 = y0 + a.half * (a.gH * l0 / w);
+    const double x1 = x0 + hcx;
+    const double y1 = y0 + hcy;
     // phi2(x1, k1, dt): U and (grad U)^T k at x1  (ode_symplectic.m:18-21)
     double I[kRec];
     eval_flow_t<TWO>(a.f0, a.f1, a.alpha0 + (double)sg * a.dalpha, x1, y1, a.bump, I);
@@ -328,9 +342,11 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
     const double k2 = k0 - a.dt * (I[2] * k0 + I[4] * l0);  // RaytracingScheme.m:14
     const double l2 = l0 - a.dt * (I[3] * k0 + I[5] * l0);  // RaytracingScheme.m:15
     // phi1(x2, k2, dt/2)
-    w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
-    x0 = x2 + a.half * (a.gH * k2 / w);
-    y0 = y2 + a.half * (a.gH * l2 / w);
+    const double w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
+    hcx = a.half * (a.gH * k2 / w);
+    hcy = a.half * (a.gH * l2 / w);
+    x0 = x2 + hcx;
+    y0 = y2 + hcy;
     k0 = k2;
     l0 = l2;
     if (a.hist_x != nullptr && ((sg + 1) % a.save_every) == 0) {
@@ -361,16 +377,15 @@ __global__ void __launch_bounds__(256) eval_kernel(FieldView f0, FieldView f1, i
 // Generic interpolate(x, y, F, dx, dy) of one nx x nyF column-major grid
 // (reads only columns < nx, as F(ig,jg) with jg <= nx does).
 __global__ void __launch_bounds__(256) interp1_kernel(const double* F, int nx, double pyF,
-                                                      double inv_py, int pow2y, double dx,
+                                                      double inv_py, double dx,
                                                       double dy, double bump, const double* x,
                                                       const double* y, int64_t n, double* out) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const double px = (double)nx;
-  const int pow2x = (nx & (nx - 1)) == 0;
   double ax, ay;
-  const int ic = cell_frac(x[p], dx, 1.0 / dx, px, 1.0 / px, pow2x, nx, ax);
-  const int jc = cell_frac(y[p], dy, 1.0 / dy, pyF, inv_py, pow2y, nx, ay);
+  const int ic = cell_frac(x[p], dx, 1.0 / dx, px, 1.0 / px, nx, ax);
+  const int jc = cell_frac(y[p], dy, 1.0 / dy, pyF, inv_py, nx, ay);
   double wx[kNT], wy[kNT];
   lagrange_w(ax, bump, wx);
   lagrange_w(ay, bump, wy);

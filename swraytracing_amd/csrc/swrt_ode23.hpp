@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, in
   __shared__ int hist[NB];
   __shared__ int kr[MAXB];
   int pbeg, pend;
-  const int tile = wg_work_range(starts, split, pbeg, pend);
+  const int tile = wg_work_range(starts, nullptr, split, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int tid = threadIdx.x;
   for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
   __shared__ double2 win[NCH * WNP];
   __shared__ double red[NT / 64];
   int pbeg, pend;
-  const int tile = wg_work_range(starts, a.split, pbeg, pend);
+  const int tile = wg_work_range(starts, nullptr, a.split, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int nx = a.f0.nx;
   stage_window_regs<TWO, T, M, NT, WS, V5>(a.f0, a.f1, ox, oy, win);

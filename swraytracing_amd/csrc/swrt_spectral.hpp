@@ -147,10 +147,17 @@ __global__ void __launch_bounds__(kSpecThreads) spectral_leapfrog_kernel(ModeGri
   if (p >= n) return;
   double x0 = xs[p], y0 = xs[n + p], k0 = ks[p], l0 = ks[n + p];
   const double half = dt / 2;
+  // drift increment of the current k: shared by a step's closing drift and
+  // the next step's opening drift (same k, same bits)
+  double hcx, hcy;
+  {
+    const double w = sqrt(f2 + gH * (k0 * k0 + l0 * l0));
+    hcx = half * (gH * k0 / w);
+    hcy = half * (gH * l0 / w);
+  }
   for (int s = 0; s < nsteps; ++s) {
-    double w = sqrt(f2 + gH * (k0 * k0 + l0 * l0));
-    const double x1 = x0 + half * (gH * k0 / w);
-    const double y1 = y0 + half * (gH * l0 / w);
+    const double x1 = x0 + hcx;
+    const double y1 = y0 + hcy;
     double d[5], I[6];
     spectral_sums<T>(g, x1, y1, d);
     psi_to_flow(d, I);
@@ -158,9 +165,11 @@ __global__ void __launch_bounds__(kSpecThreads) spectral_leapfrog_kernel(ModeGri
     const double y2 = y1 + dt * I[1];
     const double k2 = k0 - dt * (I[2] * k0 + I[4] * l0);
     const double l2 = l0 - dt * (I[3] * k0 + I[5] * l0);
-    w = sqrt(f2 + gH * (k2 * k2 + l2 * l2));
-    x0 = x2 + half * (gH * k2 / w);
-    y0 = y2 + half * (gH * l2 / w);
+    const double w = sqrt(f2 + gH * (k2 * k2 + l2 * l2));
+    hcx = half * (gH * k2 / w);
+    hcy = half * (gH * l2 / w);
+    x0 = x2 + hcx;
+    y0 = y2 + hcy;
     k0 = k2;
     l0 = l2;
   }

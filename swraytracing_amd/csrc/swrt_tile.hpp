@@ -33,6 +33,7 @@ struct TileArgs {
   double* k_out;
   int* perm_out;
   const int* starts;     // ntiles + 1 packet offsets of the tiles
+  const int* order;      // non-NULL: band position -> tile (bin_scan_kernel's longest-first order)
   int ntx;               // tiles per side
   int* next_keys;        // non-NULL: write each output packet's tile (next binning) ...
   int* next_counts;      // ... and add it to the per-tile counts (zeroed by the host)
@@ -54,21 +55,6 @@ struct TileArgs {
   const double* ivn[kMaxIntervals + 1];
   double ivdt[kMaxIntervals];
 };
-
-// Packet-state stores of the tile kernel.  SWRT_WT_STORES: write-through
-// (`sc1`, agent-scope relaxed atomic stores) so the launch ends with no dirty
-// L2 lines of its 36 MB of output to write back before the next launch.
-#ifndef SWRT_WT_STORES
-#define SWRT_WT_STORES 0
-#endif
-template <typename V>
-__device__ __forceinline__ void st_out(V* p, V v) {
-#if SWRT_WT_STORES
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
-}
 
 // Interval views by constant-index selects: a runtime index into the
 // by-value kernel argument would copy the whole argument to scratch.
@@ -94,7 +80,8 @@ __device__ __forceinline__ double iv_dt(const TileArgs& ta, int i) {
 // dispatcher hands out ever smaller work items as CUs free up at the end of
 // the launch, which narrows the spread of CU finish times (the launch ends
 // with its slowest CU).  grid = ntiles + 8*(h + 3q).
-__device__ __forceinline__ int wg_work_range(const int* starts, int split, int& pbeg, int& pend) {
+__device__ __forceinline__ int wg_work_range(const int* starts, const int* order, int split, int& pbeg,
+                                             int& pend) {
   const int b = (int)blockIdx.x, nb = (int)gridDim.x;
   int tile, part = 0, nparts = 1;
   if (split > 0) {
@@ -117,6 +104,7 @@ __device__ __forceinline__ int wg_work_range(const int* starts, int split, int& 
   } else {
     tile = (int)xcd_block(b, nb);
   }
+  if (order != nullptr) tile = order[tile];  // the tile at this band position
   pbeg = starts[tile];
   pend = starts[tile + 1];
   if (nparts > 1) {
@@ -128,7 +116,7 @@ __device__ __forceinline__ int wg_work_range(const int* starts, int split, int& 
 }
 
 __device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend) {
-  return wg_work_range(ta.starts, ta.split, pbeg, pend);
+  return wg_work_range(ta.starts, ta.order, ta.split, pbeg, pend);
 }
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
@@ -139,50 +127,12 @@ __device__ __forceinline__ int ring_diff(int a, int b, int n) {
   return d;
 }
 
-template <int T, int M>
-struct WinGeom {
-  static constexpr int W = T + 5 + 2 * M;
-  static constexpr int WN = W * W;
-  static constexpr int WNP = (WN + 63) / 64 * 64;  // whole wavefronts per chunk (DMA lanes)
-};
-
-// Stage tile (ox, oy)'s window for `nch` chunks into buf (chunk-major, WNP
-// nodes per chunk) by LDS-DMA: wave w, chunk c covers nodes e0..e0+63 with
-// destination buf[c*WNP + e0] + lane*16 (lane-linear, as the DMA requires).
-template <bool TWO, int T, int M>
-__device__ __forceinline__ void stage_window_dma(const StepArgs& a, int ox, int oy, double2* buf) {
-  using G = WinGeom<T, M>;
-  constexpr int NCH = TWO ? 6 : 3;
-  const int nx = a.f0.nx, npad = a.f0.npad;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int nwaves = blockDim.x >> 6;
-  constexpr int NJOBS = NCH * (G::WNP / 64);
-  for (int job = wave; job < NJOBS; job += nwaves) {
-    const int c = job / (G::WNP / 64);
-    const int e0 = (job % (G::WNP / 64)) * 64;
-    int e = e0 + lane;
-    if (e >= G::WN) e = G::WN - 1;  // padding lanes re-read a valid node
-    const int wi = e / G::W, wj = e % G::W;
-    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
-    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
-    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec + 2 * (c % 3);
-    const double* base = (c < 3) ? a.f0.nodes : a.f1.nodes;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(base + src),
-                                     (__attribute__((address_space(3))) void*)(buf + c * G::WNP + e0),
-                                     16, 0, 0);
-  }
-}
-
 // ds_read_b128 serves a wave64 in four 16-lane groups {0-3,12-15,20-27},
 // {4-11,16-19,28-31} and the same +32 (MI355X_MICROARCH.md §LDS); only lanes
 // of one group can conflict.  Rank of lane `lane` within its wave's run of 64
 // cell-sorted packets, so that each group takes 16 consecutive packets (few
 // distinct, near-adjacent nodes) instead of three scattered runs of 4-8.
 __device__ __forceinline__ int b128_lane_rank(int lane) {
-#ifdef SWRT_NO_LANE_REMAP
-  return lane;
-#else
   const int h = lane & 32, t = lane & 31;
   int k;
   if (t < 4) k = t;
@@ -192,7 +142,6 @@ __device__ __forceinline__ int b128_lane_rank(int lane) {
   else if (t < 28) k = 8 + (t - 20);
   else k = t;
   return h + k;
-#endif
 }
 
 template <bool TWO, int W, int WN>
@@ -201,26 +150,6 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
 #pragma unroll
   for (int f = 0; f < kRec; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
   const double2* p = lds + node0;
-#ifdef SWRT_GATHER_SPLIT
-  // one snapshot at a time: 3 (not 6) 16-B reads in flight per tap
-#pragma unroll
-  for (int sn = 0; sn < (TWO ? 2 : 1); ++sn) {
-    double* o = sn == 0 ? o0 : o1;
-    const double2* q = p + 3 * sn * WN;
-#pragma unroll
-    for (int i = 0; i < kNT; ++i) {
-#pragma unroll
-      for (int j = 0; j < kNT; ++j) {
-        const int e = i * W + j;
-        const double wij = s.wx[i] * s.wy[j];
-        const double2 a0 = q[0 * WN + e], a1 = q[1 * WN + e], a2 = q[2 * WN + e];
-        o[0] = o[0] + wij * a0.x; o[1] = o[1] + wij * a0.y;
-        o[2] = o[2] + wij * a1.x; o[3] = o[3] + wij * a1.y;
-        o[4] = o[4] + wij * a2.x; o[5] = o[5] + wij * a2.y;
-      }
-    }
-  }
-#else
 #pragma unroll
   for (int i = 0; i < kNT; ++i) {
 #pragma unroll
@@ -239,7 +168,6 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
       }
     }
   }
-#endif
 }
 
 // gather6_lds for fields with v_y == -u_x bit for bit (Slot::div_free):
@@ -370,14 +298,10 @@ __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false>
 __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
-#ifdef SWRT_WIN_STRIDE
-  constexpr int WS = SWRT_WIN_STRIDE;  // LDS row stride in nodes (>= W)
-#else
   // row stride = 12 (mod 16) nodes: any 4x4 block of window nodes falls on
   // 16 distinct ds_read_b128 bank quads (node n -> quad (n mod 16)), so lanes
   // of one 16-lane group reading a few neighbouring nodes never conflict
   constexpr int WS = W + ((12 - W % 16) + 16) % 16;
-#endif
   constexpr int WNP = W * WS;       // nodes per chunk
   constexpr bool GTWO = TWO && !WBLEND;  // two snapshots in the LDS window
   constexpr int NCH = GTWO ? (V5 ? 5 : 6) : 3;  // 16-B chunks per node
@@ -474,7 +398,6 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       // cells predicted beyond the tile sort at its edge
       const int dx_ = min(max(ring_diff(ic, ox, nx), 0), T - 1);
       const int dy_ = min(max(ring_diff(jc, oy, nx), 0), T - 1);
-#ifndef SWRT_SORT_ROWMAJOR
       // Z-order of the cell within the tile (T = 16): a run of 16 consecutive
       // packets (one ds_read_b128 lane group) stays inside a 2x2 or 4x4 block
       // of cells — with the 12 (mod 16) row stride a conflict-free read
@@ -483,9 +406,6 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
                           ? ((dy_ & 1) | ((dx_ & 1) << 1) | ((dy_ & 2) << 1) | ((dx_ & 2) << 2) |
                              ((dy_ & 4) << 2) | ((dx_ & 4) << 3) | ((dy_ & 8) << 3) | ((dx_ & 8) << 4))
                           : T * T;
-#else
-      const int key = (dx_ >= 0 && dx_ < T && dy_ >= 0 && dy_ < T) ? dx_ * T + dy_ : T * T;
-#endif
       const int r = atomicAdd(&hist[key], 1);
       kr[i] = (key << 16) | r;
     }
@@ -517,12 +437,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
     __syncthreads();
     for (int i = tid; i < nb; i += NT) {
       const int v = kr[i];
-#ifdef SWRT_ABLATE_SORT
-      order[i] = b0 + i;
-      (void)v;
-#else
       order[hist[v >> 16] + (v & 0xffff)] = srcp ? srcp[b0 + i] : b0 + i;  // input slot
-#endif
     }
     __syncthreads();
     }  // sort_cells
@@ -538,38 +453,25 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       double x0 = xin[pi], y0 = xin[a.n + pi];
       double k0 = kin[pi], l0 = kin[a.n + pi];
       const int orig = pin[pi];
+      // half-step drift of the current k, half * gH*k/omega(k)
+      // (ode_symplectic.m:10-16): the second drift of a step and the first
+      // drift of the next one use the same k (k0 = k2), hence the same
+      // value — computed once per step, bit-identical to computing it twice.
+      double hcx, hcy;
+      {
+        const double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
+        hcx = half * (a.gH * k0 / w);
+        hcy = half * (a.gH * l0 / w);
+      }
       for (int st = 0; st < a.nsteps; ++st) {
         const int64_t sg = sbase + st;
         const double alpha = a.alpha0 + (double)(ta.ivmode ? (int64_t)st : sg) * a.dalpha;
-#ifdef SWRT_FAIR_PRIO
-        {
-          // fair share between co-resident workgroups: a wave's issue
-          // priority falls as it works through its packets, so the workgroup
-          // that started later (the SQ otherwise issues oldest first) catches
-          // up and a CU's last workgroups end together
-          const int it = (b0 - pbeg) / NT + (r0 - (tid & ~63)) / NT;
-          const int niter = max(1, (pend - pbeg - (tid & ~63) + NT - 1) / NT);
-          int bucket = min(3, (4 * (it * a.nsteps + st)) / (niter * a.nsteps));
-          bucket = __builtin_amdgcn_readfirstlane(bucket);
-          if (bucket == 0) __builtin_amdgcn_s_setprio(3);
-          else if (bucket == 1) __builtin_amdgcn_s_setprio(2);
-          else if (bucket == 2) __builtin_amdgcn_s_setprio(1);
-          else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
-        double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
-        const double x1 = x0 + half * (a.gH * k0 / w);
-        const double y1 = y0 + half * (a.gH * l0 / w);
+        const double x1 = x0 + hcx;
+        const double y1 = y0 + hcy;
         Stencil sc;
         stencil_at(a.f0, x1, y1, a.bump, sc);
         const int dx_ = ring_diff(sc.ic, ox, nx), dy_ = ring_diff(sc.jc, oy, nx);
         double I[kRec], J[kRec];
-#ifdef SWRT_ABLATE_COMPUTE
-        if (true) {
-#pragma unroll
-          for (int q = 0; q < kRec; ++q) { I[q] = sc.wx[q] * 1e-30; J[q] = sc.wy[q] * 1e-30; }
-        } else
-#endif
         const bool inwin = dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M;
 #ifdef SWRT_PHASE_TIMING
         if (!inwin) atomicAdd(&nfall, 1);
@@ -598,9 +500,11 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         const double y2 = y1 + dt * I[1];
         const double k2 = k0 - dt * (I[2] * k0 + I[4] * l0);
         const double l2 = l0 - dt * (I[3] * k0 + I[5] * l0);
-        w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
-        x0 = x2 + half * (a.gH * k2 / w);
-        y0 = y2 + half * (a.gH * l2 / w);
+        const double w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
+        hcx = half * (a.gH * k2 / w);
+        hcy = half * (a.gH * l2 / w);
+        x0 = x2 + hcx;
+        y0 = y2 + hcy;
         k0 = k2;
         l0 = l2;
         if (a.hist_x != nullptr && ((sg + 1) % a.save_every) == 0) {
@@ -611,9 +515,9 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
           hk[orig] = k0; hk[a.n + orig] = l0;
         }
       }
-      st_out(&ta.x_out[po], x0); st_out(&ta.x_out[a.n + po], y0);
-      st_out(&ta.k_out[po], k0); st_out(&ta.k_out[a.n + po], l0);
-      st_out(&ta.perm_out[po], orig);
+      ta.x_out[po] = x0; ta.x_out[a.n + po] = y0;
+      ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
+      ta.perm_out[po] = orig;
       if (nkeys != nullptr) {  // fused histogram for the next re-binning
         const int ic = fast_cell(x0, a.f0.inv_dx, nx);
         const int jc = fast_cell(y0, a.f0.inv_dx, nx);

@@ -24,7 +24,6 @@ struct XkaArgs {
   const double* nodes;
   int nx, npad;
   double dx, dy, inv_dx, inv_dy, px, py, inv_px, inv_py;
-  int pow2x, pow2y;
   double C0sq, f, f2, dt, bump;
   double* st;          // 5 x n: x, y, k, l, a (column blocks)
   int64_t n;
@@ -42,8 +41,8 @@ struct XkaStencil {
 
 __device__ __forceinline__ void xka_stencil(const XkaArgs& a, double x, double y, XkaStencil& s) {
   double ax, ay;
-  s.ic = cell_frac(x, a.dx, a.inv_dx, a.px, a.inv_px, a.pow2x, a.nx, ax);
-  s.jc = cell_frac(y, a.dy, a.inv_dy, a.py, a.inv_py, a.pow2y, a.nx, ay);
+  s.ic = cell_frac(x, a.dx, a.inv_dx, a.px, a.inv_px, a.nx, ax);
+  s.jc = cell_frac(y, a.dy, a.inv_dy, a.py, a.inv_py, a.nx, ay);
   lagrange_w(ax, a.bump, s.wx);
   lagrange_w(ay, a.bump, s.wy);
 }

@@ -368,12 +368,12 @@ def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, til
     np.testing.assert_array_equal(hkg, hko)
 
 
-@pytest.mark.parametrize("variant,cell_sort", [(1, 0), (2, 0), (2, 1), (3, 0)])
+@pytest.mark.parametrize("variant,cell_sort", [(1, 0), (2, 0), (2, 1)])
 @pytest.mark.parametrize("nslots", [1, 2])
 @pytest.mark.parametrize("dt_scale", [1.0, 40.0])
 @pytest.mark.parametrize("div_free", [False, True])
 def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, nslots, dt_scale, div_free):
-    """Per-packet (1), LDS-tiled (2) and persistent LDS-tiled (3) kernels give
+    """Per-packet (1) and LDS-tiled (2) kernels give
     the oracle's bits; the large-dt case drives packets out of the LDS window
     (global fallback).  div_free: v_y stored as -u_x, so the tile kernel runs
     its five-sum window (swrt_field_div_free); the oracle sums all six."""
@@ -405,12 +405,12 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, 
     np.testing.assert_array_equal(hkg, hko)
 
 
-@pytest.mark.parametrize("variant,tail_split", [(2, (0, 0)), (2, (32, 0)), (2, (1000, 0)), (2, (16, 16)),
-                                                (2, (0, 1000)), (3, (0, 0))])
-def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split):
+@pytest.mark.parametrize("variant,tail_split,order", [(2, (0, 0), 1), (2, (32, 0), 1), (2, (1000, 0), 1),
+                                                      (2, (16, 16), 1), (2, (0, 1000), 1), (2, (0, 0), 0),
+                                                      (2, (16, 0), 0)])
+def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split, order):
     """512^2 two-snapshot field, 2e5 packets, LDS kernel with re-binning every
-    3 steps over 10 steps: random subset bit-identical to the oracle (the
-    persistent kernel walks several tiles per workgroup here; tail_split runs
+    3 steps over 10 steps: random subset bit-identical to the oracle (tail_split runs
     the last tiles of each XCD band — or all of them — as half-tile
     workgroups)."""
     nx, L = 512, 20.0
@@ -430,6 +430,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split)
     ctx.set_kernel(variant)
     ctx.set_locality(3, 0)
     ctx.set_tail_split(*tail_split)
+    ctx.set_tile_order(order)
     try:
         ctx.packets_set(x, k)
         ctx.advance(0.01, 10, 3.0, 1.0, nslots=2, alpha0=0.05, dalpha=0.1, bump=orc.BUMP_QG)
@@ -438,6 +439,7 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split)
         ctx.set_kernel(0)
         ctx.set_locality(4, 0)
         ctx.set_tail_split(*DEFAULT_TAIL_SPLIT)
+        ctx.set_tile_order(1)
     idx = np.sort(rng.choice(N, 2000, replace=False))
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.05, 0.1, nx, 2 * nx, L / nx, orc.BUMP_QG, x[idx], k[idx], 0.01,
                                        10, 3.0, 1.0)
@@ -445,10 +447,10 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split)
     np.testing.assert_array_equal(kg[idx], ko)
 
 
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [1, 2])
 def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
     """20000 packets packed into a few cells: tiles far above the
-    per-workgroup pipeline depth (the persistent kernel's overflow loop) and
+    per-workgroup sort batch (several batches per tile) and
     one-tile-heavy binning; every packet bit-identical to the oracle."""
     c = qg_case
     nx, L = c["nx"], c["L"]
@@ -476,7 +478,7 @@ def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
     np.testing.assert_array_equal(kg, ko)
 
 
-@pytest.mark.parametrize("variant,cell_sort,tail_split", [(2, 0, (0, 0)), (2, 1, (0, 0)), (3, 0, (0, 0)),
+@pytest.mark.parametrize("variant,cell_sort,tail_split", [(2, 0, (0, 0)), (2, 1, (0, 0)), (1, 0, (0, 0)),
                                                           (2, 0, (1, 0)), (2, 1, (2, 0)), (2, 0, (1, 1))])
 def test_tile_kernel_single_step_calls(ctx, oracle_lib, qg_case, variant, cell_sort, tail_split):
     """One advance call per step (the bench's pattern): with re-binning every
