@@ -43,7 +43,6 @@ import swraytracing_amd as sw  # noqa: E402
 from swraytracing_amd.dist import gather_to_root, max_over_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
-FP64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (spec)
 BYTES_STEADY = 1792          # 32+32 state + 1 snap * 6 fields * 36 taps * 8 B
 BYTES_BLEND = 3520           # 32+32 state + 2 snaps * 6 * 36 * 8 B
 
@@ -117,63 +116,110 @@ def step(ctx, w, sub):
                 bump=sw.BUMP_QG)
 
 
-def cpu_baseline(ctx, w, target_s, threads=0):
-    """The C oracle (OpenMP) on this host: same fields, same algorithm.
-    threads = 0: all of the process's threads; 1: one core."""
+def host_cpu():
+    """Where the CPU baseline ran: nproc, the process's CPU affinity and the model."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
+
+
+def cpu_baseline(ctx, w, target_s, threads):
+    """The C oracle's CPU-arranged leapfrog (oracle_leapfrog_fast: the same
+    bits as the restatement, interleaved nodes, weights shared by both
+    snapshots) built here with -O3 -march=native, OpenMP over packets, timed
+    on the same fields on a bounded sample."""
+    import tempfile
+
     from oracle import cbind
-    cbind.build()
     nx = w["nx"]
     p0 = ctx.get_field_grid(0, nx)
     p1 = ctx.get_field_grid(1, nx) if w["nslots"] == 2 else None
-    default_threads = cbind.lib().oracle_num_threads()  # OMP_NUM_THREADS (16 on the GPU box)
-    if threads > 0:
-        cbind.lib().oracle_set_threads(threads)
-    nthreads = cbind.lib().oracle_num_threads()
+    L, flags = cbind.cpu_lib(tempfile.mkdtemp(prefix="swrt_cpu_"))
+    default_threads = L.oracle_num_threads()
+    L.oracle_set_threads(threads)
+    nthreads = L.oracle_num_threads()
 
     def run(n, steps):
-        x = w["x"][:n]
-        k = w["k"][:n]
         t0 = time.perf_counter()
-        cbind.leapfrog(p0, p1, 0.5, 0.0, nx, 2 * nx, w["L"] / nx, sw.BUMP_QG, x, k, w["dt"], steps,
-                       w["f"], w["gH"])
+        cbind.leapfrog_fast(p0, p1, 0.5, 0.0, nx, 2 * nx, w["L"] / nx, sw.BUMP_QG, w["x"][:n], w["k"][:n],
+                            w["dt"] / 5, steps, w["f"], w["gH"], L=L)
         return time.perf_counter() - t0
 
-    n = min(20000 if nthreads > 1 else 2000, w["x"].shape[0])
+    n = min(8192 * max(1, nthreads // 4), w["x"].shape[0])
     run(n, 1)  # warm-up: OpenMP thread start, page faults
     t = run(n, 4)
     s1 = max(4, int(1.0 * 4 / max(t, 1e-9)))  # ~1 s calibration run
     t = run(n, s1)
-    rate = s1 * n / max(t, 1e-9)
-    steps = max(1, int(target_s * rate / n))
+    steps = max(1, int(target_s * s1 / max(t, 1e-9)))
     t = run(n, steps)
-    cbind.lib().oracle_set_threads(default_threads)
+    L.oracle_set_threads(default_threads)
     return {"value": n * steps / t, "unit": "packet-steps/s", "cores": int(nthreads), "kind": "port",
-            "sample": f"{n} packets x {steps} leapfrog steps of the same {nx}^2 two-snapshot field "
-                      f"(oracle/swrt_oracle.c, OpenMP {nthreads} threads, {t:.1f} s)"}
+            "sample": f"{n} packets x {steps} leapfrog steps (dt 0.05*dx/U0) of the bench's {nx}^2 two-snapshot "
+                      f"field, oracle_leapfrog_fast (oracle/swrt_oracle.c, same bits as the restatement), "
+                      f"{nthreads} OpenMP threads, {t:.1f} s",
+            "build": flags, "host": host_cpu()}
 
 
-FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s: 78.6 TFLOP/s counting an FMA as 2
+FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s (78.6 TFLOP/s spec counts an FMA as 2)
+LDS_CYCLES_PEAK = 256 * 2.4e9               # LDS-array cycles/s over the chip (one array per CU, 2.4 GHz)
 
 
-def load_valu(config_key):
-    path = os.path.join(ROOT, "profiles", "valu.json")
-    if not os.path.exists(path):
-        return None
+def load_pmc(config_key):
+    """PMC record of this bench configuration (tools/pmc_collect.sh -> profiles/pmc.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc.json")
     try:
         return json.load(open(path)).get(config_key)
-    except Exception:
+    except (OSError, ValueError):
         return None
 
 
-def load_traffic(config_key):
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    if not os.path.exists(path):
-        return None
-    try:
-        d = json.load(open(path))
-        return d.get(config_key)
-    except Exception:
-        return None
+def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timing_every):
+    """The dominant kernel (tile_leapfrog_kernel) against the resource that
+    bounds it.  The bit-exact stencil (mul then add, no FMA) is
+    fp64-VALU-issue bound: achieved = the kernel's PMC-counted VALU
+    instructions per launch x 64 lanes / its live HIP-event launch time,
+    peak = 256 CUs x 4 SIMDs x 16 fp64 lanes x 2.4 GHz.  HBM and the LDS
+    array are reported beside it as fractions of their own peaks."""
+    ps = N * steps_per_launch
+    B = BYTES_BLEND if nslots == 2 else BYTES_STEADY
+    r = {"bound": "valu-fp64-issue", "achieved": None, "peak": FP64_LANE_OPS_PEAK / 1e12, "unit": "Tlane-op/s",
+         "frac": None, "traffic": None,
+         "avg_launch_ms": avg_launch_s * 1e3, "timed_launches": launches, "timing_every": timing_every,
+         "packet_steps_per_launch": ps,
+         # SURVEY §8d's algorithmic bytes (taps counted as if each were read from HBM; they are
+         # re-read from LDS): an effective gather bandwidth, not an HBM fraction
+         "effective_gather_gbs": ps * B / avg_launch_s / 1e9, "gather_bytes_per_packet_step": B}
+    if pmc is None:
+        r["note"] = "no PMC record for this configuration in profiles/pmc.json (tools/pmc_collect.sh)"
+        return r
+    valu = pmc["SQ_INSTS_VALU"]
+    ach = valu * 64.0 / avg_launch_s
+    traffic = (2.0 * pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0  # KiB; FETCH doubled (gfx950)
+    compulsory = N * (36 + 36) + nslots * (nx + 5) ** 2 * 48  # state+perm in/out, the snapshots once
+    hbm = traffic / avg_launch_s / 1e9
+    pmc_s = pmc["pmc_kernel_ns"] * 1e-9
+    r.update({
+        "achieved": ach / 1e12, "frac": ach / FP64_LANE_OPS_PEAK,
+        "valu_instructions_per_launch": valu,
+        "valu_per_wave_step": valu / (N / 64.0 * steps_per_launch),
+        "traffic": traffic, "hbm_gbs": hbm, "hbm_frac": hbm / HBM_PEAK_GBS,
+        "compulsory_bytes_per_launch": compulsory, "traffic_over_compulsory": traffic / compulsory,
+        "lds_frac": pmc["SQ_LDS_IDX_ACTIVE"] / (LDS_CYCLES_PEAK * pmc_s),
+        "lds_conflict_factor": pmc["SQ_LDS_IDX_ACTIVE"] / max(1.0, pmc["SQ_LDS_IDX_ACTIVE"] - pmc["SQ_LDS_BANK_CONFLICT"]),
+        "wait_frac": pmc["SQ_WAIT_ANY"] / max(1.0, pmc["SQ_WAVE_CYCLES"]),
+        "pmc_kernel_ms": pmc_s * 1e3,
+        "source": "profiles/pmc.json: " + pmc.get("source", "") + "; kernel " + pmc.get("kernel", "")})
+    return r
 
 
 def main():
@@ -274,7 +320,6 @@ def main():
     ivs = w["intervals"]
     total_ps = N * world * args.substeps * ivs * args.steps
     value = total_ps / elapsed
-    B = BYTES_BLEND if w["nslots"] == 2 else BYTES_STEADY
     # sampled HIP-event time of the packet kernel; without samples fall back to wall time per step
     avg_launch_s = (kms / 1e3) / launches if launches > 0 else elapsed / args.steps
     # packet-steps per launch: a call's substeps run as launches of at most
@@ -288,22 +333,9 @@ def main():
         steps_per_launch = args.rebin_every
     else:
         steps_per_launch = min(args.substeps, args.rebin_every)  # approximate (uneven chunks)
-    ps_per_launch = N * steps_per_launch
-    achieved_gbs = ps_per_launch * B / avg_launch_s / 1e9
-    # fp64 VALU work per packet-step of the exact-order stencil
     key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}" + (f"_iv{ivs}" if ivs > 1 else "")
-    traffic = load_traffic(key)
-    valu = load_valu(key)
-    valu_roofline = None
-    if valu is not None and args.blend_mode == 0:
-        # the kernel is fp64-VALU-issue bound (no FMA allowed: bit-exact order):
-        # PMC-measured VALU instructions per launch x 64 lanes / launch time
-        lane_ops = valu["SQ_INSTS_VALU"] * 64.0
-        ach = lane_ops / avg_launch_s
-        valu_roofline = {"bound": "valu-fp64-issue", "achieved": ach, "peak": FP64_LANE_OPS_PEAK,
-                         "unit": "lane-ops/s", "frac": ach / FP64_LANE_OPS_PEAK,
-                         "valu_instructions_per_launch": valu["SQ_INSTS_VALU"],
-                         "source": "profiles/valu.json (rocprofv3 PMC)"}
+    pmc = load_pmc(key) if args.blend_mode == 0 and args.kernel in (0, 2) else None
+    roof = roofline(pmc, N, args.nx, w["nslots"], steps_per_launch, avg_launch_s, launches, args.timing_every)
     workload = ("qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
                 f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, {args.nx}^2x2 field, {N} packets/GPU, "
                 f"leapfrog dt {0.25 / args.substeps:g}*dx/U0 ({args.substeps} per PDE interval)"
@@ -328,24 +360,17 @@ def main():
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
                    "parallelism": f"packets sharded x{world}, field replicated"},
-        # traffic: true HBM bytes per launch (rocprofv3 PMC, profiles/traffic.json), beside the
-        # algorithmic bytes per launch that `achieved` is computed from (taps re-read from LDS)
-        "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved_gbs / HBM_PEAK_GBS,
-                     "traffic": traffic["bytes_per_launch"] if traffic else None,
-                     "traffic_detail": traffic, "algorithmic_bytes_per_launch": ps_per_launch * B,
-                     "traffic_gbs": (traffic["bytes_per_launch"] / avg_launch_s / 1e9) if traffic else None,
-                     "bytes_per_packet_step": B, "avg_launch_ms": avg_launch_s * 1e3,
-                     "timed_launches": launches, "timing_every": args.timing_every},
-        "valu_roofline": valu_roofline,
+        "roofline": roof,
         "finite": finite,
     }
     if gathered is not None:
         out["gathered_finite"] = gathered
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(ctx, w, args.cpu_seconds)
-        # SURVEY §8d also asks for the 1-core figure of the same restatement
-        out["cpu_baseline_1core"] = cpu_baseline(ctx, w, args.cpu_seconds / 3, threads=1)
+        # the GPU box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there)
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(ctx, w, args.cpu_seconds, threads)
+        # SURVEY §8d also asks for the 1-core figure of the same code
+        out["cpu_baseline_1core"] = cpu_baseline(ctx, w, args.cpu_seconds / 3, 1)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

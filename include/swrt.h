@@ -154,7 +154,8 @@ int swrt_set_cell_sort(swrt_ctx* ctx, int every_launch);
  * as two workgroups of half the tile's packets and then `quarters_per_xcd`
  * tiles run as four workgroups of a quarter each, so the end of a launch is
  * made of smaller work items and the CUs finish closer together.
- * 0, 0 = one workgroup per tile. */
+ * 0, 0 = one workgroup per tile (the default: with the longest-first tile
+ * order, swrt_set_tile_order, the split measured no faster). */
 int swrt_set_tail_split(swrt_ctx* ctx, int halves_per_xcd, int quarters_per_xcd);
 
 /* Tile order of the LDS-tiled kernels (performance only; results are

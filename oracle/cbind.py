@@ -34,11 +34,47 @@ def lib():
         L.oracle_leapfrog.argtypes = [_P, _P, _D, _D, _I, _D, _D, _D, _P, _P, _I, _D, _I, _D, _D,
                                       _I, _P, _P]
         L.oracle_leapfrog.restype = None
+        _bind_fast(L)
         L.oracle_num_threads.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
         L.oracle_set_threads.restype = None
         _lib = L
     return _lib
+
+
+_CPU_FLAGS = ["-O3", "-march=native", "-fopenmp", "-ffp-contract=off", "-fno-fast-math", "-fPIC", "-std=c11"]
+
+
+def cpu_lib(out_dir):
+    """The oracle compiled for THIS host's CPU (-O3 -march=native, no FMA
+    contraction: the same bits) into out_dir — bench.py's cpu_baseline build,
+    compiled where it runs so -march=native means that machine.  Returns
+    (ctypes lib, flags string)."""
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, "libswrt_oracle_cpu.so")
+    subprocess.run(["gcc"] + _CPU_FLAGS + ["-shared", "-o", path, os.path.join(_HERE, "swrt_oracle.c"), "-lm"],
+                   check=True)
+    L = ctypes.CDLL(path)
+    _bind_fast(L)
+    L.oracle_num_threads.restype = ctypes.c_int
+    L.oracle_set_threads.argtypes = [ctypes.c_int]
+    L.oracle_set_threads.restype = None
+    return L, "gcc " + " ".join(_CPU_FLAGS)
+
+
+def _bind_fast(L):
+    L.oracle_leapfrog_fast.argtypes = [_P, _P, _D, _D, _I, _D, _D, _D, _P, _P, _I, _D, _I, _D, _D]
+    L.oracle_leapfrog_fast.restype = None
+
+
+def leapfrog_fast(planes0, planes1, alpha0, dalpha, nx, nyF, dx, bump, x, k, dt, nsteps, f, gH, L=None):
+    """oracle_leapfrog_fast (CPU-arranged, same bits as leapfrog): -> (x, k)."""
+    L = L or lib()
+    x = np.asfortranarray(x, dtype=np.float64).copy(order="F")
+    k = np.asfortranarray(k, dtype=np.float64).copy(order="F")
+    L.oracle_leapfrog_fast(_ptr(planes0), _ptr(planes1), alpha0, dalpha, nx, float(nyF), dx, bump,
+                           x.ctypes.data_as(_P), k.ctypes.data_as(_P), x.shape[0], dt, nsteps, f, gH)
+    return x, k
 
 
 def _ptr(a):

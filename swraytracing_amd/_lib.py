@@ -27,7 +27,7 @@ LIB_PATH = os.environ.get("SWRT_LIB_PATH") or os.path.join(_HERE, "libswrt.so")
 
 SWRT_OK = 0
 # swrt_set_tail_split defaults of the library build (SWRT_TAIL_SPLIT / _QUARTERS in swrt_api.hip)
-DEFAULT_TAIL_SPLIT = (16, 0)
+DEFAULT_TAIL_SPLIT = (0, 0)
 ERRORS = {1: "SWRT_ERR_ARG", 2: "SWRT_ERR_HIP", 3: "SWRT_ERR_STATE", 4: "SWRT_ERR_ALLOC"}
 
 _D = ctypes.c_double

@@ -51,7 +51,7 @@ constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
 #define SWRT_TAIL_QUARTERS 0
 #endif
 #ifndef SWRT_TAIL_SPLIT
-#define SWRT_TAIL_SPLIT 16
+#define SWRT_TAIL_SPLIT 0
 #endif
 #ifndef SWRT_TILE_THREADS
 #define SWRT_TILE_THREADS 512

@@ -182,6 +182,29 @@ def test_numpy_and_c_oracles_bit_identical(oracle_lib, qg_case):
     np.testing.assert_array_equal(kn, kc)
 
 
+def test_cpu_arranged_leapfrog_bit_identical(oracle_lib, qg_case, tmp_path):
+    """oracle_leapfrog_fast (bench.py's cpu_baseline: interleaved padded nodes,
+    weights shared by both snapshots, drift increment once per step) gives
+    the restatement's bits, also as the -O3 -march=native build that bench.py
+    compiles on the host it times."""
+    c = qg_case
+    pl = oracle_lib.planes_of(c["flow"])
+    pl2 = oracle_lib.planes_of({n: v * 0.93 for n, v in c["flow"].items()})
+    L = c["L"]
+    rng = np.random.default_rng(9)
+    x = np.concatenate([c["x"], (rng.random((64, 2)) - 0.5) * 3 * L])  # far outside the period too
+    k = np.concatenate([c["k"], c["k"][:64]])
+    cpu, _flags = oracle_lib.cpu_lib(str(tmp_path))
+    for p1, nyF, a0, da in [(None, c["nx"], 0.0, 0.0), (pl2, 2 * c["nx"], 0.1, 0.07)]:
+        xr, kr, _, _ = oracle_lib.leapfrog(pl, p1, a0, da, c["nx"], nyF, L / c["nx"], 1e-10, x, k, c["dt"] * 7,
+                                           9, c["f"], 1.0)
+        for lib in (None, cpu):
+            xf, kf = oracle_lib.leapfrog_fast(pl, p1, a0, da, c["nx"], nyF, L / c["nx"], 1e-10, x, k,
+                                              c["dt"] * 7, 9, c["f"], 1.0, L=lib)
+            np.testing.assert_array_equal(xf, xr)
+            np.testing.assert_array_equal(kf, kr)
+
+
 def test_ode_symplectic_layout_and_leapfrog_equivalence(qg_case):
     c = qg_case
     sch = orc.SpectralSchemeOracle(c["L"], c["nx"], orc.k2g(-c["qk"] / (c["K_d2"] + c["K2"])))
