@@ -170,6 +170,42 @@ def cpu_baseline(ctx, w, target_s, threads):
             "build": flags, "host": host_cpu()}
 
 
+def driver_step(ctx, w, args, dev, distributed):
+    """The end-to-end qg2layersw_raytrace step on this GPU (swraytracing_amd.qg.
+    TwoLayerLoop, the driver's own loop body): CFL rule, 2-layer PDE step, U0
+    read-back, grid_U snapshot of the new qk and the packet interval of all
+    this rank's packets (`--substeps` leapfrog substeps), the PDE on its own
+    stream beside the packets.  Outside the metric's timed region; reported as
+    an extra key so the driver-level rate is observed by the same run."""
+    nx, L, f, Cg = w["nx"], w["L"], w["f"], math.sqrt(w["gH"])
+    qk = np.stack([w["qk1"], -w["qk1"]], axis=2)  # the driver's (q1, -q1) layers
+    model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
+    ens = sw.PacketEnsemble(w["x"], w["k"], L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * math.pi / L, nlayers=2,
+                            bump=sw.BUMP_QG, ctx=ctx)
+    U0 = model.max_speed()
+    loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps)
+    for _ in range(4):  # AB1/AB2 start-up, first-use allocations
+        loop.step()
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.driver_steps):
+        loop.step()
+    loop.flush()
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if distributed:
+        el = max_over_ranks(el, backend=args.dist_backend)
+    ms = el / args.driver_steps * 1e3
+    return {"ms_per_pde_step": ms, "steps": args.driver_steps,
+            "packet_steps_per_s": args.packets * args.world * args.substeps / (ms / 1e3),
+            "what": "TwoLayerLoop.step: CFL rule + 2-layer PDE step + U0 read-back + grid_U snapshot + "
+                    f"{args.substeps} leapfrog substeps of {args.packets} packets/GPU (qg2layersw_raytrace.m:152-197)"}
+
+
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s (78.6 TFLOP/s spec counts an FMA as 2)
 LDS_CYCLES_PEAK = 256 * 2.4e9               # LDS-array cycles/s over the chip (one array per CU, 2.4 GHz)
 
@@ -256,6 +292,8 @@ def main():
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
+    ap.add_argument("--driver-steps", type=int, default=20,
+                    help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather all trajectories to rank 0 (one all_gather)")
     args = ap.parse_args()
@@ -373,6 +411,8 @@ def main():
         out["cpu_baseline_1core"] = cpu_baseline(ctx, w, args.cpu_seconds / 3, 1)
     elif rank == 0:
         out["cpu_baseline"] = None
+    if args.driver_steps > 0 and args.mode == "blend":
+        out["driver_step"] = driver_step(ctx, w, args, dev, distributed)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

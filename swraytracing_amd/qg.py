@@ -163,8 +163,12 @@ class _IntervalGroup:
     swrt_advance_intervals call — the same bits as one advance per step.  The
     PDE runs up to k steps ahead of the packets; a frame write flushes."""
 
-    def __init__(self, ctx, ens, k, nsub):
-        self.ctx, self.ens, self.k, self.nsub = ctx, ens, max(1, min(int(k), 4)), nsub
+    def __init__(self, ctx, ens, k, nsub, integrator="leapfrog"):
+        if integrator not in ("leapfrog", "ode23"):
+            raise ValueError("integrator must be 'leapfrog' or 'ode23'")
+        self.ctx, self.ens, self.nsub, self.integrator = ctx, ens, nsub, integrator
+        # ode23 (the reference's own packet integrator) takes one interval per call
+        self.k = 1 if integrator == "ode23" else max(1, min(int(k), 4))
         self.dts = []
 
     def next_slot(self):
@@ -177,14 +181,78 @@ class _IntervalGroup:
 
     def flush(self):
         if self.dts:
-            self.ens.advance_intervals(self.dts, self.nsub)
+            if self.integrator == "ode23":
+                self.ens.advance_ode23(self.dts[0])  # ode23(ray_ode, [0, dt], y0), alpha = t/dt
+            else:
+                self.ens.advance_intervals(self.dts, self.nsub)
             self.ctx.swap_slots(0, len(self.dts))  # the last end snapshot starts the next group
             self.dts = []
 
 
+def _fresh_outputs(out_dir, fresh):
+    """write_field.m:31 appends to existing files; a driver run starting from
+    t = 0 removes earlier outputs first unless fresh=False."""
+    os.makedirs(out_dir, exist_ok=True)
+    if not fresh:
+        return
+    for name in ("packet_x", "packet_k", "packet_time", "pv", "pv_time"):
+        p = os.path.join(out_dir, name + ".bin")
+        if os.path.exists(p):
+            os.remove(p)
+
+
+class TwoLayerLoop:
+    """One iteration of qg2layersw_raytrace.m:152-197 on the device: the CFL
+    rule (:156-165) on the current U0, the PDE step, U0 of the new qk read back
+    asynchronously (collected after the packet work is queued, so the rule
+    never idles the GPU), and — once t > packet_delay — grid_U of (prev_qk,
+    qk) into the packet slots and the packet interval [t, t+dt].  Used by
+    :func:`qg2layersw_raytrace` (which adds the frame writes) and by bench.py's
+    end-to-end driver-step figure."""
+
+    def __init__(self, model, ens, dt, U0, cfl_fraction=0.25, packet_delay=0.0, nsub=5, packet_intervals=1,
+                 integrator="leapfrog", log=None):
+        self.model, self.ens, self.dt, self.U0 = model, ens, dt, U0
+        self.cfl_fraction, self.packet_delay = cfl_fraction, packet_delay
+        self.nx = model.nx
+        self.t = 0.0
+        self.steps = 0
+        self.dts = []
+        self.have_cur = False
+        self.log = log
+        self.group = _IntervalGroup(model.ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
+
+    def step(self):
+        """Returns True when the packets advanced through this PDE step."""
+        self.steps += 1
+        self.dt, changed = self.model.cfl_rule(self.dt, self.U0, self.cfl_fraction)
+        if changed and self.log is not None:
+            self.log(f"CFL condition not met, max|u|={self.U0:f}, new dt={self.dt:f}\n")
+        self.dts.append(self.dt)
+        self.model.step(self.dt)
+        self.t = self.t + self.dt
+        self.model.max_speed_async()
+        active = self.ens is not None and self.t > self.packet_delay
+        if active:
+            ny = 2 * self.nx
+            if not self.have_cur:
+                self.model.snapshot(0, which=1, layer=0, ny_period=ny)
+            self.model.snapshot(self.group.next_slot(), which=0, layer=0, ny_period=ny)
+            self.have_cur = True
+            self.group.add(self.dt)
+        else:
+            self.have_cur = False
+        self.U0 = self.model.max_speed_result()
+        return active
+
+    def flush(self):
+        if self.group is not None:
+            self.group.flush()
+
+
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
                   out_dir="data", nsub=4, max_steps=None, seed=146, verbose=False, r_drag=0.1,
-                  packet_intervals=1, ctx: Context | None = None):
+                  packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None):
     """qgsw_raytrace.m:1-180 with the PDE and the packets on the GPU.
 
     Writes ``out_dir``/packet_x.bin, packet_k.bin, packet_time.bin, pv.bin,
@@ -195,14 +263,14 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     0 to drop it.  ``packet_intervals`` (1..4): PDE steps whose packet
     intervals go to the device in one call (results identical for any
     value; 1 is faster end to end here: the PDE chain's latency, not the
-    packet launch, bounds a driver step).  Returns a dict of run facts (dt, Nsteps, steps run, frames
-    written, final t)."""
+    packet launch, bounds a driver step).  ``integrator``:
+    "leapfrog" (``nsub`` fused symplectic substeps per PDE interval) or
+    "ode23" (the reference's own ode23 over each interval, qgsw_raytrace.m:149).
+    ``fresh``: remove earlier output files first (default) or append to
+    them as write_field.m:31 does.  Returns a dict of run facts (dt, Nsteps,
+    steps run, frames written, final t)."""
     ctx = ctx if ctx is not None else Context(0)
-    os.makedirs(out_dir, exist_ok=True)
-    for name in ("packet_x", "packet_k", "packet_time", "pv", "pv_time"):
-        p = os.path.join(out_dir, name + ".bin")
-        if os.path.exists(p):
-            os.remove(p)
+    _fresh_outputs(out_dir, fresh)
     log = _Log(os.path.join(out_dir, "run.log"), verbose)
     L = 2 * math.pi
     dx = L / nx
@@ -246,7 +314,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
     nrun = Nsteps if max_steps is None else min(Nsteps, int(max_steps))
     have_cur = False
-    group = _IntervalGroup(ctx, ens, packet_intervals, nsub) if ens is not None else None
+    group = _IntervalGroup(ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
     for step in range(1, nrun + 1):
         model.step(dt)
         t = t + dt
@@ -274,18 +342,14 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
 
 def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
                         out_dir="data", nsub=5, max_steps=None, seed=5, verbose=False,
-                        packet_intervals=1, ctx: Context | None = None):
+                        packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None):
     """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
     (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and
     interpolate's 2*nx y-period).  Same packet outputs as :func:`qgsw_raytrace`;
     pv.bin holds the initial nx x nx x 2 frame only, as in the reference.
-    ``packet_intervals``: as in :func:`qgsw_raytrace`."""
+    ``packet_intervals``, ``integrator``, ``fresh``: as in :func:`qgsw_raytrace`."""
     ctx = ctx if ctx is not None else Context(0)
-    os.makedirs(out_dir, exist_ok=True)
-    for name in ("packet_x", "packet_k", "packet_time", "pv", "pv_time"):
-        p = os.path.join(out_dir, name + ".bin")
-        if os.path.exists(p):
-            os.remove(p)
+    _fresh_outputs(out_dir, fresh)
     log = _Log(os.path.join(out_dir, "run.log"), verbose)
     L = 20.0
     dx = L / nx
@@ -331,40 +395,17 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
         ens.write_frame(dt * (packet_step_start - 1), out_dir)
     write_field(model.q(), os.path.join(out_dir, "pv"))
     write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
-    step = 0
-    have_cur = False
-    dts = []
-    group = _IntervalGroup(ctx, ens, packet_intervals, nsub) if ens is not None else None
-    # U0 of the current qk is always one step ahead: its read-back is queued
-    # right after the PDE step and collected after the packet work of that
-    # step is queued, so the CFL rule (:156-165, same values, same order)
-    # never idles the GPU
-    while t <= T and (max_steps is None or step < max_steps):
-        step += 1
-        dt, changed = model.cfl_rule(dt, U0, CFL_fraction)
-        if changed:
-            log(f"CFL condition not met, max|u|={U0:f}, new dt={dt:f}\n")
-        dts.append(dt)
-        model.step(dt)
-        t = t + dt
-        model.max_speed_async()
-        if ens is not None and t > packet_delay_steps:
-            if not have_cur:
-                model.snapshot(0, which=1, layer=0, ny_period=2 * nx)
-            model.snapshot(group.next_slot(), which=0, layer=0, ny_period=2 * nx)
-            have_cur = True
-            group.add(dt)
-            if (step - packet_step_start + 1) % packet_steps_per_save == 0:
-                group.flush()
-                ens.write_frame(t, out_dir)
-                frames += 1
-        else:
-            have_cur = False
-        U0 = model.max_speed_result()
-        # (the reference only plots q every steps_per_save steps here; its
-        # pv.bin writes are commented out, qg2layersw_raytrace.m:211-239)
-    if group is not None:
-        group.flush()
+    loop = TwoLayerLoop(model, ens, dt, U0, CFL_fraction, packet_delay_steps, nsub, packet_intervals, integrator,
+                        log)
+    # (the reference only plots q every steps_per_save steps in this loop; its
+    # pv.bin writes are commented out, qg2layersw_raytrace.m:211-239)
+    while loop.t <= T and (max_steps is None or loop.steps < max_steps):
+        if loop.step() and (loop.steps - packet_step_start + 1) % packet_steps_per_save == 0:
+            loop.flush()
+            ens.write_frame(loop.t, out_dir)
+            frames += 1
+    loop.flush()
     log.close()
+    dt, dts, step, t, U0 = loop.dt, loop.dts, loop.steps, loop.t, loop.U0
     return dict(dt=dt, dts=dts, Nsteps=Nsteps, steps=step, packet_frames=frames, t=t, U0=U0,
                 packet_step_start=packet_step_start)

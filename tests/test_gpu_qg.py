@@ -342,3 +342,89 @@ def test_qg_fused_speed_and_snapshot_match_unfused(ctx):
     assert a[0] == b[0] and a[1] == b[1]
     for u, v in zip(a[2:], b[2:]):
         assert np.array_equal(np.ascontiguousarray(u).view(np.uint64), np.ascontiguousarray(v).view(np.uint64))
+
+
+def _ring_qk(nx, L, rng, Ug=0.2, kmin=10, kmax_ring=30):
+    """Production-size 2-layer state (q1, -q1) on the driver's 10 < |k| <= 30
+    ring (qg2layersw_raytrace.m:261-262) with random phases, scaled to
+    max|U| = Ug of layer 1 — built in the spectrum directly (initial_q's
+    grid loop is minutes of numpy at 512^2)."""
+    kmax = nx // 2 - 1
+    kx = np.arange(-kmax, kmax + 1)[:, None]
+    ky = np.arange(kmax + 1)[None, :]
+    r2 = kx * kx + ky * ky
+    qk = np.where((r2 > kmin ** 2) & (r2 <= kmax_ring ** 2),
+                  np.exp(2j * np.pi * rng.random((2 * kmax + 1, kmax + 1))), 0)
+    kx_, ky_, K2 = orc.wavenumber_grids(nx, L, scale=True)
+    fl = orc.grid_U(qk, 3.0, K2, kx_, ky_)
+    qk = qk * (Ug / np.sqrt((fl["u"] ** 2 + fl["v"] ** 2).max()))
+    return np.stack([qk, -qk], axis=2)
+
+
+def test_qg2_driver_loop_512_matches_oracle_pipeline(ctx, oracle_lib):
+    """The benched configuration end to end: 512^2 x 2 layers, 1e6 packets,
+    the driver's own loop body (TwoLayerLoop: adaptive CFL, PDE on the QG
+    stream with the fused post-step transforms, snapshots renamed past
+    in-flight packet reads, 5 leapfrog substeps per interval) for 6 PDE steps
+    against QG2Oracle + the oracle's grid_U + the C-oracle leapfrog on a
+    random subset of 3000 packets.  Same dt sequence, qk within QG_RTOL,
+    the last snapshot within the field tolerance, packets within TRAJ_ATOL."""
+    nx, L, f, Cg, N, nsub, nsteps = 512, 20.0, 3.0, 1.0, 1_000_000, 5, 6
+    rng = np.random.default_rng(512)
+    qk0 = _ring_qk(nx, L, rng)
+    x, k = sw.qg._packets(N, L, 4.0, f, Cg, rng)
+    model = sw.QGModel.two_layer(qk0, nx, f, Cg, L=L, ctx=ctx)
+    ens = sw.PacketEnsemble(x, k, L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * np.pi / L, nlayers=2,
+                            bump=sw.BUMP_QG, ctx=ctx)
+    U0 = model.max_speed()
+    loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=nsub)
+    for _ in range(nsteps):
+        assert loop.step()
+    loop.flush()
+    xs, ks = ens.state()
+    snap = ctx.get_field_grid(0, nx)  # grid_U of the last qk (slot 0 after the swap)
+    qk_dev = model.qk
+
+    o = orc.QG2Oracle(qk0, nx, L, f / Cg, shear_strength=0.5)
+    kx_, ky_, K2 = orc.wavenumber_grids(nx, L, scale=True)
+    idx = np.sort(rng.choice(N, 3000, replace=False))
+    xo, ko = x[idx], k[idx]
+    from tests.test_gpu_parity import _planes
+    flow = None
+    for s in range(nsteps):
+        prev = o.qk[:, :, 0].copy()
+        o.step()
+        assert abs(loop.dts[s] - o.dt) <= 1e-12 * o.dt, (s, loop.dts[s], o.dt)
+        p0 = _planes(orc.grid_U(prev, f / Cg, K2, kx_, ky_, 0.5))
+        flow = orc.grid_U(o.qk[:, :, 0], f / Cg, K2, kx_, ky_, 0.5)
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, _planes(flow), 0.5 / nsub, 1.0 / nsub, nx, 2 * nx, L / nx,
+                                           orc.BUMP_QG, xo, ko, o.dt / nsub, nsub, f, Cg ** 2)
+    assert _rel(qk_dev, o.qk) < QG_RTOL
+    for i, name in enumerate(orc.FIELD_ORDER):
+        assert _rel(snap[i], np.asarray(flow[name]).ravel(order="F")) < 1e-12, name
+    np.testing.assert_allclose(xs[idx], xo, atol=TRAJ_ATOL, rtol=0)
+    np.testing.assert_allclose(ks[idx], ko, atol=TRAJ_ATOL, rtol=0)
+    assert np.isfinite(xs).all() and np.isfinite(ks).all()
+
+
+def test_qg2_512_adaptive_cfl_matches_oracle(ctx):
+    """The 2-layer PDE alone at 512^2 with a dt large enough that the CFL rule
+    fires: same dt sequence and qk as QG2Oracle (fused transforms + QG stream,
+    the defaults), and U0 of the device equal to the oracle's."""
+    nx, L = 512, 20.0
+    qk0 = _ring_qk(nx, L, np.random.default_rng(7), Ug=0.3)
+    m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, L=L, ctx=ctx)
+    o = orc.QG2Oracle(qk0, nx, L, 3.0, shear_strength=0.5)
+    U0 = m.max_speed()
+    assert abs(U0 - o.U0) < 1e-12 * o.U0
+    o.dt = dt = 2.5 * o.dt
+    o.exps(o.dt)
+    fired = 0
+    for _ in range(5):
+        dt, U0, changed = m.cfl_update(dt, 0.25)
+        fired += changed
+        m.step(dt)
+        o.step()
+        assert abs(dt - o.dt) <= 1e-12 * o.dt
+    assert fired >= 1
+    assert _rel(m.qk, o.qk) < QG_RTOL

@@ -3,7 +3,11 @@ vs the oracle's direct sincos sum.  Not a rounding-order restatement (the
 reference has no production code for it), so compared within tolerance:
   fp64: <= 1e-12 of the field's max magnitude (phase recurrence over <= 511
         modes per row, re-seeded every row);
-  fp32: reported error study (config 5), asserted only to be < 1e-3."""
+  fp32: the config-5 envelope at 1024^2 (test_config5_fp32_envelope_1024):
+        positions within steps*dt*e_U, wavevectors within steps*dt*e_gradU
+        (e_* = the fp32 evaluation error of U / grad U at the start points),
+        at most linear growth, and the same absolute-frequency drift as fp64;
+        full table in profiles/r02_config5_fp32_study.json (tools/fp32_study.py)."""
 import numpy as np
 import pytest
 
@@ -98,3 +102,27 @@ def test_spectral_leapfrog_matches_oracle(ctx):
     # leapfrog keeps a shadow Hamiltonian: O(dt^2) oscillation, no drift (cf. the
     # ~2.5e-3 level of images/Symplectic_error/second_order_symplectic_error_dt=0.05.png)
     assert (np.abs(Om(xg, kg) - Om(x, k)) / Om(x, k)).max() < 2e-3
+
+
+def test_config5_fp32_envelope_1024(ctx):
+    """BASELINE configs[4] (symplectic_full_fourier.m:20,37,44 at 1024^2, a
+    65k subset of the 1e7-packet ensemble): fp32 and fp64 exact-kick leapfrog
+    side by side over 64 steps of dt = 0.1*dx/max(Cg, U0).  Envelope:
+      per-step bound  max|x32 - x64|(s) <= 2 * s * dt * e_U
+                      max|k32 - k64|(s) / max|k| <= 2 * s * dt * e_gradU
+      growth          error(64) / error(8) <= 8  (no faster than linear)
+      science         |drift32 - drift64| <= 1e-8 of the relative Omega_abs
+                      drift (symplectic_full_fourier.m:54-57)."""
+    from tools.fp32_study import study
+    r = study(ctx, nx=1024, stride=153, chunks=8, per_chunk=8)
+    dt, eU, eG = r["dt"], r["fp32_eval_err_U"], r["fp32_eval_err_gradU"]
+    assert 0 < eU < 1e-5 and 0 < eG < 1e-4, (eU, eG)
+    tab = r["table"]
+    for row in tab:
+        s = row["steps"]
+        assert row["max_abs_x_err"] <= 2 * s * dt * eU, row
+        assert row["max_rel_k_err"] <= 2 * s * dt * eG, row
+        assert abs(row["omega_abs_drift_fp32"] - row["omega_abs_drift_fp64"]) <= 1e-8, row
+        assert row["omega_abs_drift_fp64"] < 1e-3  # leapfrog shadow-Hamiltonian level
+    assert tab[-1]["max_abs_x_err"] <= 8 * tab[0]["max_abs_x_err"]
+    assert tab[-1]["max_rel_k_err"] <= 8 * tab[0]["max_rel_k_err"]
