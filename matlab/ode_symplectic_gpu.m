@@ -19,7 +19,7 @@ function [x, k, t] = ode_symplectic_gpu(x0, k0, dt, T, f, gH, scheme)
     end
     X0 = reshape(x0, 2, P)';   % P x 2 (packet_x layout)
     K0 = reshape(k0, 2, P)';
-    [~, ~, hx, hk] = swrt_mex('leapfrog', X0, K0, dt, Nsteps - 1, f, gH, 1, 0, 0, scheme.bump, 1);
+    [~, ~, hx, hk] = swrt_mex('leapfrog', scheme.h, X0, K0, dt, Nsteps - 1, f, gH, 1, 0, 0, scheme.bump, 1);
     % hx: P x 2 x (Nsteps-1) frames -> Nsteps x 2 x P
     x(2:end, :, :) = permute(hx, [3 2 1]);
     k(2:end, :, :) = permute(hk, [3 2 1]);

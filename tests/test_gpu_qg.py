@@ -428,3 +428,49 @@ def test_qg2_512_adaptive_cfl_matches_oracle(ctx):
         assert abs(dt - o.dt) <= 1e-12 * o.dt
     assert fired >= 1
     assert _rel(m.qk, o.qk) < QG_RTOL
+
+
+def test_integrator_substitution_preserves_omega_statistics(ctx, tmp_path):
+    """The drivers replace the reference's ode23 packet integrator
+    (qg2layersw_raytrace.m:195) by nsub fused leapfrog substeps per PDE
+    interval.  Here the 2-layer driver runs 1600 PDE steps at 128^2 with
+    20,000 packets twice from the same PDE state and packets — once with each
+    integrator (the PDE does not see the packets, so both runs see the same
+    flow) — and the science output of analysis/load_data.m:33-52,63 is
+    compared: omega = sqrt(f^2 + Cg^2 |k|^2) per packet and frame.
+      * the per-packet difference grows along the run (ode23's local error
+        control at RelTol 1e-3 vs the symplectic substeps), so the comparison
+        is statistical;
+      * mean omega(t)/f of every frame agrees within 4 standard errors;
+      * the omega distributions of the last frames agree by a two-sample KS
+        test at alpha = 0.001 (D <= 1.95 sqrt(2/N));
+      * the load_data.m energy spectrum (center .* histcounts(omega, edges),
+        300 bins) carries the same total to within 4 standard errors."""
+    from scipy import stats
+    nx, N, f, Cg = 128, 20_000, 3.0, 1.0
+    om = {}
+    for integ in ("leapfrog", "ode23"):
+        d = tmp_path / integ
+        res = sw.qg2layersw_raytrace(nx, N, 4.0, 1e5, 0.0, 0.2, f, Cg, out_dir=str(d), nsub=5, max_steps=1600,
+                                     seed=11, integrator=integ, ctx=ctx)
+        assert res["steps"] == 1600
+        k = sw.read_field(str(d / "packet_k"), N, 2, 1)  # N x 2 x frames
+        om[integ] = np.sqrt(f * f + Cg * Cg * (k ** 2).sum(axis=1))  # load_data.m:33, N x frames
+    a, b = om["leapfrog"], om["ode23"]
+    assert a.shape == b.shape and a.shape[1] == 1 + 1600 // 25
+    np.testing.assert_array_equal(a[:, 0], b[:, 0])  # same initial packets
+    # the per-packet difference grows, and the distribution evolved from its start (all omega_0 = 4f)
+    dif = np.abs(a - b).max(axis=0)
+    assert dif[-1] > 4 * dif[2], dif
+    assert a[:, -1].std() > 0.01 * f
+    for fr in range(a.shape[1]):  # mean_omega = mean(omega)/f (load_data.m:63)
+        se = np.sqrt(a[:, fr].var() / N + b[:, fr].var() / N)
+        assert abs(a[:, fr].mean() - b[:, fr].mean()) <= 4 * se + 1e-12, fr
+    wa, wb = a[:, -4:].ravel(), b[:, -4:].ravel()
+    D = stats.ks_2samp(wa, wb).statistic
+    assert D <= 1.95 * np.sqrt(2.0 / N), D  # N independent packets per run (frames are correlated)
+    edges = np.linspace(0, max(wa.max(), wb.max()), 300)
+    center = (edges[1:] + edges[:-1]) / 2
+    ea = (center * np.histogram(wa, edges)[0]).sum() / wa.size
+    eb = (center * np.histogram(wb, edges)[0]).sum() / wb.size
+    assert abs(ea - eb) <= 4 * np.sqrt(wa.var() / N + wb.var() / N) + (edges[1] - edges[0])
