@@ -40,7 +40,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import swraytracing_amd as sw  # noqa: E402
-from swraytracing_amd.dist import gather_to_root, max_over_ranks  # noqa: E402
+from swraytracing_amd.dist import gather_packets, max_over_ranks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 BYTES_STEADY = 1792          # 32+32 state + 1 snap * 6 fields * 36 taps * 8 B
@@ -350,9 +350,10 @@ def main():
     finite = bool(np.isfinite(xg).all() and np.isfinite(kg).all())
     gathered = None
     if distributed and args.gather:
-        full = gather_to_root(np.concatenate([xg, kg], axis=1), args.packets * world, world, rank,
-                              backend=args.dist_backend)
-        gathered = None if full is None else bool(np.isfinite(full).all() and full.shape[0] == args.packets * world)
+        # device-side gather of the trajectories (the frame writer's input): libswrt -> torch buffer -> all_gather
+        full = gather_packets(ctx, args.packets * world, world, rank)
+        gathered = None if full is None else bool(np.isfinite(full[0]).all() and np.isfinite(full[1]).all()
+                                                  and full[0].shape[0] == args.packets * world)
 
     N = args.packets
     ivs = w["intervals"]

@@ -128,6 +128,12 @@ int swrt_eval(swrt_ctx* ctx, const double* x, const double* y, int64_t n, int ns
 /* Upload / download packet state (N x 2 column-major x and k). */
 int swrt_packets_set(swrt_ctx* ctx, const double* x, const double* k, int64_t n);
 int swrt_packets_get(swrt_ctx* ctx, double* x, double* k);
+/* The same state in the original packet order into DEVICE buffers of this
+ * context's GPU: x_dev[i + j*ld], k_dev[i + j*ld] (N x 2 column-major with
+ * leading dimension ld >= N), enqueued on the packet stream (swrt_get_stream)
+ * without a host synchronisation — the input of a device-side gather of
+ * sharded trajectories (RCCL all_gather, swraytracing_amd/dist.py). */
+int swrt_packets_get_device(swrt_ctx* ctx, double* x_dev, double* k_dev, int64_t ld);
 int64_t swrt_packets_count(const swrt_ctx* ctx);
 
 /* Locality tuning: the packets are kept counting-sorted by spatial tile

@@ -60,6 +60,7 @@ SIGNATURES = {
     "swrt_eval": (_INT, [_VP, _P, _P, _I, _INT, _D, _D, _P]),
     "swrt_packets_set": (_INT, [_VP, _P, _P, _I]),
     "swrt_packets_get": (_INT, [_VP, _P, _P]),
+    "swrt_packets_get_device": (_INT, [_VP, _VP, _VP, ctypes.c_int64]),
     "swrt_packets_count": (_I, [_VP]),
     "swrt_set_locality": (_INT, [_VP, _I, _I]),
     "swrt_set_tile_order": (_INT, [_VP, _INT]),
@@ -259,6 +260,16 @@ class Context:
         k = np.empty((n, 2), order="F")
         self._chk(self._L.swrt_packets_get(self._h, _p(x), _p(k)), "swrt_packets_get")
         return x, k
+
+    def packets_count(self):
+        return int(self._L.swrt_packets_count(self._h))
+
+    def packets_get_device(self, x_ptr, k_ptr, ld):
+        """swrt_packets_get_device: original-order state into device buffers
+        (addresses, N x 2 column-major with leading dimension ld) on the
+        packet stream, no host sync."""
+        self._chk(self._L.swrt_packets_get_device(self._h, ctypes.c_void_p(int(x_ptr)), ctypes.c_void_p(int(k_ptr)),
+                                                  int(ld)), "swrt_packets_get_device")
 
     def set_locality(self, rebin_every=4, tile=0):
         self._chk(self._L.swrt_set_locality(self._h, int(rebin_every), int(tile)), "swrt_set_locality")

@@ -1209,11 +1209,25 @@ int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
   HIPCHK(c, hipSetDevice(c->device));
   // un-permute into the scatter buffers, then download in original order
   hipLaunchKernelGGL(unpermute_kernel, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, c->dx, c->dk,
-                     c->perm, c->n, c->dx2, c->dk2);
+                     c->perm, c->n, c->n, c->dx2, c->dk2);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(x, c->dx2, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(k, c->dk2, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_packets_get_device(swrt_ctx* c, double* x_dev, double* k_dev, int64_t ld) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (c->n == 0) return SWRT_OK;
+  if (!x_dev || !k_dev) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  if (ld < c->n) return fail(c, SWRT_ERR_ARG, "leading dimension below the packet count");
+  HIPCHK(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(unpermute_kernel, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, c->dx, c->dk,
+                     c->perm, c->n, ld, x_dev, k_dev);
+  HIPCHK(c, hipGetLastError());
   return SWRT_OK;
   GUARD_END(c)
 }

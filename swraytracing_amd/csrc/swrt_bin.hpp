@@ -191,16 +191,17 @@ __global__ void iota_kernel(int* perm, int64_t n) {
   if (p < n) perm[p] = (int)p;
 }
 
-// Binned (device) order -> original order.
-__global__ void unpermute_kernel(const double* x, const double* k, const int* perm, int64_t n,
+// Binned (device) order -> original order; outputs N x 2 column-major with
+// leading dimension ld >= n (the second column at xo + ld).
+__global__ void unpermute_kernel(const double* x, const double* k, const int* perm, int64_t n, int64_t ld,
                                  double* xo, double* ko) {
   const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const int64_t d = perm[p];
   xo[d] = x[p];
-  xo[n + d] = x[n + p];
+  xo[ld + d] = x[n + p];
   ko[d] = k[p];
-  ko[n + d] = k[n + p];
+  ko[ld + d] = k[n + p];
 }
 
 }  // namespace swrt

@@ -56,6 +56,37 @@ def gather_to_root(local: np.ndarray, n_total: int, world: int, rank: int, backe
     return np.concatenate(parts, axis=0).reshape((n_total,) + tail)
 
 
+def gather_packets(ctx, n_total: int, world: int, rank: int, group=None):
+    """Gather every rank's device-resident packets into the full (n_total, 2)
+    x and k on rank 0, in global packet order (shard_range layout), without a
+    host round trip on the sending side: libswrt writes the shard's state in
+    original order straight into a torch device buffer (swrt_packets_get_device,
+    on the library's packet stream), and one all_gather of the (4, ceil(n/world))
+    blocks runs with that stream as torch's current stream, so the collective
+    (RCCL on "nccl"; gloo stages through the host) is ordered after the write
+    with no synchronisation.  Returns (x, k) numpy arrays on rank 0, None
+    elsewhere."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device())
+    maxn = max(1, -(-n_total // world))
+    lo, hi = shard_range(n_total, world, rank)
+    if ctx.packets_count() != hi - lo:
+        raise ValueError(f"rank {rank} holds {ctx.packets_count()} packets, its shard is {hi - lo}")
+    stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
+    with torch.cuda.stream(stream):
+        buf = torch.zeros((4, maxn), dtype=torch.float64, device=dev)  # rows x, y, k, l
+        ctx.packets_get_device(buf.data_ptr(), buf.data_ptr() + 2 * maxn * 8, maxn)
+        out = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf, group=group)
+        if rank != 0:
+            torch.cuda.current_stream().synchronize()
+            return None
+        full = torch.cat([out[r][:, : shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0]]
+                          for r in range(world)], dim=1).cpu().numpy()
+    return np.ascontiguousarray(full[0:2].T), np.ascontiguousarray(full[2:4].T)
+
+
 def max_over_ranks(value: float, backend: str = "gloo", group=None) -> float:
     """MAX of a scalar over ranks (bench timing: slowest rank defines the job)."""
     import torch

@@ -156,15 +156,27 @@ class PacketEnsemble:
     """
 
     def __init__(self, x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, device=0,
-                 bump=BUMP_QG, ctx: Context | None = None):
+                 bump=BUMP_QG, ctx: Context | None = None, shard=None):
+        """``shard`` = (rank, world): x, k are the whole ensemble (the same on
+        every rank) and this rank advances its contiguous shard (SURVEY §8e);
+        frames are gathered to rank 0 on the device (dist.gather_packets) and
+        ode23's error norm is max-reduced over the ranks."""
         self.ctx = ctx if ctx is not None else Context(device)
         self.L, self.f, self.Cg, self.nx = float(L), float(f), float(Cg), int(nx)
         self.gH = self.Cg ** 2
         self.K_d2, self.shear, self.k_scale = float(K_d2), float(shear), float(k_scale)
         self.ny_period = self.nx * nlayers
         self.bump = bump
-        self.ctx.packets_set(np.asarray(x, dtype=np.float64), np.asarray(k, dtype=np.float64))
-        self.n = np.asarray(x).shape[0]
+        x = np.asarray(x, dtype=np.float64)
+        k = np.asarray(k, dtype=np.float64)
+        self.n_total = x.shape[0]
+        self.rank, self.world = shard if shard is not None else (0, 1)
+        if self.world > 1:
+            from .dist import shard_range
+            lo, hi = shard_range(self.n_total, self.world, self.rank)
+            x, k = x[lo:hi], k[lo:hi]
+        self.ctx.packets_set(x, k)
+        self.n = x.shape[0]
         self._rebin = None
 
     def set_snapshots(self, prev_qk, qk):
@@ -203,6 +215,11 @@ class PacketEnsemble:
     def advance_ode23(self, dt, rtol=1e-3, atol=1e-6, allreduce_max=None, stats=None):
         """The reference drivers' own integrator over [0, dt] with
         interpolate_U's alpha = t/dt (ode23(ray_ode, [0, dt], y0))."""
+        if allreduce_max is None and self.world > 1:
+            import torch.distributed as dist
+
+            from .dist import allreduce_max_fn
+            allreduce_max = allreduce_max_fn(backend=dist.get_backend())
         return ode23_packets(self.ctx, (0.0, dt), dt, self.f, self.Cg, nslots=2, rtol=rtol, atol=atol,
                              bump=self.bump, allreduce_max=allreduce_max, stats=stats)
 
@@ -211,8 +228,16 @@ class PacketEnsemble:
 
     def write_frame(self, t, directory):
         """qgsw_raytrace.m:159-162: wrapped x, k and t appended to
-        packet_x.bin / packet_k.bin / packet_time.bin."""
-        x, k = self.state()
+        packet_x.bin / packet_k.bin / packet_time.bin.  Sharded: a collective
+        (every rank calls it); rank 0 writes the whole ensemble."""
+        if self.world > 1:
+            from .dist import gather_packets
+            full = gather_packets(self.ctx, self.n_total, self.world, self.rank)
+            if full is None:
+                return
+            x, k = full
+        else:
+            x, k = self.state()
         L = self.L
         write_field(np.mod(x + L / 2, L) - L / 2, os.path.join(directory, "packet_x"))
         write_field(k, os.path.join(directory, "packet_k"))

@@ -189,6 +189,17 @@ class _IntervalGroup:
             self.dts = []
 
 
+def _dist_info():
+    """(rank, world) of an initialised torch.distributed job, else (0, 1)."""
+    try:
+        import torch.distributed as dist
+    except ImportError:
+        return 0, 1
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
 def _fresh_outputs(out_dir, fresh):
     """write_field.m:31 appends to existing files; a driver run starting from
     t = 0 removes earlier outputs first unless fresh=False."""
@@ -270,8 +281,10 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     them as write_field.m:31 does.  Returns a dict of run facts (dt, Nsteps,
     steps run, frames written, final t)."""
     ctx = ctx if ctx is not None else Context(0)
-    _fresh_outputs(out_dir, fresh)
-    log = _Log(os.path.join(out_dir, "run.log"), verbose)
+    rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
+    if rank == 0:
+        _fresh_outputs(out_dir, fresh)
+    log = _Log(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
     L = 2 * math.pi
     dx = L / nx
     rng = np.random.default_rng(seed)
@@ -304,14 +317,16 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     log(f"Background velocity (parameter,computed): ({U_g:f},{U0:f})\n")
     log(f"Froude Number: {Fr:f}\n")
     log(f"Deformation wavenumber: {K_d2:f}\n")
-    ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, bump=BUMP_QG, ctx=ctx) \
+    ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, bump=BUMP_QG, ctx=ctx,
+                         shard=(rank, world)) \
         if Npackets > 0 else None
     t = 0.0
     frames = 1
     if ens is not None:
         ens.write_frame(dt * (packet_step_start - 1), out_dir)
-    write_field(model.q(), os.path.join(out_dir, "pv"))
-    write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+    if rank == 0:
+        write_field(model.q(), os.path.join(out_dir, "pv"))
+        write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
     nrun = Nsteps if max_steps is None else min(Nsteps, int(max_steps))
     have_cur = False
     group = _IntervalGroup(ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
@@ -330,7 +345,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
                 frames += 1
         else:
             have_cur = False
-        if step % steps_per_save == 0:
+        if step % steps_per_save == 0 and rank == 0:
             write_field(model.q(), os.path.join(out_dir, "pv"))
             write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
     if group is not None:
@@ -349,8 +364,10 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     pv.bin holds the initial nx x nx x 2 frame only, as in the reference.
     ``packet_intervals``, ``integrator``, ``fresh``: as in :func:`qgsw_raytrace`."""
     ctx = ctx if ctx is not None else Context(0)
-    _fresh_outputs(out_dir, fresh)
-    log = _Log(os.path.join(out_dir, "run.log"), verbose)
+    rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
+    if rank == 0:
+        _fresh_outputs(out_dir, fresh)
+    log = _Log(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
     L = 20.0
     dx = L / nx
     rng = np.random.default_rng(seed)
@@ -388,13 +405,14 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     log(f"Froude Number: {Fr:f}\n")
     log(f"Deformation wavenumber: {K_d2:f}\n")
     ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=shear, k_scale=2 * math.pi / L, nlayers=2,
-                         bump=BUMP_QG, ctx=ctx) if Npackets > 0 else None
+                         bump=BUMP_QG, ctx=ctx, shard=(rank, world)) if Npackets > 0 else None
     t = 0.0
     frames = 1
     if ens is not None:
         ens.write_frame(dt * (packet_step_start - 1), out_dir)
-    write_field(model.q(), os.path.join(out_dir, "pv"))
-    write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+    if rank == 0:
+        write_field(model.q(), os.path.join(out_dir, "pv"))
+        write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
     loop = TwoLayerLoop(model, ens, dt, U0, CFL_fraction, packet_delay_steps, nsub, packet_intervals, integrator,
                         log)
     # (the reference only plots q every steps_per_save steps in this loop; its

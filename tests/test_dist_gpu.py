@@ -1,0 +1,130 @@
+"""The sharded multi-GPU path on one GPU: two processes (torch.distributed.run,
+gloo backend so both ranks may share GPU 0 — RCCL refuses two ranks on one
+device), each running the HIP packet path on its contiguous shard with the
+field replicated, then the device-side gather (swraytracing_amd.dist.
+gather_packets: swrt_packets_get_device into a torch buffer, one all_gather).
+The gathered trajectories must equal a single-process run bit for bit (the
+packet kernels are bit-exact whatever the ensemble's size, order or binning)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+WORKER = r"""
+import os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["SWRT_ROOT"])
+import swraytracing_amd as sw
+from swraytracing_amd.dist import gather_packets, shard_range
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+w = np.load(sys.argv[1])
+nx, N = int(w["nx"]), w["x"].shape[0]
+ctx = sw.Context(0)
+ctx.set_locality(4, 0)
+ctx.set_field_grid(0, w["p0"], nx, float(w["L"]), 2 * nx)
+ctx.set_field_grid(1, w["p1"], nx, float(w["L"]), 2 * nx)
+lo, hi = shard_range(N, world, rank)
+ctx.packets_set(w["x"][lo:hi], w["k"][lo:hi])
+for s in range(int(w["calls"])):
+    ctx.advance(float(w["dt"]), int(w["nsub"]), 3.0, 1.0, nslots=2, alpha0=0.1, dalpha=0.15, bump=sw.BUMP_QG)
+out = gather_packets(ctx, N, world, rank)
+if rank == 0:
+    np.savez(sys.argv[2], x=out[0], k=out[1])
+ctx.close()
+dist.destroy_process_group()
+"""
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_sharded_hip_path_gathers_bit_identical(ctx, tmp_path):
+    from oracle import swrt_oracle as orc
+    nx, L, N = 128, 20.0, 30_001  # odd: the shards differ by one packet
+    rng = np.random.default_rng(2)
+    kmax = nx // 2 - 1
+    qk = np.zeros((2 * kmax + 1, kmax + 1), complex)
+    kx = np.arange(-kmax, kmax + 1)[:, None]
+    ky = np.arange(kmax + 1)[None, :]
+    ring = (kx * kx + ky * ky > 9) & (kx * kx + ky * ky <= 100)
+    qk[ring] = 0.01 * np.exp(2j * np.pi * rng.random(ring.sum()))
+    ctx.set_field_qk(0, qk, nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+    ctx.set_field_qk(1, qk * np.exp(0.1j), nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+    p0, p1 = ctx.get_field_grid(0, nx), ctx.get_field_grid(1, nx)
+    x, k = orc.initial_packets(N, L, 4.0, 3.0, 1.0, rng)
+    w = dict(nx=nx, L=L, p0=p0, p1=p1, x=x, k=k, dt=0.02, nsub=5, calls=6)
+    np.savez(tmp_path / "in.npz", **w)
+    # single process, same calls
+    ctx.set_locality(4, 0)
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    ctx.packets_set(x, k)
+    for _ in range(w["calls"]):
+        ctx.advance(w["dt"], w["nsub"], 3.0, 1.0, nslots=2, alpha0=0.1, dalpha=0.15, bump=orc.BUMP_QG)
+    xr, kr = ctx.packets_get()
+    (tmp_path / "worker.py").write_text(WORKER)
+    env = dict(os.environ, SWRT_ROOT=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(tmp_path / "worker.py"),
+           str(tmp_path / "in.npz"), str(tmp_path / "out.npz")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = np.load(tmp_path / "out.npz")
+    assert got["x"].shape == (N, 2)
+    np.testing.assert_array_equal(got["x"], xr)
+    np.testing.assert_array_equal(got["k"], kr)
+
+
+DRIVER = r"""
+import os, sys
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["SWRT_ROOT"])
+import swraytracing_amd as sw
+torch.cuda.set_device(0)
+dist.init_process_group("gloo")
+ctx = sw.Context(0)
+sw.qg2layersw_raytrace(64, 5001, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=sys.argv[1], nsub=2, max_steps=30, seed=5,
+                       integrator=sys.argv[2], ctx=ctx)
+ctx.close()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.parametrize("integrator", ["leapfrog", "ode23"])
+def test_two_rank_driver_files_equal_single_process(ctx, tmp_path, integrator):
+    """qg2layersw_raytrace sharded over two ranks (packets split, field
+    replicated, frames gathered on the device and written by rank 0; ode23's
+    error norm max-reduced over the ranks so both take the same steps)
+    writes the same packet_x/k/time.bin and pv.bin as one process."""
+    import swraytracing_amd as sw
+    ref = tmp_path / "single"
+    sw.qg2layersw_raytrace(64, 5001, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(ref), nsub=2, max_steps=30, seed=5,
+                           integrator=integrator, ctx=ctx)
+    (tmp_path / "driver.py").write_text(DRIVER)
+    out = tmp_path / "sharded"
+    env = dict(os.environ, SWRT_ROOT=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(tmp_path / "driver.py"), str(out),
+           integrator]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for name in ("packet_x.bin", "packet_k.bin", "packet_time.bin", "pv.bin"):
+        a, b = (ref / name).read_bytes(), (out / name).read_bytes()
+        assert len(a) > 0 and a == b, name
