@@ -492,8 +492,12 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
           }
           if constexpr (TWO) {
             const double oma = 1 - alpha;
+            // V5 fields have v_y == -u_x in both snapshots (and both gathers
+            // sum them in the same order), so the blended v_y is exactly the
+            // negated blended u_x: negation commutes with every rounding
 #pragma unroll
-            for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
+            for (int q = 0; q < (V5 ? 5 : kRec); ++q) I[q] = oma * I[q] + alpha * J[q];
+            if constexpr (V5) I[5] = -I[2];
           }
         }
         const double x2 = x1 + dt * I[0];

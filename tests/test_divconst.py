@@ -51,3 +51,57 @@ def test_markstein_division_by_3_and_5_is_correctly_rounded(tmp_path):
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout
+
+
+WEIGHTS = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+static uint64_t s = 0x2545F4914F6CDD1Dull;
+static uint64_t nxt(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+static double divc(double x, int d) {  /* the kernel's div_const: exact for |d| in {1,2,4}, Markstein for 3, 5 */
+  int a = d < 0 ? -d : d; double q;
+  if (a == 1 || a == 2 || a == 4) q = x * (1.0 / a);
+  else { double R = 1.0 / a, q0 = x * R, r = fma(-q0, (double)a, x); q = fma(r, R, q0); }
+  return d < 0 ? -q : q;
+}
+static int oddp(int d) { d = d < 0 ? -d : d; while (d % 2 == 0) d /= 2; return d; }
+static double scl(int d) { double c = d < 0 ? -1.0 : 1.0; d = d < 0 ? -d : d; while (d % 2 == 0) { d /= 2; c *= 0.5; } return c; }
+int main(void) {
+  long bad = 0;
+  for (long n = 0; n < 4000000; ++n) {
+    double a;
+    if (n < 64) a = (double)n / 64.0; else { uint64_t m = nxt() >> 12; a = (double)m / 4503599627370496.0; }
+    double bump = (n & 1) ? 1e-10 : 1e-13;
+    double t[6];
+    for (int j = -2; j <= 3; ++j) t[j + 2] = (a - (double)j) + bump;
+    for (int i = -2; i <= 3; ++i) {
+      double w = 1.0, v = 1.0, c = 1.0;
+      for (int j = -2; j <= 3; ++j) {
+        if (j == i) continue;
+        w = w * t[j + 2] / (double)(j - i);   /* interpolate.m:37 (IEEE division) */
+        v = divc(v * t[j + 2], oddp(j - i));  /* odd part in the running product */
+        c *= scl(j - i);
+      }
+      v = v * c;
+      if (memcmp(&v, &w, 8) != 0) ++bad;
+    }
+  }
+  printf("%ld\n", bad);
+  return bad != 0;
+}
+"""
+
+
+def test_lagrange_weights_with_hoisted_powers_of_two_are_bit_exact(tmp_path):
+    """swrt_kernels.hpp lagrange_wi: the signs and powers of two of the five
+    divisors applied once after the running product of the odd parts give
+    interpolate.m's weights bit for bit (4e6 offsets a in [0, 1), both bumps,
+    all six weights, including the grid points a = k/64)."""
+    c = tmp_path / "w.c"
+    c.write_text(WEIGHTS)
+    exe = tmp_path / "w"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout
