@@ -385,6 +385,13 @@ int swrt_swap_slots(swrt_ctx* ctx, int a, int b);
 /* ---------------------------------------------------------------------------
  * Runtime helpers
  * ------------------------------------------------------------------------ */
+/* Hardware conformance check of the hot loop's short IEEE sequences
+ * (swrt_kernels.hpp sqrt_rn_normal, rcp_rn_normal, drift_inc's fast path —
+ * the half-step drift of ode_symplectic.m:10-16): 16*n random operands over
+ * their documented ranges, compared bit for bit with the compiler's IEEE
+ * sqrt and division on the device.  mismatches3 = {sqrt, 1/w, drift}; all
+ * zero on a conforming device.  Diagnostic; no reference counterpart. */
+int swrt_check_arith(swrt_ctx* ctx, int64_t n, uint64_t seed, int64_t* mismatches3);
 int swrt_synchronize(swrt_ctx* ctx);
 /* The hipStream_t all of ctx's work is ordered on (for external event timing). */
 int swrt_get_stream(swrt_ctx* ctx, void** stream_out);

@@ -99,6 +99,7 @@ SIGNATURES = {
     "swrt_qg_snapshot": (_INT, [_VP, _INT, _INT, _INT, _I]),
     "swrt_swap_slots": (_INT, [_VP, _INT, _INT]),
     "swrt_field_div_free": (_INT, [_VP, _INT]),
+    "swrt_check_arith": (_INT, [_VP, _I, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64)]),
     "swrt_synchronize": (_INT, [_VP]),
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
@@ -490,6 +491,14 @@ class Context:
     # ---- runtime ---------------------------------------------------------
     def synchronize(self):
         self._chk(self._L.swrt_synchronize(self._h), "swrt_synchronize")
+
+    def check_arith(self, n=1 << 20, seed=1):
+        """Bit-exactness of the hot loop's short sqrt / reciprocal / drift
+        sequences against the device's IEEE operations over 16*n random
+        operands (swrt_check_arith): mismatch counts (sqrt, 1/w, drift)."""
+        out = (ctypes.c_int64 * 3)()
+        self._chk(self._L.swrt_check_arith(self._h, int(n), int(seed), out), "swrt_check_arith")
+        return tuple(out)
 
     def stream(self):
         s = _VP()

@@ -354,6 +354,8 @@ FieldView view_of(const Slot& s) {
   v.py = (double)s.ny_period;
   v.inv_px = 1.0 / v.px;
   v.inv_py = 1.0 / v.py;
+  v.ipx = (int)s.nx;
+  v.ipy = (int)s.ny_period;
   v.inv_dx = 1.0 / v.dx;
   return v;
 }
@@ -658,6 +660,7 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
   a.dt = dt;
   a.half = dt / 2;
   a.f2 = f * f;
+  a.fastdisp = dispersion_fast(a.f2);
   a.gH = gH;
   a.alpha0 = alpha0;
   a.dalpha = dalpha;
@@ -735,6 +738,7 @@ int run_advance_intervals(swrt_ctx* c, int nint, const double* hs, int64_t nsub,
     a.dt = hs[i0];
     a.half = hs[i0] / 2;
     a.f2 = f * f;
+    a.fastdisp = dispersion_fast(a.f2);
     a.gH = gH;
     a.alpha0 = alpha0;
     a.dalpha = dalpha;
@@ -1752,6 +1756,25 @@ int swrt_omega_histogram(swrt_ctx* c, double f, double Cg, const double* edges, 
   for (int64_t i = 0; i < nbins; ++i) counts_inout[i] += (int64_t)hc[i];
   if (c->n > 0) mean = sum / (double)c->n;
   if (mean_omega_out) *mean_omega_out = mean;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_check_arith(swrt_ctx* c, int64_t n, uint64_t seed, int64_t* mismatches3) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  if (n <= 0 || !mismatches3) return fail(c, SWRT_ERR_ARG, "n must be > 0, mismatches3 non-NULL");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_scratch(c, 3 * sizeof(unsigned long long)))) return rc;
+  unsigned long long* d = (unsigned long long*)c->scratch;
+  HIPCHK(c, hipMemsetAsync(d, 0, 3 * sizeof(unsigned long long), c->stream));
+  hipLaunchKernelGGL(check_arith_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, n, seed, d);
+  HIPCHK(c, hipGetLastError());
+  unsigned long long h[3];
+  HIPCHK(c, hipMemcpyAsync(h, d, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int q = 0; q < 3; ++q) mismatches3[q] = (int64_t)h[q];
   return SWRT_OK;
   GUARD_END(c)
 }

@@ -29,6 +29,7 @@ struct FieldView {
   double dx;            // L / nx (interpolate.m dx = dy = h)
   double px, py;        // mod periods of x/dx and y/dy (nx, ny_period)
   double inv_px, inv_py;
+  int ipx, ipy;          // the periods as ints
   double inv_dx;        // RN(1/dx): locality keys, and x/dx via div_rn (correctly rounded)
 };
 
@@ -47,28 +48,143 @@ __device__ __forceinline__ double div_rn(double a, double b, double rb) {
   return __builtin_fma(r, rb, q0);
 }
 
+// a / b correctly rounded from rb = RN(1/b), as div_rn, with the sign of a
+// zero quotient kept: r = a - q0*b is formed as -(q0*b - a) (the same value,
+// exact), so a = -0 gives -0 like IEEE division (div_rn gives +0).  The
+// negations are FMA source modifiers: still one multiply and two FMAs.
+__device__ __forceinline__ double div_rn_z(double a, double b, double rb) {
+  const double q0 = a * rb;
+  const double r = __builtin_fma(q0, b, -a);
+  return __builtin_fma(-r, rb, q0);
+}
+
+// sqrt(x), correctly rounded, for 2^-767 <= x < +inf: the instruction
+// sequence the compiler emits for sqrt() (v_rsq_f64 + Goldschmidt/Newton
+// steps) without its input scaling (an identity on this range) and its
+// +-0/+inf class select (not reachable on it) — 10 instructions instead of 17.
+// Callers guarantee the range through f^2 >= 2^-767 (dispersion_fast()).
+__device__ __forceinline__ double sqrt_rn_normal(double x) {
+  const double y = __builtin_amdgcn_rsq(x);
+  double g = x * y;
+  double h = y * 0.5;
+  const double r = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, r, g);
+  double d = __builtin_fma(-g, g, x);
+  h = __builtin_fma(h, r, h);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+
+// RN(1/b) for 2^-766 <= b <= 2^1022: the compiler's IEEE division sequence
+// for 1.0/b (v_rcp_f64, two Newton steps, then q = 1*y, r = 1 - b*q and the
+// final q + r*y) without v_div_scale (which scales only outside this range)
+// and v_div_fixup (special operands only) — 7 instructions instead of 11.
+__device__ __forceinline__ double rcp_rn_normal(double b) {
+  double y = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  e = __builtin_fma(-b, y, 1.0);
+  y = __builtin_fma(y, e, y);
+  const double r = __builtin_fma(-b, y, 1.0);
+  return __builtin_fma(r, y, y);
+}
+
+// Half-step drift increment of ode_symplectic.m:10-16,
+//   (hcx, hcy) = half * (gH*k/omega, gH*l/omega),  omega = sqrt(f^2 + gH*|k|^2),
+// in IEEE operations.  fast (f^2 >= 2^-767, uniform): omega by sqrt_rn_normal
+// and both quotients from ONE correctly rounded reciprocal (div_rn_z,
+// Markstein), 23 instructions instead of 39 — the same bits for every packet
+// with |gH*k/omega| >= 2^-1022 and f^2 + gH*|k|^2 finite (|k| < ~1e154):
+// outside that the packet's state is already meaningless.
+__device__ __forceinline__ void drift_inc(double k, double l, double f2, double gH, double half, bool fast,
+                                          double& hcx, double& hcy) {
+  const double x = f2 + gH * (k * k + l * l);
+  if (fast) {
+    const double w = sqrt_rn_normal(x);
+    const double rw = rcp_rn_normal(w);
+    hcx = half * div_rn_z(gH * k, w, rw);
+    hcy = half * div_rn_z(gH * l, w, rw);
+  } else {
+    const double w = sqrt(x);
+    hcx = half * (gH * k / w);
+    hcy = half * (gH * l / w);
+  }
+}
+
+// Host-side: may drift_inc take its fast path for this f^2?
+__host__ __device__ inline bool dispersion_fast(double f2) { return f2 >= 0x1p-767 && f2 < 0x1p+1000; }
+
+// Hardware conformance check of the short sequences (swrt_check_arith):
+// random operands over their whole documented ranges, compared bit for bit
+// with the compiler's IEEE sqrt / division.  mismatches[0..2] = sqrt, 1/w,
+// drift quotients.
+__global__ void __launch_bounds__(256) check_arith_kernel(int64_t n, uint64_t seed,
+                                                          unsigned long long* mismatches) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  uint64_t s = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(p + 1));
+  auto nxt = [&]() {
+    s ^= s << 13; s ^= s >> 7; s ^= s << 17;
+    return s;
+  };
+  auto rnd = [&](int lo, int hi) {  // random positive double, exponent in [lo, hi]
+    const uint64_t m = nxt() & ((1ull << 52) - 1);
+    const int e = lo + (int)(nxt() % (uint64_t)(hi - lo + 1));
+    return __longlong_as_double((long long)(((uint64_t)(e + 1023) << 52) | m));
+  };
+  unsigned bad[3] = {0, 0, 0};
+  for (int it = 0; it < 16; ++it) {
+    const double x = rnd(-767, 1023);
+    if (__double_as_longlong(sqrt_rn_normal(x)) != __double_as_longlong(sqrt(x))) ++bad[0];
+    const double w = rnd(-383, 511);
+    if (__double_as_longlong(rcp_rn_normal(w)) != __double_as_longlong(1.0 / w)) ++bad[1];
+    const double f2 = rnd(-60, 60), gH = rnd(-30, 30);
+    const double k = (nxt() & 1 ? -1.0 : 1.0) * rnd(-40, 40), l = (nxt() & 1 ? -1.0 : 1.0) * rnd(-40, 40);
+    double hx, hy, gx, gy;
+    drift_inc(k, l, f2, gH, 0.5, true, hx, hy);
+    drift_inc(k, l, f2, gH, 0.5, false, gx, gy);
+    if (__double_as_longlong(hx) != __double_as_longlong(gx) || __double_as_longlong(hy) != __double_as_longlong(gy))
+      ++bad[2];
+  }
+  for (int q = 0; q < 3; ++q)
+    if (bad[q]) atomicAdd(&mismatches[q], (unsigned long long)bad[q]);
+}
+
+// v_cvt_i32_f64 with the hardware's defined behaviour (NaN -> 0, saturation
+// outside the int range); C++'s (int) would be undefined there.
+__device__ __forceinline__ int cvt_i32_sat(double v) {
+  int c;
+  asm("v_cvt_i32_f64 %0, %1" : "=v"(c) : "v"(v));
+  return c;
+}
+
 // interpolate.m:21-31 — xl = mod(x/dx, n); i0 = 1 + floor(xl); a = 1 + xl - i0.
 // Returns the 0-based cell reduced mod nx and the fractional offset a.
-// inv_dx = RN(1/dx) and inv_period = RN(1/period) from the host.
-// q/period is div_rn for every period: for a power of two inv_period is
-// exact, q0 = q*inv_period is already the quotient and the correction adds
-// r = 0 (a zero of either sign gives the same cell and offset), so no
-// per-lane select between a plain multiply and div_rn is needed.
+// inv_dx = RN(1/dx) and inv_period = RN(1/period) from the host, iperiod =
+// the period as an int.  q/period is div_rn for every period: for a power of
+// two inv_period is exact, q0 = q*inv_period is already the quotient and the
+// correction adds r = 0 (a zero of either sign gives the same cell and
+// offset), so no per-lane select between a plain multiply and div_rn is needed.
 __device__ __forceinline__ int cell_frac(double x, double dx, double inv_dx, double period,
-                                         double inv_period, int nx, double& a) {
+                                         double inv_period, int iperiod, int nx, double& a) {
   const double q = div_rn(x, dx, inv_dx);
   const double r = div_rn(q, period, inv_period);
   const double xl = q - floor(r) * period;   // MATLAB mod (a - floor(a/m)*m)
   const double fl = floor(xl);
   a = (1.0 + xl) - (1.0 + fl);
   // NaN/Inf positions: keep the index in range (the result is NaN anyway).
-  int c = (fl >= 0.0 && fl <= period) ? (int)fl : 0;
+  // fl outside [0, period] (or NaN: cvt gives 0) -> cell 0, as
+  // (fl >= 0 && fl <= period) ? (int)fl : 0 in two integer instructions.
+  int c = cvt_i32_sat(fl);
+  c = (unsigned)c > (unsigned)iperiod ? 0 : c;
   // c mod nx: i0 may equal the period after round-up of mod, and the 2-layer
-  // y-period is 2*nx (interpolate.m:45-46 wrap by nx).  c <= period, so one
-  // conditional subtract covers periods up to 2*nx; wider generic grids take
-  // the (rare, divergent) integer remainder.
-  if (c >= nx) c -= nx;
-  if (c >= nx) c %= nx;
+  // y-period is 2*nx (interpolate.m:45-46 wrap by nx).  Two unsigned-min
+  // subtractions (c - nx wraps above c when c < nx) reduce c <= 3nx - 1;
+  // wider generic periods (uniform) take the integer remainder.
+  c = (int)min((unsigned)c, (unsigned)(c - nx));
+  c = (int)min((unsigned)c, (unsigned)(c - nx));
+  if (iperiod >= 3 * nx) c %= nx;
   return c;
 }
 
@@ -171,8 +287,8 @@ struct Stencil {
 __device__ __forceinline__ void stencil_at(const FieldView& fv, double x, double y, double bump,
                                            Stencil& s) {
   double ax, ay;
-  s.ic = cell_frac(x, fv.dx, fv.inv_dx, fv.px, fv.inv_px, fv.nx, ax);
-  s.jc = cell_frac(y, fv.dx, fv.inv_dx, fv.py, fv.inv_py, fv.nx, ay);
+  s.ic = cell_frac(x, fv.dx, fv.inv_dx, fv.px, fv.inv_px, fv.ipx, fv.nx, ax);
+  s.jc = cell_frac(y, fv.dx, fv.inv_dx, fv.py, fv.inv_py, fv.ipy, fv.nx, ay);
   lagrange_w(ax, bump, s.wx);
   lagrange_w(ay, bump, s.wy);
 }
@@ -313,6 +429,7 @@ struct StepArgs {
   double* k;
   int64_t n;
   double dt, half, f2, gH;  // f2 = f*f
+  int fastdisp;             // dispersion_fast(f2): drift_inc's short sequences
   double alpha0, dalpha;
   int64_t s0;               // global index of the first step of this launch
   int nsteps;
@@ -345,11 +462,7 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
   // The drift after a kick and the drift that opens the next step use the
   // same k, so the increment is computed once per step (same bits).
   double hcx, hcy;
-  {
-    const double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
-    hcx = a.half * (a.gH * k0 / w);
-    hcy = a.half * (a.gH * l0 / w);
-  }
+  drift_inc(k0, l0, a.f2, a.gH, a.half, a.fastdisp, hcx, hcy);
   for (int s = 0; s < a.nsteps; ++s) {
     const int64_t sg = a.s0 + s;
     const double x1 = x0 + hcx;
@@ -362,9 +475,7 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(StepArgs a) {
     const double k2 = k0 - a.dt * (I[2] * k0 + I[4] * l0);  // RaytracingScheme.m:14
     const double l2 = l0 - a.dt * (I[3] * k0 + I[5] * l0);  // RaytracingScheme.m:15
     // phi1(x2, k2, dt/2)
-    const double w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
-    hcx = a.half * (a.gH * k2 / w);
-    hcy = a.half * (a.gH * l2 / w);
+    drift_inc(k2, l2, a.f2, a.gH, a.half, a.fastdisp, hcx, hcy);
     x0 = x2 + hcx;
     y0 = y2 + hcy;
     k0 = k2;
@@ -404,8 +515,8 @@ __global__ void __launch_bounds__(256) interp1_kernel(const double* F, int nx, d
   if (p >= n) return;
   const double px = (double)nx;
   double ax, ay;
-  const int ic = cell_frac(x[p], dx, 1.0 / dx, px, 1.0 / px, nx, ax);
-  const int jc = cell_frac(y[p], dy, 1.0 / dy, pyF, inv_py, nx, ay);
+  const int ic = cell_frac(x[p], dx, 1.0 / dx, px, 1.0 / px, nx, nx, ax);
+  const int jc = cell_frac(y[p], dy, 1.0 / dy, pyF, inv_py, (int)pyF, nx, ay);
   double wx[kNT], wy[kNT];
   lagrange_w(ax, bump, wx);
   lagrange_w(ay, bump, wy);

@@ -174,34 +174,69 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
 // five sums per snapshot from the V5 window, the same per-field order, and
 // the v_y sum as the exact negation of the u_x sum (negation commutes with
 // rounding), so the results are those of gather6_lds on the same nodes.
+//
+// Software-pipelined: tap t+1's window reads are issued before tap t's
+// arithmetic, and scheduling barriers keep that order, so a wave waits only
+// for reads issued one tap earlier (lgkmcnt 5..9 instead of draining to 0
+// every few reads).  The weights pass through an empty asm so the compiler
+// cannot hoist the 36 products wx_i*wy_j out of this path and the global
+// fallback's (both compute them): 36 hoisted products held 72 VGPRs and left
+// no room for the reads in flight.  Same operations, same order, same bits.
+#ifndef SWRT_GATHER_PIPE
+#define SWRT_GATHER_PIPE 1
+#endif
+template <bool TWO>
+struct Tap5 {
+  double2 a0, a1, c, b0, b1;
+};
+template <bool TWO, int WN>
+__device__ __forceinline__ void tap5_read(const double2* p, int e, Tap5<TWO>& t) {
+  t.a0 = p[0 * WN + e];
+  t.a1 = p[1 * WN + e];
+  if constexpr (TWO) {
+    t.c = p[2 * WN + e];
+    t.b0 = p[3 * WN + e];
+    t.b1 = p[4 * WN + e];
+  } else {
+    t.c.x = reinterpret_cast<const double*>(p + 2 * WN + e)[0];
+  }
+}
 template <bool TWO, int W, int WN>
 __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const Stencil& s,
                                             double o0[kRec], double o1[kRec]) {
 #pragma unroll
   for (int f = 0; f < 5; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
   const double2* p = lds + node0;
+  double wx[kNT], wy[kNT];
 #pragma unroll
-  for (int i = 0; i < kNT; ++i) {
+  for (int q = 0; q < kNT; ++q) {
+    wx[q] = s.wx[q];
+    wy[q] = s.wy[q];
+    asm volatile("" : "+v"(wx[q]));
+    asm volatile("" : "+v"(wy[q]));
+  }
+  Tap5<TWO> cur, nxt;
+  tap5_read<TWO, WN>(p, 0, cur);
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) {
-      const int e = i * W + j;
-      const double wij = s.wx[i] * s.wy[j];
-      const double2 a0 = p[0 * WN + e], a1 = p[1 * WN + e];
-      double2 c;
-      if constexpr (TWO)
-        c = p[2 * WN + e];
-      else
-        c.x = reinterpret_cast<const double*>(p + 2 * WN + e)[0];
-      o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
-      o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
-      o0[4] = o0[4] + wij * c.x;
-      if constexpr (TWO) {
-        const double2 b0 = p[3 * WN + e], b1 = p[4 * WN + e];
-        o1[0] = o1[0] + wij * b0.x; o1[1] = o1[1] + wij * b0.y;
-        o1[2] = o1[2] + wij * b1.x; o1[3] = o1[3] + wij * b1.y;
-        o1[4] = o1[4] + wij * c.y;
-      }
+  for (int t = 0; t < kNT * kNT; ++t) {
+    const int i = t / kNT, j = t % kNT;
+    if (t + 1 < kNT * kNT) tap5_read<TWO, WN>(p, ((t + 1) / kNT) * W + (t + 1) % kNT, nxt);
+#if SWRT_GATHER_PIPE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    const double wij = wx[i] * wy[j];
+    o0[0] = o0[0] + wij * cur.a0.x; o0[1] = o0[1] + wij * cur.a0.y;
+    o0[2] = o0[2] + wij * cur.a1.x; o0[3] = o0[3] + wij * cur.a1.y;
+    o0[4] = o0[4] + wij * cur.c.x;
+    if constexpr (TWO) {
+      o1[0] = o1[0] + wij * cur.b0.x; o1[1] = o1[1] + wij * cur.b0.y;
+      o1[2] = o1[2] + wij * cur.b1.x; o1[3] = o1[3] + wij * cur.b1.y;
+      o1[4] = o1[4] + wij * cur.c.y;
     }
+#if SWRT_GATHER_PIPE
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    if (t + 1 < kNT * kNT) cur = nxt;
   }
   o0[5] = -o0[2];
   o1[5] = -o1[2];
@@ -458,14 +493,14 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       // drift of the next one use the same k (k0 = k2), hence the same
       // value — computed once per step, bit-identical to computing it twice.
       double hcx, hcy;
-      {
-        const double w = sqrt(a.f2 + a.gH * (k0 * k0 + l0 * l0));
-        hcx = half * (a.gH * k0 / w);
-        hcy = half * (a.gH * l0 / w);
-      }
+      drift_inc(k0, l0, a.f2, a.gH, half, a.fastdisp, hcx, hcy);
+      // the blend's step index as a double, counted up by exact additions
+      // (integers < 2^53): (double)sg without an int64 conversion per step
+      double sgd = (double)(ta.ivmode ? (int64_t)0 : sbase);
       for (int st = 0; st < a.nsteps; ++st) {
         const int64_t sg = sbase + st;
-        const double alpha = a.alpha0 + (double)(ta.ivmode ? (int64_t)st : sg) * a.dalpha;
+        const double alpha = a.alpha0 + sgd * a.dalpha;
+        sgd = sgd + 1.0;
         const double x1 = x0 + hcx;
         const double y1 = y0 + hcy;
         Stencil sc;
@@ -504,9 +539,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         const double y2 = y1 + dt * I[1];
         const double k2 = k0 - dt * (I[2] * k0 + I[4] * l0);
         const double l2 = l0 - dt * (I[3] * k0 + I[5] * l0);
-        const double w = sqrt(a.f2 + a.gH * (k2 * k2 + l2 * l2));
-        hcx = half * (a.gH * k2 / w);
-        hcy = half * (a.gH * l2 / w);
+        drift_inc(k2, l2, a.f2, a.gH, half, a.fastdisp, hcx, hcy);
         x0 = x2 + hcx;
         y0 = y2 + hcy;
         k0 = k2;

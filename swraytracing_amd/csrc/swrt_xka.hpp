@@ -41,8 +41,8 @@ struct XkaStencil {
 
 __device__ __forceinline__ void xka_stencil(const XkaArgs& a, double x, double y, XkaStencil& s) {
   double ax, ay;
-  s.ic = cell_frac(x, a.dx, a.inv_dx, a.px, a.inv_px, a.nx, ax);
-  s.jc = cell_frac(y, a.dy, a.inv_dy, a.py, a.inv_py, a.nx, ay);
+  s.ic = cell_frac(x, a.dx, a.inv_dx, a.px, a.inv_px, a.nx, a.nx, ax);
+  s.jc = cell_frac(y, a.dy, a.inv_dy, a.py, a.inv_py, a.nx, a.nx, ay);
   lagrange_w(ax, a.bump, s.wx);
   lagrange_w(ay, a.bump, s.wy);
 }

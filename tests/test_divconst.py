@@ -105,3 +105,121 @@ def test_lagrange_weights_with_hoisted_powers_of_two_are_bit_exact(tmp_path):
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout
+
+
+DRIFT = r"""
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+static uint64_t s = 0x2545F4914F6CDD1Dull;
+static uint64_t nxt(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+static double rnd(int lo, int hi) {  /* random double, exponent in [lo, hi], random sign */
+  uint64_t m = nxt() & ((1ull << 52) - 1);
+  int e = lo + (int)(nxt() % (uint64_t)(hi - lo + 1));
+  uint64_t bits = ((uint64_t)(e + 1023) << 52) | m | ((nxt() & 1ull) << 63);
+  double d; memcpy(&d, &bits, 8); return d;
+}
+static int same(double a, double b) { return memcmp(&a, &b, 8) == 0; }
+/* swrt_kernels.hpp div_rn_z with rb = RN(1/b) */
+static double div_rn_z(double a, double b, double rb) {
+  double q0 = a * rb, r = fma(q0, b, -a);
+  return fma(-r, rb, q0);
+}
+int main(void) {
+  long bad = 0;
+  for (long i = 0; i < 20000000; ++i) {
+    /* drift_inc operands: gH*k over a wide range, omega >= f */
+    const double f2 = fabs(rnd(-60, 60)), gH = fabs(rnd(-30, 30));
+    const double k = rnd(-200, 200), l = rnd(-200, 200);
+    const double w = sqrt(f2 + gH * (k * k + l * l));
+    if (!isfinite(w)) continue;
+    const double rw = 1.0 / w, ak = gH * k, al = gH * l;
+    if (fabs(ak / w) < 0x1p-1022 || fabs(al / w) < 0x1p-1022) continue;  /* documented range */
+    if (!same(div_rn_z(ak, w, rw), ak / w)) ++bad;
+    if (!same(div_rn_z(al, w, rw), al / w)) ++bad;
+  }
+  /* quotients exactly representable, and signed zeros */
+  for (long m = 1; m < 2000000; ++m) {
+    const double w = (double)(2 * m + 1), a = w * (double)(m % 977 + 1) * ((m & 1) ? -1.0 : 1.0);
+    if (!same(div_rn_z(a, w, 1.0 / w), a / w)) ++bad;
+  }
+  if (!same(div_rn_z(-0.0, 3.0, 1.0 / 3.0), -0.0) || !same(div_rn_z(0.0, 3.0, 1.0 / 3.0), 0.0)) ++bad;
+  printf("%ld\n", bad);
+  return bad != 0;
+}
+"""
+
+
+def test_drift_quotients_from_one_reciprocal_are_ieee(tmp_path):
+    """drift_inc's fast path: gH*k/omega and gH*l/omega as div_rn_z from
+    RN(1/omega) equal IEEE division bit for bit (zero signs included)."""
+    c = tmp_path / "drift.c"
+    c.write_text(DRIFT)
+    exe = tmp_path / "drift"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout
+
+
+CELL = r"""
+#include <math.h>
+#include <limits.h>
+#include <stdint.h>
+#include <stdio.h>
+/* v_cvt_i32_f64: NaN -> 0, saturating */
+static int cvt_sat(double v) {
+  if (isnan(v)) return 0;
+  if (v >= 2147483647.0) return INT_MAX;
+  if (v <= -2147483648.0) return INT_MIN;
+  return (int)v;
+}
+static unsigned umin(unsigned a, unsigned b) { return a < b ? a : b; }
+static int old_c(double fl, double period, int nx) {
+  int c = (fl >= 0.0 && fl <= period) ? (int)fl : 0;
+  if (c >= nx) c -= nx;
+  if (c >= nx) c %= nx;
+  return c;
+}
+static int new_c(double fl, int iperiod, int nx) {
+  int c = cvt_sat(fl);
+  c = (unsigned)c > (unsigned)iperiod ? 0 : c;
+  c = (int)umin((unsigned)c, (unsigned)(c - nx));
+  c = (int)umin((unsigned)c, (unsigned)(c - nx));
+  if (iperiod >= 3 * nx) c %= nx;
+  return c;
+}
+int main(void) {
+  long bad = 0;
+  const int nxs[] = {1, 2, 3, 16, 64, 255, 512, 1024, 4096};
+  for (unsigned a = 0; a < sizeof nxs / sizeof nxs[0]; ++a) {
+    const int nx = nxs[a];
+    const int periods[] = {nx, 2 * nx, 3 * nx, 5 * nx + 1};
+    for (int b = 0; b < 4; ++b) {
+      const int p = periods[b];
+      for (int v = -3 * p - 5; v <= 3 * p + 5; ++v) {
+        const double fl = (double)v;
+        if (old_c(fl, (double)p, nx) != new_c(fl, p, nx)) ++bad;
+      }
+      const double spec[] = {NAN, -NAN, INFINITY, -INFINITY, -0.0, 0.0, 1e300, -1e300, 3e9, -3e9};
+      for (unsigned q = 0; q < sizeof spec / sizeof spec[0]; ++q)
+        if (old_c(spec[q], (double)p, nx) != new_c(spec[q], p, nx)) ++bad;
+    }
+  }
+  printf("%ld\n", bad);
+  return bad != 0;
+}
+"""
+
+
+def test_cell_index_integer_path_matches_reference_logic(tmp_path):
+    """cell_frac's integer tail (saturating cvt, unsigned range test, two
+    unsigned-min wraps) equals the (fl >= 0 && fl <= period) ? (int)fl : 0
+    then mod-nx logic for every integral fl in [-3p-5, 3p+5] and the special
+    values, for periods nx, 2nx, 3nx and 5nx+1."""
+    c = tmp_path / "cell.c"
+    c.write_text(CELL)
+    exe = tmp_path / "cell"
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", str(exe), str(c), "-lm"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip() == "0", out.stdout

@@ -346,6 +346,16 @@ def test_sqrt_div_correctly_rounded_on_device(ctx):
     np.testing.assert_array_equal(xg, xo)
 
 
+def test_short_ieee_sequences_match_device_ieee(ctx):
+    """The hot loop's 10-instruction sqrt, 7-instruction reciprocal and
+    one-reciprocal drift (swrt_kernels.hpp sqrt_rn_normal / rcp_rn_normal /
+    drift_inc) equal the compiler's IEEE sqrt and division bit for bit over
+    6.7e7 random operands per sequence spanning their documented ranges
+    (the division quotients' correctness from RN(1/w) is also proven on the
+    host: tests/test_divconst.py)."""
+    assert ctx.check_arith(1 << 22, seed=7) == (0, 0, 0)
+
+
 @pytest.mark.parametrize("rebin_every,tile", [(0, 0), (1, 4), (3, 8), (8, 0), (64, 16)])
 def test_spatial_binning_is_invisible(ctx, oracle_lib, qg_case, rebin_every, tile):
     """Binning only permutes the device order: final state and history frames
