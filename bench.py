@@ -255,6 +255,13 @@ def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timin
         "wait_frac": pmc["SQ_WAIT_ANY"] / max(1.0, pmc["SQ_WAVE_CYCLES"]),
         "pmc_kernel_ms": pmc_s * 1e3,
         "source": "profiles/pmc.json: " + pmc.get("source", "") + "; kernel " + pmc.get("kernel", "")})
+    if pmc.get("GRBM_GUI_ACTIVE"):
+        # GRBM_GUI_ACTIVE sums the busy cycles of the 8 XCDs: the engine clock the
+        # kernel actually ran at (below the 2.4 GHz the peaks assume under this load)
+        clk = pmc["GRBM_GUI_ACTIVE"] / 8.0 / pmc_s
+        r.update({"clock_ghz_measured": clk / 1e9,
+                  "frac_at_measured_clock": ach / (FP64_LANE_OPS_PEAK * clk / 2.4e9),
+                  "lds_frac_at_measured_clock": pmc["SQ_LDS_IDX_ACTIVE"] / (256 * clk * pmc_s)})
     return r
 
 
