@@ -202,6 +202,12 @@ struct swrt_ctx {
   int2* mode_rows = nullptr;
   int64_t mode_cap = 0;
   int64_t rows_cap = 0;
+  double2* modes_d = nullptr;  // group-padded spans (ModeGrid::Cd)
+  int* modes_d_row = nullptr;
+  float4* modes_f = nullptr;   // fp32 packed-pair copy (ModeGrid::Cf)
+  int* modes_f_row = nullptr;
+  int64_t modes_f_cap = 0;     // float4 allocated
+  int64_t modes_f_rcap = 0;
   ModeGrid mg{};
   bool modes_set = false;
   int64_t mode_active = 0;  // coefficients inside the per-row nonzero spans
@@ -851,7 +857,8 @@ void swrt_destroy(swrt_ctx* c) {
   for (void* p : {(void*)c->xka_state2, (void*)c->xka_keys, (void*)c->xka_src, (void*)c->xka_bins})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist, (void*)c->modes,
-                  (void*)c->mode_rows})
+                  (void*)c->mode_rows, (void*)c->modes_f, (void*)c->modes_f_row, (void*)c->modes_d,
+                  (void*)c->modes_d_row})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->qg.qk, (void*)c->qg.qk_prev, (void*)c->qg.Qm1, (void*)c->qg.Qm2, (void*)c->qg.E1,
                   (void*)c->qg.E2, (void*)c->qg.Z, (void*)c->qg.T, (void*)c->qg.dmax, (void*)c->qg.PZ,
@@ -1640,9 +1647,65 @@ int swrt_spectral_set_modes(swrt_ctx* c, const double* C, int64_t nkx, int64_t n
     while (hi > lo && C[2 * (j * nkx + hi - 1)] == 0.0 && C[2 * (j * nkx + hi - 1) + 1] == 0.0) --hi;
     rows[j] = make_int2(lo, hi);
   }
+  // fp32 packed-pair copy of the spans (ModeGrid::Cf): groups of 4 modes as
+  // two float4 {re_m, re_m+1, im_m, im_m+1}, zero past the span end
+  std::vector<int> frow(nky);
+  int64_t nf = 0;
+  for (int64_t j = 0; j < nky; ++j) {
+    frow[j] = (int)nf;
+    nf += 2 * (((int64_t)rows[j].y - rows[j].x + kSpecChains - 1) / kSpecChains);
+  }
+  // + zero slots: the LDS stream's chunk prefetch reads up to two chunks past
+  // the last group (SpecStream; 16-B slots in both precisions)
+  std::vector<float4> cf((size_t)(nf + 2 * kSpecChunk), make_float4(0.f, 0.f, 0.f, 0.f));
+  for (int64_t j = 0; j < nky; ++j) {
+    for (int m = rows[j].x; m < rows[j].y; ++m) {
+      const int64_t r = m - rows[j].x, q = frow[j] + 2 * (r / kSpecChains) + (r % kSpecChains) / 2;
+      const int h = (int)(r & 1);
+      float* v = reinterpret_cast<float*>(&cf[q]);
+      v[h] = (float)C[2 * (j * nkx + m)];
+      v[2 + h] = (float)C[2 * (j * nkx + m) + 1];
+    }
+  }
+  // the same groups in fp64: kSpecChains double2 per group (Cd_row = 2 * Cf_row)
+  std::vector<double2> cd((size_t)(2 * nf + 2 * kSpecChunk), make_double2(0.0, 0.0));
+  std::vector<int> drow(nky);
+  for (int64_t j = 0; j < nky; ++j) {
+    drow[j] = 2 * frow[j];
+    for (int m = rows[j].x; m < rows[j].y; ++m)
+      cd[(size_t)drow[j] + (m - rows[j].x)] = make_double2(C[2 * (j * nkx + m)], C[2 * (j * nkx + m) + 1]);
+  }
+  if ((int64_t)cd.size() > c->modes_f_cap) {
+    for (void* p : {(void*)c->modes_f, (void*)c->modes_d})
+      if (p) (void)hipFree(p);
+    c->modes_f = nullptr;
+    c->modes_d = nullptr;
+    c->modes_f_cap = 0;
+    HIPCHK(c, hipMalloc(&c->modes_f, sizeof(float4) * cd.size()));
+    HIPCHK(c, hipMalloc(&c->modes_d, sizeof(double2) * cd.size()));
+    c->modes_f_cap = (int64_t)cd.size();
+  }
+  if (nky > c->modes_f_rcap) {
+    for (void* p : {(void*)c->modes_f_row, (void*)c->modes_d_row})
+      if (p) (void)hipFree(p);
+    c->modes_f_row = nullptr;
+    c->modes_d_row = nullptr;
+    c->modes_f_rcap = 0;
+    HIPCHK(c, hipMalloc(&c->modes_f_row, sizeof(int) * nky));
+    HIPCHK(c, hipMalloc(&c->modes_d_row, sizeof(int) * nky));
+    c->modes_f_rcap = nky;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->modes_d, cd.data(), sizeof(double2) * cd.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->modes_d_row, drow.data(), sizeof(int) * nky, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->modes, C, sizeof(double2) * nkx * nky, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->mode_rows, rows.data(), sizeof(int2) * nky, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->modes_f, cf.data(), sizeof(float4) * cf.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->modes_f_row, frow.data(), sizeof(int) * nky, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->mg.Cd = c->modes_d;
+  c->mg.Cd_row = c->modes_d_row;
+  c->mg.Cf = c->modes_f;
+  c->mg.Cf_row = c->modes_f_row;
   int64_t active = 0;
   for (auto& r : rows) active += r.y - r.x;
   c->mode_active = active;

@@ -2,10 +2,13 @@
 1024^2 spectral field, fp64 vs fp32 — throughput, FP roofline and the fp32
 error growth.  Prints one JSON line.  Not the driver's bench (bench.py is).
 
-Accounting: F = 16 flop x M modes per packet-step (M = the
-dense (2kmax+1) x (kmax+1) half-plane grid the kernel sums over).
-Peaks: FP64 vector 78.6 TFLOP/s, FP32 vector 157.3 TFLOP/s (MI355X spec,
-MI355X_MICROARCH.md chip table)."""
+Accounting: F = 22 flop x M modes per packet-step (M = the modes inside the
+rows' nonzero spans, which the kernel sums): per mode and lane 5 mul + 7 FMA
++ 3 add (z = C*e, the five row sums, the phase recurrence, kx += ds) — the
+instructions of swrt_spectral.hpp's inner loop (SURVEY §8d E2 counted 16).
+Peaks: FP64 vector 78.6 TFLOP/s, FP32 vector 157.3 TFLOP/s (packed; MI355X
+spec, MI355X_MICROARCH.md chip table).  The rate includes the host copies of
+the call; the kernels' VALU-issue fractions from PMC are tools/pmc_rows.sh's."""
 import argparse
 import json
 import os
@@ -19,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import swraytracing_amd as sw  # noqa: E402
 
 PEAK = {64: 78.6, 32: 157.3}
+FLOP_PER_MODE = 22
 
 
 def main():
@@ -59,7 +63,7 @@ def main():
         xs, ks = sch.leapfrog(x, k, dt, args.steps, 3.0, 1.0)
         t = time.perf_counter() - t0
         rate = N * args.steps / t
-        tf = rate * 16 * M_active / 1e12
+        tf = rate * FLOP_PER_MODE * M_active / 1e12
         res[prec] = dict(x=xs, k=ks, rate=rate, tflops=tf, seconds=t)
     err = float(np.abs(res[32]["x"] - res[64]["x"]).max())
     errk = float(np.abs(res[32]["k"] - res[64]["k"]).max() / np.abs(res[64]["k"]).max())
@@ -74,7 +78,7 @@ def main():
                  "roofline": {"bound": "valu-fp32", "achieved": res[32]["tflops"], "peak": PEAK[32],
                               "unit": "TFLOP/s", "frac": res[32]["tflops"] / PEAK[32]},
                  "max_abs_x_err_vs_fp64": err, "max_rel_k_err_vs_fp64": errk},
-        "note": "host-buffer call incl. upload/download; 16 flop per summed mode (zero row ends skipped)",
+        "note": "host-buffer call incl. upload/download; 22 flop per summed mode (zero row ends skipped)",
     }
     print(json.dumps(out))
 
