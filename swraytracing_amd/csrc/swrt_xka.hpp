@@ -34,6 +34,47 @@ struct XkaArgs {
   const int* perm;     // binned slot -> caller's packet index (history frames); NULL: identity
 };
 
+// Per-tap dispersion of cg_sw.m:16-26: w = sqrt(f^2 + gH*K2), cx = gH*k/w,
+// cy = gH*l/w, and rw = RN(1/w) for the gradient quotients.  FAST: the short
+// sequences of drift_inc (sqrt_rn_normal, one rcp_rn_normal, Markstein
+// quotients div_rn_z) — the same bits as IEEE sqrt and division while the
+// radicand lies in [2^-767, 2^1000] (tests/test_divconst.py,
+// swrt_check_arith); a tap outside sets `bad` and the caller redoes the whole
+// interpolation with the compiler's IEEE operations (FAST = false; never
+// taken for physical fields, gH >= 0).
+struct XkaDisp {
+  double w, rw, cx, cy;
+};
+template <bool FAST>
+__device__ __forceinline__ XkaDisp xka_disp(double f2, double gH, double K2, double k, double l, bool& bad) {
+  XkaDisp d;
+  const double r = f2 + gH * K2;
+  if constexpr (FAST) {
+    bad |= !(r >= 0x1p-767 && r <= 0x1p+1000);
+    d.w = sqrt_rn_normal(r);
+    d.rw = rcp_rn_normal(d.w);
+    d.cx = div_rn_z(gH * k, d.w, d.rw);
+    d.cy = div_rn_z(gH * l, d.w, d.rw);
+  } else {
+    d.w = sqrt(r);
+    d.rw = 0.0;
+    d.cx = gH * k / d.w;
+    d.cy = gH * l / d.w;
+  }
+  return d;
+}
+// a / w and a / (2w) with the tap's dispersion (RN(1/(2w)) = RN(1/w)/2 exactly)
+template <bool FAST>
+__device__ __forceinline__ double xka_divw(double a, const XkaDisp& d) {
+  if constexpr (FAST) return div_rn_z(a, d.w, d.rw);
+  else return a / d.w;
+}
+template <bool FAST>
+__device__ __forceinline__ double xka_div2w(double a, const XkaDisp& d) {
+  if constexpr (FAST) return div_rn_z(a, 2 * d.w, 0.5 * d.rw);
+  else return a / (2 * d.w);
+}
+
 struct XkaStencil {
   int ic, jc;
   double wx[kNT], wy[kNT];
@@ -48,46 +89,56 @@ __device__ __forceinline__ void xka_stencil(const XkaArgs& a, double x, double y
 }
 
 // interpolate(x, y, U.u + C.x) and interpolate(x, y, U.v + C.y)
-// (step_packet_xka.m:42-52) with C from cg_sw.m:15-26 formed per tap.
-__device__ __forceinline__ void xka_velocity(const XkaArgs& a, double x, double y, double k, double l,
-                                             double K2, double& Iu, double& Iv) {
-  XkaStencil s;
-  xka_stencil(a, x, y, s);
+// (step_packet_xka.m:42-52) with C from cg_sw.m:15-26 formed per tap.  Rows
+// are not unrolled (6 taps each): the fully unrolled 4 RK stages + gradients
+// held 348 VGPRs, one wave per SIMD.
+template <bool FAST>
+__device__ __forceinline__ bool xka_velocity_t(const XkaArgs& a, const XkaStencil& s, double k, double l, double K2,
+                                               double& Iu, double& Iv) {
   const double* base = a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec;
   double su = 0.0, sv = 0.0;
-#pragma unroll
+  bool bad = false;
+#pragma unroll 1
   for (int i = 0; i < kNT; ++i) {
+    const double wxi = s.wx[i];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
       const double2* nd = reinterpret_cast<const double2*>(base + ((size_t)i * a.npad + j) * kXkaRec);
       const double2 uv = nd[0];
       const double H = nd[1].x;
       const double gH = a.C0sq * H;                   // cg_sw.m:16
-      const double w = sqrt(a.f2 + gH * K2);          // cg_sw.m:22
-      const double cx = gH * k / w;                   // cg_sw.m:25
-      const double cy = gH * l / w;                   // cg_sw.m:26
-      const double wij = s.wx[i] * s.wy[j];
-      su = su + wij * (uv.x + cx);
-      sv = sv + wij * (uv.y + cy);
+      // w (cg_sw.m:22), cx, cy (cg_sw.m:25-26)
+      const XkaDisp d = xka_disp<FAST>(a.f2, gH, K2, k, l, bad);
+      const double wij = wxi * s.wy[j];
+      su = su + wij * (uv.x + d.cx);
+      sv = sv + wij * (uv.y + d.cy);
     }
   }
   Iu = su;
   Iv = sv;
+  return bad;
+}
+__device__ __forceinline__ void xka_velocity(const XkaArgs& a, double x, double y, double k, double l,
+                                             double K2, double& Iu, double& Iv) {
+  XkaStencil s;
+  xka_stencil(a, x, y, s);
+  if (xka_velocity_t<true>(a, s, k, l, K2, Iu, Iv)) xka_velocity_t<false>(a, s, k, l, K2, Iu, Iv);
 }
 
 // The 7 interpolations at the new position (step_packet_xka.m:59-65):
 // u_x, u_y, v_x, v_y, gradomega.x, gradomega.y, divC.
-__device__ __forceinline__ void xka_gradients(const XkaArgs& a, double x, double y, double k, double l,
-                                              double K2, double out[7]) {
-  XkaStencil s;
-  xka_stencil(a, x, y, s);
+template <bool FAST>
+__device__ __forceinline__ bool xka_gradients_t(const XkaArgs& a, const XkaStencil& s, double k, double l, double K2,
+                                                double out[7]) {
   const double* base = a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec;
   const double kf = k * a.f, lf = l * a.f;        // k*f, l*f (cg_sw.m:29)
   const double fK2 = a.f * K2, mfK2 = (-a.f) * K2;  // f*(k^2+l^2), -f*(k^2+l^2) (cg_sw.m:30-31)
+  bool bad = false;
 #pragma unroll
   for (int q = 0; q < 7; ++q) out[q] = 0.0;
-#pragma unroll
+#pragma unroll 1
   for (int i = 0; i < kNT; ++i) {
+    const double wxi = s.wx[i];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
       const double2* nd = reinterpret_cast<const double2*>(base + ((size_t)i * a.npad + j) * kXkaRec);
@@ -95,14 +146,11 @@ __device__ __forceinline__ void xka_gradients(const XkaArgs& a, double x, double
       const double H = nd[1].x;
       const double2 g0 = nd[2], g1 = nd[3];  // (u_x, u_y), (v_x, v_y)
       const double gH = a.C0sq * H;
-      const double w = sqrt(a.f2 + gH * K2);
-      const double cx = gH * k / w;
-      const double cy = gH * l / w;
-      const double divC = (((kf * uv.y - lf * uv.x) - cx * cx) - cy * cy) / w;  // cg_sw.m:29
-      const double w2 = 2 * w;
-      const double gwx = fK2 * uv.y / w2;   // cg_sw.m:30
-      const double gwy = mfK2 * uv.x / w2;  // cg_sw.m:31
-      const double wij = s.wx[i] * s.wy[j];
+      const XkaDisp d = xka_disp<FAST>(a.f2, gH, K2, k, l, bad);
+      const double divC = xka_divw<FAST>(((kf * uv.y - lf * uv.x) - d.cx * d.cx) - d.cy * d.cy, d);  // cg_sw.m:29
+      const double gwx = xka_div2w<FAST>(fK2 * uv.y, d);   // cg_sw.m:30: / (2*w)
+      const double gwy = xka_div2w<FAST>(mfK2 * uv.x, d);  // cg_sw.m:31
+      const double wij = wxi * s.wy[j];
       out[0] = out[0] + wij * g0.x;
       out[1] = out[1] + wij * g0.y;
       out[2] = out[2] + wij * g1.x;
@@ -112,6 +160,13 @@ __device__ __forceinline__ void xka_gradients(const XkaArgs& a, double x, double
       out[6] = out[6] + wij * divC;
     }
   }
+  return bad;
+}
+__device__ __forceinline__ void xka_gradients(const XkaArgs& a, double x, double y, double k, double l,
+                                              double K2, double out[7]) {
+  XkaStencil s;
+  xka_stencil(a, x, y, s);
+  if (xka_gradients_t<true>(a, s, k, l, K2, out)) xka_gradients_t<false>(a, s, k, l, K2, out);
 }
 
 // (a + 2b + 2c + d)/6 in MATLAB's left-to-right order; /6 = (/2 exact)/3.
