@@ -2343,6 +2343,7 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   a.f2 = f * f;
   a.Cg = Cg;
   a.Cg2 = Cg * Cg;
+  a.fastdisp = dispersion_fast(a.f2);
   a.thr = thr;
   a.bump = bump;
   a.dmax = c->o_dmax;

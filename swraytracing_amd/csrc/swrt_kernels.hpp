@@ -112,6 +112,21 @@ __device__ __forceinline__ void drift_inc(double k, double l, double f2, double 
   }
 }
 
+// n1 / sqrt(r) and n2 / sqrt(r) in IEEE operations (odefun's Cg*k/s,
+// qgsw_raytrace.m:262-263): fast (r >= f^2 >= 2^-767, uniform) as drift_inc.
+__device__ __forceinline__ void quot2_sqrt(double r, double n1, double n2, bool fast, double& q1, double& q2) {
+  if (fast) {
+    const double w = sqrt_rn_normal(r);
+    const double rw = rcp_rn_normal(w);
+    q1 = div_rn_z(n1, w, rw);
+    q2 = div_rn_z(n2, w, rw);
+  } else {
+    const double w = sqrt(r);
+    q1 = n1 / w;
+    q2 = n2 / w;
+  }
+}
+
 // Host-side: may drift_inc take its fast path for this f^2?
 __host__ __device__ inline bool dispersion_fast(double f2) { return f2 >= 0x1p-767 && f2 < 0x1p+1000; }
 

@@ -38,6 +38,7 @@ struct Ode23Args {
   double inv_tmax;   // unused when tmax == 0 (steady)
   double tmax;
   double f2, Cg, Cg2;
+  int fastdisp;      // dispersion_fast(f2): quot2_sqrt's short sequences
   double c[3];       // stage coefficients (already multiplied by h)
   // STAGE 0 (tile kernel): stages 2, 3 and 4 of one attempt fused per packet;
   // ts / c[0] are stage 2's, these stages 3 and 4's
@@ -55,9 +56,10 @@ __device__ __forceinline__ void ode_rhs(const Ode23Args& a, const double ys[4], 
   double I[kRec];
   eval_flow(a.f0, a.f1, a.nslots, alpha, ys[0], ys[1], a.bump, I);
   const double k1 = ys[2], k2 = ys[3];
-  const double s = sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2));
-  fo[0] = I[0] + (a.Cg * k1) / s;
-  fo[1] = I[1] + (a.Cg * k2) / s;
+  double c1, c2;  // Cg*k./sqrt(f^2 + Cg^2|k|^2)
+  quot2_sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2), a.Cg * k1, a.Cg * k2, a.fastdisp, c1, c2);
+  fo[0] = I[0] + c1;
+  fo[1] = I[1] + c2;
   fo[2] = -(I[2] * k1 + I[4] * k2);
   fo[3] = -(I[3] * k1 + I[5] * k2);
 }
@@ -216,9 +218,10 @@ __device__ __forceinline__ void tile_rhs(const Ode23Args& a, const double2* win,
     for (int q = 0; q < kRec; ++q) I[q] = oma * I[q] + alpha * J[q];
   }
   const double k1 = ys[2], k2 = ys[3];
-  const double s = sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2));
-  fo[0] = I[0] + (a.Cg * k1) / s;
-  fo[1] = I[1] + (a.Cg * k2) / s;
+  double c1, c2;  // Cg*k./sqrt(f^2 + Cg^2|k|^2)
+  quot2_sqrt(a.f2 + a.Cg2 * (k1 * k1 + k2 * k2), a.Cg * k1, a.Cg * k2, a.fastdisp, c1, c2);
+  fo[0] = I[0] + c1;
+  fo[1] = I[1] + c2;
   fo[2] = -(I[2] * k1 + I[4] * k2);
   fo[3] = -(I[3] * k1 + I[5] * k2);
 }
@@ -271,18 +274,21 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
 #pragma unroll 1
       for (int sg = 0; sg < 3; ++sg) {
         double ts;
+        // y is re-read per stage (an L2 hit) rather than held across the
+        // gather: 8 VGPRs fewer at the loop's peak
+        const double yv[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
         if (sg == 0) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) ys[c] = y[c] + a.F[0][c * n + p] * a.c[0];
+          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + a.F[0][c * n + p] * a.c[0];
           ts = a.ts;
         } else if (sg == 1) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) ys[c] = y[c] + fo[c] * a.c3;
+          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + fo[c] * a.c3;
           ts = a.ts3;
         } else {
 #pragma unroll
           for (int c = 0; c < 4; ++c)
-            ys[c] = y[c] + (((a.F[0][c * n + p] * a.c4[0]) + a.F[1][c * n + p] * a.c4[1]) + fo[c] * a.c4[2]);
+            ys[c] = yv[c] + (((a.F[0][c * n + p] * a.c4[0]) + a.F[1][c * n + p] * a.c4[1]) + fo[c] * a.c4[2]);
           a.ynx[p] = ys[0]; a.ynx[n + p] = ys[1];
           a.ynk[p] = ys[2]; a.ynk[n + p] = ys[3];
           ts = a.ts4;
@@ -293,10 +299,11 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
         for (int c = 0; c < 4; ++c) Fo[c * n + p] = fo[c];
       }
       constexpr double E1 = -5.0 / 72.0, E2 = 1.0 / 12.0, E3 = 1.0 / 9.0, E4 = -1.0 / 8.0;
+      const double yv[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const double fe = ((a.F[0][c * n + p] * E1 + a.F[1][c * n + p] * E2) + a.F[2][c * n + p] * E3) + fo[c] * E4;
-        m = fmax(m, fabs(fe) / fmax(fmax(fabs(y[c]), fabs(ys[c])), a.thr));
+        m = fmax(m, fabs(fe) / fmax(fmax(fabs(yv[c]), fabs(ys[c])), a.thr));
       }
       continue;
     }
