@@ -72,6 +72,9 @@ struct Slot {
   bool div_free = false;    // every node's v_y is exactly -u_x (five-sum kernels apply)
   // cross-stream order (they travel with the buffers through swaps and renames):
   hipEvent_t uev = nullptr;  // last context-stream use (packet kernels, field writes)
+  hipEvent_t uref = nullptr; // the event that marks that use: uev, or the stop event attached to
+                             // the call's last packet launch (context-wide, re-recorded by later
+                             // launches: waiting on it waits for a later point, never an earlier one)
   hipEvent_t wev = nullptr;  // last QG-stream write (swrt_qg_snapshot)
   bool upend = false, wpend = false;
 };
@@ -228,6 +231,13 @@ struct swrt_ctx {
   // set only around a timed packet launch: the dispatch itself stamps them
   // (hipExtLaunchKernel), so they bracket the kernel and nothing else
   hipEvent_t kev0 = nullptr, kev1 = nullptr;
+  // stop event attached to every untimed packet launch (launch_k), and the
+  // stop event of the last stream operation of the current API call if that
+  // was a packet launch (else nullptr): SlotUse marks the slots' use with it
+  // instead of recording a separate marker, which cost ~11 us of idle GPU
+  // between dependent packet launches (tools/gap_probe.py)
+  hipEvent_t use_ev = nullptr;
+  hipEvent_t tail_ev = nullptr;
 };
 
 namespace {
@@ -252,9 +262,16 @@ struct OnQGStream {
 
 // A context-stream call that reads or writes the field slots: wait for the
 // QG-stream snapshots written into them, then mark them used by this call.
+// Slot-use events are only needed while a QG stream may write slots beside
+// the packet launches (swrt_qg_init on a separate stream); without one a
+// packet launch carries no event at all (each costs ~5 us of idle GPU at the
+// launch boundary, tools/gap_probe.py).
+bool slot_events(const swrt_ctx* c) { return c->qg_sep && c->qg.init; }
+
 struct SlotUse {
   swrt_ctx* c;
   explicit SlotUse(swrt_ctx* c_) : c(c_) {
+    c->tail_ev = nullptr;
     if (!c->qg_sep) return;
     for (Slot& s : c->slot)
       if (s.wpend) {
@@ -263,9 +280,18 @@ struct SlotUse {
       }
   }
   ~SlotUse() {
-    if (!c->qg_sep) return;
-    for (Slot& s : c->slot)
-      if (s.nodes && hipEventRecord(s.uev, c->stream) == hipSuccess) s.upend = true;
+    if (!slot_events(c)) return;
+    for (Slot& s : c->slot) {
+      if (!s.nodes) continue;
+      if (c->tail_ev) {
+        s.uref = c->tail_ev;
+        s.upend = true;
+      } else if (hipEventRecord(s.uev, c->stream) == hipSuccess) {
+        s.uref = s.uev;
+        s.upend = true;
+      }
+    }
+    c->tail_ev = nullptr;
   }
 };
 }  // namespace
@@ -459,7 +485,9 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
 // start/stop events take the kernel's own begin/end timestamps.
 template <typename F, typename... Args>
 void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
-  hipExtLaunchKernelGGL(kernel, grid, block, 0, c->stream, c->kev0, c->kev1, 0, args...);
+  hipEvent_t stop = c->kev1 ? c->kev1 : (slot_events(c) ? c->use_ev : nullptr);
+  hipExtLaunchKernelGGL(kernel, grid, block, 0, c->stream, c->kev0, stop, 0, args...);
+  c->tail_ev = stop;
 }
 
 // Time every timing_every-th leapfrog launch with a pair of HIP events.
@@ -472,6 +500,7 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next,
       hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
     else
       hipLaunchKernelGGL(leapfrog_kernel<false>, dim3(grid), dim3(256), 0, c->stream, a);
+    c->tail_ev = nullptr;
     HIPCHK(c, hipGetLastError());
     return SWRT_OK;
   }
@@ -826,6 +855,7 @@ int swrt_create(int device, swrt_ctx** out) {
   for (Slot* s = c->slot; s != c->slot + SWRT_MAX_SLOTS; ++s)
     ok = ok && hipEventCreateWithFlags(&s->uev, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s->wev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->use_ev, hipEventDisableTiming) == hipSuccess;
   if (!ok) {
     swrt_destroy(c);
     return SWRT_ERR_HIP;
@@ -846,6 +876,7 @@ void swrt_destroy(swrt_ctx* c) {
     if (s.wev) (void)hipEventDestroy(s.wev);
   };
   for (auto& s : c->slot) free_slot(s);
+  if (c->use_ev) (void)hipEventDestroy(c->use_ev);
   for (auto& s : c->spares) free_slot(s);
   for (void* p : {(void*)c->dx, (void*)c->dk, (void*)c->perm, (void*)c->dx2, (void*)c->dk2,
                   (void*)c->perm2, (void*)c->keys, (void*)c->src_idx, (void*)c->bins})
@@ -1959,6 +1990,15 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
   HIPCHK(c, hipMemsetAsync(q.Qm2, 0, hb, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   q.init = true;
+  if (c->qg_sep) {
+    // from here on packet launches mark their slot use; everything queued on
+    // the context stream so far is marked by one record per slot
+    for (Slot& sl : c->slot)
+      if (sl.nodes && hipEventRecord(sl.uev, on_qg.saved) == hipSuccess) {
+        sl.uref = sl.uev;
+        sl.upend = true;
+      }
+  }
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -2250,10 +2290,10 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   HIPCHK(c, hipSetDevice(c->device));
   if (c->qg_sep) {
     // rename a buffer still read by a queued packet launch, else wait for its last use
-    if (c->slot[slot].upend && event_pending(c->slot[slot].uev)) {
+    if (c->slot[slot].upend && event_pending(c->slot[slot].uref)) {
       int pick = -1;
       for (size_t i = 0; i < c->spares.size() && pick < 0; ++i)
-        if (!c->spares[i].upend || !event_pending(c->spares[i].uev)) pick = (int)i;
+        if (!c->spares[i].upend || !event_pending(c->spares[i].uref)) pick = (int)i;
       if (pick < 0 && c->spares.size() < kMaxSpares) {
         Slot sp;
         HIPCHK(c, hipEventCreateWithFlags(&sp.uev, hipEventDisableTiming));
@@ -2263,7 +2303,7 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
       }
       if (pick >= 0) std::swap(c->slot[slot], c->spares[pick]);  // else wait for the slot's own reader
     }
-    if (c->slot[slot].upend) HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot[slot].uev, 0));
+    if (c->slot[slot].upend) HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot[slot].uref, 0));
   }
   if ((rc = ensure_slot(c, slot, nx))) return rc;
   if ((rc = ensure_twiddles(c, (int)nx))) return rc;
