@@ -108,9 +108,12 @@ __device__ __forceinline__ int wg_work_range(const int* starts, const int* order
   pbeg = starts[tile];
   pend = starts[tile + 1];
   if (nparts > 1) {
+    // parts of whole wavefronts (64 packets) but the last: no part adds a
+    // partial wave of its own
     const int cnt = pend - pbeg;
-    pend = pbeg + (int)((int64_t)cnt * (part + 1) / nparts);
-    pbeg = pbeg + (int)((int64_t)cnt * part / nparts);
+    const int per = ((cnt + nparts - 1) / nparts + 63) & ~63;
+    pend = pbeg + min(cnt, per * (part + 1));
+    pbeg = pbeg + min(cnt, per * part);
   }
   return tile;
 }
