@@ -32,6 +32,7 @@ using namespace swrt;
 namespace {
 
 constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
+constexpr int kXkaMargin = 3;           // xka_tile_kernel: drift margin (cells) of a tile's window
 #ifndef SWRT_TILE
 #define SWRT_TILE 16
 #endif
@@ -196,6 +197,8 @@ struct swrt_ctx {
   double* xka_state2 = nullptr; // 5n: the state in binned order
   int* xka_keys = nullptr;      // n
   int* xka_src = nullptr;       // n: binned slot -> packet
+  int* xka_src2 = nullptr;      // n: a re-binning's slot -> previous slot
+  int* xka_perm2 = nullptr;     // n: composed permutation (ping-pong with xka_src)
   int* xka_bins = nullptr;      // counts | cursor | starts of the xka binning
   int64_t xka_cap = 0;
   double* xka_hist = nullptr;
@@ -885,7 +888,8 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->hk) (void)hipFree(c->hk);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->tw) (void)hipFree(c->tw);
-  for (void* p : {(void*)c->xka_state2, (void*)c->xka_keys, (void*)c->xka_src, (void*)c->xka_bins})
+  for (void* p : {(void*)c->xka_state2, (void*)c->xka_keys, (void*)c->xka_src, (void*)c->xka_bins,
+                  (void*)c->xka_src2, (void*)c->xka_perm2})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->xka_nodes, (void*)c->xka_state, (void*)c->xka_hist, (void*)c->modes,
                   (void*)c->mode_rows, (void*)c->modes_f, (void*)c->modes_f_row, (void*)c->modes_d,
@@ -1562,7 +1566,8 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
     return fail(c, SWRT_ERR_ARG, "nsteps must be a multiple of save_every");
   HIPCHK(c, hipSetDevice(c->device));
   if (n > c->xka_cap) {
-    for (void** p : {(void**)&c->xka_state, (void**)&c->xka_state2, (void**)&c->xka_keys, (void**)&c->xka_src}) {
+    for (void** p : {(void**)&c->xka_state, (void**)&c->xka_state2, (void**)&c->xka_keys, (void**)&c->xka_src,
+                     (void**)&c->xka_src2, (void**)&c->xka_perm2}) {
       if (*p) (void)hipFree(*p);
       *p = nullptr;
     }
@@ -1571,6 +1576,8 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
     HIPCHK(c, hipMalloc(&c->xka_state2, sizeof(double) * 5 * n));
     HIPCHK(c, hipMalloc(&c->xka_keys, sizeof(int) * n));
     HIPCHK(c, hipMalloc(&c->xka_src, sizeof(int) * n));
+    HIPCHK(c, hipMalloc(&c->xka_src2, sizeof(int) * n));
+    HIPCHK(c, hipMalloc(&c->xka_perm2, sizeof(int) * n));
     c->xka_cap = n;
   }
   if (!c->xka_bins) HIPCHK(c, hipMalloc(&c->xka_bins, sizeof(int) * (3 * kMaxBins + 1)));
@@ -1604,43 +1611,72 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   a.hist = frames ? c->xka_hist : nullptr;
   a.perm = nullptr;
   // larger ensembles: step the packets in spatially binned order (8 x 8-cell
-  // tiles, counting sort by index), so a wave gathers from a few nodes
+  // tiles, counting sort by index) with the LDS-tiled kernel (one workgroup
+  // per tile, xka_tile_kernel), re-binned every rebin_every steps (the
+  // context's locality setting) so the packets stay inside their tile's
+  // window; the permutation to the caller's order is composed across
+  // re-binnings and history frames are written through it
   const bool binned = n >= 4096 && c->rebin_every > 0;
-  if (binned) {
-    BinGeom g;
-    g.dx = a.dx; g.px = a.px; g.py = a.py; g.inv_px = a.inv_px; g.inv_py = a.inv_py; g.inv_dx = a.inv_dx;
-    g.nx = a.nx;
-    g.tile = 8;
-    while ((a.nx + g.tile - 1) / g.tile > 64) g.tile *= 2;
-    g.ntx = (a.nx + g.tile - 1) / g.tile;
-    const int nbins = g.ntx * g.ntx;
-    const unsigned bgrid = nblocks(n, 256 * kBinPerThread);
+  BinGeom g;
+  g.dx = a.dx; g.px = a.px; g.py = a.py; g.inv_px = a.inv_px; g.inv_py = a.inv_py; g.inv_dx = a.inv_dx;
+  g.nx = a.nx;
+  g.tile = 8;
+  while ((a.nx + g.tile - 1) / g.tile > 64) g.tile *= 2;
+  g.ntx = (a.nx + g.tile - 1) / g.tile;
+  const int nbins = g.ntx * g.ntx;
+  const bool tiled = binned && a.nx % g.tile == 0 && g.ntx >= 2 && (g.tile == 8 || g.tile == 16);
+  const unsigned bgrid = nblocks(n, 256 * kBinPerThread);
+  double* cur = c->xka_state;   // the state the next launch steps
+  double* other = c->xka_state2;
+  int* perm = nullptr;          // cur's slot -> caller's packet (nullptr: identity)
+  int* perm_other = c->xka_perm2;
+  // bin `cur` (slot -> packet permutation `perm`) into `other`, then swap
+  auto rebin_xka = [&]() -> int {
     HIPCHK(c, hipMemsetAsync(c->xka_bins, 0, sizeof(int) * nbins, c->stream));
-    hipLaunchKernelGGL(bin_count_kernel, dim3(bgrid), dim3(256), sizeof(int) * nbins, c->stream, g, c->xka_state,
-                       n, nbins, c->xka_keys, c->xka_bins);
+    hipLaunchKernelGGL(bin_count_kernel, dim3(bgrid), dim3(256), sizeof(int) * nbins, c->stream, g, cur, n, nbins,
+                       c->xka_keys, c->xka_bins);
     hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->xka_bins, nbins,
-                       c->xka_bins + kMaxBins, c->xka_bins + 2 * kMaxBins);
+                       c->xka_bins + kMaxBins, c->xka_bins + 2 * kMaxBins, nullptr, kTileThreads);
+    int* src = perm == nullptr ? c->xka_src : c->xka_src2;
     hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3(bgrid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
-                       c->xka_state, c->xka_state, nullptr, c->xka_keys, n, nbins, c->xka_bins + kMaxBins,
-                       nullptr, nullptr, nullptr, c->xka_src);
-    hipLaunchKernelGGL(xka_gather_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, c->xka_state,
-                       c->xka_src, n, c->xka_state2);
+                       cur, cur, nullptr, c->xka_keys, n, nbins, c->xka_bins + kMaxBins, nullptr, nullptr, nullptr,
+                       src);
+    hipLaunchKernelGGL(xka_gather_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, cur, src, perm, n, other,
+                       perm == nullptr ? nullptr : perm_other);
     HIPCHK(c, hipGetLastError());
-    a.st = c->xka_state2;
-    a.perm = c->xka_src;
-  }
-  for (int64_t s0 = 0; s0 < nsteps; s0 += kMaxStepsPerLaunch) {
-    a.nsteps = (int)std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
+    std::swap(cur, other);
+    if (perm == nullptr) {
+      perm = src;  // the first binning's src is the permutation itself
+    } else {
+      std::swap(perm, perm_other);
+    }
+    return SWRT_OK;
+  };
+  int rc;
+  if (binned && (rc = rebin_xka())) return rc;
+  const int64_t per_launch = tiled ? std::min<int64_t>(kMaxStepsPerLaunch, c->rebin_every) : kMaxStepsPerLaunch;
+  for (int64_t s0 = 0; s0 < nsteps; s0 += per_launch) {
+    if (tiled && s0 > 0 && (rc = rebin_xka())) return rc;
+    a.st = cur;
+    a.perm = perm;
+    a.nsteps = (int)std::min<int64_t>(per_launch, nsteps - s0);
     a.frame0 = s0 / a.save_every;
-    hipLaunchKernelGGL(xka_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, a);
+    if (tiled && g.tile == 8)
+      hipLaunchKernelGGL((xka_tile_kernel<8, kXkaMargin, 256>), dim3(nbins), dim3(256), 0, c->stream, a,
+                         (const int*)(c->xka_bins + 2 * kMaxBins), g.ntx);
+    else if (tiled)
+      hipLaunchKernelGGL((xka_tile_kernel<16, kXkaMargin, 256>), dim3(nbins), dim3(256), 0, c->stream, a,
+                         (const int*)(c->xka_bins + 2 * kMaxBins), g.ntx);
+    else
+      hipLaunchKernelGGL(xka_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, a);
     HIPCHK(c, hipGetLastError());
   }
   if (binned) {
-    hipLaunchKernelGGL(xka_scatter_back_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, c->xka_state2,
-                       c->xka_src, n, c->xka_state);
+    hipLaunchKernelGGL(xka_scatter_back_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, cur, perm, n, other);
     HIPCHK(c, hipGetLastError());
+    cur = other;
   }
-  HIPCHK(c, hipMemcpyAsync(state5, c->xka_state, sizeof(double) * 5 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(state5, cur, sizeof(double) * 5 * n, hipMemcpyDeviceToHost, c->stream));
   if (frames)
     HIPCHK(c, hipMemcpyAsync(hist5, c->xka_hist, sizeof(double) * frames * 5 * n, hipMemcpyDeviceToHost,
                              c->stream));

@@ -88,14 +88,36 @@ __device__ __forceinline__ void xka_stencil(const XkaArgs& a, double x, double y
   lagrange_w(ay, a.bump, s.wy);
 }
 
+// Tap sources of the stencil sums: the global node array, or a tile's
+// window in LDS (chunk-major: chunk c of window node e at win[c*WN + e],
+// chunks {u, v}, {H, 0}, {u_x, u_y}, {v_x, v_y}).  Same values either way.
+struct XkaGlobalTaps {
+  const double* base;  // the stencil's first tap (ic-2, jc-2) in the padded node array
+  int npad;
+  __device__ __forceinline__ const double2* at(int i, int j) const {
+    return reinterpret_cast<const double2*>(base + ((size_t)i * npad + j) * kXkaRec);
+  }
+  __device__ __forceinline__ double2 uv(int i, int j) const { return at(i, j)[0]; }
+  __device__ __forceinline__ double H(int i, int j) const { return at(i, j)[1].x; }
+  __device__ __forceinline__ double2 g0(int i, int j) const { return at(i, j)[2]; }
+  __device__ __forceinline__ double2 g1(int i, int j) const { return at(i, j)[3]; }
+};
+template <int WS, int WN>
+struct XkaLdsTaps {
+  const double2* p;  // the stencil's first tap in the window
+  __device__ __forceinline__ double2 uv(int i, int j) const { return p[0 * WN + i * WS + j]; }
+  __device__ __forceinline__ double H(int i, int j) const { return p[1 * WN + i * WS + j].x; }
+  __device__ __forceinline__ double2 g0(int i, int j) const { return p[2 * WN + i * WS + j]; }
+  __device__ __forceinline__ double2 g1(int i, int j) const { return p[3 * WN + i * WS + j]; }
+};
+
 // interpolate(x, y, U.u + C.x) and interpolate(x, y, U.v + C.y)
 // (step_packet_xka.m:42-52) with C from cg_sw.m:15-26 formed per tap.  Rows
 // are not unrolled (6 taps each): the fully unrolled 4 RK stages + gradients
 // held 348 VGPRs, one wave per SIMD.
-template <bool FAST>
-__device__ __forceinline__ bool xka_velocity_t(const XkaArgs& a, const XkaStencil& s, double k, double l, double K2,
-                                               double& Iu, double& Iv) {
-  const double* base = a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec;
+template <bool FAST, class Taps>
+__device__ __forceinline__ bool xka_velocity_t(const XkaArgs& a, const XkaStencil& s, const Taps& tp, double k,
+                                               double l, double K2, double& Iu, double& Iv) {
   double su = 0.0, sv = 0.0;
   bool bad = false;
 #pragma unroll 1
@@ -103,9 +125,8 @@ __device__ __forceinline__ bool xka_velocity_t(const XkaArgs& a, const XkaStenci
     const double wxi = s.wx[i];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
-      const double2* nd = reinterpret_cast<const double2*>(base + ((size_t)i * a.npad + j) * kXkaRec);
-      const double2 uv = nd[0];
-      const double H = nd[1].x;
+      const double2 uv = tp.uv(i, j);
+      const double H = tp.H(i, j);
       const double gH = a.C0sq * H;                   // cg_sw.m:16
       // w (cg_sw.m:22), cx, cy (cg_sw.m:25-26)
       const XkaDisp d = xka_disp<FAST>(a.f2, gH, K2, k, l, bad);
@@ -118,19 +139,17 @@ __device__ __forceinline__ bool xka_velocity_t(const XkaArgs& a, const XkaStenci
   Iv = sv;
   return bad;
 }
-__device__ __forceinline__ void xka_velocity(const XkaArgs& a, double x, double y, double k, double l,
-                                             double K2, double& Iu, double& Iv) {
-  XkaStencil s;
-  xka_stencil(a, x, y, s);
-  if (xka_velocity_t<true>(a, s, k, l, K2, Iu, Iv)) xka_velocity_t<false>(a, s, k, l, K2, Iu, Iv);
+template <class Taps>
+__device__ __forceinline__ void xka_velocity_s(const XkaArgs& a, const XkaStencil& s, const Taps& tp, double k,
+                                               double l, double K2, double& Iu, double& Iv) {
+  if (xka_velocity_t<true>(a, s, tp, k, l, K2, Iu, Iv)) xka_velocity_t<false>(a, s, tp, k, l, K2, Iu, Iv);
 }
 
 // The 7 interpolations at the new position (step_packet_xka.m:59-65):
 // u_x, u_y, v_x, v_y, gradomega.x, gradomega.y, divC.
-template <bool FAST>
-__device__ __forceinline__ bool xka_gradients_t(const XkaArgs& a, const XkaStencil& s, double k, double l, double K2,
-                                                double out[7]) {
-  const double* base = a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec;
+template <bool FAST, class Taps>
+__device__ __forceinline__ bool xka_gradients_t(const XkaArgs& a, const XkaStencil& s, const Taps& tp, double k,
+                                                double l, double K2, double out[7]) {
   const double kf = k * a.f, lf = l * a.f;        // k*f, l*f (cg_sw.m:29)
   const double fK2 = a.f * K2, mfK2 = (-a.f) * K2;  // f*(k^2+l^2), -f*(k^2+l^2) (cg_sw.m:30-31)
   bool bad = false;
@@ -141,10 +160,9 @@ __device__ __forceinline__ bool xka_gradients_t(const XkaArgs& a, const XkaStenc
     const double wxi = s.wx[i];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
-      const double2* nd = reinterpret_cast<const double2*>(base + ((size_t)i * a.npad + j) * kXkaRec);
-      const double2 uv = nd[0];
-      const double H = nd[1].x;
-      const double2 g0 = nd[2], g1 = nd[3];  // (u_x, u_y), (v_x, v_y)
+      const double2 uv = tp.uv(i, j);
+      const double H = tp.H(i, j);
+      const double2 g0 = tp.g0(i, j), g1 = tp.g1(i, j);  // (u_x, u_y), (v_x, v_y)
       const double gH = a.C0sq * H;
       const XkaDisp d = xka_disp<FAST>(a.f2, gH, K2, k, l, bad);
       const double divC = xka_divw<FAST>(((kf * uv.y - lf * uv.x) - d.cx * d.cx) - d.cy * d.cy, d);  // cg_sw.m:29
@@ -162,40 +180,97 @@ __device__ __forceinline__ bool xka_gradients_t(const XkaArgs& a, const XkaStenc
   }
   return bad;
 }
-__device__ __forceinline__ void xka_gradients(const XkaArgs& a, double x, double y, double k, double l,
-                                              double K2, double out[7]) {
-  XkaStencil s;
-  xka_stencil(a, x, y, s);
-  if (xka_gradients_t<true>(a, s, k, l, K2, out)) xka_gradients_t<false>(a, s, k, l, K2, out);
+template <class Taps>
+__device__ __forceinline__ void xka_gradients_s(const XkaArgs& a, const XkaStencil& s, const Taps& tp, double k,
+                                                double l, double K2, double out[7]) {
+  if (xka_gradients_t<true>(a, s, tp, k, l, K2, out)) xka_gradients_t<false>(a, s, tp, k, l, K2, out);
 }
+
+// The interpolations from the global node array (the per-packet kernel).
+struct XkaGlobalField {
+  __device__ __forceinline__ void vel(const XkaArgs& a, double x, double y, double k, double l, double K2,
+                                      double& u, double& v) const {
+    XkaStencil s;
+    xka_stencil(a, x, y, s);
+    const XkaGlobalTaps tp{a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec, a.npad};
+    xka_velocity_s(a, s, tp, k, l, K2, u, v);
+  }
+  __device__ __forceinline__ void grad(const XkaArgs& a, double x, double y, double k, double l, double K2,
+                                       double g[7]) const {
+    XkaStencil s;
+    xka_stencil(a, x, y, s);
+    const XkaGlobalTaps tp{a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec, a.npad};
+    xka_gradients_s(a, s, tp, k, l, K2, g);
+  }
+};
+
+// ... or from a tile's LDS window when the stencil lies inside it (the
+// margin M covers the packet's motion within the launch), else globally.
+template <int T, int M, int WS, int WN>
+struct XkaTileField {
+  const double2* win;
+  int ox, oy;
+  __device__ __forceinline__ bool inside(const XkaStencil& s, int nx, int& node0) const {
+    int dx_ = s.ic - ox, dy_ = s.jc - oy;
+    if (dx_ >= nx / 2) dx_ -= nx;
+    if (dx_ < -nx / 2) dx_ += nx;
+    if (dy_ >= nx / 2) dy_ -= nx;
+    if (dy_ < -nx / 2) dy_ += nx;
+    node0 = (dx_ + M) * WS + (dy_ + M);
+    return dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M;
+  }
+  __device__ __forceinline__ void vel(const XkaArgs& a, double x, double y, double k, double l, double K2,
+                                      double& u, double& v) const {
+    XkaStencil s;
+    xka_stencil(a, x, y, s);
+    int node0;
+    if (inside(s, a.nx, node0)) {
+      xka_velocity_s(a, s, XkaLdsTaps<WS, WN>{win + node0}, k, l, K2, u, v);
+    } else {
+      const XkaGlobalTaps tp{a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec, a.npad};
+      xka_velocity_s(a, s, tp, k, l, K2, u, v);
+    }
+  }
+  __device__ __forceinline__ void grad(const XkaArgs& a, double x, double y, double k, double l, double K2,
+                                       double g[7]) const {
+    XkaStencil s;
+    xka_stencil(a, x, y, s);
+    int node0;
+    if (inside(s, a.nx, node0)) {
+      xka_gradients_s(a, s, XkaLdsTaps<WS, WN>{win + node0}, k, l, K2, g);
+    } else {
+      const XkaGlobalTaps tp{a.nodes + ((size_t)s.ic * a.npad + s.jc) * kXkaRec, a.npad};
+      xka_gradients_s(a, s, tp, k, l, K2, g);
+    }
+  }
+};
 
 // (a + 2b + 2c + d)/6 in MATLAB's left-to-right order; /6 = (/2 exact)/3.
 __device__ __forceinline__ double rk4_mean(double a, double b, double c, double d) {
   return div_const<3>((((a + 2 * b) + 2 * c) + d) * 0.5);
 }
 
-// step_packet_xka.m:38-91 — one lane per packet, nsteps steps.
-__global__ void __launch_bounds__(256) xka_kernel(XkaArgs a) {
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= a.n) return;
+// step_packet_xka.m:38-91 for packet p (state slot p), a.nsteps steps.
+template <class Field>
+__device__ __forceinline__ void xka_advance(const XkaArgs& a, const Field& fld, int64_t p) {
   const int64_t n = a.n;
   double x = a.st[p], y = a.st[n + p], k = a.st[2 * n + p], l = a.st[3 * n + p], ac = a.st[4 * n + p];
   const double dt = a.dt;
   for (int s = 0; s < a.nsteps; ++s) {
     const double K2 = k * k + l * l;  // cg_sw.m:22 (k^2+l^2)
     double u, v;
-    xka_velocity(a, x, y, k, l, K2, u, v);
+    fld.vel(a, x, y, k, l, K2, u, v);
     const double x1 = dt * u, y1 = dt * v;
-    xka_velocity(a, x + x1 * 0.5, y + y1 * 0.5, k, l, K2, u, v);
+    fld.vel(a, x + x1 * 0.5, y + y1 * 0.5, k, l, K2, u, v);
     const double x2 = dt * u, y2 = dt * v;
-    xka_velocity(a, x + x2 * 0.5, y + y2 * 0.5, k, l, K2, u, v);
+    fld.vel(a, x + x2 * 0.5, y + y2 * 0.5, k, l, K2, u, v);
     const double x3 = dt * u, y3 = dt * v;
-    xka_velocity(a, x + x3, y + y3, k, l, K2, u, v);
+    fld.vel(a, x + x3, y + y3, k, l, K2, u, v);
     const double x4 = dt * u, y4 = dt * v;
     const double X = x + rk4_mean(x1, x2, x3, x4);  // step_packet_xka.m:54-55
     const double Y = y + rk4_mean(y1, y2, y3, y4);
     double g[7];
-    xka_gradients(a, X, Y, k, l, K2, g);
+    fld.grad(a, X, Y, k, l, K2, g);
     const double uxi = g[0], uyi = g[1], vxi = g[2], vyi = g[3], oxi = g[4], oyi = g[5], dci = g[6];
     // step_packet_xka.m:69-82
     const double k1 = dt * (((-uxi) * k - vxi * l) - oxi);
@@ -227,17 +302,64 @@ __global__ void __launch_bounds__(256) xka_kernel(XkaArgs a) {
   a.st[p] = x; a.st[n + p] = y; a.st[2 * n + p] = k; a.st[3 * n + p] = l; a.st[4 * n + p] = ac;
 }
 
+// One lane per packet, interpolations from the global node array.
+__global__ void __launch_bounds__(256) xka_kernel(XkaArgs a) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= a.n) return;
+  xka_advance(a, XkaGlobalField{}, p);
+}
+
+// LDS-tiled form over spatially binned packets (swrt_xka_step): one
+// workgroup per T x T-cell tile stages the tile's window of node records —
+// the tile, the stencil reach and an M-cell margin, rows padded to a 12
+// (mod 16) stride — into LDS, then its lanes step the tile's packets with
+// every tap of an in-window stencil read from LDS (5 interpolations x 36 taps
+// per packet-step; the per-packet kernel gathered them from L1/L2, which
+// bounded it).  A stencil outside the window reads global memory.  Same
+// operations in the same order: the same bits.
+template <int T, int M, int NT>
+__global__ void __launch_bounds__(NT) xka_tile_kernel(XkaArgs a, const int* starts, int ntx) {
+  constexpr int W = T + 5 + 2 * M;
+  constexpr int WS = W + ((12 - W % 16) + 16) % 16;
+  constexpr int WN = W * WS;
+  __shared__ double2 win[4 * WN];
+  const int tile = (int)xcd_block(blockIdx.x, gridDim.x);
+  const int pbeg = starts[tile], pend = starts[tile + 1];
+  if (pbeg == pend) return;  // uniform: no barrier is skipped by part of the block
+  const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
+  const int nx = a.nx;
+  for (int e = threadIdx.x; e < W * W; e += NT) {
+    const int wi = e / W, wj = e % W;
+    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
+    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
+    const double2* src = reinterpret_cast<const double2*>(a.nodes + ((size_t)(gx + kPadLo) * a.npad + (gy + kPadLo)) * kXkaRec);
+    const double2 c0 = src[0], c1 = src[1], c2 = src[2], c3 = src[3];
+    const int d = wi * WS + wj;
+    win[0 * WN + d] = c0;
+    win[1 * WN + d] = c1;
+    win[2 * WN + d] = c2;
+    win[3 * WN + d] = c3;
+  }
+  __syncthreads();
+  const XkaTileField<T, M, WS, WN> fld{win, ox, oy};
+  for (int p = pbeg + (int)threadIdx.x; p < pend; p += NT) xka_advance(a, fld, p);
+}
+
 // Spatial order for the xka lanes (swrt_xka_step): the 5 x n state gathered
 // into binned order (src from bin_scatter_kernel<true>), and scattered back.
 // Neighbouring lanes then read the same few node records, which the L1/L2
 // serve: the gathers dominate the unbinned kernel.  Order only: every packet
 // is stepped by the same operations whatever its lane.
-__global__ void xka_gather_kernel(const double* st, const int* src, int64_t n, double* out) {
+// perm != NULL (a re-binning of already binned state): also compose the
+// permutation to the caller's order, perm_out[d] = perm[src[d]].
+__global__ void xka_gather_kernel(const double* st, const int* src, const int* perm, int64_t n, double* out,
+                                  int* perm_out) {
   const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n) return;
   const int64_t p = src[d];
 #pragma unroll
   for (int q = 0; q < 5; ++q) out[q * n + d] = st[q * n + p];
+  if (perm != nullptr) perm_out[d] = perm[p];
 }
 
 __global__ void xka_scatter_back_kernel(const double* st, const int* src, int64_t n, double* out) {

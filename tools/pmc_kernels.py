@@ -15,7 +15,7 @@ import os
 import sys
 
 PEAK = 256 * 4 * 16 * 2.4e9
-KEEP = ("xka_kernel", "spectral_", "omega_hist", "tile_leapfrog", "ode23")
+KEEP = ("xka_", "spectral_", "omega_hist", "tile_leapfrog", "ode23")
 
 
 def main(out):
