@@ -552,17 +552,19 @@ def test_step_packet_xka_bitexact(ctx, nx):
                 assert hist[n][i, j] == P[n], (i, j, n, hist[n][i, j], P[n])
 
 
-def test_step_packet_xka_binned_order_is_invisible(ctx):
-    """Ensembles >= 4096 packets are stepped in spatially binned order
-    (swrt_xka_step): final states and every history frame are bit-identical
-    to the unbinned lane order (itself pinned to the literal oracle above),
-    and the first packets match the oracle directly."""
+@pytest.mark.parametrize("nx,steps", [(64, 6), (1024, 9)])
+def test_step_packet_xka_binned_order_is_invisible(ctx, nx, steps):
+    """Ensembles >= 4096 packets are stepped in spatially binned order by the
+    LDS-tiled kernel (swrt_xka_step; 8x8-cell tiles at 64^2, 16x16 at 1024^2),
+    re-binned every 4 steps: final states and every history frame are
+    bit-identical to the unbinned lane order of the per-packet kernel (itself
+    pinned to the literal oracle above), and the first packets match the
+    oracle directly."""
     import swraytracing_amd as sw
-    nx = 64
     U, G, H = _rsw_background(nx)
     dx = 2 * np.pi / nx
     rng = np.random.default_rng(11)
-    npk, steps, dt, C0, f = 6000, 6, 0.3 * dx, 1.0, 4.0
+    npk, dt, C0, f = 6000, 0.3 * dx, 1.0, 4.0
     P0 = {"x": rng.uniform(0, 2 * np.pi, npk), "y": rng.uniform(-7, 7, npk),
           "k": 40 * np.cos(np.arange(npk)), "l": 40 * np.sin(np.arange(npk)), "a": np.ones(npk)}
     ctx.set_locality(4, 0)

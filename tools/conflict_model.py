@@ -55,6 +55,7 @@ def main():
     ap.add_argument("--tiles", type=int, default=6, help="side of the block of tiles simulated")
     ap.add_argument("--cfl", type=float, default=0.05, help="leapfrog dt in units of dx/U0 (bench: 0.05)")
     ap.add_argument("--cycle", type=int, default=20, help="steps between re-binnings (bench: 20)")
+    ap.add_argument("--launch", type=int, default=5, help="steps per launch (bench: 5)")
     args = ap.parse_args()
     nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
     rng = np.random.default_rng(146)
@@ -105,7 +106,15 @@ def main():
         policies[f"x0 + {frac:g} R dt cg"] = X[0] + frac * R * dt * cg0
     policies[f"x1 + 0.5 R dt (cg + U(x1))"] = x1_0 + 0.5 * R * dt * (cg0 + U)
     policies["exact x1 each step (sort every step)"] = None
+    # the tile order of the 0.5 lead, then every launch (args.launch steps)
+    # each wave's 64 packets re-ordered among its lanes by the Z-order of
+    # their cell led half a launch (the wave keeps its packets)
+    lead = X[0] + 0.5 * R * dt * cg0
+    policies["0.5 lead + in-wave re-sort per launch"] = ("wave", lead)
     for name, keypos in policies.items():
+        wave_mode = isinstance(keypos, tuple)
+        if wave_mode:
+            keypos = keypos[1]
         tot = np.zeros(R)
         base = np.zeros(R)
         for tx in range(nt):
@@ -116,6 +125,15 @@ def main():
                     c = cells(kp[m])
                     key = zorder(np.clip(c[:, 0] - tx * T, 0, T - 1), np.clip(c[:, 1] - ty * T, 0, T - 1))
                     order = m[np.argsort(key, kind="stable")]
+                    if wave_mode:
+                        j0 = (j // args.launch) * args.launch
+                        wk = X[j0] + 0.5 * args.launch * dt * (K[j0] / np.sqrt(f * f + (K[j0] ** 2).sum(1))[:, None])
+                        order = order.copy()
+                        for w0_ in range(0, len(order), 64):
+                            blk = order[w0_:w0_ + 64]
+                            cw = cells(wk[blk])
+                            kk = zorder(np.clip(cw[:, 0] - tx * T, 0, T - 1), np.clip(cw[:, 1] - ty * T, 0, T - 1))
+                            order[w0_:w0_ + 64] = blk[np.argsort(kk, kind="stable")]
                     cj = cells(x1(j)[order])
                     node = (cj[:, 0] - tx * T + M) * WS + (cj[:, 1] - ty * T + M)
                     for w0_ in range(0, len(order), 64):
