@@ -185,9 +185,6 @@ __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const
 // cannot hoist the 36 products wx_i*wy_j out of this path and the global
 // fallback's (both compute them): 36 hoisted products held 72 VGPRs and left
 // no room for the reads in flight.  Same operations, same order, same bits.
-#ifndef SWRT_GATHER_PIPE
-#define SWRT_GATHER_PIPE 1
-#endif
 template <bool TWO>
 struct Tap5 {
   double2 a0, a1, c, b0, b1;
@@ -224,9 +221,7 @@ __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const
   for (int t = 0; t < kNT * kNT; ++t) {
     const int i = t / kNT, j = t % kNT;
     if (t + 1 < kNT * kNT) tap5_read<TWO, WN>(p, ((t + 1) / kNT) * W + (t + 1) % kNT, nxt);
-#if SWRT_GATHER_PIPE
     __builtin_amdgcn_sched_barrier(0);
-#endif
     const double wij = wx[i] * wy[j];
     o0[0] = o0[0] + wij * cur.a0.x; o0[1] = o0[1] + wij * cur.a0.y;
     o0[2] = o0[2] + wij * cur.a1.x; o0[3] = o0[3] + wij * cur.a1.y;
@@ -236,9 +231,7 @@ __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const
       o1[2] = o1[2] + wij * cur.b1.x; o1[3] = o1[3] + wij * cur.b1.y;
       o1[4] = o1[4] + wij * cur.c.y;
     }
-#if SWRT_GATHER_PIPE
     __builtin_amdgcn_sched_barrier(0);
-#endif
     if (t + 1 < kNT * kNT) cur = nxt;
   }
   o0[5] = -o0[2];
