@@ -147,29 +147,75 @@ __device__ __forceinline__ int b128_lane_rank(int lane) {
   return h + k;
 }
 
+// Six-sum form (host-given fields): the weights kept per path, and — for one
+// snapshot — the next tap's reads issued before this tap's arithmetic, as in
+// gather5_lds below (with two snapshots the 12 reads in flight would spill).
+template <bool TWO>
+struct Tap6 {
+  double2 a0, a1, a2, b0, b1, b2;
+};
+template <bool TWO, int WN>
+__device__ __forceinline__ void tap6_read(const double2* p, int e, Tap6<TWO>& t) {
+  t.a0 = p[0 * WN + e];
+  t.a1 = p[1 * WN + e];
+  t.a2 = p[2 * WN + e];
+  if constexpr (TWO) {
+    t.b0 = p[3 * WN + e];
+    t.b1 = p[4 * WN + e];
+    t.b2 = p[5 * WN + e];
+  }
+}
 template <bool TWO, int W, int WN>
 __device__ __forceinline__ void gather6_lds(const double2* lds, int node0, const Stencil& s,
                                             double o0[kRec], double o1[kRec]) {
 #pragma unroll
   for (int f = 0; f < kRec; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
   const double2* p = lds + node0;
+  double wx[kNT], wy[kNT];
 #pragma unroll
-  for (int i = 0; i < kNT; ++i) {
+  for (int q = 0; q < kNT; ++q) {
+    wx[q] = s.wx[q];
+    wy[q] = s.wy[q];
+    asm volatile("" : "+v"(wx[q]));
+    asm volatile("" : "+v"(wy[q]));
+  }
+  if constexpr (TWO) {
 #pragma unroll
-    for (int j = 0; j < kNT; ++j) {
-      const int e = i * W + j;
-      const double wij = s.wx[i] * s.wy[j];
-      const double2 a0 = p[0 * WN + e], a1 = p[1 * WN + e], a2 = p[2 * WN + e];
-      o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
-      o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
-      o0[4] = o0[4] + wij * a2.x; o0[5] = o0[5] + wij * a2.y;
-      if constexpr (TWO) {
+    for (int i = 0; i < kNT; ++i) {
+#pragma unroll
+      for (int j = 0; j < kNT; ++j) {
+        const int e = i * W + j;
+        const double wij = wx[i] * wy[j];
+        const double2 a0 = p[0 * WN + e], a1 = p[1 * WN + e], a2 = p[2 * WN + e];
+        o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
+        o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
+        o0[4] = o0[4] + wij * a2.x; o0[5] = o0[5] + wij * a2.y;
         const double2 b0 = p[3 * WN + e], b1 = p[4 * WN + e], b2 = p[5 * WN + e];
         o1[0] = o1[0] + wij * b0.x; o1[1] = o1[1] + wij * b0.y;
         o1[2] = o1[2] + wij * b1.x; o1[3] = o1[3] + wij * b1.y;
         o1[4] = o1[4] + wij * b2.x; o1[5] = o1[5] + wij * b2.y;
       }
     }
+    return;
+  }
+  Tap6<TWO> cur, nxt;
+  tap6_read<TWO, WN>(p, 0, cur);
+#pragma unroll
+  for (int t = 0; t < kNT * kNT; ++t) {
+    const int i = t / kNT, j = t % kNT;
+    if (t + 1 < kNT * kNT) tap6_read<TWO, WN>(p, ((t + 1) / kNT) * W + (t + 1) % kNT, nxt);
+    if constexpr (!TWO) __builtin_amdgcn_sched_barrier(0);
+    const double wij = wx[i] * wy[j];
+    o0[0] = o0[0] + wij * cur.a0.x; o0[1] = o0[1] + wij * cur.a0.y;
+    o0[2] = o0[2] + wij * cur.a1.x; o0[3] = o0[3] + wij * cur.a1.y;
+    o0[4] = o0[4] + wij * cur.a2.x; o0[5] = o0[5] + wij * cur.a2.y;
+    if constexpr (TWO) {
+      o1[0] = o1[0] + wij * cur.b0.x; o1[1] = o1[1] + wij * cur.b0.y;
+      o1[2] = o1[2] + wij * cur.b1.x; o1[3] = o1[3] + wij * cur.b1.y;
+      o1[4] = o1[4] + wij * cur.b2.x; o1[5] = o1[5] + wij * cur.b2.y;
+    }
+    if constexpr (!TWO) __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < kNT * kNT) cur = nxt;
   }
 }
 
