@@ -11,5 +11,5 @@ grep '^{' $OUT/bench.log | python -c 'import json,sys; d=json.loads(sys.stdin.re
 timeout -k 10 300 python tools/bench_pipeline.py --ode23 > $OUT/pipeline.json 2>&1 || exit $?
 tail -1 $OUT/pipeline.json
 export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --no-cpu-baseline > $OUT/prof.log 2>&1 || exit $?
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o bench --output-format csv -- python3 bench.py --no-cpu-baseline --driver-steps 0 > $OUT/prof.log 2>&1 || exit $?
 head -3 $OUT/prof/bench_kernel_stats.csv
