@@ -268,9 +268,16 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
     double fo[4];
     if constexpr (STAGE == 0) {
       // stages 2, 3, 4 of the attempt in one pass (a rolled loop: one copy of
-      // the gather, so registers stay at the single-stage count); the stage
-      // derivatives go to memory as in the separate stages and are re-read
-      // where those read them: same bits
+      // the gather, so registers stay at the single-stage count).  The sums
+      // that combine the stage derivatives are carried in registers, added
+      // to as each derivative appears, in the reference's order:
+      //   s4 = (F1*c4[0] + F2*c4[1]) [+ F3*c4[2] at stage 4],
+      //   fe = ((F1*E1 + F2*E2) + F3*E3) + F4*E4,
+      // so F1 is read once and the stage-2/3 derivatives never go to memory
+      // (only F4 does: the next step's F1, FSAL) — the same bits as the
+      // separate stages, which store and re-read them.
+      constexpr double E1 = -5.0 / 72.0, E2 = 1.0 / 12.0, E3 = 1.0 / 9.0, E4 = -1.0 / 8.0;
+      double s4[4], fe[4];
 #pragma unroll 1
       for (int sg = 0; sg < 3; ++sg) {
         double ts;
@@ -279,7 +286,12 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
         const double yv[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
         if (sg == 0) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + a.F[0][c * n + p] * a.c[0];
+          for (int c = 0; c < 4; ++c) {
+            const double f1 = a.F[0][c * n + p];
+            ys[c] = yv[c] + f1 * a.c[0];
+            s4[c] = f1 * a.c4[0];
+            fe[c] = f1 * E1;
+          }
           ts = a.ts;
         } else if (sg == 1) {
 #pragma unroll
@@ -287,23 +299,30 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
           ts = a.ts3;
         } else {
 #pragma unroll
-          for (int c = 0; c < 4; ++c)
-            ys[c] = yv[c] + (((a.F[0][c * n + p] * a.c4[0]) + a.F[1][c * n + p] * a.c4[1]) + fo[c] * a.c4[2]);
+          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + (s4[c] + fo[c] * a.c4[2]);
           a.ynx[p] = ys[0]; a.ynx[n + p] = ys[1];
           a.ynk[p] = ys[2]; a.ynk[n + p] = ys[3];
           ts = a.ts4;
         }
         tile_rhs<TWO, T, M, WS, WNP, V5>(a, win, ox, oy, nx, alpha_of(a, ts), ys, fo);
-        double* Fo = sg == 0 ? a.F[1] : (sg == 1 ? a.F[2] : a.F[3]);  // no runtime index into the argument
+        if (sg == 0) {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) Fo[c * n + p] = fo[c];
+          for (int c = 0; c < 4; ++c) {
+            s4[c] = s4[c] + fo[c] * a.c4[1];
+            fe[c] = fe[c] + fo[c] * E2;
+          }
+        } else if (sg == 1) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) fe[c] = fe[c] + fo[c] * E3;
+        }
       }
-      constexpr double E1 = -5.0 / 72.0, E2 = 1.0 / 12.0, E3 = 1.0 / 9.0, E4 = -1.0 / 8.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a.F[3][c * n + p] = fo[c];
       const double yv[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const double fe = ((a.F[0][c * n + p] * E1 + a.F[1][c * n + p] * E2) + a.F[2][c * n + p] * E3) + fo[c] * E4;
-        m = fmax(m, fabs(fe) / fmax(fmax(fabs(yv[c]), fabs(ys[c])), a.thr));
+        const double e = fe[c] + fo[c] * E4;
+        m = fmax(m, fabs(e) / fmax(fmax(fabs(yv[c]), fabs(ys[c])), a.thr));
       }
       continue;
     }
