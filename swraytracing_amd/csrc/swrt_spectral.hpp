@@ -10,15 +10,16 @@
 // u_x = -psi_xy, u_y = -psi_yy, v_x = psi_xx, v_y = psi_xy.
 //
 // One lane per packet; all lanes read the same coefficient at the same time
-// (LDS broadcasts of a block-staged stream, SpecStream) and each lane walks a row with the phase
-// recurrence e <- e*exp(1i*s*x) (re-seeded
-// with sincos at the start of every row), accumulating the five row sums
+// (LDS broadcasts of a block-staged stream, SpecStream) and each lane walks a
+// row with the phase recurrence e <- e*exp(1i*s*x) (re-seeded with sincos at
+// the start of every row), accumulating the five row sums
 //   A0 = sum Im z, A1 = sum kx Im z, B0 = sum Re z, B1 = sum kx Re z,
 //   B2 = sum kx^2 Re z   (z = C*e)
 // that the ky weights then combine: psi_x -= A1, psi_y -= ky*A0,
 // psi_xx -= B2, psi_xy -= ky*B1, psi_yy -= ky^2*B0.
-// FP-VALU bound (≈14 flops per mode per packet); T = double or float
-// (the fp32 tolerance study of config 5).
+// FP-VALU bound (15 instructions, 22 flop per mode per packet); the kernels
+// take T = double or float (float: packed math, the fp32 tolerance study of
+// config 5).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,8 +28,8 @@ namespace swrt {
 
 struct ModeGrid {
   const double2* C;  // nkx x nky column-major (i fastest): row j = fixed ky
-  // row j's nonzero span zero-padded to whole groups of kSpecChains modes
-  // (+ one zero group at the end of the array), starting at Cd[Cd_row[j]]
+  // row j's nonzero span zero-padded to whole groups of kSpecChains modes,
+  // starting at Cd[Cd_row[j]] (the array padded past its end for SpecStream)
   const double2* Cd;
   const int* Cd_row;
   const int2* rows;  // per row: [first, last+1) of the nonzero coefficients
@@ -42,11 +43,6 @@ struct ModeGrid {
 };
 
 constexpr int kSpecThreads = 256;
-
-template <typename T>
-struct cplx {
-  T re, im;
-};
 
 // Five derivative sums of psi at (x, y).  Every lane of the block walks the
 // same coefficient at the same time (SpecStream); zero head/tail segments of
@@ -68,7 +64,7 @@ constexpr int kSpecChunk = 512;                              // slots (8 KB) per
 constexpr int kSpecPer = kSpecChunk / kSpecThreads;         // slots per thread per chunk
 
 struct SpecStream {
-  const uint4* src;  // the slot array (padded past the end by one chunk)
+  const uint4* src;  // the slot array (padded past the end by two chunks)
   uint4* buf;        // __shared__ [2][kSpecChunk]
   int base;          // slot index of the chunk in buf[cur]
   int cur;
@@ -121,8 +117,7 @@ __device__ __forceinline__ void spectral_sums(const ModeGrid& g, double x, doubl
       A0[c] = A1[c] = B0[c] = B1[c] = B2[c] = 0;
     }
     const double ds = kSpecChains * g.s;
-    // row j's span, zero-padded to whole groups of kSpecChains modes (+ one
-    // group past the end for the prefetch)
+    // row j's span, zero-padded to whole groups of kSpecChains modes
     const int s0 = g.Cd_row[j];
     const int ngroups = (rg.y - rg.x + kSpecChains - 1) / kSpecChains;
     {
