@@ -1610,6 +1610,9 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   a.save_every = save_every > 0 ? save_every : 1;
   a.hist = frames ? c->xka_hist : nullptr;
   a.perm = nullptr;
+  a.st_in = a.st;
+  a.src = nullptr;
+  a.perm_out = nullptr;
   // larger ensembles: step the packets in spatially binned order (8 x 8-cell
   // tiles, counting sort by index) with the LDS-tiled kernel (one workgroup
   // per tile, xka_tile_kernel), re-binned every rebin_every steps (the
@@ -1626,30 +1629,25 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   const int nbins = g.ntx * g.ntx;
   const bool tiled = binned && a.nx % g.tile == 0 && g.ntx >= 2 && (g.tile == 8 || g.tile == 16);
   const unsigned bgrid = nblocks(n, 256 * kBinPerThread);
-  double* cur = c->xka_state;   // the state the next launch steps
+  // Binning is index-only: the scatter writes the source slot of every binned
+  // slot and the launch that follows reads its packets through it into the
+  // other state buffer, composing the permutation to the caller's order
+  double* cur = c->xka_state;   // the state the next launch reads
   double* other = c->xka_state2;
   int* perm = nullptr;          // cur's slot -> caller's packet (nullptr: identity)
   int* perm_other = c->xka_perm2;
-  // bin `cur` (slot -> packet permutation `perm`) into `other`, then swap
+  const int* src = nullptr;     // pending re-binning (cur's slots, binned order)
   auto rebin_xka = [&]() -> int {
     HIPCHK(c, hipMemsetAsync(c->xka_bins, 0, sizeof(int) * nbins, c->stream));
     hipLaunchKernelGGL(bin_count_kernel, dim3(bgrid), dim3(256), sizeof(int) * nbins, c->stream, g, cur, n, nbins,
                        c->xka_keys, c->xka_bins);
     hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->xka_bins, nbins,
                        c->xka_bins + kMaxBins, c->xka_bins + 2 * kMaxBins, nullptr, kTileThreads);
-    int* src = perm == nullptr ? c->xka_src : c->xka_src2;
     hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3(bgrid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
                        cur, cur, nullptr, c->xka_keys, n, nbins, c->xka_bins + kMaxBins, nullptr, nullptr, nullptr,
-                       src);
-    hipLaunchKernelGGL(xka_gather_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, cur, src, perm, n, other,
-                       perm == nullptr ? nullptr : perm_other);
+                       c->xka_src2);
     HIPCHK(c, hipGetLastError());
-    std::swap(cur, other);
-    if (perm == nullptr) {
-      perm = src;  // the first binning's src is the permutation itself
-    } else {
-      std::swap(perm, perm_other);
-    }
+    src = c->xka_src2;
     return SWRT_OK;
   };
   int rc;
@@ -1657,8 +1655,17 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
   const int64_t per_launch = tiled ? std::min<int64_t>(kMaxStepsPerLaunch, c->rebin_every) : kMaxStepsPerLaunch;
   for (int64_t s0 = 0; s0 < nsteps; s0 += per_launch) {
     if (tiled && s0 > 0 && (rc = rebin_xka())) return rc;
-    a.st = cur;
+    a.st_in = cur;
+    a.src = src;
     a.perm = perm;
+    if (src) {  // out of place: into the other buffer, with the composed permutation
+      int* pout = perm == nullptr ? c->xka_src : perm_other;
+      a.st = other;
+      a.perm_out = pout;
+    } else {
+      a.st = cur;
+      a.perm_out = nullptr;
+    }
     a.nsteps = (int)std::min<int64_t>(per_launch, nsteps - s0);
     a.frame0 = s0 / a.save_every;
     if (tiled && g.tile == 8)
@@ -1670,6 +1677,15 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
     else
       hipLaunchKernelGGL(xka_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, a);
     HIPCHK(c, hipGetLastError());
+    if (src) {
+      std::swap(cur, other);
+      if (perm == nullptr) {
+        perm = c->xka_src;
+      } else {
+        std::swap(perm, perm_other);
+      }
+      src = nullptr;
+    }
   }
   if (binned) {
     hipLaunchKernelGGL(xka_scatter_back_kernel, dim3(nblocks(n, 256)), dim3(256), 0, c->stream, cur, perm, n, other);

@@ -25,13 +25,17 @@ struct XkaArgs {
   int nx, npad;
   double dx, dy, inv_dx, inv_dy, px, py, inv_px, inv_py;
   double C0sq, f, f2, dt, bump;
-  double* st;          // 5 x n: x, y, k, l, a (column blocks)
+  double* st;          // 5 x n: x, y, k, l, a (column blocks) — the output, slot p
+  const double* st_in; // the input state (== st: in place)
+  const int* src;      // non-NULL: slot p's packet is input slot src[p] (a re-binning read
+                       // through by the launch that follows it; st_in != st)
   int64_t n;
   int nsteps;
   int64_t save_every;
   double* hist;        // frames of 5 x n (NULL: none)
   int64_t frame0;
-  const int* perm;     // binned slot -> caller's packet index (history frames); NULL: identity
+  const int* perm;     // input slot -> caller's packet index (history frames); NULL: identity
+  int* perm_out;       // non-NULL (with src): the output slots' permutation, perm[src[p]]
 };
 
 // Per-tap dispersion of cg_sw.m:16-26: w = sqrt(f^2 + gH*K2), cx = gH*k/w,
@@ -254,7 +258,11 @@ __device__ __forceinline__ double rk4_mean(double a, double b, double c, double 
 template <class Field>
 __device__ __forceinline__ void xka_advance(const XkaArgs& a, const Field& fld, int64_t p) {
   const int64_t n = a.n;
-  double x = a.st[p], y = a.st[n + p], k = a.st[2 * n + p], l = a.st[3 * n + p], ac = a.st[4 * n + p];
+  const int64_t pi = a.src ? (int64_t)a.src[p] : p;  // input slot
+  double x = a.st_in[pi], y = a.st_in[n + pi], k = a.st_in[2 * n + pi], l = a.st_in[3 * n + pi],
+         ac = a.st_in[4 * n + pi];
+  const int64_t o = a.perm ? (int64_t)a.perm[pi] : pi;  // the caller's packet index
+  if (a.perm_out) a.perm_out[p] = (int)o;
   const double dt = a.dt;
   for (int s = 0; s < a.nsteps; ++s) {
     const double K2 = k * k + l * l;  // cg_sw.m:22 (k^2+l^2)
@@ -293,9 +301,8 @@ __device__ __forceinline__ void xka_advance(const XkaArgs& a, const Field& fld, 
     y = Y;
     k = Kn;
     l = Ln;
-    if (a.hist != nullptr && ((s + 1) % a.save_every) == 0) {
+    if (a.hist != nullptr && ((s + 1) % a.save_every) == 0) {  // frames in the caller's packet order
       double* h = a.hist + (a.frame0 + (s + 1) / a.save_every - 1) * 5 * n;
-      const int64_t o = a.perm ? a.perm[p] : p;  // frames in the caller's packet order
       h[o] = x; h[n + o] = y; h[2 * n + o] = k; h[3 * n + o] = l; h[4 * n + o] = ac;
     }
   }
@@ -345,23 +352,12 @@ __global__ void __launch_bounds__(NT) xka_tile_kernel(XkaArgs a, const int* star
   for (int p = pbeg + (int)threadIdx.x; p < pend; p += NT) xka_advance(a, fld, p);
 }
 
-// Spatial order for the xka lanes (swrt_xka_step): the 5 x n state gathered
-// into binned order (src from bin_scatter_kernel<true>), and scattered back.
-// Neighbouring lanes then read the same few node records, which the L1/L2
-// serve: the gathers dominate the unbinned kernel.  Order only: every packet
-// is stepped by the same operations whatever its lane.
-// perm != NULL (a re-binning of already binned state): also compose the
-// permutation to the caller's order, perm_out[d] = perm[src[d]].
-__global__ void xka_gather_kernel(const double* st, const int* src, const int* perm, int64_t n, double* out,
-                                  int* perm_out) {
-  const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (d >= n) return;
-  const int64_t p = src[d];
-#pragma unroll
-  for (int q = 0; q < 5; ++q) out[q * n + d] = st[q * n + p];
-  if (perm != nullptr) perm_out[d] = perm[p];
-}
-
+// Spatial order for the xka lanes (swrt_xka_step): the launch after each
+// re-binning reads its packets through the binned source index (XkaArgs::src)
+// and writes them in binned order; the final state is scattered back to the
+// caller's order through the composed permutation.  Neighbouring lanes then
+// read the same few node records.  Order only: every packet is stepped by the
+// same operations whatever its lane.
 __global__ void xka_scatter_back_kernel(const double* st, const int* src, int64_t n, double* out) {
   const int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= n) return;
