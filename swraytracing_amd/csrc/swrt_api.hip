@@ -414,6 +414,8 @@ int run_fft_pass(swrt_ctx* c, double2* Z, int n, int nb, int inverse) {
   // radix-2 Stockham, 256 lanes per vector (measured faster than a radix-8
   // register variant at 512: 8.8 vs 9.7 us per 4-transform pass)
   const size_t lds = sizeof(double2) * 2 * n;
+  // 256 lanes per vector (measured faster than 128 or 64 at 512^2: PDE step
+  // 0.089 vs 0.097 / 0.114 ms, profiles/r02_v20_fft_threads_ab.jsonl)
   hipLaunchKernelGGL(fft_vec_kernel, dim3((unsigned)nvec), dim3(256), lds, c->stream, Z, n, logn, c->tw, inverse);
   HIPCHK(c, hipGetLastError());
   return SWRT_OK;
@@ -2121,7 +2123,8 @@ int qg_post(swrt_ctx* c) {
   if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
   // Jacobian and the CFL speed over every layer's u + i v (layer 1, then
   // layer 0: contiguous); the spectrum of J then lands in PT[0, nn)
-  hipLaunchKernelGGL(qg_jacobian_max_kernel, grid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ,
+  const dim3 jgrid((unsigned)nblocks(q.nn, 256 * kQgMaxPer));
+  hipLaunchKernelGGL(qg_jacobian_max_kernel, jgrid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ,
                      (const double2*)(q.PT + 2 * nl * q.nn), q.g.shear, q.dmax);
   HIPCHK(c, hipGetLastError());
   if ((rc = run_fft_pass(c, q.PZ, n, 1, 0))) return rc;

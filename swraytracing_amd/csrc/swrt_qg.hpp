@@ -390,13 +390,17 @@ __global__ void __launch_bounds__(256) qg_post_spectra_kernel(const double2* qk,
 
 // qg_jacobian_kernel + qg_max_speed2_kernel over the same grid points:
 // J1 + i J2, and max (u + shear)^2 + v^2 over the nl u+iv planes at `uv`.
+// Grid-stride (kQgMaxPer points per thread), the max reduced by wave
+// shuffles and one LDS pass, one atomic per block: the one-point-per-thread
+// form with a block-wide LDS tree took 16.5 us at 512^2 (1.8 TB/s).
+constexpr int kQgMaxPer = 4;
 __global__ void __launch_bounds__(256) qg_jacobian_max_kernel(const double2* T, int nl, int64_t nn, double2* Zj,
                                                               const double2* uv, double shear,
                                                               unsigned long long* dmax) {
-  __shared__ double red[256];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ double red[256 / 64];
   double m = 0.0;
-  if (i < nn) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nn; i += stride) {
     double J[2] = {0.0, 0.0};
     for (int l = 0; l < nl; ++l) {
       const double2 P = T[(2 * l) * nn + i], Q = T[(2 * l + 1) * nn + i];
@@ -410,13 +414,14 @@ __global__ void __launch_bounds__(256) qg_jacobian_max_kernel(const double2* T, 
       m = s2 > m ? s2 : m;
     }
   }
-  red[threadIdx.x] = m;
+  for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + s]);
-    __syncthreads();
+  if (threadIdx.x == 0) {
+    double b = red[0];
+    for (int w = 1; w < 256 / 64; ++w) b = fmax(b, red[w]);
+    atomicMax(dmax, (unsigned long long)__double_as_longlong(b));
   }
-  if (threadIdx.x == 0) atomicMax(dmax, (unsigned long long)__double_as_longlong(red[0]));
 }
 
 }  // namespace swrt
