@@ -182,7 +182,7 @@ struct swrt_ctx {
   double* hx = nullptr;
   double* hk = nullptr;
   int64_t hframes = 0;
-  int64_t hcap = 0;  // frames allocated
+  int64_t hcap = 0;  // doubles allocated per history buffer (frames x 2 x n)
   int64_t steps_done = 0;  // global step counter since history reset (for save cadence)
   // scratch
   void* scratch = nullptr;
@@ -416,7 +416,8 @@ int run_fft_pass(swrt_ctx* c, double2* Z, int n, int nb, int inverse) {
   const size_t lds = sizeof(double2) * 2 * n;
   // 256 lanes per vector (measured faster than 128 or 64 at 512^2: PDE step
   // 0.089 vs 0.097 / 0.114 ms, profiles/r02_v20_fft_threads_ab.jsonl)
-  hipLaunchKernelGGL(fft_vec_kernel, dim3((unsigned)nvec), dim3(256), lds, c->stream, Z, n, logn, c->tw, inverse);
+  hipLaunchKernelGGL(fft_vec_kernel<false>, dim3((unsigned)nvec), dim3(256), lds, c->stream, Z, Z, n, logn, c->tw,
+                     inverse, (int)nvec);
   HIPCHK(c, hipGetLastError());
   return SWRT_OK;
 }
@@ -428,15 +429,28 @@ int run_transpose(swrt_ctx* c, const double2* in, double2* out, int n, int nb) {
   return SWRT_OK;
 }
 
-// Inverse 2-D transform of nb spectra in layout [c + n*r] (ky contiguous);
-// result in layout [r + n*c] (x contiguous) in `out`.
-int inverse_2d(swrt_ctx* c, double2* Z, double2* out, int n, int nb) {
+// 2-D transform of nb n x n blocks: a pass along the contiguous index of Z (in
+// place), then a pass along the other index reading Z's columns and writing
+// `out` transposed ([r + n*c] for Z in [c + n*r]).  Z keeps the first pass.
+int transform_2d(swrt_ctx* c, double2* Z, double2* out, int n, int nb, int inverse) {
   int rc;
-  if ((rc = run_fft_pass(c, Z, n, nb, 1))) return rc;   // along ky
-  if ((rc = run_transpose(c, Z, out, n, nb))) return rc;
-  if ((rc = run_fft_pass(c, out, n, nb, 1))) return rc;  // along kx
+  if ((rc = run_fft_pass(c, Z, n, nb, inverse))) return rc;
+  const int64_t nvec = (int64_t)n * nb;
+  if (nvec % 8) {  // tiny grids: the XCD mapping needs 8 | nvec
+    if ((rc = run_transpose(c, Z, out, n, nb))) return rc;
+    return run_fft_pass(c, out, n, nb, inverse);
+  }
+  int logn = 0;
+  while ((1 << logn) < n) ++logn;
+  hipLaunchKernelGGL(fft_vec_kernel<true>, dim3((unsigned)nvec), dim3(256), sizeof(double2) * 2 * n, c->stream, Z,
+                     out, n, logn, c->tw, inverse, (int)nvec);
+  HIPCHK(c, hipGetLastError());
   return SWRT_OK;
 }
+
+// Inverse 2-D transform of nb spectra in layout [c + n*r] (ky contiguous);
+// result in layout [r + n*c] (x contiguous) in `out`.
+int inverse_2d(swrt_ctx* c, double2* Z, double2* out, int n, int nb) { return transform_2d(c, Z, out, n, nb, 1); }
 
 // Shared tail of set_field_psi / set_field_qk / swrt_qg_snapshot: fk half
 // plane in device memory, read at fk[(kx + kmax)*sx + ky*sy].
@@ -802,20 +816,27 @@ int run_advance_intervals(swrt_ctx* c, int nint, const double* hs, int64_t nsub,
   return SWRT_OK;
 }
 
-// grow the history frames (keeps the existing ones)
+// grow the history frames (keeps the existing ones).  The capacity is kept in
+// doubles, not frames: a frame is 2 x n doubles and n changes with every
+// swrt_packets_set, so a frame count sized for a smaller ensemble must not
+// pass the check.
 int ensure_history(swrt_ctx* c, int64_t new_frames) {
-  if (new_frames <= 0 || c->hframes + new_frames <= c->hcap) return SWRT_OK;
-  const int64_t ncap = std::max<int64_t>(c->hframes + new_frames, 2 * c->hcap);
+  const int64_t per = 2 * c->n;
+  const int64_t need = (c->hframes + new_frames) * per;
+  if (new_frames <= 0 || need <= c->hcap) return SWRT_OK;
+  const int64_t ncap = std::max<int64_t>(need, 2 * c->hcap);
   double *nx_ = nullptr, *nk_ = nullptr;
-  HIPCHK(c, hipMalloc(&nx_, sizeof(double) * 2 * c->n * ncap));
-  HIPCHK(c, hipMalloc(&nk_, sizeof(double) * 2 * c->n * ncap));
-  if (c->hframes > 0) {
-    HIPCHK(c, hipMemcpyAsync(nx_, c->hx, sizeof(double) * 2 * c->n * c->hframes, hipMemcpyDeviceToDevice,
-                             c->stream));
-    HIPCHK(c, hipMemcpyAsync(nk_, c->hk, sizeof(double) * 2 * c->n * c->hframes, hipMemcpyDeviceToDevice,
-                             c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMalloc(&nx_, sizeof(double) * ncap));
+  if (hipMalloc(&nk_, sizeof(double) * ncap) != hipSuccess) {
+    (void)hipFree(nx_);
+    return fail(c, SWRT_ERR_ALLOC, "history allocation failed");
   }
+  if (c->hframes > 0) {
+    HIPCHK(c, hipMemcpyAsync(nx_, c->hx, sizeof(double) * per * c->hframes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(nk_, c->hk, sizeof(double) * per * c->hframes, hipMemcpyDeviceToDevice, c->stream));
+  }
+  // the old buffers may still be read or written by queued work
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   if (c->hx) (void)hipFree(c->hx);
   if (c->hk) (void)hipFree(c->hk);
   c->hx = nx_;
@@ -981,9 +1002,7 @@ int swrt_set_field_psi(swrt_ctx* c, int slot, const double* psi_grid, int64_t nx
   hipLaunchKernelGGL(real_to_complex_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, raw,
                      Z, nn);
   HIPCHK(c, hipGetLastError());
-  if ((rc = run_fft_pass(c, Z, n, 1, 0))) return rc;  // along x
-  if ((rc = run_transpose(c, Z, T, n, 1))) return rc;
-  if ((rc = run_fft_pass(c, T, n, 1, 0))) return rc;  // along y; T: [c + n*r]
+  if ((rc = transform_2d(c, Z, T, n, 1, 0))) return rc;  // along x, then y; T: [c + n*r]
   hipLaunchKernelGGL(crop_half_kernel, dim3(nblocks(nhalf, 256)), dim3(256), 0, c->stream, T, n, fk);
   HIPCHK(c, hipGetLastError());
   if ((rc = fields_from_halfplane(c, slot, fk, n, 0, 0.0, 1.0, 0.0, 1, Z, T, 1, 2 * (n / 2 - 1) + 1))) return rc;
@@ -1057,9 +1076,7 @@ int swrt_g2k(swrt_ctx* c, const double* fg, int64_t nx, double* fk_out) {
   HIPCHK(c, hipMemcpyAsync(raw, fg, sizeof(double) * nn, hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL(real_to_complex_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, raw, Z, nn);
   HIPCHK(c, hipGetLastError());
-  if ((rc = run_fft_pass(c, Z, n, 1, 0))) return rc;
-  if ((rc = run_transpose(c, Z, T, n, 1))) return rc;
-  if ((rc = run_fft_pass(c, T, n, 1, 0))) return rc;
+  if ((rc = transform_2d(c, Z, T, n, 1, 0))) return rc;
   hipLaunchKernelGGL(crop_half_kernel, dim3(nblocks(nhalf, 256)), dim3(256), 0, c->stream, T, n, fk);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipMemcpyAsync(fk_out, fk, sizeof(double2) * nhalf, hipMemcpyDeviceToHost, c->stream));
@@ -1519,9 +1536,7 @@ int swrt_xka_set_rsw(swrt_ctx* c, const double* state3, int64_t nx, double f, do
   // g2k.m:8 fft2 of u, v, eta (raytrace_sw.m:26-28)
   hipLaunchKernelGGL(real_to_complex_kernel, dim3(nblocks(3 * nn, 256)), dim3(256), 0, c->stream, planes, Z, 3 * nn);
   HIPCHK(c, hipGetLastError());
-  if ((rc = run_fft_pass(c, Z, n, 3, 0))) return rc;
-  if ((rc = run_transpose(c, Z, T, n, 3))) return rc;
-  if ((rc = run_fft_pass(c, T, n, 3, 0))) return rc;
+  if ((rc = transform_2d(c, Z, T, n, 3, 0))) return rc;
   // projection + gradients + fulspec (raytrace_sw.m:25-41), then 4 inverse transforms
   hipLaunchKernelGGL(rsw_spectra_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, n, f, Cg * Cg, Z);
   HIPCHK(c, hipGetLastError());
@@ -2089,9 +2104,7 @@ int qg_step_launches(swrt_ctx* c, double dt, int abstep) {
   double2* Zj = q.Z;  // J1 + i J2, grid layout (x contiguous)
   hipLaunchKernelGGL(qg_jacobian_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.T, nl, q.nn, Zj);
   HIPCHK(c, hipGetLastError());
-  if ((rc = run_fft_pass(c, Zj, n, 1, 0))) return rc;   // along x
-  if ((rc = run_transpose(c, Zj, q.T, n, 1))) return rc;
-  if ((rc = run_fft_pass(c, q.T, n, 1, 0))) return rc;  // along y: [ky + n*kx]
+  if ((rc = transform_2d(c, Zj, q.T, n, 1, 0))) return rc;  // along x, then y: [ky + n*kx]
   return qg_update_launch(c, dt, abstep, q.T);
 }
 
@@ -2127,9 +2140,7 @@ int qg_post(swrt_ctx* c) {
   hipLaunchKernelGGL(qg_jacobian_max_kernel, jgrid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ,
                      (const double2*)(q.PT + 2 * nl * q.nn), q.g.shear, q.dmax);
   HIPCHK(c, hipGetLastError());
-  if ((rc = run_fft_pass(c, q.PZ, n, 1, 0))) return rc;
-  if ((rc = run_transpose(c, q.PZ, q.PT, n, 1))) return rc;
-  if ((rc = run_fft_pass(c, q.PT, n, 1, 0))) return rc;
+  if ((rc = transform_2d(c, q.PZ, q.PT, n, 1, 0))) return rc;
   q.post_valid = true;
   return SWRT_OK;
 }

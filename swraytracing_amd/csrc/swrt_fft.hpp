@@ -16,13 +16,32 @@ namespace swrt {
 // Stockham autosort, radix 2: stage with stride s, half-length m = n/(2s):
 //   y[q + s*2p] = a + b,  y[q + s*(2p+1)] = (a - b) * w^(p*s),
 //   a = x[q + s*p], b = x[q + s*(p+m)].
-__global__ void __launch_bounds__(256) fft_vec_kernel(double2* data, int n, int logn,
-                                                      const double2* tw, int inverse) {
+//
+// TIN (the second pass of a 2-D transform, fused with the transpose between
+// the passes): vector i of batch b is read down the column in[b*n*n + i + n*j]
+// and written contiguously to out[b*n*n + i*n + j] — the same values as a
+// transpose followed by an in-place pass, without the transpose's round trip
+// through memory.  Blocks are mapped so that consecutive columns run on the
+// same XCD at the same time (block k of XCD x = blockIdx % 8 takes vector
+// x*nvec/8 + k): the 8 columns of each 128-B line are read by neighbouring
+// workgroups through the same L2.
+template <bool TIN>
+__global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2* data, int n, int logn,
+                                                      const double2* tw, int inverse, int nvec) {
   extern __shared__ double2 sbuf[];
   double2* xa = sbuf;
   double2* ya = sbuf + n;
-  double2* v = data + (size_t)blockIdx.x * n;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) xa[i] = v[i];
+  double2* v;
+  if constexpr (TIN) {
+    const int vec = (int)(blockIdx.x & 7) * (nvec >> 3) + (int)(blockIdx.x >> 3);
+    const int b = vec >> logn, i = vec & (n - 1);
+    const double2* src = in + ((size_t)b << (2 * logn)) + i;
+    for (int j = threadIdx.x; j < n; j += blockDim.x) xa[j] = src[(size_t)j * n];
+    v = data + (size_t)vec * n;
+  } else {
+    v = data + (size_t)blockIdx.x * n;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) xa[i] = v[i];
+  }
   __syncthreads();
   const int half = n >> 1;
   int s = 1, logs = 0;

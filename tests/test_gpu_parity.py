@@ -99,6 +99,29 @@ def test_leapfrog_bitexact_steady_with_history(ctx, oracle_lib, qg_case):
     np.testing.assert_array_equal(hkg, hko)
 
 
+def test_history_capacity_follows_the_packet_count(ctx, oracle_lib, qg_case):
+    """A small ensemble with many frames, then a 64x larger one with few: the
+    history capacity is counted in doubles (frames x 2 x n), so the second
+    call grows the buffers (a capacity counted in frames let it write past
+    them — found through a test order that ran the interval tests after
+    these)."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    pl = _planes(c["flow"])
+    ctx.set_field_grid(0, pl, nx, L)
+    xs, ks = c["x"][:16], c["k"][:16]
+    ctx.leapfrog(xs, ks, c["dt"], 64, c["f"], 1.0, bump=orc.BUMP_SW, save_every=1)
+    rng = np.random.default_rng(3)
+    xb = np.concatenate([c["x"] + rng.normal(0, 1e-3, c["x"].shape) for _ in range(4)])
+    kb = np.concatenate([c["k"]] * 4)
+    xg, kg, hxg, hkg = ctx.leapfrog(xb, kb, c["dt"], 8, c["f"], 1.0, bump=orc.BUMP_SW, save_every=4)
+    xo, ko, hxo, hko = oracle_lib.leapfrog(pl, None, 0, 0, nx, nx, L / nx, orc.BUMP_SW, xb, kb, c["dt"], 8,
+                                           c["f"], 1.0, save_every=4)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(hxg, hxo)
+    np.testing.assert_array_equal(hkg, hko)
+
+
 def test_leapfrog_blend_bitexact(ctx, oracle_lib, qg_case):
     c = qg_case
     nx, L = c["nx"], c["L"]
