@@ -342,14 +342,14 @@ int ensure_twiddles(swrt_ctx* c, int n) {
     (void)hipFree(c->tw);
   }
   c->tw = nullptr;
-  std::vector<double2> h(n / 2);
-  for (int k = 0; k < n / 2; ++k) {
+  std::vector<double2> h(n);  // k < n: the radix-4 stages read w^(3*p*s) < w^(3n/4)
+  for (int k = 0; k < n; ++k) {
     // exp(-2*pi*i*k/n); long double for the argument reduction
     const long double th = -2.0L * 3.14159265358979323846264338327950288L * (long double)k / (long double)n;
     h[k] = make_double2((double)cosl(th), (double)sinl(th));
   }
-  HIPCHK(c, hipMalloc(&c->tw, sizeof(double2) * (n / 2)));
-  HIPCHK(c, hipMemcpyAsync(c->tw, h.data(), sizeof(double2) * (n / 2), hipMemcpyHostToDevice,
+  HIPCHK(c, hipMalloc(&c->tw, sizeof(double2) * n));
+  HIPCHK(c, hipMemcpyAsync(c->tw, h.data(), sizeof(double2) * n, hipMemcpyHostToDevice,
                            c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->tw_n = n;
@@ -407,17 +407,26 @@ int pack_slot(swrt_ctx* c, int slot, const double* dplanes, double shear) {
   return SWRT_OK;
 }
 
+// FFT kernel variant (swrt_fft.hpp): radix 4 in one LDS buffer with n/4
+// lanes for n <= 1024, else radix 4 ping-pong with 128 lanes.  At 512^2 x 2
+// layers (8-vector inverse + 1-vector forward 2-D transforms per step) the
+// one-buffer form takes the PDE step from 0.078 (radix 2, 256 lanes) / 0.077
+// (radix 4 ping-pong) to 0.073 ms (profiles/r02_v21_fft_mode_ab.log).
+template <bool TIN>
+void launch_fft(swrt_ctx* c, const double2* in, double2* out, int n, int logn, int nvec, int inverse) {
+  if (n <= 1024)
+    hipLaunchKernelGGL((fft_vec_kernel<TIN, 2>), dim3((unsigned)nvec), dim3(n / 4), sizeof(double2) * n, c->stream,
+                       in, out, n, logn, c->tw, inverse, nvec);
+  else
+    hipLaunchKernelGGL((fft_vec_kernel<TIN, 1>), dim3((unsigned)nvec), dim3(128), sizeof(double2) * 2 * n, c->stream,
+                       in, out, n, logn, c->tw, inverse, nvec);
+}
+
 int run_fft_pass(swrt_ctx* c, double2* Z, int n, int nb, int inverse) {
   int logn = 0;
   while ((1 << logn) < n) ++logn;
   const int64_t nvec = (int64_t)n * nb;
-  // radix-2 Stockham, 256 lanes per vector (measured faster than a radix-8
-  // register variant at 512: 8.8 vs 9.7 us per 4-transform pass)
-  const size_t lds = sizeof(double2) * 2 * n;
-  // 256 lanes per vector (measured faster than 128 or 64 at 512^2: PDE step
-  // 0.089 vs 0.097 / 0.114 ms, profiles/r02_v20_fft_threads_ab.jsonl)
-  hipLaunchKernelGGL(fft_vec_kernel<false>, dim3((unsigned)nvec), dim3(256), lds, c->stream, Z, Z, n, logn, c->tw,
-                     inverse, (int)nvec);
+  launch_fft<false>(c, Z, Z, n, logn, (int)nvec, inverse);
   HIPCHK(c, hipGetLastError());
   return SWRT_OK;
 }
@@ -442,8 +451,7 @@ int transform_2d(swrt_ctx* c, double2* Z, double2* out, int n, int nb, int inver
   }
   int logn = 0;
   while ((1 << logn) < n) ++logn;
-  hipLaunchKernelGGL(fft_vec_kernel<true>, dim3((unsigned)nvec), dim3(256), sizeof(double2) * 2 * n, c->stream, Z,
-                     out, n, logn, c->tw, inverse, (int)nvec);
+  launch_fft<true>(c, Z, out, n, logn, (int)nvec, inverse);
   HIPCHK(c, hipGetLastError());
   return SWRT_OK;
 }

@@ -2,9 +2,9 @@
 //
 // Replaces MATLAB's fft2/ifft2/fftshift in qg_flow_ray_trace/{g2k,k2g,fulspec}.m
 // and the spectral algebra of grid_U.m / SpectralScheme.m:12-35.  A 2-D
-// transform is two passes of a batched 1-D radix-2 Stockham FFT (one 256-lane
-// workgroup per length-n vector, ping-pong in LDS) with a tiled LDS transpose
-// in between.  Runs once per snapshot (amortised over all packets).
+// transform is two passes of a batched 1-D radix-4 Stockham FFT (one n/4-lane
+// workgroup per length-n vector in one LDS buffer), the second reading the
+// first's columns (no transpose pass).  Runs once per snapshot / PDE step.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -12,8 +12,9 @@
 namespace swrt {
 
 // Batched length-n complex FFT over contiguous vectors data[b*n + i].
-// tw[k] = exp(-2*pi*i*k/n), k < n/2.  inverse: conjugate twiddles, no scaling.
-// Stockham autosort, radix 2: stage with stride s, half-length m = n/(2s):
+// tw[k] = exp(-2*pi*i*k/n), k < n.  inverse: conjugate twiddles, no scaling.
+// Stockham autosort in radix-4 stages (r4_butterfly) and, for odd log2 n, a
+// last radix-2 stage; a radix-2 stage with stride s, half-length m = n/(2s):
 //   y[q + s*2p] = a + b,  y[q + s*(2p+1)] = (a - b) * w^(p*s),
 //   a = x[q + s*p], b = x[q + s*(p+m)].
 //
@@ -25,12 +26,38 @@ namespace swrt {
 // same XCD at the same time (block k of XCD x = blockIdx % 8 takes vector
 // x*nvec/8 + k): the 8 columns of each 128-B line are read by neighbouring
 // workgroups through the same L2.
-template <bool TIN>
+// One radix-4 Stockham butterfly (stride s = 4^(logs/2), quarter-length
+// m = n/(4s), b = q + s*p):  a_j = x[b + j*n/4],
+//   y_k = DFT4(a)_k * w^(k*p*s)  goes to  x'[q + s*(4p + k)];  returns q + 4sp.
+__device__ __forceinline__ int r4_butterfly(const double2* xa, int b, int quarter, int s, int logs,
+                                            const double2* tw, int inverse, double2 y[4]) {
+  const int q = b & (s - 1);
+  const int p = b >> logs;
+  const double2 a0 = xa[b], a1 = xa[b + quarter], a2 = xa[b + 2 * quarter], a3 = xa[b + 3 * quarter];
+  const double2 t0 = make_double2(a0.x + a2.x, a0.y + a2.y), t1 = make_double2(a0.x - a2.x, a0.y - a2.y);
+  const double2 t2 = make_double2(a1.x + a3.x, a1.y + a3.y), u = make_double2(a1.x - a3.x, a1.y - a3.y);
+  // (a1 - a3) * (-i) forward, * (+i) inverse
+  const double2 t3 = inverse ? make_double2(-u.y, u.x) : make_double2(u.y, -u.x);
+  const int e = p * s;
+  double2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
+  if (inverse) { w1.y = -w1.y; w2.y = -w2.y; w3.y = -w3.y; }
+  const double2 b1 = make_double2(t1.x + t3.x, t1.y + t3.y), b2 = make_double2(t0.x - t2.x, t0.y - t2.y);
+  const double2 b3 = make_double2(t1.x - t3.x, t1.y - t3.y);
+  y[0] = make_double2(t0.x + t2.x, t0.y + t2.y);
+  y[1] = make_double2(b1.x * w1.x - b1.y * w1.y, b1.x * w1.y + b1.y * w1.x);
+  y[2] = make_double2(b2.x * w2.x - b2.y * w2.y, b2.x * w2.y + b2.y * w2.x);
+  y[3] = make_double2(b3.x * w3.x - b3.y * w3.y, b3.x * w3.y + b3.y * w3.x);
+  return q + 4 * s * p;
+}
+
+// MODE 1: radix-4 stages (+ one radix-2 stage for odd log2 n), ping-pong
+// LDS; 2: the same in one LDS buffer, blockDim = n/4 (n <= 1024).
+template <bool TIN, int MODE>
 __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2* data, int n, int logn,
                                                       const double2* tw, int inverse, int nvec) {
   extern __shared__ double2 sbuf[];
   double2* xa = sbuf;
-  double2* ya = sbuf + n;
+  double2* ya = MODE == 2 ? sbuf : sbuf + n;
   double2* v;
   if constexpr (TIN) {
     const int vec = (int)(blockIdx.x & 7) * (nvec >> 3) + (int)(blockIdx.x >> 3);
@@ -43,9 +70,44 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2
     for (int i = threadIdx.x; i < n; i += blockDim.x) xa[i] = v[i];
   }
   __syncthreads();
-  const int half = n >> 1;
   int s = 1, logs = 0;
-  for (int st = 0; st < logn; ++st) {
+  if constexpr (MODE == 2) {
+    // one LDS buffer, blockDim == n/4: each lane holds its butterfly's four
+    // values in registers between the read and the write of a stage
+    const int b = threadIdx.x, quarter = n >> 2, half = n >> 1;
+    for (; logs + 2 <= logn; logs += 2, s <<= 2) {
+      double2 y[4];
+      const int o = r4_butterfly(xa, b, quarter, s, logs, tw, inverse, y);
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xa[o + k * s] = y[k];
+      __syncthreads();
+    }
+    if (logs < logn) {  // last stage radix 2: s = n/2, p = 0, twiddle 1
+      const double2 a0 = xa[b], c0 = xa[b + half], a1 = xa[b + quarter], c1 = xa[b + quarter + half];
+      __syncthreads();
+      xa[b] = make_double2(a0.x + c0.x, a0.y + c0.y);
+      xa[b + half] = make_double2(a0.x - c0.x, a0.y - c0.y);
+      xa[b + quarter] = make_double2(a1.x + c1.x, a1.y + c1.y);
+      xa[b + quarter + half] = make_double2(a1.x - c1.x, a1.y - c1.y);
+      __syncthreads();
+      logs = logn;
+    }
+  } else {
+    const int quarter = n >> 2;
+    for (; logs + 2 <= logn; logs += 2, s <<= 2) {
+      for (int b = threadIdx.x; b < quarter; b += blockDim.x) {
+        double2 y[4];
+        const int o = r4_butterfly(xa, b, quarter, s, logs, tw, inverse, y);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ya[o + k * s] = y[k];
+      }
+      __syncthreads();
+      double2* t = xa; xa = ya; ya = t;
+    }
+  }
+  const int half = n >> 1;
+  for (; logs < logn; ++logs, s <<= 1) {
     const int m = half >> logs;  // half-length of the current sub-transform
     for (int b = threadIdx.x; b < half; b += blockDim.x) {
       const int q = b & (s - 1);
@@ -60,8 +122,6 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2
     }
     __syncthreads();
     double2* t = xa; xa = ya; ya = t;
-    s <<= 1;
-    ++logs;
   }
   for (int i = threadIdx.x; i < n; i += blockDim.x) v[i] = xa[i];
 }

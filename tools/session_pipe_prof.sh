@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pipe -o pipe --output-format csv -- python3 tools/bench_pipeline.py --steps 20 > gpurun_out/prof_pipe.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_pipe -o pipe --output-format csv -- python3 tools/bench_pipeline.py --steps 20 $PIPE_ARGS > gpurun_out/prof_pipe.log 2>&1
 echo "prof rc=$?"
 grep '^{' gpurun_out/prof_pipe.log | cut -c1-400
 python3 - <<'PY'
