@@ -478,10 +478,6 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
     hipLaunchKernelGGL(pack_pairs_kernel, dim3(n / 16, n / 16), dim3(256), 0, c->stream, T, n, (int)s.npad, shear,
                        s.nodes);
     HIPCHK(c, hipGetLastError());
-    const int64_t ghosts = 2 * (int64_t)(s.npad - n) * s.npad;
-    hipLaunchKernelGGL(halo_nodes_kernel, dim3(nblocks(ghosts, 256)), dim3(256), 0, c->stream, s.nodes, n,
-                       (int)s.npad);
-    HIPCHK(c, hipGetLastError());
     if (with_psi) {
       hipLaunchKernelGGL(psi_plane_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T + 3 * nn, s.psi, nn);
       HIPCHK(c, hipGetLastError());
@@ -2144,11 +2140,24 @@ int qg_post(swrt_ctx* c) {
   if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
   // Jacobian and the CFL speed over every layer's u + i v (layer 1, then
   // layer 0: contiguous); the spectrum of J then lands in PT[0, nn)
-  const dim3 jgrid((unsigned)nblocks(q.nn, 256 * kQgMaxPer));
-  hipLaunchKernelGGL(qg_jacobian_max_kernel, jgrid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ,
-                     (const double2*)(q.PT + 2 * nl * q.nn), q.g.shear, q.dmax);
-  HIPCHK(c, hipGetLastError());
-  if ((rc = transform_2d(c, q.PZ, q.PT, n, 1, 0))) return rc;
+  const double2* uvT = q.PT + 2 * nl * q.nn;
+  if (n <= 1024) {
+    // J computed in the load of the forward transform's first pass (same
+    // values, same per-vector FFT as the separate kernel + transform_2d)
+    int logn = 0;
+    while ((1 << logn) < n) ++logn;
+    hipLaunchKernelGGL(fft_jacobian_rows_kernel, dim3((unsigned)n), dim3(n / 4), sizeof(double2) * n, c->stream,
+                       (const double2*)q.PT, nl, n, logn, uvT, q.g.shear, q.dmax, (const double2*)c->tw, q.PZ);
+    HIPCHK(c, hipGetLastError());
+    launch_fft<true>(c, q.PZ, q.PT, n, logn, n, 0);
+    HIPCHK(c, hipGetLastError());
+  } else {
+    const dim3 jgrid((unsigned)nblocks(q.nn, 256 * kQgMaxPer));
+    hipLaunchKernelGGL(qg_jacobian_max_kernel, jgrid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ,
+                       uvT, q.g.shear, q.dmax);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = transform_2d(c, q.PZ, q.PT, n, 1, 0))) return rc;
+  }
   q.post_valid = true;
   return SWRT_OK;
 }
@@ -2388,10 +2397,6 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
     const double2* T = q.PT + (3 * q.g.nl - 1) * q.nn;
     hipLaunchKernelGGL(pack_pairs_kernel, dim3(nx / 16, nx / 16), dim3(256), 0, c->stream, T, (int)nx, (int)s.npad,
                        q.g.shear, s.nodes);
-    HIPCHK(c, hipGetLastError());
-    const int64_t ghosts = 2 * (int64_t)(s.npad - nx) * s.npad;
-    hipLaunchKernelGGL(halo_nodes_kernel, dim3(nblocks(ghosts, 256)), dim3(256), 0, c->stream, s.nodes, (int)nx,
-                       (int)s.npad);
     HIPCHK(c, hipGetLastError());
     s.has_psi = false;
     s.div_free = true;

@@ -50,6 +50,32 @@ __device__ __forceinline__ int r4_butterfly(const double2* xa, int b, int quarte
   return q + 4 * s * p;
 }
 
+// All stages of one length-n vector in ONE LDS buffer xa, blockDim == n/4:
+// each lane holds its butterfly's four values in registers between the read
+// and the write of a stage.  Ends after a __syncthreads (xa holds the result).
+__device__ __forceinline__ void fft_stages_one_buffer(double2* xa, int n, int logn, const double2* tw,
+                                                      int inverse) {
+  const int b = threadIdx.x, quarter = n >> 2, half = n >> 1;
+  int s = 1, logs = 0;
+  for (; logs + 2 <= logn; logs += 2, s <<= 2) {
+    double2 y[4];
+    const int o = r4_butterfly(xa, b, quarter, s, logs, tw, inverse, y);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xa[o + k * s] = y[k];
+    __syncthreads();
+  }
+  if (logs < logn) {  // last stage radix 2: s = n/2, p = 0, twiddle 1
+    const double2 a0 = xa[b], c0 = xa[b + half], a1 = xa[b + quarter], c1 = xa[b + quarter + half];
+    __syncthreads();
+    xa[b] = make_double2(a0.x + c0.x, a0.y + c0.y);
+    xa[b + half] = make_double2(a0.x - c0.x, a0.y - c0.y);
+    xa[b + quarter] = make_double2(a1.x + c1.x, a1.y + c1.y);
+    xa[b + quarter + half] = make_double2(a1.x - c1.x, a1.y - c1.y);
+    __syncthreads();
+  }
+}
+
 // MODE 1: radix-4 stages (+ one radix-2 stage for odd log2 n), ping-pong
 // LDS; 2: the same in one LDS buffer, blockDim = n/4 (n <= 1024).
 template <bool TIN, int MODE>
@@ -72,27 +98,8 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2
   __syncthreads();
   int s = 1, logs = 0;
   if constexpr (MODE == 2) {
-    // one LDS buffer, blockDim == n/4: each lane holds its butterfly's four
-    // values in registers between the read and the write of a stage
-    const int b = threadIdx.x, quarter = n >> 2, half = n >> 1;
-    for (; logs + 2 <= logn; logs += 2, s <<= 2) {
-      double2 y[4];
-      const int o = r4_butterfly(xa, b, quarter, s, logs, tw, inverse, y);
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < 4; ++k) xa[o + k * s] = y[k];
-      __syncthreads();
-    }
-    if (logs < logn) {  // last stage radix 2: s = n/2, p = 0, twiddle 1
-      const double2 a0 = xa[b], c0 = xa[b + half], a1 = xa[b + quarter], c1 = xa[b + quarter + half];
-      __syncthreads();
-      xa[b] = make_double2(a0.x + c0.x, a0.y + c0.y);
-      xa[b + half] = make_double2(a0.x - c0.x, a0.y - c0.y);
-      xa[b + quarter] = make_double2(a1.x + c1.x, a1.y + c1.y);
-      xa[b + quarter + half] = make_double2(a1.x - c1.x, a1.y - c1.y);
-      __syncthreads();
-      logs = logn;
-    }
+    fft_stages_one_buffer(xa, n, logn, tw, inverse);
+    logs = logn;
   } else {
     const int quarter = n >> 2;
     for (; logs + 2 <= logn; logs += 2, s <<= 2) {
@@ -126,6 +133,47 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2
   for (int i = threadIdx.x; i < n; i += blockDim.x) v[i] = xa[i];
 }
 
+
+// The forward transform of J (qgsw_raytrace.m:282-283 / qg2layersw_raytrace.m:
+// 313-315) with the Jacobian computed in its first pass's load: vector y
+// (blockIdx.x) of J1 + i J2, J_l = psix.*qy - psiy.*qx from the inverse
+// transforms T[2l] = psi_x + i psi_y, T[2l+1] = q_x + i q_y (layout [x + n*y]),
+// transformed along x into Zj's row y — the values qg_jacobian_max_kernel
+// writes, through the same per-vector FFT.  Also the CFL max of
+// (u + shear)^2 + v^2 over the nl u+iv planes at uv (one atomic per block).
+// blockDim == n/4 (n <= 1024).
+__global__ void __launch_bounds__(256) fft_jacobian_rows_kernel(const double2* T, int nl, int n, int logn,
+                                                                const double2* uv, double shear,
+                                                                unsigned long long* dmax, const double2* tw,
+                                                                double2* Zj) {
+  extern __shared__ double2 sbuf[];
+  __shared__ unsigned long long bmax;  // bits of a non-negative double: integer max == double max
+  if (threadIdx.x == 0) bmax = 0ull;
+  __syncthreads();
+  const int64_t nn = (int64_t)n * n;
+  const int64_t row = (int64_t)blockIdx.x * n;
+  double m = 0.0;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) {
+    const int64_t i = row + j;
+    double J[2] = {0.0, 0.0};
+    for (int l = 0; l < nl; ++l) {
+      const double2 P = T[(2 * l) * nn + i], Q = T[(2 * l + 1) * nn + i];
+      J[l] = P.x * Q.y - P.y * Q.x;
+    }
+    sbuf[j] = make_double2(J[0], J[1]);
+    for (int l = 0; l < nl; ++l) {
+      const double2 z = uv[l * nn + i];
+      const double u = z.x + shear, v = z.y;
+      const double s2 = u * u + v * v;
+      m = s2 > m ? s2 : m;
+    }
+  }
+  atomicMax(&bmax, (unsigned long long)__double_as_longlong(m));  // LDS atomic
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(dmax, bmax);
+  fft_stages_one_buffer(sbuf, n, logn, tw, 0);
+  for (int j = threadIdx.x; j < n; j += blockDim.x) Zj[row + j] = sbuf[j];
+}
 
 // out[c + n*r] = in[r + n*c] for batch of nb n x n complex matrices.
 __global__ void transpose_kernel(const double2* in, double2* out, int n) {
@@ -281,7 +329,10 @@ __global__ void fulspec_kernel(const double2* fk, int n, double2* Z, int sx, int
 // divergence-free, and grid_U.m:8-9's separate transform of i ky vk equals
 // -(i kx uk) up to the transform's roundoff.  The exact identity lets the
 // packet kernels carry five stencil sums instead of six (swrt_tile.hpp).
-// Ghost nodes are filled by halo_nodes_kernel afterwards.
+// The periodic ghost records (2 below, npad - n - 2 above in each direction,
+// kPadTot = 5: 2 + 3) are written by the same thread as copies of
+// their interior node, so no halo pass follows.  A node x sits at padded
+// row x + 2, and at x + 2 - n (x >= n - 2) and x + 2 + n (x < npad - n - 2).
 __global__ void __launch_bounds__(256) pack_pairs_kernel(const double2* T, int n, int npad, double shear,
                                                          double* nodes) {
   __shared__ double2 tile[3][16][17];
@@ -293,40 +344,20 @@ __global__ void __launch_bounds__(256) pack_pairs_kernel(const double2* T, int n
   __syncthreads();
   // write: thread (tx, ty) -> node x = x0 + ty, y = y0 + tx
   const double2 a = tile[0][tx][ty], b = tile[1][tx][ty], c = tile[2][tx][ty];
-  double* dst = nodes + ((int64_t)(x0 + ty + 2) * npad + (y0 + tx + 2)) * 6;
-  dst[0] = a.x + shear;
-  dst[1] = a.y;
-  dst[2] = b.x;
-  dst[3] = b.y;
-  dst[4] = c.x;
-  dst[5] = -b.x;
-}
-
-// Periodic ghost records of the padded node array (2 below, 3 above in each
-// direction) copied from their interior images.
-__global__ void halo_nodes_kernel(double* nodes, int nx, int npad) {
-  const int nghost_rows = npad - nx;  // 5 full padded rows/columns
-  const int64_t per = (int64_t)nghost_rows * npad;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= 2 * per) return;
-  int ip, jp;
-  if (idx < per) {  // ghost rows (all columns)
-    const int g = (int)idx / npad;
-    jp = (int)idx % npad;
-    ip = g < 2 ? g : nx + g;  // 0,1 and nx+2..nx+4
-  } else {          // ghost columns of the interior rows
-    const int64_t j = idx - per;
-    const int g = (int)(j / npad);
-    ip = (int)(j % npad);
-    jp = g < 2 ? g : nx + g;
-    if (ip < 2 || ip >= nx + 2) return;  // corners done by the row part
-  }
-  int ig = ((ip - 2) % nx + nx) % nx, jg = ((jp - 2) % nx + nx) % nx;
-  if ((ip >= 2 && ip < nx + 2) && (jp >= 2 && jp < nx + 2)) return;
-  const double* src = nodes + ((int64_t)(ig + 2) * npad + (jg + 2)) * 6;
-  double* dst = nodes + ((int64_t)ip * npad + jp) * 6;
+  const double rec[6] = {a.x + shear, a.y, b.x, b.y, c.x, -b.x};
+  const int x = x0 + ty, y = y0 + tx, hi = npad - n - 2;
+  // padded rows/columns holding node x (y): x + 2, and its ghost images
+  const int px[3] = {x + 2, x >= n - 2 ? x + 2 - n : -1, x < hi ? x + 2 + n : -1};
+  const int py[3] = {y + 2, y >= n - 2 ? y + 2 - n : -1, y < hi ? y + 2 + n : -1};
+  for (int i = 0; i < 3; ++i) {
+    if (px[i] < 0) continue;
+    for (int j = 0; j < 3; ++j) {
+      if (py[j] < 0) continue;
+      double* dst = nodes + ((int64_t)px[i] * npad + py[j]) * 6;
 #pragma unroll
-  for (int f = 0; f < 6; ++f) dst[f] = src[f];
+      for (int f = 0; f < 6; ++f) dst[f] = rec[f];
+    }
+  }
 }
 
 // psi plane of the packed transform T3 (layout [x + n*y]).

@@ -171,6 +171,27 @@ def test_qg_snapshot_is_grid_U(ctx, which):
         assert _rel(got[i], np.asarray(flow[name]).ravel(order="F")) < 1e-12
 
 
+@pytest.mark.parametrize("nx", [16, 64])
+def test_qk_snapshot_ghost_records(ctx, nx):
+    """pack_pairs_kernel writes the periodic ghost records itself: the node
+    array of swrt_set_field_qk evaluates, at points in every edge and corner
+    cell, bit for bit like the same planes packed by swrt_set_field_grid."""
+    L = 20.0
+    rng = np.random.default_rng(4)
+    qk = _two_layer_case(nx)[:, :, 0]
+    ctx.set_field_qk(0, qk, nx, L, 3.0, 0.5, 2 * np.pi / L, 2 * nx)
+    ctx.set_field_grid(1, ctx.get_field_grid(0, nx), nx, L, 2 * nx)
+    dx = L / nx
+    edge = np.concatenate([np.arange(-3, 4) * dx, L / 2 + np.arange(-4, 4) * dx, -L / 2 + np.arange(-4, 4) * dx])
+    X, Y = np.meshgrid(edge, edge)
+    x = np.concatenate([X.ravel(), rng.uniform(-L, L, 2000)]) + 1e-3 * dx
+    y = np.concatenate([Y.ravel(), rng.uniform(-2 * L, 2 * L, 2000)]) - 2e-3 * dx
+    a = ctx.eval(x, y, nslots=1, bump=orc.BUMP_QG)
+    ctx.swap_slots(0, 1)
+    b = ctx.eval(x, y, nslots=1, bump=orc.BUMP_QG)
+    np.testing.assert_array_equal(a, b)
+
+
 def test_swap_slots(ctx):
     nx = 32
     a = np.random.default_rng(1).random((6, nx * nx))
