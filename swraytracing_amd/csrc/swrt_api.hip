@@ -876,11 +876,11 @@ int swrt_create(int device, swrt_ctx** out) {
     return SWRT_ERR_HIP;
   }
   // the QG stream at the highest priority: its short dependent kernels are
-  // dispatched ahead of the waiting workgroups of a packet launch
+  // dispatched ahead of the waiting workgroups of a packet launch (measured
+  // neither faster nor slower than the default priority)
   int prio_least = 0, prio_greatest = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-  const char* qp = std::getenv("SWRT_QG_PRIO");
-  const int prio = (qp && std::atoi(qp) == 0) ? prio_least : prio_greatest;
+  const int prio = prio_greatest;
   bool ok = hipStreamCreateWithPriority(&c->qstream, hipStreamNonBlocking, prio) == hipSuccess;
   for (Slot* s = c->slot; s != c->slot + SWRT_MAX_SLOTS; ++s)
     ok = ok && hipEventCreateWithFlags(&s->uev, hipEventDisableTiming) == hipSuccess &&
