@@ -47,6 +47,7 @@ struct Ode23Args {
   double thr;        // AbsTol / RelTol
   double bump;
   unsigned long long* dmax;
+  unsigned long long* dmax_clear;  // the other max slot, zeroed for the next call (NULL: none)
   const int* order;  // tile kernel: binned slots in in-tile cell order (NULL: slot order)
   int split;         // tile kernel: half-tile workgroups at the end of each XCD band
 };
@@ -77,6 +78,7 @@ __device__ __forceinline__ void block_max_to(double m, unsigned long long* out) 
 
 template <int STAGE>
 __global__ void __launch_bounds__(256) ode23_stage_kernel(Ode23Args a) {
+  if (a.dmax_clear && blockIdx.x == 0 && threadIdx.x == 0) *a.dmax_clear = 0ull;
   const int64_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int64_t n = a.n;
   double m = 0.0;
@@ -234,6 +236,7 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
   constexpr int NCH = TWO ? (V5 ? 5 : 6) : 3;
   __shared__ double2 win[NCH * WNP];
   __shared__ double red[NT / 64];
+  if (a.dmax_clear && blockIdx.x == 0 && threadIdx.x == 0) *a.dmax_clear = 0ull;
   int pbeg, pend;
   const int tile = wg_work_range(starts, nullptr, a.split, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
