@@ -2135,14 +2135,31 @@ int qg_post(swrt_ctx* c) {
   // Jacobian inputs | layer-1 u+iv | swrt_qg_snapshot(which 0, layer 0)'s
   // grid_U spectra (grid_U.m inversion, ky-fastest half plane) — one launch
   double2* uv = q.PZ + 2 * nl * q.nn;
-  if (nl == 2)
-    hipLaunchKernelGGL(qg_post_spectra_kernel<2>, grid, block, 0, c->stream, (const double2*)q.qk, q.g, q.nhalf,
-                       q.PZ, uv, uv + q.nn, q.dmax);
-  else
-    hipLaunchKernelGGL(qg_post_spectra_kernel<1>, grid, block, 0, c->stream, (const double2*)q.qk, q.g, q.nhalf,
-                       q.PZ, uv, uv, q.dmax);
-  HIPCHK(c, hipGetLastError());
-  if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
+  if (nb * n / 4 <= 1024) {
+    // spectra fused into the first inverse pass (qg_post_rows_kernel), then
+    // the column pass — the same values as the three launches below
+    int logn = 0;
+    while ((1 << logn) < n) ++logn;
+    const size_t lds = sizeof(double2) * nb * n;
+    if (nl == 2)
+      hipLaunchKernelGGL(qg_post_rows_kernel<2>, dim3((unsigned)n), dim3(nb * n / 4), lds, c->stream,
+                         (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
+    else
+      hipLaunchKernelGGL(qg_post_rows_kernel<1>, dim3((unsigned)n), dim3(nb * n / 4), lds, c->stream,
+                         (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
+    HIPCHK(c, hipGetLastError());
+    launch_fft<true>(c, q.PZ, q.PT, n, logn, nb * n, 1);
+    HIPCHK(c, hipGetLastError());
+  } else {
+    if (nl == 2)
+      hipLaunchKernelGGL(qg_post_spectra_kernel<2>, grid, block, 0, c->stream, (const double2*)q.qk, q.g, q.nhalf,
+                         q.PZ, uv, uv + q.nn, q.dmax);
+    else
+      hipLaunchKernelGGL(qg_post_spectra_kernel<1>, grid, block, 0, c->stream, (const double2*)q.qk, q.g, q.nhalf,
+                         q.PZ, uv, uv, q.dmax);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
+  }
   // Jacobian and the CFL speed over every layer's u + i v (layer 1, then
   // layer 0: contiguous); the spectrum of J then lands in PT[0, nn)
   const double2* uvT = q.PT + 2 * nl * q.nn;

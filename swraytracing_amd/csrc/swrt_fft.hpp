@@ -52,10 +52,12 @@ __device__ __forceinline__ int r4_butterfly(const double2* xa, int b, int quarte
 
 // All stages of one length-n vector in ONE LDS buffer xa, blockDim == n/4:
 // each lane holds its butterfly's four values in registers between the read
-// and the write of a stage.  Ends after a __syncthreads (xa holds the result).
-__device__ __forceinline__ void fft_stages_one_buffer(double2* xa, int n, int logn, const double2* tw,
+// and the write of a stage; b = the lane's butterfly (0..n/4-1).  The
+// barriers are the whole workgroup's: several vectors of one length may run
+// side by side.  Ends after a __syncthreads (xa holds the result).
+__device__ __forceinline__ void fft_stages_one_buffer(double2* xa, int b, int n, int logn, const double2* tw,
                                                       int inverse) {
-  const int b = threadIdx.x, quarter = n >> 2, half = n >> 1;
+  const int quarter = n >> 2, half = n >> 1;
   int s = 1, logs = 0;
   for (; logs + 2 <= logn; logs += 2, s <<= 2) {
     double2 y[4];
@@ -98,7 +100,7 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2
   __syncthreads();
   int s = 1, logs = 0;
   if constexpr (MODE == 2) {
-    fft_stages_one_buffer(xa, n, logn, tw, inverse);
+    fft_stages_one_buffer(xa, threadIdx.x, n, logn, tw, inverse);
     logs = logn;
   } else {
     const int quarter = n >> 2;
@@ -171,7 +173,7 @@ __global__ void __launch_bounds__(256) fft_jacobian_rows_kernel(const double2* T
   atomicMax(&bmax, (unsigned long long)__double_as_longlong(m));  // LDS atomic
   __syncthreads();
   if (threadIdx.x == 0) atomicMax(dmax, bmax);
-  fft_stages_one_buffer(sbuf, n, logn, tw, 0);
+  fft_stages_one_buffer(sbuf, threadIdx.x, n, logn, tw, 0);
   for (int j = threadIdx.x; j < n; j += blockDim.x) Zj[row + j] = sbuf[j];
 }
 
@@ -227,8 +229,25 @@ __device__ __forceinline__ double2 mul_mik(double k, double2 z) { return make_do
 // mode 0: psik = fk (SpectralScheme path); mode 1: psik = -qk./(K_d2 + K2).
 // The half plane is read at fk[(kx + kmax)*sx + ky*sy]: (1, 2kmax+1) for the
 // host's column-major layout, (kmax+1, 1) for the QG state's ky-fastest one.
-__device__ __forceinline__ void spectra_at(int64_t idx, const double2* fk, int n, int mode, double K_d2, double kscale,
-                               int with_psi, double2* Z, int sx, int sy) {
+// Where the spectra element functions put plane `pl` of full-spectrum index
+// idx: an n*n block per plane in global memory, or one row per plane in LDS
+// (the row-fused first FFT pass) — same values either way.
+struct GlobalPlanes {
+  double2* Z;
+  int64_t nn;
+  __device__ __forceinline__ void operator()(int pl, int64_t idx, double2 v) const { Z[pl * nn + idx] = v; }
+};
+struct LdsRowPlanes {
+  double2* row;  // plane pl's row at row + pl*n
+  int n;
+  __device__ __forceinline__ void operator()(int pl, int64_t idx, double2 v) const {
+    row[pl * n + ((int)idx & (n - 1))] = v;
+  }
+};
+
+template <class Sink>
+__device__ __forceinline__ void spectra_to(int64_t idx, const double2* fk, int n, int mode, double K_d2, double kscale,
+                                           int with_psi, Sink out, int sx, int sy) {
   const int64_t nn = (int64_t)n * n;
   if (idx >= nn) return;
   const int sh_ = __ffs(n) - 1;  // n is a power of two
@@ -271,10 +290,14 @@ __device__ __forceinline__ void spectra_at(int64_t idx, const double2* fk, int n
     z[2] = make_double2(a[4].x - a[5].y, a[4].y + a[5].x);
     z[3] = a[6];
   }
-  Z[idx] = z[0];
-  Z[nn + idx] = z[1];
-  Z[2 * nn + idx] = z[2];
-  if (with_psi) Z[3 * nn + idx] = z[3];
+  out(0, idx, z[0]);
+  out(1, idx, z[1]);
+  out(2, idx, z[2]);
+  if (with_psi) out(3, idx, z[3]);
+}
+__device__ __forceinline__ void spectra_at(int64_t idx, const double2* fk, int n, int mode, double K_d2, double kscale,
+                                           int with_psi, double2* Z, int sx, int sy) {
+  spectra_to(idx, fk, n, mode, K_d2, kscale, with_psi, GlobalPlanes{Z, (int64_t)n * n}, sx, sy);
 }
 
 __global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, double kscale,

@@ -90,8 +90,8 @@ __device__ __forceinline__ void qg2_B(double K2, double K_d2, double& b11, doubl
 // contiguous) and layer l, Z[2l] = psi_x + i psi_y, Z[2l+1] = q_x + i q_y with
 // the Hermitian completion of fulspec.m (kx < 0 on ky = 0 and ky < 0 from
 // their conjugate partners; Nyquist row/column zero).
-template <int NL>
-__device__ __forceinline__ void qg_jac_spectra_at(int64_t idx, const double2* qk, QGDev g, double2* Z) {
+template <int NL, class Sink>
+__device__ __forceinline__ void qg_jac_spectra_to(int64_t idx, const double2* qk, QGDev g, Sink out) {
   const int n = g.n;
   const int64_t nn = (int64_t)n * n;
   if (idx >= nn) return;
@@ -126,9 +126,13 @@ __device__ __forceinline__ void qg_jac_spectra_at(int64_t idx, const double2* qk
     cd px = ik(kxs, ps[l]), py = ik(kys, ps[l]), qx = ik(kxs, q[l]), qy = ik(kys, q[l]);
     if (cj) { px.y = -px.y; py.y = -py.y; qx.y = -qx.y; qy.y = -qy.y; }
     if (!inband) px = py = qx = qy = cmk(0.0, 0.0);
-    Z[(2 * l) * nn + idx] = pack2(px, py);
-    Z[(2 * l + 1) * nn + idx] = pack2(qx, qy);
+    out(2 * l, idx, pack2(px, py));
+    out(2 * l + 1, idx, pack2(qx, qy));
   }
+}
+template <int NL>
+__device__ __forceinline__ void qg_jac_spectra_at(int64_t idx, const double2* qk, QGDev g, double2* Z) {
+  qg_jac_spectra_to<NL>(idx, qk, g, GlobalPlanes{Z, (int64_t)g.n * g.n});
 }
 
 template <int NL>
@@ -316,8 +320,8 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
 
 // u + i v per layer from grid_U's inversion psik = -qk./(K_d2+K2) (grid_U.m:2-6),
 // for the CFL speed (qg2layersw_raytrace.m:156-158); layout [c + n*r].
-template <int NL>
-__device__ __forceinline__ void qg_vel_spectra_at(int64_t idx, const double2* qk, QGDev g, double2* Z) {
+template <int NL, class Sink>
+__device__ __forceinline__ void qg_vel_spectra_to(int64_t idx, const double2* qk, QGDev g, Sink out) {
   const int n = g.n;
   const int64_t nn = (int64_t)n * n;
   if (idx >= nn) return;
@@ -343,8 +347,12 @@ __device__ __forceinline__ void qg_vel_spectra_at(int64_t idx, const double2* qk
       if (hx == 0 && hy == 0) { u.y = 0.0; v.y = 0.0; }
       if (cj) { u.y = -u.y; v.y = -v.y; }
     }
-    Z[l * nn + idx] = pack2(u, v);
+    out(l, idx, pack2(u, v));
   }
+}
+template <int NL>
+__device__ __forceinline__ void qg_vel_spectra_at(int64_t idx, const double2* qk, QGDev g, double2* Z) {
+  qg_vel_spectra_to<NL>(idx, qk, g, GlobalPlanes{Z, (int64_t)g.n * g.n});
 }
 
 template <int NL>
@@ -386,6 +394,39 @@ __global__ void __launch_bounds__(256) qg_post_spectra_kernel(const double2* qk,
   qg_jac_spectra_at<NL>(idx, qk, g, Zjac);
   if constexpr (NL == 2) qg_vel_spectra_at<1>(idx, qk + nhalf, g, Zuv1);
   spectra_at(idx, qk, g.n, 1, g.K_d2, g.kscale, 0, Zsnap, g.n / 2, 1);
+}
+
+// qg_post_spectra_kernel fused with the first pass of the batched inverse
+// 2-D FFT: workgroup r builds row r (ky contiguous) of every post-step plane
+// in LDS with the same element functions, runs the NB inverse row FFTs side
+// by side (n/4 lanes each, fft_stages_one_buffer) and writes the pass's
+// output (plane t, row r at out[t*n*n + r*n]) — bit for bit what the
+// spectra launch + in-place pass write, without the planes' round trip
+// through memory.  blockDim = NB*n/4 <= 1024, dynamic LDS NB*n double2.
+template <int NL>
+__global__ void __launch_bounds__(1024) qg_post_rows_kernel(const double2* qk, QGDev g, int64_t nhalf, int logn,
+                                                            const double2* tw, double2* out,
+                                                            unsigned long long* dmax) {
+  constexpr int NB = 2 * NL + (NL - 1) + 3;
+  extern __shared__ double2 rows[];
+  const int n = g.n;
+  const int64_t nn = (int64_t)n * n;
+  const int r = blockIdx.x;
+  if (r == 0 && threadIdx.x == 0) *dmax = 0ull;
+  for (int e = threadIdx.x; e < 2 * n; e += blockDim.x) {
+    const int64_t idx = (int64_t)(e < n ? e : e - n) + (int64_t)n * r;
+    if (e < n) {
+      qg_jac_spectra_to<NL>(idx, qk, g, LdsRowPlanes{rows, n});
+    } else {
+      if constexpr (NL == 2) qg_vel_spectra_to<1>(idx, qk + nhalf, g, LdsRowPlanes{rows + 2 * NL * n, n});
+      spectra_to(idx, qk, n, 1, g.K_d2, g.kscale, 0, LdsRowPlanes{rows + (2 * NL + NL - 1) * n, n}, n / 2, 1);
+    }
+  }
+  __syncthreads();
+  const int q = n >> 2;
+  fft_stages_one_buffer(rows + (threadIdx.x / q) * n, threadIdx.x % q, n, logn, tw, 1);
+  for (int e = threadIdx.x; e < NB * n; e += blockDim.x)
+    out[(int64_t)(e / n) * nn + (int64_t)r * n + (e % n)] = rows[e];
 }
 
 // qg_jacobian_kernel + qg_max_speed2_kernel over the same grid points:
