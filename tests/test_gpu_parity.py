@@ -165,8 +165,10 @@ def _close_field(a, b, rtol=FIELD_RTOL):
     assert err <= rtol, f"relative field error {err:.3e} > {rtol:.1e}"
 
 
-@pytest.mark.parametrize("nx", [32, 64, 256, 512])
+@pytest.mark.parametrize("nx", [8, 16, 32, 64, 256, 512, 1024, 2048, 4096])
 def test_g2k_k2g_vs_numpy(ctx, nx):
+    """Every FFT shape: one-buffer radix 4 (n <= 1024, odd and even log2 n),
+    ping-pong radix 4 (2048, 4096)."""
     X, Y = periodic_grid(nx)
     rng = np.random.default_rng(nx)
     f = np.zeros_like(X)

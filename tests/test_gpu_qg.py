@@ -340,10 +340,13 @@ def test_qg_stream_overlap_and_fusion_bit_identical(ctx, tmp_path, layers):
         ctx.qg_set_fused(True)
 
 
-def test_qg_fused_speed_and_snapshot_match_unfused(ctx):
+@pytest.mark.parametrize("nx", [64, 512, 1024, 2048])
+def test_qg_fused_speed_and_snapshot_match_unfused(ctx, nx):
     """U0 and the layer-0 snapshot of the current qk from the post-step
-    transforms equal the separate calls' bit for bit (2 layers, AB3 steps)."""
-    nx = 64
+    transforms equal the separate calls' bit for bit (2 layers, AB3 steps).
+    The sizes cover every post-step shape: spectra fused into the row pass
+    (<= 512), the Jacobian fused into the forward row pass (<= 1024), the
+    one-buffer FFT (<= 1024) and the ping-pong FFT (2048)."""
     out = {}
     try:
         for fused in (False, True):
