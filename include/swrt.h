@@ -303,6 +303,17 @@ int swrt_ode23_f1(swrt_ctx* ctx, double t, double tmax, double f, double Cg, int
 int swrt_ode23_attempt(swrt_ctx* ctx, double t, double h, double tnew, double tmax, double f, double Cg,
                        int nslots, double thr, double bump, double* err_raw_out);
 int swrt_ode23_accept(swrt_ctx* ctx);
+/* [~, y] = ode23(odefun, [t0 tfinal], y) for the device-resident packets with
+ * MATLAB's controller (RelTol rtol, AbsTol atol, MaxStep 0.1*|tfinal - t0|,
+ * max-norm error, initial-step heuristic, step update) in the library: the
+ * f1 / attempt / accept sequence above without a host interpreter between
+ * attempts.  Writes the accepted times (t0 first) to ts_out[0 .. *nts_out)
+ * (SWRT_ERR_ARG beyond ts_cap) and {steps, failed, attempts} to stats3_out
+ * (may be NULL).  Single rank: a sharded ensemble needs the error norm's
+ * allreduce between attempts (swraytracing_amd.integrate.ode23_packets). */
+int swrt_ode23_run(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
+                   double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
+                   int64_t* stats3_out);
 
 /* ---------------------------------------------------------------------------
  * QG PDE stepper: the snapshots' producer, device-resident

@@ -86,6 +86,8 @@ SIGNATURES = {
     "swrt_ode23_f1": (_INT, [_VP, _D, _D, _D, _D, _INT, _D, _D, ctypes.POINTER(_D)]),
     "swrt_ode23_attempt": (_INT, [_VP, _D, _D, _D, _D, _D, _D, _INT, _D, _D, ctypes.POINTER(_D)]),
     "swrt_ode23_accept": (_INT, [_VP]),
+    "swrt_ode23_run": (_INT, [_VP, _D, _D, _D, _D, _D, _INT, _D, _D, _D, _P, _I, ctypes.POINTER(_I),
+                              ctypes.POINTER(_I)]),
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_set_graphs": (_INT, [_VP, _INT]),
@@ -423,6 +425,17 @@ class Context:
 
     def ode23_accept(self):
         self._chk(self._L.swrt_ode23_accept(self._h), "swrt_ode23_accept")
+
+    def ode23_run(self, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_cap=100_000):
+        """swrt_ode23_run: the whole ode23 call with the controller in the
+        library.  Returns (accepted times, {steps, failed, attempts})."""
+        ts = np.empty(ts_cap)
+        nts = _I()
+        st = (_I * 3)()
+        self._chk(self._L.swrt_ode23_run(self._h, float(t0), float(tfinal), float(tmax), float(f), float(Cg),
+                                         int(nslots), float(rtol), float(atol), float(bump), _p(ts), int(ts_cap),
+                                         ctypes.byref(nts), st), "swrt_ode23_run")
+        return ts[:nts.value].copy(), {"steps": st[0], "failed": st[1], "attempts": st[2]}
 
     # ---- QG PDE stepper (swrt_qg_*) ---------------------------------------
     def qg_init(self, params: QGParams, nx, qk):

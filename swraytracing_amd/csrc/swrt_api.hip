@@ -2632,6 +2632,95 @@ int swrt_ode23_accept(swrt_ctx* c) {
   return SWRT_OK;
 }
 
+// MATLAB ode23's step-size controller (the restatement of
+// swraytracing_amd/integrate.py ode23_packets, operation for operation:
+// std::pow is the C pow() Python's float ** calls, min/max keep Python's
+// tie order) around the device stages, without a host interpreter between
+// attempts.  Single-rank: the sharded form needs the error norm's allreduce
+// and stays in Python.
+namespace {
+double np_spacing(double t) {  // numpy.spacing
+  const double a = std::fabs(t);
+  const double d = std::nextafter(a, INFINITY) - a;
+  return std::signbit(t) ? -d : d;
+}
+}  // namespace
+
+int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
+                   double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
+                   int64_t* stats3_out) {
+  if (!c) return SWRT_ERR_ARG;
+  if (!ts_out || ts_cap < 1 || !nts_out) return fail(c, SWRT_ERR_ARG, "ts_out / ts_cap / nts_out");
+  const double tdir = std::copysign(1.0, tfinal - t0);
+  const double pw = 1.0 / 3.0;
+  rtol = std::max(rtol, 100 * 2.220446049250313e-16);
+  const double thr = atol / rtol;
+  const double htspan = std::fabs(tfinal - t0);
+  const double hmax = 0.1 * htspan;
+  double t = t0;
+  double raw = 0.0;
+  int rc;
+  if ((rc = swrt_ode23_f1(c, t, tmax, f, Cg, nslots, thr, bump, &raw))) return rc;
+  const double rh = raw / (0.8 * std::pow(rtol, pw));
+  double absh = std::min(hmax, htspan);
+  if (absh * rh > 1) absh = 1.0 / rh;
+  absh = std::max(absh, 16 * np_spacing(t));
+  int64_t nts = 0;
+  ts_out[nts++] = t;
+  bool done = false;
+  int64_t nfailed = 0, attempts = 0;
+  while (!done) {
+    const double hmin = 16 * np_spacing(t);
+    absh = std::min(hmax, std::max(hmin, absh));
+    double h = tdir * absh;
+    if (1.1 * absh >= std::fabs(tfinal - t)) {
+      h = tfinal - t;
+      absh = std::fabs(h);
+      done = true;
+    }
+    bool nofailed = true;
+    double tnew, err;
+    while (true) {
+      tnew = t + h * 1.0;
+      if (done) tnew = tfinal;
+      ++attempts;
+      if ((rc = swrt_ode23_attempt(c, t, h, tnew, tmax, f, Cg, nslots, thr, bump, &raw))) return rc;
+      err = absh * raw;
+      h = tnew - t;
+      if (err > rtol) {
+        ++nfailed;
+        if (absh <= hmin) return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
+        if (nofailed) {
+          nofailed = false;
+          absh = std::max(hmin, absh * std::max(0.5, 0.8 * std::pow(rtol / err, pw)));
+        } else {
+          absh = std::max(hmin, 0.5 * absh);
+        }
+        h = tdir * absh;
+        done = false;
+      } else {
+        break;
+      }
+    }
+    if ((rc = swrt_ode23_accept(c))) return rc;
+    t = tnew;
+    if (nts >= ts_cap) return fail(c, SWRT_ERR_ARG, "ode23: more steps than ts_cap");
+    ts_out[nts++] = t;
+    if (done) break;
+    if (nofailed) {
+      const double temp = 1.25 * std::pow(err / rtol, pw);
+      absh = temp > 0.2 ? absh / temp : 5.0 * absh;
+    }
+  }
+  *nts_out = nts;
+  if (stats3_out) {
+    stats3_out[0] = nts - 1;
+    stats3_out[1] = nfailed;
+    stats3_out[2] = attempts;
+  }
+  return SWRT_OK;
+}
+
 #ifdef SWRT_PHASE_TIMING
 // diagnostic build only (not in include/swrt.h): copy out / clear the tile
 // kernel's per-workgroup phase stamps (8 u64 per tile).

@@ -1,4 +1,5 @@
-"""GPU ode23 (swrt_ode23_* stages + the host controller ode23_packets) against
+"""GPU ode23 (swrt_ode23_* stages + the controller, in the library (swrt_ode23_run)
+or in Python (ode23_packets)) against
 the oracle's restatement of MATLAB ode23 with the drivers' odefun
 (qgsw_raytrace.m:143-150,259-265).  Every stage is the same IEEE-754 op
 sequence as the oracle (same stencil code, correctly rounded sqrt/division,
@@ -18,8 +19,9 @@ def _y0(x, k):
     return np.concatenate([x[:, 0], x[:, 1], k[:, 0], k[:, 1]])
 
 
+@pytest.mark.parametrize("controller", ["library", "python"])
 @pytest.mark.parametrize("rebin", [0, 4])
-def test_ode23_packets_bitexact(ctx, qg_case, rebin):
+def test_ode23_packets_bitexact(ctx, qg_case, rebin, controller):
     c = qg_case
     nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
     flow1 = c["flow"]
@@ -32,7 +34,7 @@ def test_ode23_packets_bitexact(ctx, qg_case, rebin):
     try:
         ctx.packets_set(x, k)
         st = {}
-        ts = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, stats=st)
+        ts = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, stats=st, controller=controller)
         xg, kg = ctx.packets_get()
     finally:
         ctx.set_locality(4, 0)
@@ -49,8 +51,10 @@ def test_ode23_packets_bitexact(ctx, qg_case, rebin):
     np.testing.assert_array_equal(kg[:, 1], yo[3 * n:])
 
 
-def test_ode23_rejections_happen_and_match(ctx, qg_case):
-    """A loose start (tiny rtol) forces rejected steps; still bit-identical."""
+@pytest.mark.parametrize("controller", ["library", "python"])
+def test_ode23_rejections_happen_and_match(ctx, qg_case, controller):
+    """A loose start (tiny rtol) forces rejected steps; still bit-identical
+    (the controller in the library, swrt_ode23_run, or the Python loop)."""
     c = qg_case
     nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
     flow1 = c["flow"]
@@ -61,7 +65,7 @@ def test_ode23_rejections_happen_and_match(ctx, qg_case):
     tmax = 60 * c["dt"]
     ctx.packets_set(x, k)
     st = {}
-    ts = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, rtol=1e-6, atol=1e-9, stats=st)
+    ts = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, rtol=1e-6, atol=1e-9, stats=st, controller=controller)
     xg, kg = ctx.packets_get()
     so = {}
     to, yo = orc.ode23(orc.raytracing_rhs(flow1, flow2, f, Cg, tmax, L / nx), [0.0, tmax], _y0(x, k),

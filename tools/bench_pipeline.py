@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--nsub", type=int, default=5, help="leapfrog substeps per PDE interval (5: 0.05*dx/U0 each)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ode23", action="store_true", help="also time the drivers' ode23 over one PDE interval")
+    ap.add_argument("--ode23-controller", default=None, choices=["library", "python"],
+                    help="ode23 step-size controller: in the C library (default) or the Python loop (A/B)")
     ap.add_argument("--qg-graphs", action="store_true", help="hipGraph replay of the QG step (A/B; default off)")
     ap.add_argument("--one-stream", action="store_true", help="QG PDE on the packet stream (A/B)")
     ap.add_argument("--no-fused", action="store_true", help="separate transforms per QG call (A/B)")
@@ -100,13 +102,13 @@ def main():
     ode = None
     if args.ode23:
         # one warm-up interval (first-use allocations), then the mean of 5
-        ens.advance_ode23(state["dt"])
+        ens.advance_ode23(state["dt"], controller=args.ode23_controller)
         st = {}
         reps = 5
         ctx.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            ens.advance_ode23(state["dt"], stats=st)
+            ens.advance_ode23(state["dt"], stats=st, controller=args.ode23_controller)
         ctx.synchronize()
         ms = (time.perf_counter() - t0) * 1e3 / reps
         ode = {"interval_ms": ms, **st, "rhs_evals": 1 + 3 * st["attempts"],
