@@ -103,7 +103,8 @@ struct QGState {
   // 2-D FFT, computed once per qk on first use
   double2* PZ = nullptr;
   double2* PT = nullptr;
-  bool post_valid = false;
+  bool post_valid = false;      // both phases of qg_post done for the current qk
+  bool post_inv_valid = false;  // its first phase (the inverse transforms)
   double exp_dt = -1.0;        // dt of the current E1/E2
   // replayable AB3 steps (hipGraph), one per qk buffer parity, for one dt
   hipGraphExec_t gexec[2] = {nullptr, nullptr};
@@ -1966,6 +1967,7 @@ int swrt_qg_set_fused(swrt_ctx* c, int on) {
   if (rc) return rc;
   c->qg_fused = on != 0;
   c->qg.post_valid = false;
+  c->qg.post_inv_valid = false;
   return SWRT_OK;
 }
 
@@ -2119,10 +2121,14 @@ int qg_step_launches(swrt_ctx* c, double dt, int abstep) {
 
 // Post-step transforms of the current qk (fused mode), see QGState::PZ.
 // Every transform is the one the unfused calls make (same spectra kernels,
-// same per-vector FFT), so results are bit-identical to them.
-int qg_post(swrt_ctx* c) {
+// same per-vector FFT), so results are bit-identical to them.  Two phases:
+// the inverse transforms (all a snapshot needs) and the Jacobian + CFL max
+// + forward transform of J (what the speed and the next step need), so a
+// snapshot's pack — and the packet launch waiting for it — need not queue
+// behind the second phase.
+int qg_post_inverse(swrt_ctx* c) {
   QGState& q = c->qg;
-  if (q.post_valid) return SWRT_OK;
+  if (q.post_inv_valid) return SWRT_OK;
   const int n = q.g.n, nl = q.g.nl;
   const int nb = 2 * nl + (nl - 1) + 3;  // Jacobian inputs | layer-1 u+iv | layer-0 grid_U (u+iv first)
   if (!q.PZ) {
@@ -2160,6 +2166,17 @@ int qg_post(swrt_ctx* c) {
     HIPCHK(c, hipGetLastError());
     if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
   }
+  q.post_inv_valid = true;
+  return SWRT_OK;
+}
+
+int qg_post(swrt_ctx* c) {
+  QGState& q = c->qg;
+  if (q.post_valid) return SWRT_OK;
+  int rc;
+  if ((rc = qg_post_inverse(c))) return rc;
+  const int n = q.g.n, nl = q.g.nl;
+  const dim3 block(256);
   // Jacobian and the CFL speed over every layer's u + i v (layer 1, then
   // layer 0: contiguous); the spectrum of J then lands in PT[0, nn)
   const double2* uvT = q.PT + 2 * nl * q.nn;
@@ -2247,6 +2264,7 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
     }
     if (rc) return rc;
     q.post_valid = false;
+    q.post_inv_valid = false;
     std::swap(q.qk, q.qk_prev);
     q.steps += 1;
     q.t = q.t + dt;
@@ -2276,7 +2294,8 @@ int qg_speed_launch(swrt_ctx* c) {
     hipLaunchKernelGGL(qg_vel_spectra_kernel<1>, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.qk, q.g, q.Z);
   HIPCHK(c, hipGetLastError());
   if ((rc = inverse_2d(c, q.Z, q.T, n, nl))) return rc;
-  q.post_valid = false;  // dmax is overwritten
+  q.post_valid = false;  // dmax is overwritten (and the first phase clears it)
+  q.post_inv_valid = false;
   HIPCHK(c, hipMemsetAsync(q.dmax, 0, sizeof(unsigned long long), c->stream));
   hipLaunchKernelGGL(qg_max_speed2_kernel, dim3(256), dim3(256), 0, c->stream, q.T, q.nn * nl, q.g.shear, q.dmax);
   HIPCHK(c, hipGetLastError());
@@ -2415,7 +2434,7 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   Slot& s = c->slot[slot];
   if (c->qg_fused && which == 0 && layer == 0 && nx % 16 == 0) {
     // layer 0's grid_U of the current qk is part of the post-step transforms
-    if ((rc = qg_post(c))) return rc;
+    if ((rc = qg_post_inverse(c))) return rc;
     const double2* T = q.PT + (3 * q.g.nl - 1) * q.nn;
     hipLaunchKernelGGL(pack_pairs_kernel, dim3(nx / 16, nx / 16), dim3(256), 0, c->stream, T, (int)nx, (int)s.npad,
                        q.g.shear, s.nodes);
