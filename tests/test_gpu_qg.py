@@ -349,23 +349,32 @@ def test_qg_fused_speed_and_snapshot_match_unfused(ctx, nx):
     one-buffer FFT (<= 1024) and the ping-pong FFT (2048)."""
     out = {}
     try:
-        for fused in (False, True):
-            ctx.qg_set_fused(fused)
+        # fused with the speed first (both post-step phases, then the pack) and
+        # with the snapshot first (the inverse phase alone, the Jacobian phase
+        # on the speed request that follows)
+        for mode in ("unfused", "fused", "fused-snapshot-first"):
+            ctx.qg_set_fused(mode != "unfused")
             m = sw.QGModel.two_layer(_two_layer_case(nx, seed=11), nx, 3.0, 1.0, L=20.0, ctx=ctx)
             dt = 0.25 * (20.0 / nx) / m.max_speed()
             for _ in range(4):
                 m.step(dt)
-            U0 = m.max_speed()
-            m.snapshot(0, which=0, ny_period=2 * nx)
+            if mode == "fused-snapshot-first":
+                m.snapshot(0, which=0, ny_period=2 * nx)
+                U0 = m.max_speed()
+            else:
+                U0 = m.max_speed()
+                m.snapshot(0, which=0, ny_period=2 * nx)
             m.step(dt)
             m.snapshot(1, which=0, ny_period=2 * nx)
-            out[fused] = (U0, m.max_speed(), ctx.get_field_grid(0, nx), ctx.get_field_grid(1, nx), m.qk)
+            out[mode] = (U0, m.max_speed(), ctx.get_field_grid(0, nx), ctx.get_field_grid(1, nx), m.qk)
     finally:
         ctx.qg_set_fused(True)
-    a, b = out[False], out[True]
-    assert a[0] == b[0] and a[1] == b[1]
-    for u, v in zip(a[2:], b[2:]):
-        assert np.array_equal(np.ascontiguousarray(u).view(np.uint64), np.ascontiguousarray(v).view(np.uint64))
+    a = out["unfused"]
+    for mode in ("fused", "fused-snapshot-first"):
+        b = out[mode]
+        assert a[0] == b[0] and a[1] == b[1]
+        for u, v in zip(a[2:], b[2:]):
+            assert np.array_equal(np.ascontiguousarray(u).view(np.uint64), np.ascontiguousarray(v).view(np.uint64))
 
 
 def _ring_qk(nx, L, rng, Ug=0.2, kmin=10, kmax_ring=30):
