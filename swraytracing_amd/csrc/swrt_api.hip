@@ -227,12 +227,18 @@ struct swrt_ctx {
   int o_order_split = 0;       // ... and launch shape
   double* o_ynx = nullptr;
   double* o_ynk = nullptr;
+  // a third state set (x, k, F) for swrt_ode23_run's speculative attempt
+  double* o_spx = nullptr;
+  double* o_spk = nullptr;
+  double* o_spF = nullptr;
   int64_t o_cap = 0;
-  // two max slots used in turn: each ode23 launch zeroes the other one for the
-  // next call (no memset launch between attempts); read back through pinned o_hmax
+  // three max slots used in turn: each ode23 launch zeroes the next one for
+  // the next launch (no memset launch between attempts); each is read back
+  // through its pinned o_hmax slot, o_ev marking the copy
   unsigned long long* o_dmax = nullptr;
   int o_dmax_cur = 0;
   unsigned long long* o_hmax = nullptr;
+  hipEvent_t o_ev[3] = {nullptr, nullptr, nullptr};
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -933,9 +939,13 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->qg.hmax) (void)hipHostFree(c->qg.hmax);
   if (c->o_hmax) (void)hipHostFree(c->o_hmax);
+  for (hipEvent_t e : c->o_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
   qg_drop_graphs(c->qg);
   if (c->o_order) (void)hipFree(c->o_order);
+  for (void* p : {(void*)c->o_spx, (void*)c->o_spk, (void*)c->o_spF})
+    if (p) (void)hipFree(p);
   for (void* p : {(void*)c->oF[0], (void*)c->oF[1], (void*)c->oF[2], (void*)c->oF[3], (void*)c->o_ynx,
                   (void*)c->o_ynk, (void*)c->o_dmax})
     if (p) (void)hipFree(p);
@@ -2479,21 +2489,27 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   if (nslots == 2 && c->slot[1].nx != c->slot[0].nx) return fail(c, SWRT_ERR_ARG, "slots differ in nx");
   if (c->o_cap < c->cap) {
     for (double*& p : c->oF) { if (p) (void)hipFree(p); p = nullptr; }
-    if (c->o_ynx) (void)hipFree(c->o_ynx);
-    if (c->o_ynk) (void)hipFree(c->o_ynk);
-    c->o_ynx = c->o_ynk = nullptr;
+    for (double** p : {&c->o_ynx, &c->o_ynk, &c->o_spx, &c->o_spk, &c->o_spF}) {
+      if (*p) (void)hipFree(*p);
+      *p = nullptr;
+    }
     c->o_cap = 0;
     for (double*& p : c->oF) HIPCHK(c, hipMalloc(&p, sizeof(double) * 4 * c->cap));
     HIPCHK(c, hipMalloc(&c->o_ynx, sizeof(double) * 2 * c->cap));
     HIPCHK(c, hipMalloc(&c->o_ynk, sizeof(double) * 2 * c->cap));
+    HIPCHK(c, hipMalloc(&c->o_spx, sizeof(double) * 2 * c->cap));
+    HIPCHK(c, hipMalloc(&c->o_spk, sizeof(double) * 2 * c->cap));
+    HIPCHK(c, hipMalloc(&c->o_spF, sizeof(double) * 4 * c->cap));
     c->o_cap = c->cap;
   }
   if (!c->o_dmax) {
-    HIPCHK(c, hipMalloc(&c->o_dmax, 2 * sizeof(unsigned long long)));
-    HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, 2 * sizeof(unsigned long long), c->stream));
+    HIPCHK(c, hipMalloc(&c->o_dmax, 3 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, 3 * sizeof(unsigned long long), c->stream));
     c->o_dmax_cur = 0;
   }
-  if (!c->o_hmax) HIPCHK(c, hipHostMalloc(&c->o_hmax, sizeof(unsigned long long)));
+  if (!c->o_hmax) HIPCHK(c, hipHostMalloc(&c->o_hmax, 3 * sizeof(unsigned long long)));
+  for (hipEvent_t& e : c->o_ev)
+    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   a.f0 = view_of(c->slot[0]);
   a.f1 = nslots == 2 ? view_of(c->slot[1]) : a.f0;
   a.nslots = nslots;
@@ -2512,21 +2528,39 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   a.thr = thr;
   a.bump = bump;
   a.dmax = c->o_dmax + c->o_dmax_cur;
-  a.dmax_clear = c->o_dmax + (1 - c->o_dmax_cur);
+  a.dmax_clear = c->o_dmax + (c->o_dmax_cur + 1) % 3;
+  a.gate = nullptr;
+  a.gate_scale = 0.0;
+  a.gate_limit = 0.0;
   a.order = nullptr;
   a.split = 0;
   return SWRT_OK;
 }
 
-// the max of the launch just queued (slot o_dmax_cur), then the slots swap
+// ode23: f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2);
+// h4 = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew
+void attempt_coeffs(Ode23Args& a, double t, double h, double tnew) {
+  a.ts = t + h * 0.5;
+  a.c[0] = h * 0.5;
+  a.ts3 = t + h * 0.75;
+  a.c3 = h * 0.75;
+  const double h4 = tnew - t;
+  a.ts4 = tnew;
+  a.c4[0] = h4 * (2.0 / 9.0);
+  a.c4[1] = h4 * (1.0 / 3.0);
+  a.c4[2] = h4 * (4.0 / 9.0);
+}
+
+// the max of the launch just queued (slot o_dmax_cur), then the next slot
 int read_max(swrt_ctx* c, double* out) {
-  const unsigned long long* dm = c->o_dmax + c->o_dmax_cur;
-  c->o_dmax_cur ^= 1;
+  const int slot = c->o_dmax_cur;
+  c->o_dmax_cur = (slot + 1) % 3;
   if (!out) return SWRT_OK;
-  HIPCHK(c, hipMemcpyAsync(c->o_hmax, dm, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->o_hmax + slot, c->o_dmax + slot, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                           c->stream));
   // (spinning on an event instead measured within noise: 2.55-2.59 vs 2.60-2.62 ms)
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  std::memcpy(out, c->o_hmax, sizeof(double));
+  std::memcpy(out, c->o_hmax + slot, sizeof(double));
   return SWRT_OK;
 }
 }  // namespace
@@ -2626,15 +2660,7 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
   // ode23: f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2);
   // h = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew — one launch (stage 0:
   // the tile kernel runs the three stages per packet, registers between them)
-  a.ts = t + h * 0.5;
-  a.c[0] = h * 0.5;
-  a.ts3 = t + h * 0.75;
-  a.c3 = h * 0.75;
-  const double h4 = tnew - t;
-  a.ts4 = tnew;
-  a.c4[0] = h4 * (2.0 / 9.0);
-  a.c4[1] = h4 * (1.0 / 3.0);
-  a.c4[2] = h4 * (4.0 / 9.0);
+  attempt_coeffs(a, t, h, tnew);
   if ((rc = ode23_launch<0>(c, a))) return rc;
   return read_max(c, err_raw_out);
   GUARD_END(c)
@@ -2670,6 +2696,8 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
                    int64_t* stats3_out) {
   if (!c) return SWRT_ERR_ARG;
   if (!ts_out || ts_cap < 1 || !nts_out) return fail(c, SWRT_ERR_ARG, "ts_out / ts_cap / nts_out");
+  GUARD_BEGIN
+  SlotUse slot_use(c);
   const double tdir = std::copysign(1.0, tfinal - t0);
   const double pw = 1.0 / 3.0;
   rtol = std::max(rtol, 100 * 2.220446049250313e-16);
@@ -2680,6 +2708,61 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
   double raw = 0.0;
   int rc;
   if ((rc = swrt_ode23_f1(c, t, tmax, f, Cg, nslots, thr, bump, &raw))) return rc;
+  Ode23Args base;
+  if ((rc = ode23_prepare(c, nslots, base, tmax, f, Cg, thr, bump))) return rc;
+  // three state sets (x, k, F1/F4): an attempt reads set `from` and writes
+  // ynew and F4 into set `to`; the accepted one becomes the current set
+  struct Set {
+    double *x, *k, *F;
+  } S[3] = {{c->dx, c->dk, c->oF[0]}, {c->o_ynx, c->o_ynk, c->oF[3]}, {c->o_spx, c->o_spk, c->o_spF}};
+  int cur = 0;
+  auto commit = [&]() {  // the current set becomes the packets (and F1), the others the spares
+    const int o1 = (cur + 1) % 3, o2 = (cur + 2) % 3;
+    c->dx = S[cur].x; c->dk = S[cur].k; c->oF[0] = S[cur].F;
+    c->o_ynx = S[o1].x; c->o_ynk = S[o1].k; c->oF[3] = S[o1].F;
+    c->o_spx = S[o2].x; c->o_spk = S[o2].k; c->o_spF = S[o2].F;
+    c->keys_fresh = false;
+    c->cells_sorted = false;
+  };
+  auto queue = [&](int from, int to, double ta, double ha, double tnewa, const unsigned long long* gate,
+                   double gscale, double glimit, int* slot) -> int {
+    Ode23Args a = base;
+    a.yx = S[from].x;
+    a.yk = S[from].k;
+    a.F[0] = S[from].F;
+    a.F[3] = S[to].F;
+    a.ynx = S[to].x;
+    a.ynk = S[to].k;
+    attempt_coeffs(a, ta, ha, tnewa);
+    const int sl = c->o_dmax_cur;
+    a.dmax = c->o_dmax + sl;
+    a.dmax_clear = c->o_dmax + (sl + 1) % 3;
+    a.gate = gate;
+    a.gate_scale = gscale;
+    a.gate_limit = glimit;
+    int r;
+    if ((r = ode23_launch<0>(c, a))) return r;
+    HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl, c->o_dmax + sl, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             c->stream));
+    HIPCHK(c, hipEventRecord(c->o_ev[sl], c->stream));
+    c->o_dmax_cur = (sl + 1) % 3;
+    *slot = sl;
+    return SWRT_OK;
+  };
+  // While the host waits for an attempt's error, the next attempt is already
+  // queued on the guess "accepted, next step MaxStep (or the clamp to
+  // tfinal)", gated on the device: it runs only if err = absh*raw <
+  // 0.5119*rtol, which with absh = MaxStep and a first try makes the
+  // controller's next absh certainly >= MaxStep (1.25*(err/rtol)^(1/3) < 1
+  // with margin for pow's last bit) — so then it is exactly the attempt the
+  // controller asks for next (checked again), and a wrong guess costs one
+  // empty launch instead of a whole attempt.
+  const double gate_limit = 0.5119 * rtol;
+  struct Spec {
+    bool on, ran;
+    int slot, from, to;
+    double t, h, tnew;
+  } spec{false, false, 0, 0, 0, 0.0, 0.0, 0.0};
   const double rh = raw / (0.8 * std::pow(rtol, pw));
   double absh = std::min(hmax, htspan);
   if (absh * rh > 1) absh = 1.0 / rh;
@@ -2699,16 +2782,49 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
     }
     bool nofailed = true;
     double tnew, err;
+    int to;
     while (true) {
       tnew = t + h * 1.0;
       if (done) tnew = tfinal;
       ++attempts;
-      if ((rc = swrt_ode23_attempt(c, t, h, tnew, tmax, f, Cg, nslots, thr, bump, &raw))) return rc;
+      int slot;
+      if (spec.on && spec.ran && spec.from == cur && spec.t == t && spec.h == h && spec.tnew == tnew) {
+        slot = spec.slot;
+        to = spec.to;
+      } else {
+        to = (cur + 1) % 3;
+        if ((rc = queue(cur, to, t, h, tnew, nullptr, 0.0, 0.0, &slot))) return rc;
+      }
+      spec.on = false;
+      if (!done && nofailed && absh == hmax) {
+        const double t2 = tnew;
+        const double hmin2 = 16 * np_spacing(t2);
+        double absh2 = std::min(hmax, std::max(hmin2, hmax));
+        double h2 = tdir * absh2;
+        bool done2 = false;
+        if (1.1 * absh2 >= std::fabs(tfinal - t2)) {
+          h2 = tfinal - t2;
+          absh2 = std::fabs(h2);
+          done2 = true;
+        }
+        const double tnew2 = done2 ? tfinal : t2 + h2 * 1.0;
+        const int sto = 3 - cur - to;
+        int sl2;
+        if ((rc = queue(to, sto, t2, h2, tnew2, c->o_dmax + slot, absh, gate_limit, &sl2))) return rc;
+        spec = {true, false, sl2, to, sto, t2, h2, tnew2};
+      }
+      HIPCHK(c, hipEventSynchronize(c->o_ev[slot]));
+      std::memcpy(&raw, c->o_hmax + slot, sizeof(double));
       err = absh * raw;
+      spec.ran = spec.on && err < gate_limit;  // the device's gate, the same operation
       h = tnew - t;
       if (err > rtol) {
         ++nfailed;
-        if (absh <= hmin) return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
+        if (absh <= hmin) {
+          HIPCHK(c, hipStreamSynchronize(c->stream));  // a queued guess may still be running
+          commit();
+          return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
+        }
         if (nofailed) {
           nofailed = false;
           absh = std::max(hmin, absh * std::max(0.5, 0.8 * std::pow(rtol / err, pw)));
@@ -2721,9 +2837,13 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
         break;
       }
     }
-    if ((rc = swrt_ode23_accept(c))) return rc;
+    cur = to;  // accept: y = ynew, F1 = F4
     t = tnew;
-    if (nts >= ts_cap) return fail(c, SWRT_ERR_ARG, "ode23: more steps than ts_cap");
+    if (nts >= ts_cap) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      commit();
+      return fail(c, SWRT_ERR_ARG, "ode23: more steps than ts_cap");
+    }
     ts_out[nts++] = t;
     if (done) break;
     if (nofailed) {
@@ -2731,6 +2851,9 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
       absh = temp > 0.2 ? absh / temp : 5.0 * absh;
     }
   }
+  // everything queued has finished: the last attempt (done) queues no guess,
+  // and every earlier guess precedes it on the stream
+  commit();
   *nts_out = nts;
   if (stats3_out) {
     stats3_out[0] = nts - 1;
@@ -2738,6 +2861,7 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
     stats3_out[2] = attempts;
   }
   return SWRT_OK;
+  GUARD_END(c)
 }
 
 #ifdef SWRT_PHASE_TIMING

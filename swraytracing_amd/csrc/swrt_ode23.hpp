@@ -47,7 +47,13 @@ struct Ode23Args {
   double thr;        // AbsTol / RelTol
   double bump;
   unsigned long long* dmax;
-  unsigned long long* dmax_clear;  // the other max slot, zeroed for the next call (NULL: none)
+  unsigned long long* dmax_clear;  // the next max slot, zeroed for the next launch (NULL: none)
+  // Speculative attempt (swrt_ode23_run): run only if gate_scale * (the
+  // previous attempt's raw error max at *gate) < gate_limit — the condition
+  // under which the controller certainly accepts that attempt and asks for
+  // this one; otherwise every workgroup returns at once.  NULL: always run.
+  const unsigned long long* gate;
+  double gate_scale, gate_limit;
   const int* order;  // tile kernel: binned slots in in-tile cell order (NULL: slot order)
   int split;         // tile kernel: half-tile workgroups at the end of each XCD band
 };
@@ -79,6 +85,7 @@ __device__ __forceinline__ void block_max_to(double m, unsigned long long* out) 
 template <int STAGE>
 __global__ void __launch_bounds__(256) ode23_stage_kernel(Ode23Args a) {
   if (a.dmax_clear && blockIdx.x == 0 && threadIdx.x == 0) *a.dmax_clear = 0ull;
+  if (a.gate && !(a.gate_scale * __longlong_as_double((long long)*a.gate) < a.gate_limit)) return;
   const int64_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const int64_t n = a.n;
   double m = 0.0;
@@ -237,6 +244,7 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
   __shared__ double2 win[NCH * WNP];
   __shared__ double red[NT / 64];
   if (a.dmax_clear && blockIdx.x == 0 && threadIdx.x == 0) *a.dmax_clear = 0ull;
+  if (a.gate && !(a.gate_scale * __longlong_as_double((long long)*a.gate) < a.gate_limit)) return;
   int pbeg, pend;
   const int tile = wg_work_range(starts, nullptr, a.split, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
