@@ -1,11 +1,11 @@
-"""Throughput bench: packet-steps/s @ 512^2 field, 1e6 packets per GPU.
+"""Throughput bench: packet-steps/s @ 512^2 field, 1e6 packets; 1/2/4/8 GPUs.
 
 Workload (BASELINE.json configs[3], the metric's config): two-layer QG
 background (qg2layersw_raytrace.m: L = 20, wavenumbers scaled by 2*pi/L,
 shear_strength 0.5, packets advected in layer 1 so interpolate's y-period is
 2*nx), two spectral snapshots (prev_qk, qk) prepared on the GPU by grid_U
 (swrt_set_field_qk), 1e6 packets on the omega0 = 4f ring (f = 3, Cg = 1,
-Ug = 0.2) per GPU.  One bench step = one PDE interval dt = 0.25*dx/U0
+Ug = 0.2).  One bench step = one PDE interval dt = 0.25*dx/U0
 (CFL_fraction of qg2layersw_raytrace.m:31) advanced by `--substeps` (5)
 fused leapfrog steps with the interpolate_U time blend, i.e. packet steps
 of 0.05*dx/U0 — the step SURVEY §8d's metric is defined on (qgsw_raytrace.m's
@@ -15,9 +15,16 @@ move between re-binnings (`--rebin-every` 20 steps here).  Synthetic data:
 random phase ring spectrum 10 < |k| <= 30 (initial_q's ring), normalised so
 max|U| = Ug; a second snapshot with slightly rotated phases.
 
-Multi-GPU: one process per GPU (torch.distributed.run), packets sharded by
-rank (weak scaling: 1e6 per GPU), field replicated, no data-path collective;
-barrier + device sync around the timed region, max time over ranks.
+Multi-GPU: one process per GPU, packets sharded by rank, field replicated,
+no data-path collective; barrier + device sync around the timed region, max
+time over ranks.  `--scaling strong` (default): the metric's fixed 1e6-packet
+ensemble split over the ranks (configs[3], "1e6 packets, sharded
+8xMI355X"); `--scaling weak`: `--packets` per GPU.  `--gpus N` without a
+torch.distributed environment launches `python -m torch.distributed.run
+--nproc-per-node N bench.py ...` as a CHILD process (never an exec) and
+relays its rank-0 line; under torch.distributed.run, WORLD_SIZE must equal
+`--gpus`.  At N = 1 the line also carries `strong_scaling_forecast`: the
+same workload timed at the shard sizes of 2/4/8 GPUs.
 
 Prints ONE JSON line on rank 0.
 """
@@ -27,21 +34,17 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
 
-# torch first: libswrt must bind to the HIP runtime torch loads (one runtime).
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import swraytracing_amd as sw  # noqa: E402
-from swraytracing_amd.dist import gather_packets, max_over_ranks  # noqa: E402
-
+METRIC = "packet-steps/sec @ 512² field, 1e6 packets; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 BYTES_STEADY = 1792          # 32+32 state + 1 snap * 6 fields * 36 taps * 8 B
 BYTES_BLEND = 3520           # 32+32 state + 2 snaps * 6 * 36 * 8 B
@@ -60,7 +63,12 @@ def ring_spectrum(nx, kmin, kmax_ring, rng, phase_shift=0.0):
     return qk
 
 
-def build_workload(ctx, args, rng):
+def build_workload(ctx, args, lo, hi, n_total):
+    """The replicated field (every rank draws the same spectra from `seed`)
+    and this rank's packets [lo, hi) of the n_total-packet ensemble (the same
+    ensemble at any world size: positions drawn for all n_total packets,
+    ring angles 2*pi*i/n_total)."""
+    rng = np.random.default_rng(args.seed)
     nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
     K_d2 = f / Cg
     ks = 2 * np.pi / L
@@ -87,19 +95,18 @@ def build_workload(ctx, args, rng):
     p = ctx.get_field_grid(0, nx)
     U0 = math.sqrt(float((p[0] ** 2 + p[1] ** 2).max()))
     dt = 0.25 * (L / nx) / U0  # qg2layersw_raytrace.m:31,78
-    N = args.packets
     w0 = 4.0
     wf = math.sqrt((w0 ** 2 - 1) * f ** 2 / Cg ** 2)
-    i = np.arange(1, N + 1, dtype=np.float64) + args.rank * N
-    Ntot = N * args.world
-    k = np.stack([wf * np.cos(2 * np.pi * i / Ntot), wf * np.sin(2 * np.pi * i / Ntot)], axis=1)
+    i = np.arange(lo + 1, hi + 1, dtype=np.float64)
+    k = np.stack([wf * np.cos(2 * np.pi * i / n_total), wf * np.sin(2 * np.pi * i / n_total)], axis=1)
     if getattr(args, "positions", "uniform") == "stratified":
         # diagnostic: every 16x16-cell tile gets the same number of packets
+        N = hi - lo
         nt = max(1, nx // 16)
         t = np.arange(N) % (nt * nt)
         x = np.stack([(t // nt) * 16 + 16 * rng.random(N), (t % nt) * 16 + 16 * rng.random(N)], axis=1) * (L / nx)
     else:
-        x = L * rng.random((N, 2)) - L / 2
+        x = (L * rng.random((n_total, 2)) - L / 2)[lo:hi]
     return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
                 K_d2=K_d2, ks=ks, shear=shear, intervals=getattr(args, "intervals", 1) if nslots == 2 else 1)
 
@@ -117,7 +124,8 @@ def step(ctx, w, sub):
 
 
 def host_cpu():
-    """Where the CPU baseline ran: nproc, the process's CPU affinity and the model."""
+    """Where the CPU baseline ran: nproc, the process's CPU affinity, the
+    cgroup CPU quota (cores) when one is set, and the CPU model."""
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -130,7 +138,13 @@ def host_cpu():
         aff = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         aff = None
-    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cpu_model": model}
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota, "cpu_model": model}
 
 
 def cpu_baseline(ctx, w, target_s, threads):
@@ -170,28 +184,32 @@ def cpu_baseline(ctx, w, target_s, threads):
             "build": flags, "host": host_cpu()}
 
 
-def driver_step(ctx, w, args, dev, distributed):
+def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", nsteps=None):
     """The end-to-end qg2layersw_raytrace step on this GPU (swraytracing_amd.qg.
     TwoLayerLoop, the driver's own loop body): CFL rule, 2-layer PDE step, U0
     read-back, grid_U snapshot of the new qk and the packet interval of all
-    this rank's packets (`--substeps` leapfrog substeps), the PDE on its own
-    stream beside the packets.  Outside the metric's timed region; reported as
-    an extra key so the driver-level rate is observed by the same run."""
+    this rank's packets (`--substeps` leapfrog substeps, or the reference's
+    own ode23 over the interval), the PDE on its own stream beside the
+    packets.  Outside the metric's timed region; reported as extra keys so
+    the driver-level rates are observed by the same run."""
     nx, L, f, Cg = w["nx"], w["L"], w["f"], math.sqrt(w["gH"])
+    nsteps = args.driver_steps if nsteps is None else nsteps
     qk = np.stack([w["qk1"], -w["qk1"]], axis=2)  # the driver's (q1, -q1) layers
     model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
     ens = sw.PacketEnsemble(w["x"], w["k"], L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * math.pi / L, nlayers=2,
                             bump=sw.BUMP_QG, ctx=ctx)
     U0 = model.max_speed()
-    loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps)
+    loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
+                           integrator=integrator)
     for _ in range(4):  # AB1/AB2 start-up, first-use allocations
         loop.step()
+    loop.flush()
     ctx.synchronize()
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.driver_steps):
+    for _ in range(nsteps):
         loop.step()
     loop.flush()
     ctx.synchronize()
@@ -199,11 +217,17 @@ def driver_step(ctx, w, args, dev, distributed):
     el = time.perf_counter() - t0
     if distributed:
         el = max_over_ranks(el, backend=args.dist_backend)
-    ms = el / args.driver_steps * 1e3
-    return {"ms_per_pde_step": ms, "steps": args.driver_steps,
-            "packet_steps_per_s": args.packets * args.world * args.substeps / (ms / 1e3),
-            "what": "TwoLayerLoop.step: CFL rule + 2-layer PDE step + U0 read-back + grid_U snapshot + "
-                    f"{args.substeps} leapfrog substeps of {args.packets} packets/GPU (qg2layersw_raytrace.m:152-197)"}
+    ms = el / nsteps * 1e3
+    what = (f"TwoLayerLoop.step: CFL rule + 2-layer PDE step + U0 read-back + grid_U snapshot + "
+            + (f"{args.substeps} leapfrog substeps" if integrator == "leapfrog" else "ode23 over the interval "
+               "(qg2layersw_raytrace.m:195: RelTol 1e-3, AbsTol 1e-6, MaxStep 0.1*dt)")
+            + f" of {w['x'].shape[0]} packets/GPU (qg2layersw_raytrace.m:152-197)")
+    out = {"ms_per_pde_step": ms, "steps": nsteps, "what": what}
+    if integrator == "leapfrog":
+        out["packet_steps_per_s"] = n_total * args.substeps / (ms / 1e3)
+    else:
+        out["packet_intervals_per_s"] = n_total / (ms / 1e3)
+    return out
 
 
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s (78.6 TFLOP/s spec counts an FMA as 2)
@@ -211,12 +235,22 @@ LDS_CYCLES_PEAK = 256 * 2.4e9               # LDS-array cycles/s over the chip (
 
 
 def load_pmc(config_key):
-    """PMC record of this bench configuration (tools/pmc_collect.sh -> profiles/pmc.json)."""
+    """PMC record of this bench configuration (tools/pmc_collect.sh ->
+    profiles/pmc.json), only if it was collected on the device code being
+    timed (its code_object_sha256 = the loaded libswrt's .hip_fatbin hash);
+    returns (record or None, note)."""
     path = os.path.join(ROOT, "profiles", "pmc.json")
     try:
-        return json.load(open(path)).get(config_key)
+        rec = json.load(open(path)).get(config_key)
     except (OSError, ValueError):
-        return None
+        rec = None
+    if rec is None:
+        return None, f"no PMC record for {config_key} in profiles/pmc.json (tools/pmc_collect.sh)"
+    have = sw._lib.device_code_sha256()
+    if rec.get("code_object_sha256") != have:
+        return None, (f"profiles/pmc.json[{config_key}] was collected on device code "
+                      f"{str(rec.get('code_object_sha256'))[:12]}, the library timed is {have[:12]}: frac not computed")
+    return rec, "PMC bound to device code " + have[:12]
 
 
 def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timing_every):
@@ -236,7 +270,6 @@ def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timin
          # re-read from LDS): an effective gather bandwidth, not an HBM fraction
          "effective_gather_gbs": ps * B / avg_launch_s / 1e9, "gather_bytes_per_packet_step": B}
     if pmc is None:
-        r["note"] = "no PMC record for this configuration in profiles/pmc.json (tools/pmc_collect.sh)"
         return r
     valu = pmc["SQ_INSTS_VALU"]
     ach = valu * 64.0 / avg_launch_s
@@ -265,13 +298,19 @@ def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timin
     return r
 
 
-def main():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks); without a torch.distributed environment N > 1 launches the ranks as a child "
+                         "torch.distributed.run; under one it must equal WORLD_SIZE (default: WORLD_SIZE)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="strong: --packets in total, sharded over the ranks (the metric's fixed 1e6); "
+                         "weak: --packets per GPU")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nx", type=int, default=512)
-    ap.add_argument("--packets", type=int, default=1_000_000, help="packets per GPU (weak scaling)")
+    ap.add_argument("--packets", type=int, default=1_000_000,
+                    help="packets in total (strong scaling) or per GPU (weak)")
     ap.add_argument("--substeps", type=int, default=5,
                     help="leapfrog steps per bench step (PDE interval 0.25*dx/U0; 5 -> 0.05*dx/U0 per step)")
     ap.add_argument("--intervals", type=int, default=1,
@@ -282,6 +321,8 @@ def main():
                     help="initial packet positions (stratified: equal packets per tile, a diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-forecast", action="store_true",
+                    help="at N = 1, skip the strong-scaling forecast (the workload at 2/4/8-GPU shard sizes)")
     ap.add_argument("--rebin-every", type=int, default=20, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
@@ -301,9 +342,121 @@ def main():
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
     ap.add_argument("--driver-steps", type=int, default=20,
                     help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
+    ap.add_argument("--ode23-steps", type=int, default=4,
+                    help="then this many driver steps with the reference's ode23 packet integrator (0: skip)")
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather all trajectories to rank 0 (one all_gather)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launcher_cmd(args, argv, env):
+    """The child command that runs this bench on `--gpus` ranks, or None when
+    this process is itself a rank (WORLD_SIZE set) or one GPU was asked for.
+    Raises if a torch.distributed environment disagrees with --gpus."""
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if args.gpus is not None and args.gpus != int(world):
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return None
+    if args.gpus is None or args.gpus <= 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def relay(cmd):
+    """Run the ranks as a child process; the rank-0 JSON line goes to stdout,
+    everything else to stderr as it arrives.  Returns the child's exit code."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    for line in proc.stdout:
+        t = line.strip()
+        if t.startswith("{") and '"metric"' in t:
+            print(t, flush=True)
+        else:
+            print(line, end="", file=sys.stderr, flush=True)
+    return proc.wait()
+
+
+def _imports():
+    """torch and the library, imported only in a rank (never in the launcher)."""
+    global torch, dist, sw, gather_packets, max_over_ranks, shard_range
+    import torch  # noqa: F401  (first: libswrt binds to the HIP runtime torch loads)
+    import torch.distributed as dist  # noqa: F401
+
+    import swraytracing_amd as sw  # noqa: F401
+    from swraytracing_amd.dist import gather_packets, max_over_ranks, shard_range  # noqa: F401
+
+
+def steps_per_launch_of(args, ivs):
+    """Packet-steps per launch: a call's substeps run as launches of at most
+    `rebin_every` steps, cut at the re-binning points (swrt_advance)."""
+    if ivs > 1 and args.rebin_every > 0 and args.rebin_every % args.substeps == 0 and args.kernel in (0, 2):
+        return args.substeps * min(ivs, 4, args.rebin_every // args.substeps)  # whole intervals, up to 4
+    if args.rebin_every <= 0 or args.rebin_every % args.substeps == 0:
+        return min(args.substeps, 64)
+    if args.substeps % args.rebin_every == 0:
+        return args.rebin_every
+    return min(args.substeps, args.rebin_every)  # approximate (uneven chunks)
+
+
+def timed(ctx, w, args, dev, steps, warmup, barrier=None):
+    """warmup untimed steps, then `steps` timed ones bracketed by a device
+    sync (and the caller's barrier); returns (elapsed s, sampled kernel ms, launches)."""
+    for _ in range(warmup):
+        step(ctx, w, args.substeps)
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    if barrier:
+        barrier()
+    ctx.set_timing(args.timing_every)
+    ctx.kernel_time(reset=True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(ctx, w, args.substeps)
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if barrier:
+        barrier()
+    kms, launches = ctx.kernel_time(reset=True)
+    ctx.set_timing(0)
+    return t1 - t0, kms, launches
+
+
+def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu):
+    """One GPU timed on the packets rank 0 of a G-GPU strong-scaling run
+    holds (the first ceil(n_total/G) of the same ensemble) for G = 2, 4, 8:
+    forecast value = G x that rate (the field is replicated and the timed path
+    has no collective), efficiency = rate(shard) / rate(n_total)."""
+    out = {}
+    x, k = w["x"], w["k"]
+    for G in (2, 4, 8):
+        n = -(-n_total // G)
+        ctx.packets_set(x[:n], k[:n])
+        el, kms, launches = timed(ctx, w, args, dev, args.steps, args.warmup)
+        rate = n * args.substeps * w["intervals"] * args.steps / el
+        out[str(G)] = {"packets_per_gpu": n, "value_1gpu": rate, "forecast_value": G * rate,
+                       "efficiency": rate / rate_1gpu, "ms_per_step": el / args.steps * 1e3,
+                       "avg_launch_ms": (kms / launches) if launches else None}
+    ctx.packets_set(x, k)
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    cmd = launcher_cmd(args, argv, os.environ)
+    if cmd is not None:
+        sys.exit(relay(cmd))
+    _imports()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -317,6 +470,8 @@ def main():
         dist.init_process_group(backend=args.dist_backend, init_method="env://")
     dev = torch.device("cuda", device)
 
+    n_total = args.packets if args.scaling == "strong" else args.packets * world
+    lo, hi = shard_range(n_total, world, rank)
     ctx = sw.Context(device)
     ctx.set_locality(args.rebin_every, args.tile)
     ctx.set_kernel(args.kernel)
@@ -326,31 +481,14 @@ def main():
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
     if args.tile_order >= 0:
         ctx.set_tile_order(args.tile_order)
-    rng = np.random.default_rng(args.seed + rank)
-    w = build_workload(ctx, args, rng)
+    w = build_workload(ctx, args, lo, hi, n_total)
     ctx.packets_set(w["x"], w["k"])
 
-    def barrier_sync():
-        ctx.synchronize()
-        torch.cuda.synchronize(dev)
+    def barrier():
         if distributed:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step(ctx, w, args.substeps)
-    barrier_sync()
-    ctx.set_timing(args.timing_every)
-    ctx.kernel_time(reset=True)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(ctx, w, args.substeps)
-    ctx.synchronize()
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if distributed:
-        dist.barrier()
-    elapsed = t1 - t0
-    kms, launches = ctx.kernel_time(reset=True)
+    elapsed, kms, launches = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
     if distributed:
         elapsed = max_over_ranks(elapsed, backend=args.dist_backend)
     xg, kg = ctx.packets_get()
@@ -358,36 +496,28 @@ def main():
     gathered = None
     if distributed and args.gather:
         # device-side gather of the trajectories (the frame writer's input): libswrt -> torch buffer -> all_gather
-        full = gather_packets(ctx, args.packets * world, world, rank)
+        full = gather_packets(ctx, n_total, world, rank)
         gathered = None if full is None else bool(np.isfinite(full[0]).all() and np.isfinite(full[1]).all()
-                                                  and full[0].shape[0] == args.packets * world)
+                                                  and full[0].shape[0] == n_total)
 
-    N = args.packets
+    N = hi - lo
     ivs = w["intervals"]
-    total_ps = N * world * args.substeps * ivs * args.steps
+    total_ps = n_total * args.substeps * ivs * args.steps
     value = total_ps / elapsed
     # sampled HIP-event time of the packet kernel; without samples fall back to wall time per step
     avg_launch_s = (kms / 1e3) / launches if launches > 0 else elapsed / args.steps
-    # packet-steps per launch: a call's substeps run as launches of at most
-    # `rebin_every` steps, cut at the re-binning points (swrt_advance)
-    if ivs > 1 and args.rebin_every > 0 and args.rebin_every % args.substeps == 0 and args.kernel in (0, 2):
-        # whole intervals per launch, up to 4, never across a re-binning
-        steps_per_launch = args.substeps * min(ivs, 4, args.rebin_every // args.substeps)
-    elif args.rebin_every <= 0 or args.rebin_every % args.substeps == 0:
-        steps_per_launch = min(args.substeps, 64)
-    elif args.substeps % args.rebin_every == 0:
-        steps_per_launch = args.rebin_every
-    else:
-        steps_per_launch = min(args.substeps, args.rebin_every)  # approximate (uneven chunks)
+    spl = steps_per_launch_of(args, ivs)
     key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}" + (f"_iv{ivs}" if ivs > 1 else "")
-    pmc = load_pmc(key) if args.blend_mode == 0 and args.kernel in (0, 2) else None
-    roof = roofline(pmc, N, args.nx, w["nslots"], steps_per_launch, avg_launch_s, launches, args.timing_every)
+    pmc, pmc_note = (load_pmc(key) if args.blend_mode == 0 and args.kernel in (0, 2)
+                     else (None, "PMC only for the default bit-exact tile kernel"))
+    roof = roofline(pmc, N, args.nx, w["nslots"], spl, avg_launch_s, launches, args.timing_every)
+    roof["pmc_note"] = pmc_note
     workload = ("qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
-                f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, {args.nx}^2x2 field, {N} packets/GPU, "
-                f"leapfrog dt {0.25 / args.substeps:g}*dx/U0 ({args.substeps} per PDE interval)"
-                + (f", {ivs} PDE intervals per call" if ivs > 1 else ""))
+                f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, {args.nx}^2x2 field, {n_total} packets "
+                f"({args.scaling} scaling, {N} on rank 0's GPU), leapfrog dt {0.25 / args.substeps:g}*dx/U0 "
+                f"({args.substeps} per PDE interval)" + (f", {ivs} PDE intervals per call" if ivs > 1 else ""))
     out = {
-        "metric": "packet-steps/sec @ 512² field, 1e6 packets; 1/2/4/8-GPU scaling",
+        "metric": METRIC,
         "value": value,
         "unit": "packet-steps/s",
         "n_gpus": world,
@@ -395,32 +525,45 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,  # one step = `intervals` PDE intervals
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic",
         "config": {"workload": workload,
-                   "nx": args.nx, "packets_per_gpu": N, "substeps_per_step": args.substeps,
+                   "nx": args.nx, "packets_total": n_total, "packets_per_gpu": N, "substeps_per_step": args.substeps,
                    "pde_dt": "0.25*dx/U0", "leapfrog_dt": f"{0.25 / args.substeps:g}*dx/U0",
-                   "steps_per_launch": steps_per_launch, "intervals_per_step": ivs,
+                   "steps_per_launch": spl, "intervals_per_step": ivs,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
-                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split, "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
-                   "parallelism": f"packets sharded x{world}, field replicated"},
+                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split,
+                   "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
+                   "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,
         "finite": finite,
     }
     if gathered is not None:
         out["gathered_finite"] = gathered
+    if world == 1 and not args.no_forecast and args.scaling == "strong" and args.intervals == 1:
+        out["strong_scaling_forecast"] = strong_scaling_forecast(ctx, w, args, dev, n_total, value)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the GPU box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there)
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(ctx, w, args.cpu_seconds, threads)
-        # SURVEY §8d also asks for the 1-core figure of the same code
+        # all host cores (every CPU this process may run on) and 1 core
+        try:
+            allc = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            allc = os.cpu_count() or 1
+        if allc != threads:
+            out["cpu_baseline_all_cores"] = cpu_baseline(ctx, w, args.cpu_seconds * 2 / 3, allc)
         out["cpu_baseline_1core"] = cpu_baseline(ctx, w, args.cpu_seconds / 3, 1)
     elif rank == 0:
         out["cpu_baseline"] = None
     if args.driver_steps > 0 and args.mode == "blend":
-        out["driver_step"] = driver_step(ctx, w, args, dev, distributed)
+        out["driver_step"] = driver_step(ctx, w, args, dev, distributed, n_total)
+    if args.ode23_steps > 0 and args.mode == "blend" and world == 1:
+        # (single rank: a sharded ode23 needs the error norm's allreduce, PacketEnsemble(shard=...))
+        out["driver_step_ode23"] = driver_step(ctx, w, args, dev, distributed, n_total, integrator="ode23",
+                                               nsteps=args.ode23_steps)
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

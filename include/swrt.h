@@ -90,6 +90,15 @@ int swrt_set_field_psi(swrt_ctx* ctx, int slot, const double* psi_grid, int64_t 
 int swrt_set_field_qk(swrt_ctx* ctx, int slot, const double* qk_interleaved, int64_t nx, double L,
                       double K_d2, double shear, double k_scale, int64_t ny_period);
 
+/* grid_U(g2k(q)) into `slot` from a gridded PV frame q (nx x nx fp64,
+ * column-major): the stored-field consumer's read_field -> g2k -> grid_U
+ * (symplectic_full_fourier.m:18-20, read_field.m:37-98, g2k.m:8-9,
+ * grid_U.m:1-18) with both transforms on the device — the same result as
+ * swrt_g2k followed by swrt_set_field_qk, without the spectrum's round
+ * trip through host memory.  Arguments as swrt_set_field_qk. */
+int swrt_set_field_q(swrt_ctx* ctx, int slot, const double* q_grid, int64_t nx, double L, double K_d2,
+                     double shear, double k_scale, int64_t ny_period);
+
 /* g2k(fg) (g2k.m:5-9): nx x nx real grid (column-major) -> the
  * (2kmax+1) x (kmax+1) half-plane spectrum fftshift(fft2(fg))/nx^2 cropped,
  * interleaved complex, column-major.  GPU FFT. */
@@ -102,6 +111,12 @@ int swrt_k2g(swrt_ctx* ctx, const double* fk_interleaved, int64_t nx, double* fg
 int swrt_get_field_grid(swrt_ctx* ctx, int slot, double* fields6_out);
 /* Download the filtered psi grid of the last swrt_set_field_psi (nx*nx). */
 int swrt_get_psi_grid(swrt_ctx* ctx, int slot, double* psi_out);
+
+/* nx of the grid held by field slot `slot` (the size swrt_get_field_grid /
+ * swrt_get_psi_grid write: 6 / 1 planes of nx x nx); -1 when the slot is
+ * unset or the index is out of range.  Front-ends size their outputs from
+ * this, never from a caller's argument. */
+int64_t swrt_field_grid(const swrt_ctx* ctx, int slot);
 
 /* ---------------------------------------------------------------------------
  * Point evaluation (L2 boundary API)
@@ -307,9 +322,12 @@ int swrt_ode23_accept(swrt_ctx* ctx);
  * MATLAB's controller (RelTol rtol, AbsTol atol, MaxStep 0.1*|tfinal - t0|,
  * max-norm error, initial-step heuristic, step update) in the library: the
  * f1 / attempt / accept sequence above without a host interpreter between
- * attempts.  Writes the accepted times (t0 first) to ts_out[0 .. *nts_out)
- * (SWRT_ERR_ARG beyond ts_cap) and {steps, failed, attempts} to stats3_out
- * (may be NULL).  Single rank: a sharded ensemble needs the error norm's
+ * attempts.  Writes the accepted times (t0 first) to ts_out[0 .. min(*nts_out,
+ * ts_cap)): ts_cap bounds only the times recorded, the interval always
+ * completes and *nts_out counts every accepted time.  {steps, failed,
+ * attempts} go to stats3_out (may be NULL).  If the step size falls below
+ * hmin (MATLAB's "unable to meet integration tolerances") the packets are
+ * left at the last accepted time and SWRT_ERR_STATE is returned.  Single rank: a sharded ensemble needs the error norm's
  * allreduce between attempts (swraytracing_amd.integrate.ode23_packets). */
 int swrt_ode23_run(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                    double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
@@ -384,6 +402,11 @@ int swrt_qg_get(swrt_ctx* ctx, double* qk_out, double* t_out, int64_t* steps_out
 /* q = k2g(qk) per layer: nx x nx x nlayers column-major (pv.bin frames,
  * qgsw_raytrace.m:167-170). */
 int swrt_qg_get_q(swrt_ctx* ctx, double* q_out);
+
+/* nx of the QG state and (if nlayers_out) its layer count; -1 before
+ * swrt_qg_init.  swrt_qg_get writes (nx-1) x nx/2 x nlayers complex values,
+ * swrt_qg_get_q nx x nx x nlayers reals. */
+int64_t swrt_qg_grid(const swrt_ctx* ctx, int* nlayers_out);
 /* grid_U of the current (which = 0) or previous (which = 1) qk of one layer
  * straight into packet field slot `slot` (qgsw_raytrace.m:141-142,
  * qg2layersw_raytrace.m:187-188: layer 1, u += shear_strength), no host copy.

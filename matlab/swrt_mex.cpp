@@ -85,6 +85,25 @@ static void need(int nrhs, int n, const char* cmd) {
   if (nrhs < n) mexErrMsgIdAndTxt("swrt:arg", "%s: expected %d arguments after the command", cmd, n - 1);
 }
 
+// The library's own grid sizes size every output (a caller's nx that does not
+// match is an error, never a buffer size).
+static int64_t slot_grid(swrt_ctx* c, int slot, int64_t nx_arg) {
+  const int64_t nx = swrt_field_grid(c, slot);
+  if (nx < 0) mexErrMsgIdAndTxt("swrt:state", "field slot %d is not set", slot);
+  if (nx_arg != nx) mexErrMsgIdAndTxt("swrt:arg", "slot %d holds an %lld grid, not %lld", slot, (long long)nx,
+                                      (long long)nx_arg);
+  return nx;
+}
+
+static int64_t qg_grid(swrt_ctx* c, int64_t nx_arg, int nl_arg, int* nl) {
+  const int64_t nx = swrt_qg_grid(c, nl);
+  if (nx < 0) mexErrMsgIdAndTxt("swrt:state", "swrt_qg_init not called");
+  if (nx_arg != nx || nl_arg != *nl)
+    mexErrMsgIdAndTxt("swrt:arg", "the QG state is %lld x %lld x %d, not %lld x %lld x %d", (long long)nx,
+                      (long long)nx, *nl, (long long)nx_arg, (long long)nx_arg, nl_arg);
+  return nx;
+}
+
 void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   if (nrhs < 1 || !mxIsChar(prhs[0])) mexErrMsgIdAndTxt("swrt:arg", "first argument: command");
   char cmd[64];
@@ -142,7 +161,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   }
   if (!strcmp(cmd, "get_fields")) {  // (slot, nx) -> nx x nx x 6
     need(na, 3, cmd);
-    const int64_t nx = (int64_t)scalar(a[2]);
+    const int64_t nx = slot_grid(c, (int)scalar(a[1]), (int64_t)scalar(a[2]));
     const mwSize dims[3] = {(mwSize)nx, (mwSize)nx, 6};
     plhs[0] = mxCreateNumericArray(3, dims, mxDOUBLE_CLASS, mxREAL);
     check(c, swrt_get_field_grid(c, (int)scalar(a[1]), mxGetDoubles(plhs[0])), "swrt_get_field_grid");
@@ -150,7 +169,7 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   }
   if (!strcmp(cmd, "get_psi")) {  // (slot, nx) -> nx x nx
     need(na, 3, cmd);
-    const int64_t nx = (int64_t)scalar(a[2]);
+    const int64_t nx = slot_grid(c, (int)scalar(a[1]), (int64_t)scalar(a[2]));
     plhs[0] = mxCreateDoubleMatrix((mwSize)nx, (mwSize)nx, mxREAL);
     check(c, swrt_get_psi_grid(c, (int)scalar(a[1]), mxGetDoubles(plhs[0])), "swrt_get_psi_grid");
     return;
@@ -298,8 +317,8 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     need(na, 3, cmd);
     double t = 0.0;
     int64_t steps = 0;
-    const int64_t nx = (int64_t)scalar(a[1]);
-    const int nl = (int)scalar(a[2]);
+    int nl = 0;
+    const int64_t nx = qg_grid(c, (int64_t)scalar(a[1]), (int)scalar(a[2]), &nl);
     const mwSize dims[3] = {(mwSize)(nx - 1), (mwSize)(nx / 2), (mwSize)nl};
     plhs[0] = mxCreateNumericArray(nl > 1 ? 3 : 2, dims, mxDOUBLE_CLASS, mxCOMPLEX);
     check(c, swrt_qg_get(c, (double*)mxGetComplexDoubles(plhs[0]), &t, &steps), "swrt_qg_get");
@@ -309,8 +328,8 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
   }
   if (!strcmp(cmd, "qg_get_q")) {  // (nx, nlayers) -> q nx x nx [x nlayers]
     need(na, 3, cmd);
-    const int64_t nx = (int64_t)scalar(a[1]);
-    const int nl = (int)scalar(a[2]);
+    int nl = 0;
+    const int64_t nx = qg_grid(c, (int64_t)scalar(a[1]), (int)scalar(a[2]), &nl);
     const mwSize dims[3] = {(mwSize)nx, (mwSize)nx, (mwSize)nl};
     plhs[0] = mxCreateNumericArray(nl > 1 ? 3 : 2, dims, mxDOUBLE_CLASS, mxREAL);
     check(c, swrt_qg_get_q(c, mxGetDoubles(plhs[0])), "swrt_qg_get_q");

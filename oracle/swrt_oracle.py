@@ -632,15 +632,20 @@ def step_packet_xka(P, U, GradU, H, C0, f, dx, dy, dt):
     return out
 
 
-def rsw_background(S, f, Cg):
+def rsw_background(S, f, Cg, L=2 * math.pi):
     """ray_trace_sw/raytrace_sw.m:16-52: geostrophic part of an RSW state.
 
-    S: nx x nx x 3 grid state [u v eta] (raytrace_sw.m:12).  Integer
-    wavenumbers (L = 2*pi, :84).  Returns dict(U={u, v}, GradU={u_x, u_y,
-    v_x, v_y}, H = 1 + eta_g, etag), the inputs of step_packet_xka."""
+    S: nx x nx x 3 grid state [u v eta] (raytrace_sw.m:12).  The script's
+    integer wavenumbers are those of L = 2*pi (:84); another period scales
+    them by 2*pi/L (exactly 1.0 at 2*pi, so the script's values are
+    unchanged).  Returns dict(U={u, v}, GradU={u_x, u_y, v_x, v_y},
+    H = 1 + eta_g, etag), the inputs of step_packet_xka."""
     S = np.asarray(S, dtype=np.float64)
     nx = S.shape[0]
-    kx_, ky_, K2_ = wavenumber_grids(nx)  # :16-18
+    kx_, ky_, _ = wavenumber_grids(nx)  # :16-18
+    ks = (2 * math.pi) / L
+    kx_, ky_ = kx_ * ks, ky_ * ks
+    K2_ = kx_ ** 2 + ky_ ** 2
     gH0 = Cg ** 2  # :22
     sig2_ = f ** 2 + gH0 * K2_  # :25
     uk = g2k(S[:, :, 0])  # :26-28

@@ -10,6 +10,7 @@ from .integrate import (PacketEnsemble, ode23_packets, ode_symplectic, raytrace_
                         step_packet_xka)
 from .io import read_field, write_field
 from .qg import QGModel, TwoLayerLoop, qg2layersw_raytrace, qgsw_raytrace
+from .stored import read_frame, trace_stored
 from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, FourierScheme, RaytracingScheme, SnapshotPairScheme,
                      SpectralScheme, g2k, grid_U, interpolate, interpolate_U, k2g)
 
@@ -18,5 +19,5 @@ __all__ = [
     "rsw_background", "step_packet_xka",
     "read_field", "write_field", "QGModel", "TwoLayerLoop", "qgsw_raytrace", "qg2layersw_raytrace",
     "BUMP_QG", "BUMP_SW", "DifferenceScheme", "FourierScheme", "RaytracingScheme", "SnapshotPairScheme",
-    "SpectralScheme", "g2k", "grid_U", "interpolate", "interpolate_U", "k2g",
+    "SpectralScheme", "g2k", "grid_U", "interpolate", "interpolate_U", "k2g", "read_frame", "trace_stored",
 ]

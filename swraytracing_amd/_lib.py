@@ -52,8 +52,10 @@ SIGNATURES = {
     "swrt_set_field_grid": (_INT, [_VP, _INT, _P, _I, _D, _I]),
     "swrt_set_field_psi": (_INT, [_VP, _INT, _P, _I, _D]),
     "swrt_set_field_qk": (_INT, [_VP, _INT, _P, _I, _D, _D, _D, _D, _I]),
+    "swrt_set_field_q": (_INT, [_VP, _INT, _P, _I, _D, _D, _D, _D, _I]),
     "swrt_get_field_grid": (_INT, [_VP, _INT, _P]),
     "swrt_get_psi_grid": (_INT, [_VP, _INT, _P]),
+    "swrt_field_grid": (_I, [_VP, _INT]),
     "swrt_g2k": (_INT, [_VP, _P, _I, _P]),
     "swrt_k2g": (_INT, [_VP, _P, _I, _P]),
     "swrt_interpolate": (_INT, [_VP, _P, _I, _I, _D, _D, _D, _P, _P, _I, _P]),
@@ -98,6 +100,7 @@ SIGNATURES = {
     "swrt_qg_max_speed_result": (_INT, [_VP, ctypes.POINTER(_D)]),
     "swrt_qg_get": (_INT, [_VP, _P, ctypes.POINTER(_D), ctypes.POINTER(ctypes.c_int64)]),
     "swrt_qg_get_q": (_INT, [_VP, _P]),
+    "swrt_qg_grid": (_I, [_VP, ctypes.POINTER(_INT)]),
     "swrt_qg_snapshot": (_INT, [_VP, _INT, _INT, _INT, _I]),
     "swrt_swap_slots": (_INT, [_VP, _INT, _INT]),
     "swrt_field_div_free": (_INT, [_VP, _INT]),
@@ -113,6 +116,32 @@ _lib = None
 
 class SwrtError(RuntimeError):
     pass
+
+
+def device_code_sha256(path=None):
+    """sha256 of the device code embedded in a libswrt build (its ELF
+    .hip_fatbin section: every gfx950 kernel, none of the host code).  PMC
+    records carry it (tools/pmc_merge.py), so counters collected on one
+    build are never divided by the launch time of another (bench.py)."""
+    import hashlib
+    import struct
+    with open(path or LIB_PATH, "rb") as fh:
+        b = fh.read()
+    if b[:4] != b"\x7fELF" or b[4] != 2 or b[5] != 1:
+        raise ValueError("not a little-endian ELF64 file")
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+
+    def sec(i):
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", b, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = b.index(b"\0", stroff + name)
+        if b[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(b[off:off + size]).hexdigest()
+    raise ValueError("no .hip_fatbin section")
 
 
 def load():
@@ -191,7 +220,31 @@ class Context:
                                             float(shear), float(k_scale), ny_period),
                   "swrt_set_field_qk")
 
-    def get_field_grid(self, slot, nx):
+    def set_field_q(self, slot, q, L, K_d2, shear=0.0, k_scale=1.0, ny_period=0):
+        """grid_U(g2k(q)) into `slot` from a gridded PV frame (swrt_set_field_q)."""
+        q = np.asarray(q, dtype=np.float64)
+        nx = q.shape[0]
+        if q.shape != (nx, nx):
+            raise ValueError("q must be nx x nx")
+        buf = _f64(q.ravel(order="F"))
+        self._chk(self._L.swrt_set_field_q(self._h, slot, _p(buf), nx, float(L), float(K_d2), float(shear),
+                                           float(k_scale), int(ny_period)), "swrt_set_field_q")
+
+    def field_grid(self, slot):
+        """nx of field slot `slot` (swrt_field_grid); raises if unset."""
+        nx = int(self._L.swrt_field_grid(self._h, int(slot)))
+        if nx < 0:
+            raise SwrtError(f"field slot {slot} is not set")
+        return nx
+
+    def _slot_nx(self, slot, nx):
+        have = self.field_grid(slot)
+        if nx is not None and int(nx) != have:
+            raise ValueError(f"slot {slot} holds a {have}^2 grid, not {nx}^2")
+        return have
+
+    def get_field_grid(self, slot, nx=None):
+        nx = self._slot_nx(slot, nx)
         out = np.empty(6 * nx * nx)
         self._chk(self._L.swrt_get_field_grid(self._h, slot, _p(out)), "swrt_get_field_grid")
         return out.reshape(6, nx * nx)
@@ -204,7 +257,8 @@ class Context:
             self._chk(rc, "swrt_field_div_free")
         return rc == 1
 
-    def get_psi_grid(self, slot, nx):
+    def get_psi_grid(self, slot, nx=None):
+        nx = self._slot_nx(slot, nx)
         out = np.empty(nx * nx)
         self._chk(self._L.swrt_get_psi_grid(self._h, slot, _p(out)), "swrt_get_psi_grid")
         return out.reshape((nx, nx), order="F")
@@ -435,7 +489,8 @@ class Context:
         self._chk(self._L.swrt_ode23_run(self._h, float(t0), float(tfinal), float(tmax), float(f), float(Cg),
                                          int(nslots), float(rtol), float(atol), float(bump), _p(ts), int(ts_cap),
                                          ctypes.byref(nts), st), "swrt_ode23_run")
-        return ts[:nts.value].copy(), {"steps": st[0], "failed": st[1], "attempts": st[2]}
+        # ts_cap bounds the recorded times only (the interval always completes)
+        return ts[:min(nts.value, ts_cap)].copy(), {"steps": st[0], "failed": st[1], "attempts": st[2]}
 
     # ---- QG PDE stepper (swrt_qg_*) ---------------------------------------
     def qg_init(self, params: QGParams, nx, qk):

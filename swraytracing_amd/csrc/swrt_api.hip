@@ -1074,6 +1074,51 @@ int swrt_set_field_qk(swrt_ctx* c, int slot, const double* qk_interleaved, int64
   GUARD_END(c)
 }
 
+int swrt_set_field_q(swrt_ctx* c, int slot, const double* q_grid, int64_t nx, double L, double K_d2,
+                     double shear, double k_scale, int64_t ny_period) {
+  int rc = check_slot_args(c, slot, nx);
+  if (rc) return rc;
+  GUARD_BEGIN
+  SlotUse slot_use(c);
+  if (!q_grid) return fail(c, SWRT_ERR_ARG, "q_grid is NULL");
+  if (!is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two for the GPU FFT");
+  if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
+  if (ny_period == 0) ny_period = nx;
+  if (ny_period % nx) return fail(c, SWRT_ERR_ARG, "ny_period must be a multiple of nx");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_slot(c, slot, nx))) return rc;
+  if ((rc = ensure_twiddles(c, (int)nx))) return rc;
+  const int n = (int)nx;
+  const int64_t nn = nx * nx;
+  const int kmax = n / 2 - 1;
+  const int64_t nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
+  // scratch: Z (3 nn complex) | T (3 nn complex) | fk (nhalf complex) | raw (nn double)
+  const size_t zb = sizeof(double2) * 3 * nn;
+  if ((rc = ensure_scratch(c, 2 * zb + sizeof(double2) * nhalf + sizeof(double) * nn))) return rc;
+  char* base = (char*)c->scratch;
+  double2* Z = (double2*)base;
+  double2* T = (double2*)(base + zb);
+  double2* fk = (double2*)(base + 2 * zb);
+  double* raw = (double*)(base + 2 * zb + sizeof(double2) * nhalf);
+  HIPCHK(c, hipMemcpyAsync(raw, q_grid, sizeof(double) * nn, hipMemcpyHostToDevice, c->stream));
+  // qk = g2k(q) (g2k.m:8-9), exactly swrt_g2k's transform, kept on the device
+  hipLaunchKernelGGL(real_to_complex_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, raw, Z, nn);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = transform_2d(c, Z, T, n, 1, 0))) return rc;
+  hipLaunchKernelGGL(crop_half_kernel, dim3(nblocks(nhalf, 256)), dim3(256), 0, c->stream, T, n, fk);
+  HIPCHK(c, hipGetLastError());
+  // grid_U(qk) (grid_U.m:1-18): the same path as swrt_set_field_qk
+  if ((rc = fields_from_halfplane(c, slot, fk, n, 1, K_d2, k_scale, shear, 0, Z, T, 1, 2 * kmax + 1))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  Slot& s = c->slot[slot];
+  s.L = L;
+  s.ny_period = ny_period;
+  s.set = true;
+  c->keys_fresh = false;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
 int swrt_g2k(swrt_ctx* c, const double* fg, int64_t nx, double* fk_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
@@ -1558,7 +1603,8 @@ int swrt_xka_set_rsw(swrt_ctx* c, const double* state3, int64_t nx, double f, do
   HIPCHK(c, hipGetLastError());
   if ((rc = transform_2d(c, Z, T, n, 3, 0))) return rc;
   // projection + gradients + fulspec (raytrace_sw.m:25-41), then 4 inverse transforms
-  hipLaunchKernelGGL(rsw_spectra_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, n, f, Cg * Cg, Z);
+  hipLaunchKernelGGL(rsw_spectra_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, n, f, Cg * Cg,
+                     (2.0 * M_PI) / L, Z);
   HIPCHK(c, hipGetLastError());
   if ((rc = inverse_2d(c, Z, T, n, 4))) return rc;
   hipLaunchKernelGGL(rsw_unpack_kernel, dim3(nblocks(nn, 256)), dim3(256), 0, c->stream, T, nn, planes);
@@ -1591,13 +1637,24 @@ int swrt_xka_get_fields(swrt_ctx* c, double* fields7_out) {
 
 int64_t swrt_xka_grid(const swrt_ctx* c) { return c ? c->xka_nx : -1; }
 
+int64_t swrt_field_grid(const swrt_ctx* c, int slot) {
+  if (!c || slot < 0 || slot >= SWRT_MAX_SLOTS || !c->slot[slot].set) return -1;
+  return c->slot[slot].nx;
+}
+
+int64_t swrt_qg_grid(const swrt_ctx* c, int* nlayers_out) {
+  if (nlayers_out) *nlayers_out = (c && c->qg.init) ? c->qg.g.nl : 0;
+  if (!c || !c->qg.init) return -1;
+  return c->qg.g.n;
+}
+
 int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, double dt, int64_t nsteps,
                   int64_t save_every, double* hist5) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
   if (!c->xka_nodes) return fail(c, SWRT_ERR_STATE, "call swrt_xka_set_fields first");
   if (n < 0 || nsteps < 0 || save_every < 0) return fail(c, SWRT_ERR_ARG, "negative size");
-  if (n == 0) return SWRT_OK;
+  if (n == 0 || nsteps == 0) return SWRT_OK;  // nothing to advance: state5 unchanged, no frames
   if (!state5) return fail(c, SWRT_ERR_ARG, "state is NULL");
   if (hist5 && save_every > 0 && nsteps % save_every)
     return fail(c, SWRT_ERR_ARG, "nsteps must be a multiple of save_every");
@@ -1704,7 +1761,7 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
       a.perm_out = nullptr;
     }
     a.nsteps = (int)std::min<int64_t>(per_launch, nsteps - s0);
-    a.frame0 = s0 / a.save_every;
+    a.step0 = s0;
     if (tiled && g.tile == 8)
       hipLaunchKernelGGL((xka_tile_kernel<8, kXkaMargin, 256>), dim3(nbins), dim3(256), 0, c->stream, a,
                          (const int*)(c->xka_bins + 2 * kMaxBins), g.ntx);
@@ -2839,12 +2896,10 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
     }
     cur = to;  // accept: y = ynew, F1 = F4
     t = tnew;
-    if (nts >= ts_cap) {
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      commit();
-      return fail(c, SWRT_ERR_ARG, "ode23: more steps than ts_cap");
-    }
-    ts_out[nts++] = t;
+    // ts_cap bounds the times recorded, never the integration: the interval
+    // always completes and nts_out counts every accepted time
+    if (nts < ts_cap) ts_out[nts] = t;
+    ++nts;
     if (done) break;
     if (nofailed) {
       const double temp = 1.25 * std::pow(err / rtol, pw);

@@ -21,7 +21,7 @@ namespace swrt {
 
 // F: forward FFT2 of the 3 state planes, layout [c + n*r] per block (r: kx FFT
 // index, c: ky FFT index), unnormalised.  Z: 4 output spectra, same layout.
-__global__ void rsw_spectra_kernel(const double2* F, int n, double f, double gH0, double2* Z) {
+__global__ void rsw_spectra_kernel(const double2* F, int n, double f, double gH0, double ks, double2* Z) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nn = (int64_t)n * n;
   if (idx >= nn) return;
@@ -43,7 +43,8 @@ __global__ void rsw_spectra_kernel(const double2* F, int n, double f, double gH0
     const double2 uk = make_double2(U.x / nn_d, U.y / nn_d);
     const double2 vk = make_double2(V.x / nn_d, V.y / nn_d);
     const double2 ek = make_double2(E.x / nn_d, E.y / nn_d);
-    const double kxd = (double)hx, kyd = (double)hy;
+    // raytrace_sw.m:16 integer wavenumbers (L = 2*pi: ks = 1.0 exactly); any other L scales them
+    const double kxd = (double)hx * ks, kyd = (double)hy * ks;
     const double K2 = kxd * kxd + kyd * kyd;
     const double sig2 = f * f + gH0 * K2;                                     // :25
     const double2 w = make_double2(kxd * vk.x - kyd * uk.x, kxd * vk.y - kyd * uk.y);

@@ -33,7 +33,7 @@ struct XkaArgs {
   int nsteps;
   int64_t save_every;
   double* hist;        // frames of 5 x n (NULL: none)
-  int64_t frame0;
+  int64_t step0;       // global index of this launch's first step (frames: (step0+s+1) % save_every == 0)
   const int* perm;     // input slot -> caller's packet index (history frames); NULL: identity
   int* perm_out;       // non-NULL (with src): the output slots' permutation, perm[src[p]]
 };
@@ -301,8 +301,9 @@ __device__ __forceinline__ void xka_advance(const XkaArgs& a, const Field& fld, 
     y = Y;
     k = Kn;
     l = Ln;
-    if (a.hist != nullptr && ((s + 1) % a.save_every) == 0) {  // frames in the caller's packet order
-      double* h = a.hist + (a.frame0 + (s + 1) / a.save_every - 1) * 5 * n;
+    const int64_t sg = a.step0 + s + 1;  // global steps done; launches need not align with save_every
+    if (a.hist != nullptr && (sg % a.save_every) == 0) {  // frames in the caller's packet order
+      double* h = a.hist + (sg / a.save_every - 1) * 5 * n;
       h[o] = x; h[n + o] = y; h[2 * n + o] = k; h[3 * n + o] = l; h[4 * n + o] = ac;
     }
   }

@@ -23,6 +23,7 @@ import numpy as np
 from ._lib import Context, QGParams
 from .integrate import PacketEnsemble
 from .io import write_field
+from .runlog import RunLog, parameter_block
 from .scheme import BUMP_QG
 
 
@@ -138,23 +139,6 @@ def _packets(N, L, near_inertial_factor, f, Cg, rng):
     k = np.stack([wf * np.cos(2 * np.pi * i / N), wf * np.sin(2 * np.pi * i / N)], axis=1)
     x = L * rng.random((N, 2)) - L / 2
     return x, k
-
-
-class _Log:
-    def __init__(self, path, verbose):
-        self.f = open(path, "w") if path else None
-        self.verbose = verbose
-
-    def __call__(self, msg):
-        if self.verbose:
-            print(msg, end="")
-        if self.f:
-            self.f.write(msg)
-            self.f.flush()
-
-    def close(self):
-        if self.f:
-            self.f.close()
 
 
 class _IntervalGroup:
@@ -284,7 +268,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
     if rank == 0:
         _fresh_outputs(out_dir, fresh)
-    log = _Log(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
+    log = RunLog(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
     L = 2 * math.pi
     dx = L / nx
     rng = np.random.default_rng(seed)
@@ -304,19 +288,8 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     dt = CFL_fraction * dx / U0
     Nsteps = math.ceil(T / dt)
     packet_step_start = math.ceil(packet_delay / dt)
-    log(f"Resolution: {nx}x{nx}\n")
-    log(f"Number of packets: {Npackets}\n")
-    log(f"Initial wavenumber radius: {near_inertial_factor * f:f}\n")
-    log(f"Time step: {dt:f}\n")
-    log(f"Simulation time: {T:f}\n")
-    log(f"Spin-up time: {packet_delay:f}\n")
-    log(f"Steps per save: {steps_per_save}\n")
-    log(f"Steps per packet save: {packet_steps_per_save}\n")
-    log(f"Coriolis parameter: {f:f}\n")
-    log(f"Group velocity: {Cg:f}\n")
-    log(f"Background velocity (parameter,computed): ({U_g:f},{U0:f})\n")
-    log(f"Froude Number: {Fr:f}\n")
-    log(f"Deformation wavenumber: {K_d2:f}\n")
+    log(parameter_block(nx, Npackets, near_inertial_factor * f, dt, T, packet_delay, steps_per_save,
+                        packet_steps_per_save, f, Cg, U_g, U0, Fr, K_d2))
     ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, bump=BUMP_QG, ctx=ctx,
                          shard=(rank, world)) \
         if Npackets > 0 else None
@@ -330,6 +303,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     nrun = Nsteps if max_steps is None else min(Nsteps, int(max_steps))
     have_cur = False
     group = _IntervalGroup(ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
+    log.start()
     for step in range(1, nrun + 1):
         model.step(dt)
         t = t + dt
@@ -348,8 +322,11 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
         if step % steps_per_save == 0 and rank == 0:
             write_field(model.q(), os.path.join(out_dir, "pv"))
             write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+        log.progress(step, Nsteps)
     if group is not None:
         group.flush()
+    ctx.synchronize()
+    log.finish()
     log.close()
     return dict(dt=dt, Nsteps=Nsteps, steps=nrun, packet_frames=frames, t=t, U0=U0,
                 packet_step_start=packet_step_start)
@@ -367,7 +344,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
     if rank == 0:
         _fresh_outputs(out_dir, fresh)
-    log = _Log(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
+    log = RunLog(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
     L = 20.0
     dx = L / nx
     rng = np.random.default_rng(seed)
@@ -391,19 +368,8 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     dt = CFL_fraction * dx / U0
     Nsteps = math.ceil(T / dt)
     packet_step_start = math.ceil(packet_delay_steps / dt)
-    log(f"Resolution: {nx}x{nx}\n")
-    log(f"Number of packets: {Npackets}\n")
-    log(f"Initial wavenumber radius: {near_inertial_factor * f:f}\n")
-    log(f"Initial time step: {dt:f}\n")
-    log(f"Simulation time: {T:f}\n")
-    log(f"Spin-up time: {packet_delay_steps:f}\n")
-    log(f"Steps per save: {steps_per_save}\n")
-    log(f"Steps per packet save: {packet_steps_per_save}\n")
-    log(f"Coriolis parameter: {f:f}\n")
-    log(f"Group velocity: {Cg:f}\n")
-    log(f"Background velocity (parameter,computed): ({U_g:f},{U0:f})\n")
-    log(f"Froude Number: {Fr:f}\n")
-    log(f"Deformation wavenumber: {K_d2:f}\n")
+    log(parameter_block(nx, Npackets, near_inertial_factor * f, dt, T, packet_delay_steps, steps_per_save,
+                        packet_steps_per_save, f, Cg, U_g, U0, Fr, K_d2, two_layer=True))
     ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=shear, k_scale=2 * math.pi / L, nlayers=2,
                          bump=BUMP_QG, ctx=ctx, shard=(rank, world)) if Npackets > 0 else None
     t = 0.0
@@ -417,12 +383,16 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
                         log)
     # (the reference only plots q every steps_per_save steps in this loop; its
     # pv.bin writes are commented out, qg2layersw_raytrace.m:211-239)
+    log.start()
     while loop.t <= T and (max_steps is None or loop.steps < max_steps):
         if loop.step() and (loop.steps - packet_step_start + 1) % packet_steps_per_save == 0:
             loop.flush()
             ens.write_frame(loop.t, out_dir)
             frames += 1
+        log.progress(loop.steps, Nsteps)
     loop.flush()
+    ctx.synchronize()
+    log.finish()
     log.close()
     dt, dts, step, t, U0 = loop.dt, loop.dts, loop.steps, loop.t, loop.U0
     return dict(dt=dt, dts=dts, Nsteps=Nsteps, steps=step, packet_frames=frames, t=t, U0=U0,

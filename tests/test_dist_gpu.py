@@ -128,3 +128,24 @@ def test_two_rank_driver_files_equal_single_process(ctx, tmp_path, integrator):
     for name in ("packet_x.bin", "packet_k.bin", "packet_time.bin", "pv.bin"):
         a, b = (ref / name).read_bytes(), (out / name).read_bytes()
         assert len(a) > 0 and a == b, name
+
+
+def test_bench_gpus_2_strong_scaling_line(tmp_path):
+    """`bench.py --gpus 2` with no torch.distributed environment launches two
+    ranks as a child torch.distributed.run (gloo: both share GPU 0) and relays
+    rank 0's line: n_gpus 2, the metric's 1e6 packets split 5e5 per GPU."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                            "MASTER_PORT")}
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--steps", "3", "--warmup", "1", "--driver-steps", "0", "--ode23-steps", "0",
+                        "--no-cpu-baseline", "--gather"], cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert out["config"]["packets_total"] == 1_000_000 and out["config"]["packets_per_gpu"] == 500_000
+    assert out["value"] > 0 and out["finite"] and out["gathered_finite"]

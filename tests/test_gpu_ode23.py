@@ -76,6 +76,27 @@ def test_ode23_rejections_happen_and_match(ctx, qg_case, controller):
     np.testing.assert_array_equal(np.concatenate([xg[:, 0], xg[:, 1], kg[:, 0], kg[:, 1]]), yo)
 
 
+def test_ode23_run_ts_cap_bounds_times_only(ctx, qg_case):
+    """A ts_cap smaller than the step count truncates the recorded times; the
+    interval still completes with the full-cap state."""
+    c = qg_case
+    nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    ctx.set_field_grid(0, _planes(c["flow"]), nx, L)
+    ctx.set_field_grid(1, _planes({n: np.asarray(v) * 1.3 for n, v in c["flow"].items()}), nx, L)
+    x, k = c["x"][:128], c["k"][:128]
+    tmax = 40 * c["dt"]
+    out = []
+    for cap in (100_000, 3):
+        ctx.packets_set(x, k)
+        ts, st = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG, ts_cap=cap)
+        out.append((ts, st, *ctx.packets_get()))
+    (ts_a, st_a, xa, ka), (ts_b, st_b, xb, kb) = out
+    assert st_a == st_b and st_a["steps"] > 3
+    np.testing.assert_array_equal(ts_b, ts_a[:3])
+    np.testing.assert_array_equal(xb, xa)
+    np.testing.assert_array_equal(kb, ka)
+
+
 def test_packet_ensemble_ode23_interval(ctx, qg_case):
     """PacketEnsemble.advance_ode23 == ode23(ray_ode, [0, dt], y0) with the
     snapshots in slots 0/1 (the drivers' packet branch)."""

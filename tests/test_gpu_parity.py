@@ -609,6 +609,48 @@ def test_step_packet_xka_binned_order_is_invisible(ctx, nx, steps):
                 assert binned[n][i, j] == P[n]
 
 
+@pytest.mark.parametrize("save_every", [3, 8])
+def test_xka_binned_history_frames_any_save_every(ctx, save_every):
+    """Binned xka launches are cut every rebin_every (4) steps; frames are
+    picked by the global step, so save_every need not divide the launch
+    length: every frame equals the unbinned single-launch path's."""
+    nx = 64
+    U, G, H = _rsw_background(nx)
+    dx = 2 * np.pi / nx
+    rng = np.random.default_rng(12)
+    n, dt, nsteps = 6000, 0.3 * dx, 24
+    st = np.stack([rng.uniform(0, 2 * np.pi, n), rng.uniform(-7, 7, n), 40 * np.cos(np.arange(n)),
+                   40 * np.sin(np.arange(n)), np.ones(n)], axis=1)
+    ctx.xka_set_fields(U, G, H, dx, dx)
+    ctx.set_locality(4, 0)
+    sb, hb = ctx.xka_step(st, 1.0, 4.0, dt, nsteps, save_every)
+    ctx.set_locality(0, 0)
+    try:
+        sp, hp = ctx.xka_step(st, 1.0, 4.0, dt, nsteps, save_every)
+    finally:
+        ctx.set_locality(4, 0)
+    assert hb.shape == (nsteps // save_every, n, 5)
+    np.testing.assert_array_equal(sb, sp)
+    np.testing.assert_array_equal(hb, hp)
+    np.testing.assert_array_equal(hb[-1], sb)
+
+
+def test_xka_zero_steps_leaves_state(ctx):
+    """nsteps == 0 on a binned-size ensemble: no launch, state unchanged."""
+    nx = 64
+    U, G, H = _rsw_background(nx)
+    dx = 2 * np.pi / nx
+    rng = np.random.default_rng(13)
+    n = 6000
+    st = np.stack([rng.uniform(0, 2 * np.pi, n), rng.uniform(0, 2 * np.pi, n), rng.normal(size=n),
+                   rng.normal(size=n), np.ones(n)], axis=1)
+    ctx.xka_set_fields(U, G, H, dx, dx)
+    ctx.set_locality(4, 0)
+    s0, h0 = ctx.xka_step(st, 1.0, 4.0, 0.1 * dx, 0, 0)
+    assert h0 is None
+    np.testing.assert_array_equal(s0, st)
+
+
 def test_step_packet_xka_scalar_api(ctx):
     import swraytracing_amd as sw
     nx = 32

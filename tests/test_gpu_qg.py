@@ -217,6 +217,7 @@ def test_qgsw_driver_packets_match_oracle_pipeline(ctx, oracle_lib, tmp_path):
     tg = sw.read_field(str(tmp_path / "packet_time"))
     frames = 1 + 12 // 5
     assert xg.shape == (N, 2, frames) and tg.shape == (1, frames)
+    _load_data_reads(tmp_path, nx, N, f, Cg, 0.2)
     # oracle pipeline from the same initial state
     rng = np.random.default_rng(146)
     L = 2 * np.pi
@@ -251,8 +252,24 @@ def test_qg2layer_driver_runs_and_writes(ctx, tmp_path):
     assert np.isfinite(xg).all()
     pv = sw.read_field(str(tmp_path / "pv"), nx, nx, 2)
     assert pv.shape == (nx, nx, 2)
-    log = open(tmp_path / "run.log").read()
-    assert "Resolution: 64x64" in log and "Froude Number" in log
+    _load_data_reads(tmp_path, nx, N, 3.0, 1.0, 0.2)
+
+
+def _load_data_reads(d, nx, N, f, Cg, Ug):
+    """analysis/load_data.m:18-32 on a driver's output directory, unchanged:
+    the five textscan calls on run.log (header offsets 10 and 7), then
+    read_field(packet_time) and read_field(packet_x/k, Npackets, 2, 1, 1:frames)."""
+    from tests.matlab_textscan import load_data_header
+    h = load_data_header(str(d / "run.log"))
+    assert h["resolution"] == (nx, nx) and h["Npackets"] == N
+    assert h["f"] == f and h["Cg"] == Cg and h["Ug"][0] == Ug and h["Ug"][1] > 0
+    t = sw.read_field(str(d / "packet_time"))
+    frames = t.shape[1]
+    for name in ("packet_x", "packet_k"):
+        a = sw.read_field(str(d / name), h["Npackets"], 2, 1, list(range(1, frames + 1)))
+        a = a.reshape(N, 2, frames)
+        assert np.isfinite(a).all()
+    assert open(d / "run.log").read().rstrip("\n").split("\n")[-1].startswith("Real time elapsed: ")
 
 
 def test_golden_qg_fixture(ctx):

@@ -76,6 +76,18 @@ def test_xka_set_rsw_other_parameters(ctx):
     _fields_close(ctx, orc.rsw_background(S, f, Cg))
 
 
+def test_xka_set_rsw_non_2pi_period(ctx):
+    """L = 20: wavenumbers scaled by 2*pi/L on the device as in the oracle
+    (raytrace_sw.m itself uses L = 2*pi); dx = L/nx for the packet steps."""
+    f, Cg, nx, L = 2.0, 1.0, 64, 20.0
+    S = balanced_state(nx, f, Cg, seed=9)
+    ctx.xka_set_rsw(S, f, Cg, L)
+    bg = orc.rsw_background(S, f, Cg, L)
+    _fields_close(ctx, bg)
+    # the 2*pi fields differ: the scaling is real
+    assert _rel(orc.rsw_background(S, f, Cg)["GradU"]["u_x"], bg["GradU"]["u_x"]) > 1e-3
+
+
 def test_matlab_wave_has_no_geostrophic_background_on_device(ctx, mat):
     S = np.stack([mat["u"], mat["v"], mat["h"]], axis=2)
     ctx.xka_set_rsw(S, 1.0, 1.0)

@@ -56,6 +56,11 @@ def main():
         v.sort()
         rec[c] = v[len(v) // 2]
     rec["source"] = "rocprofv3 --pmc passes (tools/pmc_collect.sh), median dispatch"
+    # bind the counters to the device code they were collected on (bench.py
+    # refuses a record whose hash differs from the library it times)
+    sys.path.insert(0, ROOT)
+    from swraytracing_amd._lib import device_code_sha256
+    rec["code_object_sha256"] = device_code_sha256()
     out = {config_key(args): rec}
     json.dump(out, open(os.path.join(d, "pmc.json"), "w"), indent=1, sort_keys=True)
     print(json.dumps(out))
