@@ -321,6 +321,8 @@ def parse_args(argv=None):
                     help="initial packet positions (stratified: equal packets per tile, a diagnostic)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-fma", action="store_true",
+                    help="skip the extra line of the opt-in FMA gather mode (swrt_set_gather_mode 1, tolerance parity)")
     ap.add_argument("--no-forecast", action="store_true",
                     help="at N = 1, skip the strong-scaling forecast (the workload at 2/4/8-GPU shard sizes)")
     ap.add_argument("--rebin-every", type=int, default=20, help="steps between spatial re-binning (0: off)")
@@ -542,6 +544,20 @@ def main(argv=None):
     }
     if gathered is not None:
         out["gathered_finite"] = gathered
+    if not args.no_fma and args.blend_mode == 0 and args.kernel in (0, 2):
+        # the opt-in FMA gather (tolerance parity, tests/test_gpu_parity.py::test_fma_gather_mode_tolerance):
+        # the same workload and packets, timed the same way; the headline stays bit-exact
+        ctx.packets_set(w["x"], w["k"])
+        ctx.set_gather_mode(1)
+        el2, kms2, l2 = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
+        ctx.set_gather_mode(0)
+        if distributed:
+            el2 = max_over_ranks(el2, backend=args.dist_backend)
+        ctx.packets_set(w["x"], w["k"])
+        out["fma_gather"] = {"value": total_ps / el2, "ms_per_step": el2 / args.steps * 1e3,
+                             "avg_launch_ms": (kms2 / l2) if l2 else None, "vs_exact": elapsed / el2,
+                             "parity": "tolerance: stencil sums and blend by fused multiply-add, "
+                                       "<= 1e-13 relative per step vs the bit-exact path"}
     if world == 1 and not args.no_forecast and args.scaling == "strong" and args.intervals == 1:
         out["strong_scaling_forecast"] = strong_scaling_forecast(ctx, w, args, dev, n_total, value)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -196,6 +196,18 @@ int swrt_set_tile_order(swrt_ctx* ctx, int longest_first);
  * advance one step each. */
 int swrt_set_blend_mode(swrt_ctx* ctx, int mode);
 
+/* Opt-in stencil arithmetic of the LDS-tiled packet kernel for fields with
+ * v_y == -u_x (every field the library derives from psi / qk): 1 = each
+ * tap's wij*F added by one fused multiply-add (and the snapshot blend as
+ * (1-alpha)*I1 + alpha*I2 with one FMA), which drops ~350 of the ~1,100 VALU
+ * instructions of a packet-step; the sums keep interpolate.m:43-49's order
+ * but round once per tap instead of twice, so results agree with the
+ * reference to tolerance (per step ~1e-15 relative), not bit for bit.
+ * 0 (default) = mul then add, bit-identical to the reference's arithmetic.
+ * Other kernels (host-given six-field windows, the per-packet kernel, ode23,
+ * xka) always use mul then add. */
+int swrt_set_gather_mode(swrt_ctx* ctx, int mode);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

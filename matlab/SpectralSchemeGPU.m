@@ -3,19 +3,22 @@ classdef SpectralSchemeGPU < RaytracingScheme
     % library through swrt_mex: same constructor signature, same properties
     % (U_field, GradU_field, psi_field, L; SpectralScheme.m:3) and the same
     % U / grad_U / streamfunction results (bit-identical interpolation
-    % arithmetic on the device's fields).  Each instance owns a library
-    % context (handle h) holding its fields, as each SpectralScheme owns its
-    % fields (SpectralScheme.m:28-35); release(scheme) frees it early,
-    % otherwise it lives until the MEX file is cleared.
+    % arithmetic on the device's fields).  Each instance holds a library
+    % context with its fields, as each SpectralScheme owns its fields
+    % (SpectralScheme.m:28-35).  The context is a SwrtContext (a handle
+    % object): copies of a scheme share it and it is destroyed with its last
+    % reference, so building one scheme per snapshot does not accumulate
+    % device memory; release(scheme) frees it early for every copy.
     properties
-        L, nx, bump, psi_field, h
+        L, nx, bump, psi_field, ctx
     end
     properties (Dependent)
+        h                       % the swrt_mex handle of ctx (errors once released)
         U_field, GradU_field    % downloaded from the device on access
     end
     methods
         function obj = SpectralSchemeGPU(L, nx, psi_field)
-            obj.h = swrt_mex('create', 0);
+            obj.ctx = SwrtContext(0);
             obj.L = L;
             obj.nx = nx;
             obj.bump = 1e-13;   % ray_trace_sw/interpolate.m (addpath order of the original ctor)
@@ -33,8 +36,12 @@ classdef SpectralSchemeGPU < RaytracingScheme
             s.u_x = F(:,:,3); s.u_y = F(:,:,4); s.v_x = F(:,:,5); s.v_y = F(:,:,6);
         end
 
+        function h = get.h(obj)
+            h = obj.ctx.id();
+        end
+
         function release(obj)
-            swrt_mex('destroy', obj.h);
+            obj.ctx.release();
         end
 
         function psi = streamfunction(obj, x, y, t)

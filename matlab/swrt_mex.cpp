@@ -14,7 +14,8 @@
 // Build (MATLAB R2018a+, interleaved complex):
 //   mex -R2018a -I../include swrt_mex.cpp -L../swraytracing_amd -lswrt
 // Usage (see SpectralSchemeGPU.m, ode_symplectic_gpu.m, ode23_packets_gpu.m):
-//   h = swrt_mex('create', device);   swrt_mex('destroy', h)
+//   h = swrt_mex('create', device);   swrt_mex('destroy', h)    % through SwrtContext (a handle class)
+//   n = swrt_mex('live')                                        % open contexts
 //   swrt_mex('set_field_psi', h, slot, psi_grid, L)           % SpectralScheme ctor
 //   swrt_mex('set_field_qk', h, slot, qk, L, K_d2, shear, kscale, ny_period)   % grid_U
 //   swrt_mex('set_field_grid', h, slot, u, v, ux, uy, vx, vy, L, ny_period)
@@ -50,6 +51,12 @@ static void cleanup() {
       c = nullptr;
     }
   g_ctx.clear();
+}
+
+static size_t live_contexts() {
+  size_t n = 0;
+  for (swrt_ctx* c : g_ctx) n += c != nullptr;
+  return n;
 }
 
 static double scalar(const mxArray* a) { return mxGetScalar(a); }
@@ -90,7 +97,7 @@ static void need(int nrhs, int n, const char* cmd) {
 static int64_t slot_grid(swrt_ctx* c, int slot, int64_t nx_arg) {
   const int64_t nx = swrt_field_grid(c, slot);
   if (nx < 0) mexErrMsgIdAndTxt("swrt:state", "field slot %d is not set", slot);
-  if (nx_arg != nx) mexErrMsgIdAndTxt("swrt:arg", "slot %d holds an %lld grid, not %lld", slot, (long long)nx,
+  if (nx_arg != nx) mexErrMsgIdAndTxt("swrt:arg", "slot %d holds a %lld^2 grid, not %lld^2", slot, (long long)nx,
                                       (long long)nx_arg);
   return nx;
 }
@@ -114,21 +121,24 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     swrt_ctx* c = nullptr;
     const int rc = swrt_create(dev, &c);
     if (rc != SWRT_OK) mexErrMsgIdAndTxt("swrt:create", "swrt_create failed (code %d)", rc);
-    if (g_ctx.empty()) {
-      mexAtExit(cleanup);
-      mexLock();
-    }
-    g_ctx.push_back(c);
+    if (g_ctx.empty()) mexAtExit(cleanup);
+    if (live_contexts() == 0) mexLock();  // stay loaded while a context is open
+    g_ctx.push_back(c);  // handles are never reused: a stale copy of a closed one fails, never aliases
     plhs[0] = mxCreateDoubleScalar((double)g_ctx.size());
+    return;
+  }
+  if (!strcmp(cmd, "live")) {  // () -> number of open contexts (SwrtContext lifetime tests)
+    plhs[0] = mxCreateDoubleScalar((double)live_contexts());
     return;
   }
   swrt_ctx* c = handle(nrhs, prhs);
   const mxArray** a = prhs + 1;  // a[1] = first argument after the handle
   const int na = nrhs - 1;
 
-  if (!strcmp(cmd, "destroy")) {
+  if (!strcmp(cmd, "destroy")) {  // SwrtContext.delete: the last reference to a context is gone
     swrt_destroy(c);
     g_ctx[(size_t)scalar(prhs[1]) - 1] = nullptr;
+    if (live_contexts() == 0) mexUnlock();  // `clear mex` may unload the gateway again
     return;
   }
   if (!strcmp(cmd, "set_field_psi")) {  // (slot, psi, L)

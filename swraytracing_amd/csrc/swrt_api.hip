@@ -178,6 +178,7 @@ struct swrt_ctx {
   bool tile_order = SWRT_TILE_ORDER;  // LDS-tiled launches take each XCD band's tiles longest first
   bool qg_graphs = SWRT_QG_GRAPHS;         // replay steady QG steps as hipGraphs
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
+  int gather_mode = 0;      // 0: stencil sums mul then add (bit-exact); 1: fused multiply-add (tolerance)
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
   double* hx = nullptr;
@@ -698,13 +699,21 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
     launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(wgrid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
-    if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free))
-      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
-               dim3(kTileThreads), t);
-    else
+    if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)) {
+      if (c->gather_mode == 1)
+        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true>, dim3(wgrid),
+                 dim3(kTileThreads), t);
+      else
+        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
+                 dim3(kTileThreads), t);
+    } else {
       launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, dim3(wgrid), dim3(kTileThreads), t);
+    }
   } else {
-    if (c->slot[0].div_free)
+    if (c->slot[0].div_free && c->gather_mode == 1)
+      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true, true>, dim3(wgrid),
+               dim3(kTileThreads), t);
+    else if (c->slot[0].div_free)
       launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
                dim3(kTileThreads), t);
     else
@@ -1374,6 +1383,13 @@ int swrt_set_blend_mode(swrt_ctx* c, int mode) {
   if (!c) return SWRT_ERR_ARG;
   if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "blend mode must be 0 or 1");
   c->blend_mode = mode;
+  return SWRT_OK;
+}
+
+int swrt_set_gather_mode(swrt_ctx* c, int mode) {
+  if (!c) return SWRT_ERR_ARG;
+  if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "gather mode must be 0 or 1");
+  c->gather_mode = mode;
   return SWRT_OK;
 }
 

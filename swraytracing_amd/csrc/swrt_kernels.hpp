@@ -354,7 +354,18 @@ __device__ __forceinline__ void interp6(const FieldView& fv, double x, double y,
 // scheduling barrier after every tap, so at most one tap's 6 records are in
 // flight: the register-light global fallback of the LDS-tiled kernels, whose
 // hot path then needs no spills.  Rare path; its speed is secondary.
-template <bool TWO>
+// acc + w*v: mul then add (the reference's rounding, bit-exact) or, in the
+// opt-in FMA gather mode (swrt_set_gather_mode 1), one fused multiply-add —
+// the same sum with one rounding fewer per tap (tolerance parity).
+template <bool FMA>
+__device__ __forceinline__ double madd(double acc, double w, double v) {
+  if constexpr (FMA)
+    return __builtin_fma(w, v, acc);
+  else
+    return acc + w * v;
+}
+
+template <bool TWO, bool FMA = false>
 __device__ __forceinline__ void gather6_lean(const double* nodes0, const double* nodes1, int npad,
                                              const Stencil& s, double o0[kRec], double o1[kRec]) {
 #pragma unroll
@@ -369,14 +380,14 @@ __device__ __forceinline__ void gather6_lean(const double* nodes0, const double*
     for (int j = 0; j < kNT; ++j) {
       const double wij = s.wx[i] * s.wy[j];
       const double2 a0 = r0[3 * j + 0], a1 = r0[3 * j + 1], a2 = r0[3 * j + 2];
-      o0[0] = o0[0] + wij * a0.x; o0[1] = o0[1] + wij * a0.y;
-      o0[2] = o0[2] + wij * a1.x; o0[3] = o0[3] + wij * a1.y;
-      o0[4] = o0[4] + wij * a2.x; o0[5] = o0[5] + wij * a2.y;
+      o0[0] = madd<FMA>(o0[0], wij, a0.x); o0[1] = madd<FMA>(o0[1], wij, a0.y);
+      o0[2] = madd<FMA>(o0[2], wij, a1.x); o0[3] = madd<FMA>(o0[3], wij, a1.y);
+      o0[4] = madd<FMA>(o0[4], wij, a2.x); o0[5] = madd<FMA>(o0[5], wij, a2.y);
       if constexpr (TWO) {
         const double2 b0 = r1[3 * j + 0], b1 = r1[3 * j + 1], b2 = r1[3 * j + 2];
-        o1[0] = o1[0] + wij * b0.x; o1[1] = o1[1] + wij * b0.y;
-        o1[2] = o1[2] + wij * b1.x; o1[3] = o1[3] + wij * b1.y;
-        o1[4] = o1[4] + wij * b2.x; o1[5] = o1[5] + wij * b2.y;
+        o1[0] = madd<FMA>(o1[0], wij, b0.x); o1[1] = madd<FMA>(o1[1], wij, b0.y);
+        o1[2] = madd<FMA>(o1[2], wij, b1.x); o1[3] = madd<FMA>(o1[3], wij, b1.y);
+        o1[4] = madd<FMA>(o1[4], wij, b2.x); o1[5] = madd<FMA>(o1[5], wij, b2.y);
       }
       __builtin_amdgcn_sched_barrier(0);
     }

@@ -247,7 +247,7 @@ __device__ __forceinline__ void tap5_read(const double2* p, int e, Tap5<TWO>& t)
     t.c.x = reinterpret_cast<const double*>(p + 2 * WN + e)[0];
   }
 }
-template <bool TWO, int W, int WN>
+template <bool TWO, int W, int WN, bool FMA = false>
 __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const Stencil& s,
                                             double o0[kRec], double o1[kRec]) {
 #pragma unroll
@@ -269,13 +269,13 @@ __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const
     if (t + 1 < kNT * kNT) tap5_read<TWO, WN>(p, ((t + 1) / kNT) * W + (t + 1) % kNT, nxt);
     __builtin_amdgcn_sched_barrier(0);
     const double wij = wx[i] * wy[j];
-    o0[0] = o0[0] + wij * cur.a0.x; o0[1] = o0[1] + wij * cur.a0.y;
-    o0[2] = o0[2] + wij * cur.a1.x; o0[3] = o0[3] + wij * cur.a1.y;
-    o0[4] = o0[4] + wij * cur.c.x;
+    o0[0] = madd<FMA>(o0[0], wij, cur.a0.x); o0[1] = madd<FMA>(o0[1], wij, cur.a0.y);
+    o0[2] = madd<FMA>(o0[2], wij, cur.a1.x); o0[3] = madd<FMA>(o0[3], wij, cur.a1.y);
+    o0[4] = madd<FMA>(o0[4], wij, cur.c.x);
     if constexpr (TWO) {
-      o1[0] = o1[0] + wij * cur.b0.x; o1[1] = o1[1] + wij * cur.b0.y;
-      o1[2] = o1[2] + wij * cur.b1.x; o1[3] = o1[3] + wij * cur.b1.y;
-      o1[4] = o1[4] + wij * cur.c.y;
+      o1[0] = madd<FMA>(o1[0], wij, cur.b0.x); o1[1] = madd<FMA>(o1[1], wij, cur.b0.y);
+      o1[2] = madd<FMA>(o1[2], wij, cur.b1.x); o1[3] = madd<FMA>(o1[3], wij, cur.b1.y);
+      o1[4] = madd<FMA>(o1[4], wij, cur.c.y);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < kNT * kNT) cur = nxt;
@@ -372,8 +372,11 @@ __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 #define SWRT_TILE_MIN_WAVES 4
 #endif
 
-template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false>
+// FMA (opt-in gather mode 1, V5 windows only): the stencil sums and the
+// snapshot blend as fused multiply-adds — tolerance parity, not bits.
+template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false, bool FMA = false>
 __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
+  static_assert(!FMA || (V5 && !WBLEND), "the FMA gather exists for the five-sum window only");
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
   // row stride = 12 (mod 16) nodes: any 4x4 block of window nodes falls on
   // 16 distinct ds_read_b128 bank quads (node n -> quad (n mod 16)), so lanes
@@ -561,11 +564,11 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         } else {
           if (inwin) {
             if constexpr (V5)
-              gather5_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+              gather5_lds<TWO, WS, WNP, FMA>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
             else
               gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
           } else {
-            gather6_lean<TWO>(fa.nodes, fb.nodes, npad, sc, I, J);
+            gather6_lean<TWO, FMA>(fa.nodes, fb.nodes, npad, sc, I, J);
           }
           if constexpr (TWO) {
             const double oma = 1 - alpha;
@@ -573,7 +576,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
             // sum them in the same order), so the blended v_y is exactly the
             // negated blended u_x: negation commutes with every rounding
 #pragma unroll
-            for (int q = 0; q < (V5 ? 5 : kRec); ++q) I[q] = oma * I[q] + alpha * J[q];
+            for (int q = 0; q < (V5 ? 5 : kRec); ++q) I[q] = madd<FMA>(oma * I[q], alpha, J[q]);
             if constexpr (V5) I[5] = -I[2];
           }
         }

@@ -714,6 +714,49 @@ def test_blend_in_window_mode_tolerance(ctx, oracle_lib, qg_case, dt_scale):
     np.testing.assert_allclose(kg, ko, rtol=rtol, atol=atol)
 
 
+@pytest.mark.parametrize("n_cells", [1, 3])
+def test_fma_gather_mode_tolerance(ctx, oracle_lib, n_cells):
+    """swrt_set_gather_mode(1): the stencil sums and the snapshot blend by
+    fused multiply-add (one rounding per tap instead of two).  Tolerance
+    parity against the bit-exact oracle on the bench's device-derived 512^2
+    fields (five-sum window): <= 1e-13 relative per step over 20 steps
+    (k, |x|); the default mode stays bit-identical (same launch, mode 0)."""
+    import argparse
+    import bench
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=200_000, world=1, rank=0, seed=146, mode="blend")
+    w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
+    assert ctx.field_div_free(0) and ctx.field_div_free(1)
+    nsteps, sub = 20, 5
+    # n_cells = 3: a 3x longer step, so some packets leave the LDS window (global FMA fallback)
+    h = w["dt"] / sub * n_cells
+    ctx.set_locality(20, 0)
+    out = {}
+    try:
+        for mode in (1, 0):
+            ctx.set_gather_mode(mode)
+            ctx.packets_set(w["x"], w["k"])
+            for _ in range(nsteps // sub):
+                ctx.advance(h, sub, w["f"], w["gH"], nslots=2, alpha0=0.5 / sub, dalpha=1.0 / sub, bump=orc.BUMP_QG)
+            out[mode] = ctx.packets_get()
+    finally:
+        ctx.set_gather_mode(0)
+        ctx.set_locality(4, 0)
+    p0, p1 = ctx.get_field_grid(0), ctx.get_field_grid(1)
+    idx = np.sort(np.random.default_rng(9).choice(args.packets, 2000, replace=False))
+    xo, ko = w["x"][idx], w["k"][idx]
+    for _ in range(nsteps // sub):
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.5 / sub, 1.0 / sub, 512, 1024, w["L"] / 512, orc.BUMP_QG,
+                                           xo, ko, h, sub, w["f"], w["gH"])
+    np.testing.assert_array_equal(out[0][0][idx], xo)   # mode 0: bit-exact
+    np.testing.assert_array_equal(out[0][1][idx], ko)
+    xf, kf = out[1][0][idx], out[1][1][idx]
+    tol = nsteps * 1e-13
+    assert np.abs(xf - xo).max() <= tol * np.abs(xo).max()
+    assert np.abs(kf - ko).max() <= tol * np.abs(ko).max()
+    assert not np.array_equal(xf, xo)  # the FMA path really ran
+
+
 @pytest.mark.parametrize("substeps,rebin_every,calls", [(5, 20, 10), (1, 4, 12)])
 def test_bench_configuration_subset_bitexact(ctx, oracle_lib, substeps, rebin_every, calls):
     """The headline bench configuration itself (bench.py: 2-layer 512^2 field,
@@ -724,11 +767,12 @@ def test_bench_configuration_subset_bitexact(ctx, oracle_lib, substeps, rebin_ev
     packets bit-identical to the C oracle on the same device-prepared fields."""
     import argparse
     import bench
+    bench._imports()
     args = argparse.Namespace(nx=512, packets=1_000_000, world=1, rank=0, seed=146, mode="blend")
     ctx.set_locality(rebin_every, 0)
     ctx.set_kernel(0)
     try:
-        w = bench.build_workload(ctx, args, np.random.default_rng(146))
+        w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
         ctx.packets_set(w["x"], w["k"])
         for _ in range(calls):
             bench.step(ctx, w, substeps)

@@ -334,3 +334,60 @@ def test_ode23_packets_gpu_m_matches_python_controller(mex, ctx, qg_case):
     np.testing.assert_array_equal(xm, xp)
     np.testing.assert_array_equal(km, kp)
     assert len(tm) > 2
+
+
+class _SwrtContext:
+    """matlab/SwrtContext.m restated (a MATLAB handle object: delete runs when
+    its last reference goes, release() closes it for every holder)."""
+
+    def __init__(self, mex, device=0.0):
+        self.mex = mex
+        self.h = mex("create", device)
+
+    def id(self):
+        if self.h == 0:
+            raise MexError("swrt:state: closed context")
+        return self.h
+
+    def release(self):
+        if self.h != 0:
+            self.mex("destroy", self.h)
+            self.h = 0
+
+    def __del__(self):
+        self.release()
+
+
+@pytest.mark.gpu
+def test_scheme_contexts_freed_with_last_reference(mex):
+    """One SpectralSchemeGPU per snapshot (50 of them, each dropped after
+    use) keeps at most one context open; value copies share one SwrtContext
+    (SpectralSchemeGPU.m ctx), which stays open until the last copy goes."""
+    import gc
+    nx = 64
+    base = mex("live")
+    peak = 0
+    for i in range(50):
+        ctx = _SwrtContext(mex)                      # SpectralSchemeGPU ctor: obj.ctx = SwrtContext(0)
+        mex("set_field_psi", ctx.id(), 0.0, _psi(nx, i), 2 * np.pi)
+        peak = max(peak, mex("live") - base)
+        del ctx
+        gc.collect()
+    assert peak == 1 and mex("live") == base
+    a = _SwrtContext(mex)
+    copy = a                                         # s2 = s1: a value copy holds the same handle object
+    mex("set_field_psi", a.id(), 0.0, _psi(nx, 1), 2 * np.pi)
+    del a
+    gc.collect()
+    assert mex("live") == base + 1                   # the copy keeps it open
+    F = mex("get_fields", copy.id(), 0.0, float(nx))
+    assert F.shape == (nx, nx, 6)
+    with pytest.raises(MexError, match=r"holds a 64\^2 grid, not 32\^2"):
+        mex("get_fields", copy.id(), 0.0, 32.0)      # the library's size, never the caller's
+    h = copy.h
+    copy.release()                                   # release(scheme): closed for every copy
+    assert mex("live") == base
+    with pytest.raises(MexError, match="closed context"):
+        copy.id()
+    with pytest.raises(MexError, match="invalid or closed context handle"):
+        mex("get_fields", h, 0.0, float(nx))
