@@ -330,6 +330,8 @@ def parse_args(argv=None):
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
     ap.add_argument("--blend-mode", type=int, default=0,
                     help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
+    ap.add_argument("--lanes-per-packet", type=int, default=0,
+                    help="LDS-tiled launches: 0 auto (paired lanes below 384 packets per tile), 1, 2 (same bits)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--tail-split", type=int, default=-1,
@@ -479,6 +481,7 @@ def main(argv=None):
     ctx.set_kernel(args.kernel)
     ctx.set_cell_sort(args.cell_sort)
     ctx.set_blend_mode(args.blend_mode)
+    ctx.set_lanes_per_packet(args.lanes_per_packet)
     if args.tail_split >= 0:
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
     if args.tile_order >= 0:
@@ -537,6 +540,7 @@ def main(argv=None):
                    "steps_per_launch": spl, "intervals_per_step": ivs,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split,
+                   "lanes_per_packet": args.lanes_per_packet,
                    "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,
@@ -571,6 +575,10 @@ def main(argv=None):
             allc = os.cpu_count() or 1
         if allc != threads:
             out["cpu_baseline_all_cores"] = cpu_baseline(ctx, w, args.cpu_seconds * 2 / 3, allc)
+            out["cpu_baseline_all_cores"]["note"] = (
+                f"{allc} OpenMP threads = every CPU this process may run on; the job's cgroup CPU quota "
+                f"({host_cpu()['cgroup_cpu_quota']} cores) caps them, so cpu_baseline's {threads} threads is the "
+                f"faster figure on this box")
         out["cpu_baseline_1core"] = cpu_baseline(ctx, w, args.cpu_seconds / 3, 1)
     elif rank == 0:
         out["cpu_baseline"] = None

@@ -208,6 +208,16 @@ int swrt_set_blend_mode(swrt_ctx* ctx, int mode);
  * xka) always use mul then add. */
 int swrt_set_gather_mode(swrt_ctx* ctx, int mode);
 
+/* Lanes per packet of the LDS-tiled two-snapshot launch (fields with v_y ==
+ * -u_x): 1 = one lane advances a packet; 2 = two lanes of one wave share it
+ * (one computes the x weights and snapshot 1's five stencil sums, the other
+ * the y weights and snapshot 2's; cross-lane swaps combine them), so a tile
+ * with few packets still keeps two waves per SIMD busy — small shards of a
+ * strongly scaled ensemble.  0 (default) = 2 below SWRT_PAIR_BELOW packets
+ * per tile on average, else 1.  Every sum keeps the reference's order:
+ * results are bit-identical for any setting. */
+int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

@@ -71,6 +71,7 @@ SIGNATURES = {
     "swrt_set_tail_split": (_INT, [_VP, _INT, _INT]),
     "swrt_set_blend_mode": (_INT, [_VP, _INT]),
     "swrt_set_gather_mode": (_INT, [_VP, _INT]),
+    "swrt_set_lanes_per_packet": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_advance_intervals": (_INT, [_VP, _INT, _VP, _I, _D, _D, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
@@ -344,6 +345,10 @@ class Context:
         """swrt_set_gather_mode: 0 bit-exact mul-then-add stencil sums (default),
         1 fused multiply-add (tolerance parity, fewer VALU instructions)."""
         self._chk(self._L.swrt_set_gather_mode(self._h, int(mode)), "swrt_set_gather_mode")
+
+    def set_lanes_per_packet(self, lanes=0):
+        """swrt_set_lanes_per_packet: 0 auto (paired lanes for small tiles), 1, 2; same bits."""
+        self._chk(self._L.swrt_set_lanes_per_packet(self._h, int(lanes)), "swrt_set_lanes_per_packet")
 
     def set_blend_mode(self, mode=0):
         """0: bit-exact interpolate-then-blend; 1: blend in the LDS window (tolerance parity)."""

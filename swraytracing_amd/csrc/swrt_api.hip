@@ -60,6 +60,11 @@ constexpr int kXkaMargin = 3;           // xka_tile_kernel: drift margin (cells)
 constexpr int kTile = SWRT_TILE;                // LDS tile kernel: cells per tile side
 constexpr int kMargin = SWRT_MARGIN;            // LDS tile kernel: drift margin (cells)
 constexpr int kTileThreads = SWRT_TILE_THREADS;
+#ifndef SWRT_PAIR_BELOW
+#define SWRT_PAIR_BELOW 384
+#endif
+// paired-lane tile launches (swrt_tile.hpp PAIR) below this many packets per tile
+constexpr int kPairBelow = SWRT_PAIR_BELOW;
 
 struct Slot {
   double* nodes = nullptr;  // padded interleaved records
@@ -179,6 +184,7 @@ struct swrt_ctx {
   bool qg_graphs = SWRT_QG_GRAPHS;         // replay steady QG steps as hipGraphs
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   int gather_mode = 0;      // 0: stencil sums mul then add (bit-exact); 1: fused multiply-add (tolerance)
+  int lanes_per_packet = 0; // LDS-tiled two-snapshot launches: 1, 2 (paired lanes), 0 = by packets per tile
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
   double* hx = nullptr;
@@ -700,7 +706,17 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(wgrid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
     if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)) {
-      if (c->gather_mode == 1)
+      // paired lanes when the tiles hold few packets (a workgroup would have
+      // one or two busy waves): two waves per packet run instead of one
+      const bool pair = c->lanes_per_packet == 2 ||
+                        (c->lanes_per_packet == 0 && c->n < (int64_t)kPairBelow * (int64_t)grid);
+      if (pair && c->gather_mode == 1)
+        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true, true>, dim3(wgrid),
+                 dim3(kTileThreads), t);
+      else if (pair)
+        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, false, true>, dim3(wgrid),
+                 dim3(kTileThreads), t);
+      else if (c->gather_mode == 1)
         launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true>, dim3(wgrid),
                  dim3(kTileThreads), t);
       else
@@ -1390,6 +1406,13 @@ int swrt_set_gather_mode(swrt_ctx* c, int mode) {
   if (!c) return SWRT_ERR_ARG;
   if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "gather mode must be 0 or 1");
   c->gather_mode = mode;
+  return SWRT_OK;
+}
+
+int swrt_set_lanes_per_packet(swrt_ctx* c, int lanes) {
+  if (!c) return SWRT_ERR_ARG;
+  if (lanes < 0 || lanes > 2) return fail(c, SWRT_ERR_ARG, "lanes per packet must be 0 (auto), 1 or 2");
+  c->lanes_per_packet = lanes;
   return SWRT_OK;
 }
 

@@ -284,6 +284,74 @@ __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const
   o1[5] = -o1[2];
 }
 
+// ---- paired lanes (small ensembles) ---------------------------------------
+// With few packets per tile a workgroup has one or two busy waves, one wave
+// per SIMD, and a lone wave issues far below the SIMD's rate.  The PAIR form
+// of the tile kernel advances each packet on two lanes of one wave, lane p
+// and lane p + 32: lane half h = 0 computes the x weights and snapshot 0's
+// five stencil sums, h = 1 the y weights and snapshot 1's — each sum in the
+// reference's order, so the results are those of the one-lane kernel bit for
+// bit — and v_permlane32_swap hands each half's values to the other.
+//
+// v_permlane32_swap_b32 exchanges lanes 32-63 of its first register with
+// lanes 0-31 of its second; given the same value v in both, the first comes
+// back as v of the lower half on every lane and the second as v of the
+// upper half: the h = 0 and h = 1 values of the lane's packet.
+__device__ __forceinline__ void halves_u32(unsigned v, unsigned& lo, unsigned& hi) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  lo = r[0];
+  hi = r[1];
+}
+__device__ __forceinline__ void halves_f64(double v, double& lo, double& hi) {
+  unsigned l0, l1, u0, u1;
+  halves_u32((unsigned)__double2loint(v), l0, l1);
+  halves_u32((unsigned)__double2hiint(v), u0, u1);
+  lo = __hiloint2double((int)u0, (int)l0);
+  hi = __hiloint2double((int)u1, (int)l1);
+}
+
+// One half's five sums of the V5 window (gather5_lds's snapshot h): chunks
+// 3h and 3h+1 hold {u,v} and {u_x,u_y}, chunk 2 holds {v_x of 0, v_x of 1}.
+// Same per-field order, pipelined one tap ahead as gather5_lds.
+template <int W, int WN, bool FMA = false>
+__device__ __forceinline__ void gather5_half(const double2* lds, int node0, int h, const double wx[kNT],
+                                             const double wy[kNT], double o[5]) {
+#pragma unroll
+  for (int f = 0; f < 5; ++f) o[f] = -0.0;
+  const double2* p = lds + node0 + 3 * h * WN;
+  const double* pc = reinterpret_cast<const double*>(lds + node0 + 2 * WN) + h;
+  double2 a0 = p[0], a1 = p[WN];
+  double c = pc[0];
+#pragma unroll
+  for (int t = 0; t < kNT * kNT; ++t) {
+    const int i = t / kNT, j = t % kNT;
+    double2 n0, n1;
+    double nc;
+    if (t + 1 < kNT * kNT) {
+      const int e = ((t + 1) / kNT) * W + (t + 1) % kNT;
+      n0 = p[e];
+      n1 = p[WN + e];
+      nc = pc[2 * e];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const double wij = wx[i] * wy[j];
+    o[0] = madd<FMA>(o[0], wij, a0.x); o[1] = madd<FMA>(o[1], wij, a0.y);
+    o[2] = madd<FMA>(o[2], wij, a1.x); o[3] = madd<FMA>(o[3], wij, a1.y);
+    o[4] = madd<FMA>(o[4], wij, c);
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < kNT * kNT) {
+      a0 = n0;
+      a1 = n1;
+      c = nc;
+    }
+  }
+}
+
+// pair_rank: the packet (0..31) of lane t (0..31) within the wave's run of 32
+// cell-sorted packets, so each ds_read_b128 lane group (b128_lane_rank's
+// 16-lane groups, the upper half mirroring the lower) takes 16 consecutive
+// packets.
+
 // Stage tile (ox, oy)'s window into LDS, chunk-major (chunk c of node e at
 // win[c*WN + e]): node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx.
 // Register staging: each lane copies whole 48-B records, 3 or 6 loads back
@@ -374,9 +442,12 @@ __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 
 // FMA (opt-in gather mode 1, V5 windows only): the stencil sums and the
 // snapshot blend as fused multiply-adds — tolerance parity, not bits.
-template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false, bool FMA = false>
+// PAIR (small ensembles): two lanes per packet (paired lanes, above); the
+// two-snapshot five-sum window only.
+template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false, bool FMA = false, bool PAIR = false>
 __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
   static_assert(!FMA || (V5 && !WBLEND), "the FMA gather exists for the five-sum window only");
+  static_assert(!PAIR || (TWO && V5 && !WBLEND), "paired lanes split the two snapshots of the five-sum window");
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
   // row stride = 12 (mod 16) nodes: any 4x4 block of window nodes falls on
   // 16 distinct ds_read_b128 bank quads (node n -> quad (n mod 16)), so lanes
@@ -525,6 +596,109 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
 
     // 3. advance the packets in sorted order (lane -> rank remapped for the
     //    ds_read_b128 lane groups; every rank of the batch is still taken once)
+    if constexpr (PAIR) {
+      const int h = (tid >> 5) & 1;  // this lane's half: x weights + snapshot 0, or y weights + snapshot 1
+      const double cper = h ? a.f0.py : a.f0.px, inv_cper = h ? a.f0.inv_py : a.f0.inv_px;
+      const int icper = h ? a.f0.ipy : a.f0.ipx;
+      for (int r0 = (tid >> 6) * 32; r0 < nb; r0 += NT / 2) {
+        const int r = r0 + (lane_rank & 31);
+        if (r >= nb) continue;
+        const int64_t pi = sortc ? order[r] : b0 + r;
+        const int64_t po = b0 + r;
+        double x0 = xin[pi], y0 = xin[a.n + pi];
+        double k0 = kin[pi], l0 = kin[a.n + pi];
+        const int orig = pin[pi];
+        double hcx, hcy;
+        drift_inc(k0, l0, a.f2, a.gH, half, a.fastdisp, hcx, hcy);
+        double sgd = (double)(ta.ivmode ? (int64_t)0 : sbase);
+        for (int st = 0; st < a.nsteps; ++st) {
+          const int64_t sg = sbase + st;
+          const double alpha = a.alpha0 + sgd * a.dalpha;
+          sgd = sgd + 1.0;
+          const double x1 = x0 + hcx;
+          const double y1 = y0 + hcy;
+          // this half's coordinate: its cell, offset and six 1-D weights
+          // (stencil_at's operations for x or y), then both halves' on every lane
+          double am;
+          const int cm = cell_frac(h ? y1 : x1, a.f0.dx, a.f0.inv_dx, cper, inv_cper, icper, nx, am);
+          double wm[kNT];
+          lagrange_w(am, a.bump, wm);
+          unsigned ic_, jc_;
+          halves_u32((unsigned)cm, ic_, jc_);
+          const int ic = (int)ic_, jc = (int)jc_;
+          double wx[kNT], wy[kNT];
+#pragma unroll
+          for (int q = 0; q < kNT; ++q) halves_f64(wm[q], wx[q], wy[q]);
+          const int dx_ = ring_diff(ic, ox, nx), dy_ = ring_diff(jc, oy, nx);
+          const bool inwin = dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M;
+          double S[kRec];
+          if (inwin) {
+#pragma unroll
+            for (int q = 0; q < kNT; ++q) {
+              asm volatile("" : "+v"(wx[q]));
+              asm volatile("" : "+v"(wy[q]));
+            }
+            gather5_half<WS, WNP, FMA>(win, (dx_ + M) * WS + (dy_ + M), h, wx, wy, S);
+          } else {
+            Stencil sc;
+            sc.ic = ic;
+            sc.jc = jc;
+#pragma unroll
+            for (int q = 0; q < kNT; ++q) { sc.wx[q] = wx[q]; sc.wy[q] = wy[q]; }
+            double dummy[kRec];
+            const double* own = h ? fb.nodes : fa.nodes;
+            gather6_lean<false, FMA>(own, own, npad, sc, S, dummy);
+          }
+          double I[kRec], J[kRec];
+#pragma unroll
+          for (int q = 0; q < 5; ++q) halves_f64(S[q], I[q], J[q]);
+          const double oma = 1 - alpha;
+#pragma unroll
+          for (int q = 0; q < 5; ++q) I[q] = madd<FMA>(oma * I[q], alpha, J[q]);
+          I[5] = -I[2];
+          const double x2 = x1 + dt * I[0];
+          const double y2 = y1 + dt * I[1];
+          const double k2 = k0 - dt * (I[2] * k0 + I[4] * l0);
+          const double l2 = l0 - dt * (I[3] * k0 + I[5] * l0);
+          drift_inc(k2, l2, a.f2, a.gH, half, a.fastdisp, hcx, hcy);
+          x0 = x2 + hcx;
+          y0 = y2 + hcy;
+          k0 = k2;
+          l0 = l2;
+          if (a.hist_x != nullptr && ((sg + 1) % a.save_every) == 0) {
+            const int64_t fr = a.frame0 + (sg + 1) / a.save_every - 1;
+            if (h == 0) {
+              double* hx = a.hist_x + fr * 2 * a.n;
+              hx[orig] = x0; hx[a.n + orig] = y0;
+            } else {
+              double* hk = a.hist_k + fr * 2 * a.n;
+              hk[orig] = k0; hk[a.n + orig] = l0;
+            }
+          }
+        }
+        if (h == 0) {
+          ta.x_out[po] = x0; ta.x_out[a.n + po] = y0;
+          ta.perm_out[po] = orig;
+        } else {
+          ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
+        }
+        if (nkeys != nullptr && h == 0) {  // fused histogram for the next re-binning (as below)
+          const int ic = fast_cell(x0, a.f0.inv_dx, nx);
+          const int jc = fast_cell(y0, a.f0.inv_dx, nx);
+          const int ntx_ = ta.ntx;
+          const int ntx2 = ic / T, nty2 = jc / T;
+          nkeys[po] = ntx2 * ntx_ + nty2;
+          const int ddx = ring_diff(ntx2, tx, ntx_), ddy = ring_diff(nty2, ty, ntx_);
+          if (ddx != 0 || ddy != 0) {
+            atomicAdd(&nbr[4], -1);
+            if (ddx >= -1 && ddx <= 1 && ddy >= -1 && ddy <= 1)
+              atomicAdd(&nbr[(ddx + 1) * 3 + (ddy + 1)], 1);
+            else
+              atomicAdd(&ta.next_counts[ntx2 * ntx_ + nty2], 1);
+          }
+        }
+      }
+    } else
     for (int r0 = tid & ~63; r0 < nb; r0 += NT) {
       const int r = r0 + lane_rank;
       if (r >= nb) continue;

@@ -440,6 +440,79 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, 
     np.testing.assert_array_equal(hkg, hko)
 
 
+@pytest.mark.parametrize("lanes", [1, 2])
+@pytest.mark.parametrize("dt_scale,cell_sort", [(1.0, 0), (40.0, 0), (1.0, 1), (40.0, 1)])
+def test_lanes_per_packet_bitexact(ctx, oracle_lib, qg_case, lanes, dt_scale, cell_sort):
+    """The LDS-tiled two-snapshot launch with one lane per packet or two
+    (paired lanes: x weights + snapshot 1 sums on one lane, y weights +
+    snapshot 2 on the other, swapped across the wave's halves): the oracle's
+    bits, history frames included; dt x 40 drives packets onto the global
+    fallback gather.  N = 3000 is not a multiple of 32, so waves end with
+    partial pairs."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    p0 = _planes(c["flow"])
+    p1 = _planes({n: np.asarray(v) * 0.8 for n, v in c["flow"].items()})
+    p0[5], p1[5] = -p0[2], -p1[2]  # five-sum window
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    rng = np.random.default_rng(31)
+    N = 3000
+    x = (rng.random((N, 2)) - 0.5) * L
+    th = rng.random(N) * 2 * np.pi
+    k = 3.0 * np.stack([np.cos(th), np.sin(th)], axis=1)
+    dt = c["dt"] * dt_scale
+    ctx.set_kernel(2)
+    ctx.set_cell_sort(cell_sort)
+    ctx.set_locality(5, 0)
+    ctx.set_lanes_per_packet(lanes)
+    try:
+        xg, kg, hxg, hkg = ctx.leapfrog(x, k, dt, 12, c["f"], 1.0, nslots=2, alpha0=0.1, dalpha=0.07,
+                                        bump=orc.BUMP_QG, save_every=3)
+    finally:
+        ctx.set_lanes_per_packet(0)
+        ctx.set_cell_sort(0)
+        ctx.set_kernel(0)
+        ctx.set_locality(4, 0)
+    xo, ko, hxo, hko = oracle_lib.leapfrog(p0, p1, 0.1, 0.07, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, dt, 12,
+                                           c["f"], 1.0, save_every=3)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
+    np.testing.assert_array_equal(hxg, hxo)
+    np.testing.assert_array_equal(hkg, hko)
+
+
+@pytest.mark.parametrize("N", [125_000, 20_000])
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_small_shard_bench_field_bitexact(ctx, oracle_lib, N, lanes):
+    """A strong-scaling shard of the bench ensemble (1.25e5 = 1e6 / 8 GPUs,
+    and a 2e4 tail) on the bench's device-derived 512^2 fields, one and two
+    lanes per packet: a random subset bit-identical to the C oracle."""
+    import argparse
+    import bench
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=1_000_000, world=8, rank=0, seed=146, mode="blend")
+    w = bench.build_workload(ctx, args, 0, N, args.packets)
+    ctx.set_locality(20, 0)
+    ctx.set_lanes_per_packet(lanes)
+    try:
+        ctx.packets_set(w["x"], w["k"])
+        for _ in range(6):
+            bench.step(ctx, w, 5)
+        xg, kg = ctx.packets_get()
+    finally:
+        ctx.set_lanes_per_packet(0)
+        ctx.set_locality(4, 0)
+    p0, p1 = ctx.get_field_grid(0), ctx.get_field_grid(1)
+    idx = np.sort(np.random.default_rng(3).choice(N, 2000, replace=False))
+    xo, ko = w["x"][idx], w["k"][idx]
+    for _ in range(6):
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.2, 512, 1024, w["L"] / 512, orc.BUMP_QG, xo, ko,
+                                           w["dt"] / 5, 5, w["f"], w["gH"])
+    np.testing.assert_array_equal(xg[idx], xo)
+    np.testing.assert_array_equal(kg[idx], ko)
+
+
 @pytest.mark.parametrize("variant,tail_split,order", [(2, (0, 0), 1), (2, (32, 0), 1), (2, (1000, 0), 1),
                                                       (2, (16, 16), 1), (2, (0, 1000), 1), (2, (0, 0), 0),
                                                       (2, (16, 0), 0)])
@@ -482,8 +555,8 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split,
     np.testing.assert_array_equal(kg[idx], ko)
 
 
-@pytest.mark.parametrize("variant", [1, 2])
-def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
+@pytest.mark.parametrize("variant,lanes", [(1, 0), (2, 1), (2, 2)])
+def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant, lanes):
     """20000 packets packed into a few cells: tiles far above the
     per-workgroup sort batch (several batches per tile) and
     one-tile-heavy binning; every packet bit-identical to the oracle."""
@@ -501,10 +574,12 @@ def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant):
     k = 3.0 * np.stack([np.cos(th), np.sin(th)], axis=1)
     ctx.set_kernel(variant)
     ctx.set_locality(2, 0)
+    ctx.set_lanes_per_packet(lanes)
     try:
         xg, kg, _, _ = ctx.leapfrog(x, k, c["dt"], 9, c["f"], 1.0, nslots=2, alpha0=0.2, dalpha=0.05,
                                     bump=orc.BUMP_QG)
     finally:
+        ctx.set_lanes_per_packet(0)
         ctx.set_kernel(0)
         ctx.set_locality(4, 0)
     xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.2, 0.05, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, c["dt"], 9,

@@ -20,7 +20,7 @@ from oracle import swrt_oracle as orc
 
 pytestmark = pytest.mark.gpu
 
-FIELD_RTOL = 1e-13
+FIELD_RTOL = 1e-12  # GPU vs numpy FFT relative to the field max (second derivatives of a broadband q)
 
 
 @pytest.fixture(scope="module")
@@ -51,7 +51,7 @@ def test_set_field_q_is_g2k_then_grid_U(ctx, pv_series):
     np.testing.assert_array_equal(a, ctx.get_field_grid(1))
     kx_, ky_, K2 = orc.wavenumber_grids(nx)
     flow = orc.grid_U(orc.g2k(q), f / Cg, K2, kx_, ky_)
-    for i, name in enumerate(("u", "v", "u_x", "u_y", "v_x", "v_y")):
+    for i, name in enumerate(orc.FIELD_ORDER):
         ref = np.asarray(flow[name]).ravel(order="F")
         assert np.abs(a[i] - ref).max() <= FIELD_RTOL * np.abs(ref).max(), name
 

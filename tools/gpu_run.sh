@@ -24,6 +24,6 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step bench 400 python bench.py
   export TMPDIR=/tmp
-  step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --driver-steps 0
+  step prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --driver-steps 0 --ode23-steps 0 --no-fma --no-forecast
 fi
 exit 0
