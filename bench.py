@@ -332,6 +332,8 @@ def parse_args(argv=None):
                     help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
     ap.add_argument("--lanes-per-packet", type=int, default=0,
                     help="LDS-tiled launches: 0 auto (paired lanes below 384 packets per tile), 1, 2 (same bits)")
+    ap.add_argument("--tile-cells", type=int, default=0,
+                    help="LDS-tiled launches: cells per tile side, 0 auto (32 for small ensembles), 16, 32 (same bits)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--tail-split", type=int, default=-1,
@@ -482,6 +484,7 @@ def main(argv=None):
     ctx.set_cell_sort(args.cell_sort)
     ctx.set_blend_mode(args.blend_mode)
     ctx.set_lanes_per_packet(args.lanes_per_packet)
+    ctx.set_tile_cells(args.tile_cells)
     if args.tail_split >= 0:
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
     if args.tile_order >= 0:
@@ -540,7 +543,7 @@ def main(argv=None):
                    "steps_per_launch": spl, "intervals_per_step": ivs,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split,
-                   "lanes_per_packet": args.lanes_per_packet,
+                   "lanes_per_packet": args.lanes_per_packet, "tile_cells": args.tile_cells,
                    "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,

@@ -218,6 +218,16 @@ int swrt_set_gather_mode(swrt_ctx* ctx, int mode);
  * results are bit-identical for any setting. */
 int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
 
+/* Cells per tile side of the LDS-tiled leapfrog launches (the spatial
+ * binning and each workgroup's window): 16, or 32 — one 1024-thread
+ * workgroup per CU whose 151 KB two-snapshot window fills the LDS, for
+ * ensembles too small to keep 16x16-cell workgroups busy (a strong-scaling
+ * shard: ~120 packets per 16x16 tile at 1.25e5 packets on 512^2).  32 applies
+ * to two divergence-free snapshots in the bit-exact blend order; other
+ * launches keep 16.  0 (default) = 32 below SWRT_BIG_TILE_BELOW packets per
+ * 16x16 tile on average, else 16.  Results are bit-identical for any setting. */
+int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

@@ -72,6 +72,7 @@ SIGNATURES = {
     "swrt_set_blend_mode": (_INT, [_VP, _INT]),
     "swrt_set_gather_mode": (_INT, [_VP, _INT]),
     "swrt_set_lanes_per_packet": (_INT, [_VP, _INT]),
+    "swrt_set_tile_cells": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_advance_intervals": (_INT, [_VP, _INT, _VP, _I, _D, _D, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
@@ -349,6 +350,10 @@ class Context:
     def set_lanes_per_packet(self, lanes=0):
         """swrt_set_lanes_per_packet: 0 auto (paired lanes for small tiles), 1, 2; same bits."""
         self._chk(self._L.swrt_set_lanes_per_packet(self._h, int(lanes)), "swrt_set_lanes_per_packet")
+
+    def set_tile_cells(self, cells=0):
+        """swrt_set_tile_cells: 0 auto (32x32-cell tiles for small ensembles), 16, 32; same bits."""
+        self._chk(self._L.swrt_set_tile_cells(self._h, int(cells)), "swrt_set_tile_cells")
 
     def set_blend_mode(self, mode=0):
         """0: bit-exact interpolate-then-blend; 1: blend in the LDS window (tolerance parity)."""

@@ -65,6 +65,18 @@ constexpr int kTileThreads = SWRT_TILE_THREADS;
 #endif
 // paired-lane tile launches (swrt_tile.hpp PAIR) below this many packets per tile
 constexpr int kPairBelow = SWRT_PAIR_BELOW;
+// Small ensembles (a strong-scaling shard): 32x32-cell tiles, one 1024-thread
+// workgroup per CU (its 151 KB window fills the LDS), below this many packets
+// per 16x16-cell tile on average.  A 16x16 tile of a 1.25e5-packet shard
+// holds ~120 packets — two busy waves, one per SIMD, each exposed to every
+// LDS read's latency; the 32x32 tile gives 7-8 busy waves per CU and stages
+// each window node once per CU instead of ~2.9 times.
+#ifndef SWRT_BIG_TILE_BELOW
+#define SWRT_BIG_TILE_BELOW 600
+#endif
+constexpr int kBigTile = 32;
+constexpr int kBigTileThreads = 1024;
+constexpr int kBigTileBelow = SWRT_BIG_TILE_BELOW;
 
 struct Slot {
   double* nodes = nullptr;  // padded interleaved records
@@ -185,6 +197,8 @@ struct swrt_ctx {
   int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   int gather_mode = 0;      // 0: stencil sums mul then add (bit-exact); 1: fused multiply-add (tolerance)
   int lanes_per_packet = 0; // LDS-tiled two-snapshot launches: 1, 2 (paired lanes), 0 = by packets per tile
+  int tile_mode = 0;        // leapfrog tile size: 0 auto (32 for small ensembles), 16, 32
+  int bin_tile = 0;         // cells per tile side of the current binning
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
   double* hx = nullptr;
@@ -605,6 +619,21 @@ bool use_tile_kernel(const swrt_ctx* c) {
   return c->kernel == 0 && c->slot[0].nx >= 2 * kTile;
 }
 
+// Tile side of the LDS-tiled leapfrog for this call: 32 for small ensembles
+// on two divergence-free snapshots (the kernel's only 32-cell instantiation),
+// else kTile.  slot0..slot0+nslots-1 are the snapshots the call reads.
+int leap_tile(const swrt_ctx* c, int nslots, int slot0 = 0) {
+  if (!use_tile_kernel(c) || c->tile_mode == 16) return kTile;
+  bool v5 = nslots >= 2;
+  for (int i = 0; i < nslots; ++i) v5 = v5 && c->slot[slot0 + i].div_free;
+  const int64_t nx = c->slot[slot0].nx;
+  if (!v5 || c->blend_mode != 0 || c->lanes_per_packet == 2 || nx % kBigTile != 0 || nx / kBigTile < 2)
+    return kTile;
+  if (c->tile_mode == 32) return kBigTile;
+  const int64_t tiles16 = (nx / kTile) * (nx / kTile);
+  return c->n < (int64_t)kBigTileBelow * tiles16 ? kBigTile : kTile;
+}
+
 int tile_cells(const swrt_ctx* c, int64_t nx) {
   if (use_tile_kernel(c)) return kTile;
   if (c->tile > 0) return (int)std::min<int64_t>(c->tile, nx);
@@ -619,13 +648,13 @@ int tile_cells(const swrt_ctx* c, int64_t nx) {
 // the tile launch that follows reads through it and writes the packets in
 // binned order (saves moving 36 B per packet twice).  Callers other than the
 // leapfrog loop need the packets moved (indirect = false).
-int rebin(swrt_ctx* c, bool indirect) {
+int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
   const Slot& s = c->slot[0];
   const FieldView v = view_of(s);
   BinGeom g;
   g.dx = v.dx; g.px = v.px; g.py = v.py; g.inv_px = v.inv_px; g.inv_py = v.inv_py; g.inv_dx = v.inv_dx;
   g.nx = v.nx;
-  g.tile = tile_cells(c, s.nx);
+  g.tile = tile > 0 ? tile : tile_cells(c, s.nx);
   g.ntx = (int)((s.nx + g.tile - 1) / g.tile);
   const int nbins = g.ntx * g.ntx;
   if (nbins > kMaxBins) return fail(c, SWRT_ERR_ARG, "too many spatial bins (raise tile size)");
@@ -639,9 +668,11 @@ int rebin(swrt_ctx* c, bool indirect) {
   }
   c->keys_fresh = false;
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins,
-                     c->bins + 2 * kMaxBins, c->tile_order ? tile_order_of(c) : nullptr, kTileThreads);
+                     c->bins + 2 * kMaxBins, c->tile_order ? tile_order_of(c) : nullptr,
+                     g.tile == kBigTile ? kBigTileThreads : kTileThreads);
   HIPCHK(c, hipGetLastError());
   c->counts_zero = true;
+  c->bin_tile = g.tile;
   if (indirect) {
     hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
                        c->dx, c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2,
@@ -678,7 +709,8 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   t.perm_out = c->perm2;
   t.starts = c->bins + 2 * kMaxBins;
   t.order = c->tile_order ? tile_order_of(c) : nullptr;
-  t.ntx = (int)((a.f0.nx + kTile - 1) / kTile);
+  const bool big = c->bin_tile == kBigTile;
+  t.ntx = (int)((a.f0.nx + c->bin_tile - 1) / c->bin_tile);
   const unsigned grid = (unsigned)(t.ntx * t.ntx);
   // half-tile workgroups at the end of each XCD band (swrt_tile.hpp wg_work)
   unsigned extra = 0;
@@ -702,7 +734,16 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     t.next_keys = c->keys;
     t.next_counts = c->bins;
   }
-  if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
+  if (big) {  // leap_tile chose 32-cell tiles: two divergence-free snapshots (checked again here)
+    if (a.nslots != 2 || !(iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)))
+      return fail(c, SWRT_ERR_STATE, "32-cell tiles need two divergence-free snapshots");
+    if (c->gather_mode == 1)
+      launch_k(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true, true>, dim3(wgrid),
+               dim3(kBigTileThreads), t);
+    else
+      launch_k(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true>, dim3(wgrid),
+               dim3(kBigTileThreads), t);
+  } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
     launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(wgrid), dim3(kTileThreads), t);
   } else if (a.nslots == 2) {
     if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)) {
@@ -769,8 +810,9 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
     int64_t chunk = std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
     if (c->blend_mode == 1 && nslots == 2 && use_tile_kernel(c)) chunk = 1;  // alpha fixed per launch
     if (c->rebin_every > 0) {
-      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every) {
-        int rc = rebin(c, use_tile_kernel(c));
+      const int want = leap_tile(c, nslots, sa);
+      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every || (use_tile_kernel(c) && c->bin_tile != want)) {
+        int rc = rebin(c, use_tile_kernel(c), use_tile_kernel(c) ? want : 0);
         if (rc) return rc;
       }
       chunk = std::min<int64_t>(chunk, c->rebin_every - c->steps_since_bin);
@@ -802,8 +844,9 @@ int run_advance_intervals(swrt_ctx* c, int nint, const double* hs, int64_t nsub,
   while (i0 < nint) {
     int k = 0;
     if (fused) {
-      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every) {
-        int rc = rebin(c, true);
+      const int want = leap_tile(c, std::min(nint - i0, kMaxIntervals) + 1, i0);
+      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every || c->bin_tile != want) {
+        int rc = rebin(c, true, want);
         if (rc) return rc;
       }
       k = (int)std::min<int64_t>({(int64_t)(nint - i0), (c->rebin_every - c->steps_since_bin) / nsub,
@@ -1406,6 +1449,16 @@ int swrt_set_gather_mode(swrt_ctx* c, int mode) {
   if (!c) return SWRT_ERR_ARG;
   if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "gather mode must be 0 or 1");
   c->gather_mode = mode;
+  return SWRT_OK;
+}
+
+int swrt_set_tile_cells(swrt_ctx* c, int cells) {
+  if (!c) return SWRT_ERR_ARG;
+  if (cells != 0 && cells != kTile && cells != kBigTile) return fail(c, SWRT_ERR_ARG, "tile cells must be 0, 16 or 32");
+  c->tile_mode = cells;
+  c->bin_valid = false;
+  c->keys_fresh = false;
+  c->src_pending = false;
   return SWRT_OK;
 }
 
@@ -2734,7 +2787,7 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
   // one spatial re-binning per ode23 call (the packet order is free: the
   // error norm is a max over all components)
   if (c->rebin_every > 0 && c->slot[0].set) {
-    if ((rc = rebin(c, false))) return rc;
+    if ((rc = rebin(c, false, use_tile_kernel(c) ? kTile : 0))) return rc;  // the ode23 tile kernel's 16x16 tiles
   }
   Ode23Args a;
   if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;

@@ -457,7 +457,8 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
   constexpr bool GTWO = TWO && !WBLEND;  // two snapshots in the LDS window
   constexpr int NCH = GTWO ? (V5 ? 5 : 6) : 3;  // 16-B chunks per node
   constexpr int NB = T * T + 1;     // in-tile cell bins + "elsewhere"
-  constexpr int MAXB = 2 * NT;      // packets sorted per batch
+  // packets sorted per batch (the 32x32-cell tile's window leaves ~8 KB of LDS for the batch arrays)
+  constexpr int MAXB = T >= 32 ? 512 : 2 * NT;
   __shared__ double2 win[NCH * WNP];
   __shared__ int hist[NB];
   __shared__ int kr[MAXB];          // key << 16 | rank
@@ -553,10 +554,17 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       // packets (one ds_read_b128 lane group) stays inside a 2x2 or 4x4 block
       // of cells — with the 12 (mod 16) row stride a conflict-free read
       // (measured: bank-conflict cycles -36 %, LDS busy -15 %)
-      const int key = (dx_ >= 0 && dx_ < T && dy_ >= 0 && dy_ < T)
-                          ? ((dy_ & 1) | ((dx_ & 1) << 1) | ((dy_ & 2) << 1) | ((dx_ & 2) << 2) |
-                             ((dy_ & 4) << 2) | ((dx_ & 4) << 3) | ((dy_ & 8) << 3) | ((dx_ & 8) << 4))
-                          : T * T;
+      int key;
+      if constexpr (T == 16) {
+        key = (dx_ >= 0 && dx_ < T && dy_ >= 0 && dy_ < T)
+                  ? ((dy_ & 1) | ((dx_ & 1) << 1) | ((dy_ & 2) << 1) | ((dx_ & 2) << 2) |
+                     ((dy_ & 4) << 2) | ((dx_ & 4) << 3) | ((dy_ & 8) << 3) | ((dx_ & 8) << 4))
+                  : T * T;
+      } else {  // the same interleave for any power-of-two T
+        key = 0;
+#pragma unroll
+        for (int b = 0; (1 << b) < T; ++b) key |= (((dy_ >> b) & 1) << (2 * b)) | (((dx_ >> b) & 1) << (2 * b + 1));
+      }
       const int r = atomicAdd(&hist[key], 1);
       kr[i] = (key << 16) | r;
     }

@@ -440,9 +440,9 @@ def test_kernel_variants_bitexact(ctx, oracle_lib, qg_case, variant, cell_sort, 
     np.testing.assert_array_equal(hkg, hko)
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
+@pytest.mark.parametrize("lanes,cells", [(1, 16), (2, 16), (1, 32)])
 @pytest.mark.parametrize("dt_scale,cell_sort", [(1.0, 0), (40.0, 0), (1.0, 1), (40.0, 1)])
-def test_lanes_per_packet_bitexact(ctx, oracle_lib, qg_case, lanes, dt_scale, cell_sort):
+def test_lanes_per_packet_bitexact(ctx, oracle_lib, qg_case, lanes, cells, dt_scale, cell_sort):
     """The LDS-tiled two-snapshot launch with one lane per packet or two
     (paired lanes: x weights + snapshot 1 sums on one lane, y weights +
     snapshot 2 on the other, swapped across the wave's halves): the oracle's
@@ -466,10 +466,12 @@ def test_lanes_per_packet_bitexact(ctx, oracle_lib, qg_case, lanes, dt_scale, ce
     ctx.set_cell_sort(cell_sort)
     ctx.set_locality(5, 0)
     ctx.set_lanes_per_packet(lanes)
+    ctx.set_tile_cells(cells)
     try:
         xg, kg, hxg, hkg = ctx.leapfrog(x, k, dt, 12, c["f"], 1.0, nslots=2, alpha0=0.1, dalpha=0.07,
                                         bump=orc.BUMP_QG, save_every=3)
     finally:
+        ctx.set_tile_cells(0)
         ctx.set_lanes_per_packet(0)
         ctx.set_cell_sort(0)
         ctx.set_kernel(0)
@@ -483,8 +485,8 @@ def test_lanes_per_packet_bitexact(ctx, oracle_lib, qg_case, lanes, dt_scale, ce
 
 
 @pytest.mark.parametrize("N", [125_000, 20_000])
-@pytest.mark.parametrize("lanes", [1, 2])
-def test_small_shard_bench_field_bitexact(ctx, oracle_lib, N, lanes):
+@pytest.mark.parametrize("lanes,cells", [(1, 16), (2, 16), (1, 32)])
+def test_small_shard_bench_field_bitexact(ctx, oracle_lib, N, lanes, cells):
     """A strong-scaling shard of the bench ensemble (1.25e5 = 1e6 / 8 GPUs,
     and a 2e4 tail) on the bench's device-derived 512^2 fields, one and two
     lanes per packet: a random subset bit-identical to the C oracle."""
@@ -495,12 +497,14 @@ def test_small_shard_bench_field_bitexact(ctx, oracle_lib, N, lanes):
     w = bench.build_workload(ctx, args, 0, N, args.packets)
     ctx.set_locality(20, 0)
     ctx.set_lanes_per_packet(lanes)
+    ctx.set_tile_cells(cells)
     try:
         ctx.packets_set(w["x"], w["k"])
         for _ in range(6):
             bench.step(ctx, w, 5)
         xg, kg = ctx.packets_get()
     finally:
+        ctx.set_tile_cells(0)
         ctx.set_lanes_per_packet(0)
         ctx.set_locality(4, 0)
     p0, p1 = ctx.get_field_grid(0), ctx.get_field_grid(1)
@@ -555,8 +559,8 @@ def test_tile_kernel_large_ensemble_subset(ctx, oracle_lib, variant, tail_split,
     np.testing.assert_array_equal(kg[idx], ko)
 
 
-@pytest.mark.parametrize("variant,lanes", [(1, 0), (2, 1), (2, 2)])
-def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant, lanes):
+@pytest.mark.parametrize("variant,lanes,cells", [(1, 0, 0), (2, 1, 16), (2, 2, 16), (2, 1, 32)])
+def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant, lanes, cells):
     """20000 packets packed into a few cells: tiles far above the
     per-workgroup sort batch (several batches per tile) and
     one-tile-heavy binning; every packet bit-identical to the oracle."""
@@ -575,10 +579,12 @@ def test_tile_kernel_dense_cluster(ctx, oracle_lib, qg_case, variant, lanes):
     ctx.set_kernel(variant)
     ctx.set_locality(2, 0)
     ctx.set_lanes_per_packet(lanes)
+    ctx.set_tile_cells(cells)
     try:
         xg, kg, _, _ = ctx.leapfrog(x, k, c["dt"], 9, c["f"], 1.0, nslots=2, alpha0=0.2, dalpha=0.05,
                                     bump=orc.BUMP_QG)
     finally:
+        ctx.set_tile_cells(0)
         ctx.set_lanes_per_packet(0)
         ctx.set_kernel(0)
         ctx.set_locality(4, 0)

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--substeps", type=int, default=5)
     ap.add_argument("--rebin-every", type=int, default=20)
     ap.add_argument("--dump", default="", help="save every sample's raw stamps (npz) for offline analysis")
+    ap.add_argument("--lanes-per-packet", type=int, default=0)
     args = ap.parse_args()
     args.world, args.rank, args.seed = 1, 0, 146
     lib = _lib.load()
@@ -43,8 +44,9 @@ def main():
     ctx.set_kernel(2)
     if args.tail_split >= 0:
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
-    rng = np.random.default_rng(146)
-    w = bench.build_workload(ctx, args, rng)
+    ctx.set_lanes_per_packet(args.lanes_per_packet)
+    bench._imports()
+    w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
     ctx.packets_set(w["x"], w["k"])
     for _ in range(8):
         bench.step(ctx, w, args.substeps)
@@ -111,7 +113,7 @@ def main():
             n_round1=int(np.sum(P[:, 0] < 2.0)),
             corr_compute_packets=float(np.corrcoef(comp, d[:, 6])[0, 1]),
             compute_us_by_packets={f"{lo}-{lo + 64}": float(np.median(comp[(d[:, 6] >= lo) & (d[:, 6] < lo + 64)]))
-                                   for lo in range(832, 1152, 64) if np.any((d[:, 6] >= lo) & (d[:, 6] < lo + 64))},
+                                   for lo in range(0, 1152, 64) if np.any((d[:, 6] >= lo) & (d[:, 6] < lo + 64))},
             compute_us_deciles=[float(v) for v in np.percentile(comp, np.arange(0, 101, 10))],
             compute_us_by_xcc={int(x): float(np.median(comp[xcc == x])) for x in np.unique(xcc)},
             compute_us_round1_by_xcc={int(x): float(np.median(comp[(xcc == x) & (P[:, 0] < 2.0)]))
