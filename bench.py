@@ -331,9 +331,9 @@ def parse_args(argv=None):
     ap.add_argument("--blend-mode", type=int, default=0,
                     help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
     ap.add_argument("--lanes-per-packet", type=int, default=0,
-                    help="LDS-tiled launches: 0 auto (paired lanes below 384 packets per tile), 1, 2 (same bits)")
+                    help="LDS-tiled launches: 0 auto (build threshold, off by default), 1, 2 (same bits)")
     ap.add_argument("--tile-cells", type=int, default=0,
-                    help="LDS-tiled launches: cells per tile side, 0 auto (32 for small ensembles), 16, 32 (same bits)")
+                    help="LDS-tiled launches: cells per tile side, 0 auto (build threshold, off by default), 16, 32 (same bits)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--tail-split", type=int, default=-1,

@@ -214,8 +214,9 @@ int swrt_set_gather_mode(swrt_ctx* ctx, int mode);
  * the y weights and snapshot 2's; cross-lane swaps combine them), so a tile
  * with few packets still keeps two waves per SIMD busy — small shards of a
  * strongly scaled ensemble.  0 (default) = 2 below SWRT_PAIR_BELOW packets
- * per tile on average, else 1.  Every sum keeps the reference's order:
- * results are bit-identical for any setting. */
+ * per tile on average (build default 0: measured no faster, see
+ * swrt_api.hip), else 1.  Every sum keeps the reference's order: results are
+ * bit-identical for any setting. */
 int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
 
 /* Cells per tile side of the LDS-tiled leapfrog launches (the spatial
@@ -225,7 +226,8 @@ int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
  * shard: ~120 packets per 16x16 tile at 1.25e5 packets on 512^2).  32 applies
  * to two divergence-free snapshots in the bit-exact blend order; other
  * launches keep 16.  0 (default) = 32 below SWRT_BIG_TILE_BELOW packets per
- * 16x16 tile on average, else 16.  Results are bit-identical for any setting. */
+ * 16x16 tile on average (build default 0: measured no faster), else 16.
+ * Results are bit-identical for any setting. */
 int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
 
 /* Advance the device-resident packets by nsteps leapfrog steps

@@ -348,11 +348,11 @@ class Context:
         self._chk(self._L.swrt_set_gather_mode(self._h, int(mode)), "swrt_set_gather_mode")
 
     def set_lanes_per_packet(self, lanes=0):
-        """swrt_set_lanes_per_packet: 0 auto (paired lanes for small tiles), 1, 2; same bits."""
+        """swrt_set_lanes_per_packet: 0 auto (build threshold; off by default), 1, 2; same bits."""
         self._chk(self._L.swrt_set_lanes_per_packet(self._h, int(lanes)), "swrt_set_lanes_per_packet")
 
     def set_tile_cells(self, cells=0):
-        """swrt_set_tile_cells: 0 auto (32x32-cell tiles for small ensembles), 16, 32; same bits."""
+        """swrt_set_tile_cells: 0 auto (build threshold; off by default), 16, 32; same bits."""
         self._chk(self._L.swrt_set_tile_cells(self._h, int(cells)), "swrt_set_tile_cells")
 
     def set_blend_mode(self, mode=0):

@@ -60,19 +60,23 @@ constexpr int kXkaMargin = 3;           // xka_tile_kernel: drift margin (cells)
 constexpr int kTile = SWRT_TILE;                // LDS tile kernel: cells per tile side
 constexpr int kMargin = SWRT_MARGIN;            // LDS tile kernel: drift margin (cells)
 constexpr int kTileThreads = SWRT_TILE_THREADS;
+// Paired-lane tile launches (swrt_tile.hpp PAIR) below this many packets per
+// tile, and 32x32-cell tiles (one 1024-thread workgroup per CU, its 151 KB
+// window filling the LDS) below SWRT_BIG_TILE_BELOW packets per 16x16 tile.
+// Both target small shards (~120 packets per 16x16 tile at 1.25e5 packets on
+// 512^2: one busy wave per SIMD) and both are bit-identical, but neither was
+// faster on the hardware (1.25e5: 60.0 / 62.0 vs 58.1-61.2 us per 5-step
+// launch; 32x32 at 5e5: 171 vs 129 us; profiles/r03_small_shard.md): at that
+// density the 16 lanes of a ds_read_b128 group read 16 distinct nodes and the
+// LDS bank conflicts double (2.0-2.3 vs 1.22 cycles per access), which more
+// busy waves cannot hide.  Auto-selection is therefore off (0); both stay
+// available through swrt_set_lanes_per_packet / swrt_set_tile_cells.
 #ifndef SWRT_PAIR_BELOW
-#define SWRT_PAIR_BELOW 384
+#define SWRT_PAIR_BELOW 0
 #endif
-// paired-lane tile launches (swrt_tile.hpp PAIR) below this many packets per tile
 constexpr int kPairBelow = SWRT_PAIR_BELOW;
-// Small ensembles (a strong-scaling shard): 32x32-cell tiles, one 1024-thread
-// workgroup per CU (its 151 KB window fills the LDS), below this many packets
-// per 16x16-cell tile on average.  A 16x16 tile of a 1.25e5-packet shard
-// holds ~120 packets — two busy waves, one per SIMD, each exposed to every
-// LDS read's latency; the 32x32 tile gives 7-8 busy waves per CU and stages
-// each window node once per CU instead of ~2.9 times.
 #ifndef SWRT_BIG_TILE_BELOW
-#define SWRT_BIG_TILE_BELOW 600
+#define SWRT_BIG_TILE_BELOW 0
 #endif
 constexpr int kBigTile = 32;
 constexpr int kBigTileThreads = 1024;

@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--cfl", type=float, default=0.05, help="leapfrog dt in units of dx/U0 (bench: 0.05)")
     ap.add_argument("--cycle", type=int, default=20, help="steps between re-binnings (bench: 20)")
     ap.add_argument("--launch", type=int, default=5, help="steps per launch (bench: 5)")
+    ap.add_argument("--packets", type=int, default=1_000_000, help="ensemble size (a strong-scaling shard: 125000)")
     args = ap.parse_args()
     nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
     rng = np.random.default_rng(146)
@@ -71,7 +72,7 @@ def main():
     U0 = math.sqrt(float((np.asarray(fl1["u"]) ** 2 + np.asarray(fl1["v"]) ** 2).max()))
     dx = L / nx
     dt = args.cfl * dx / U0
-    N = 1_000_000
+    N = args.packets
     x = L * rng.random((N, 2)) - L / 2
     i = np.arange(1, N + 1)
     wf = math.sqrt(15 * f * f)
@@ -111,7 +112,34 @@ def main():
     # their cell led half a launch (the wave keeps its packets)
     lead = X[0] + 0.5 * R * dt * cg0
     policies["0.5 lead + in-wave re-sort per launch"] = ("wave", lead)
+    policies["class deal per step (quad of x1, over the tile)"] = "deal"
     for name, keypos in policies.items():
+        if isinstance(keypos, str):  # per step: deal the tile's packets to 16-lane groups by LDS slot class
+            tot = np.zeros(R)
+            base = np.zeros(R)
+            for tx in range(nt):
+                for ty in range(nt):
+                    m = np.where((tile0[:, 0] == tx) & (tile0[:, 1] == ty))[0]
+                    if len(m) == 0:
+                        continue
+                    for j in range(R):
+                        cj = cells(x1(j)[m])
+                        node = (cj[:, 0] - tx * T + M) * WS + (cj[:, 1] - ty * T + M)
+                        q = node % 16
+                        o = np.argsort(q, kind="stable")
+                        G = -(-len(m) // 16)
+                        grp_of = np.empty(len(m), int)
+                        grp_of[o] = np.arange(len(m)) % G
+                        for g in range(G):
+                            nd = np.unique(node[grp_of == g])
+                            if len(nd) == 0:
+                                continue
+                            tot[j] += np.bincount(nd % 16, minlength=16).max()
+                            base[j] += 1
+            per = tot / base
+            print(f"{name:42s} LDS cycles / conflict-free: first {per[0]:.3f} mid {per[R // 2]:.3f} last {per[-1]:.3f}"
+                  f"   mean {tot.sum() / base.sum():.3f}")
+            continue
         wave_mode = isinstance(keypos, tuple)
         if wave_mode:
             keypos = keypos[1]
