@@ -334,6 +334,8 @@ def parse_args(argv=None):
                     help="LDS-tiled launches: 0 auto (build threshold, off by default), 1, 2 (same bits)")
     ap.add_argument("--tile-cells", type=int, default=0,
                     help="LDS-tiled launches: cells per tile side, 0 auto (build threshold, off by default), 16, 32 (same bits)")
+    ap.add_argument("--packet-streams", type=int, default=1,
+                    help="LDS-tiled launches split over 1 or 2 streams (swrt_set_packet_streams; same bits)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--tail-split", type=int, default=-1,
@@ -485,6 +487,7 @@ def main(argv=None):
     ctx.set_blend_mode(args.blend_mode)
     ctx.set_lanes_per_packet(args.lanes_per_packet)
     ctx.set_tile_cells(args.tile_cells)
+    ctx.set_packet_streams(args.packet_streams)
     if args.tail_split >= 0:
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
     if args.tile_order >= 0:
@@ -544,6 +547,7 @@ def main(argv=None):
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split,
                    "lanes_per_packet": args.lanes_per_packet, "tile_cells": args.tile_cells,
+                   "packet_streams": args.packet_streams,
                    "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,

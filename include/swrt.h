@@ -230,6 +230,17 @@ int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
  * Results are bit-identical for any setting. */
 int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
 
+/* Packet streams of the LDS-tiled leapfrog: 1 (default) or 2.  With 2 every
+ * launch runs as two half launches — alternate tiles of each XCD band — on
+ * the context's packet stream and a second stream.  Between re-binnings the
+ * halves advance disjoint packet ranges, so the second stream's launch k
+ * overlaps the first stream's launch k+1: one half's tail runs under the
+ * other's body instead of leaving CUs idle at every launch boundary.  Any
+ * call that reads the packets (or re-bins them) first orders the second
+ * stream's work before its own; swrt_synchronize waits for both.  Results
+ * are bit-identical for either setting. */
+int swrt_set_packet_streams(swrt_ctx* ctx, int streams);
+
 /* Advance the device-resident packets by nsteps leapfrog steps
  * (ode_symplectic.m:13-37: drift dt/2 with gH*k/omega, kick dt with U(x1)
  * and (grad U(x1))^T k1 (RaytracingScheme.m:9-16), drift dt/2).  The kick of

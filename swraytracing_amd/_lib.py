@@ -73,6 +73,7 @@ SIGNATURES = {
     "swrt_set_gather_mode": (_INT, [_VP, _INT]),
     "swrt_set_lanes_per_packet": (_INT, [_VP, _INT]),
     "swrt_set_tile_cells": (_INT, [_VP, _INT]),
+    "swrt_set_packet_streams": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_advance_intervals": (_INT, [_VP, _INT, _VP, _I, _D, _D, _D, _D, _D, _I]),
     "swrt_history_frames": (_I, [_VP]),
@@ -354,6 +355,10 @@ class Context:
     def set_tile_cells(self, cells=0):
         """swrt_set_tile_cells: 0 auto (build threshold; off by default), 16, 32; same bits."""
         self._chk(self._L.swrt_set_tile_cells(self._h, int(cells)), "swrt_set_tile_cells")
+
+    def set_packet_streams(self, streams=1):
+        """swrt_set_packet_streams: 1, or 2 (tile launches split over two streams; same bits)."""
+        self._chk(self._L.swrt_set_packet_streams(self._h, int(streams)), "swrt_set_packet_streams")
 
     def set_blend_mode(self, mode=0):
         """0: bit-exact interpolate-then-blend; 1: blend in the LDS window (tolerance parity)."""

@@ -202,6 +202,17 @@ struct swrt_ctx {
   int gather_mode = 0;      // 0: stencil sums mul then add (bit-exact); 1: fused multiply-add (tolerance)
   int lanes_per_packet = 0; // LDS-tiled two-snapshot launches: 1, 2 (paired lanes), 0 = by packets per tile
   int tile_mode = 0;        // leapfrog tile size: 0 auto (32 for small ensembles), 16, 32
+  // Two packet streams (swrt_set_packet_streams 2): each LDS-tiled leapfrog
+  // launch runs as two half launches — alternate band positions of every XCD
+  // band — on `stream` and `stream2`.  Within a re-binning cycle the halves
+  // touch disjoint packet ranges, so stream2's launch k overlaps stream's
+  // launch k+1 (one half's tail under the other's body).  stream2's work is
+  // joined back into `stream` (join_b) before anything else reads the packets.
+  int packet_streams = 1;
+  hipStream_t stream2 = nullptr;
+  hipStream_t stream0 = nullptr;  // the packet stream (`stream` outside OnQGStream)
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  bool b_pending = false;         // stream2 holds packet work not yet ordered before stream's
   int bin_tile = 0;         // cells per tile side of the current binning
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -349,7 +360,20 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
       return fail(ctx, SWRT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));    \
   } while (0)
 
-#define GUARD_BEGIN try {
+// GUARD_BEGIN also orders any pending second-stream packet work before the
+// call (join_b); the split-launch entry points use GUARD_BEGIN_KEEP_SPLIT.
+#define HIPCHK_RC(expr)       \
+  do {                        \
+    const int rc_ = (expr);   \
+    if (rc_) return rc_;      \
+  } while (0)
+#define GUARD_BEGIN_KEEP_SPLIT try {
+#define GUARD_BEGIN               \
+  try {                           \
+    {                             \
+      const int jrc_ = join_b(c); \
+      if (jrc_) return jrc_;      \
+    }
 #define GUARD_END(ctx)                                                \
   }                                                                   \
   catch (const std::bad_alloc&) {                                     \
@@ -358,6 +382,15 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
   catch (...) {                                                       \
     return fail(ctx, SWRT_ERR_STATE, "unexpected C++ exception");     \
   }
+
+// Order stream2's queued packet work before the packet stream's next work.
+int join_b(swrt_ctx* c) {
+  if (!c || !c->b_pending) return SWRT_OK;
+  HIPCHK(c, hipEventRecord(c->join_ev, c->stream2));
+  HIPCHK(c, hipStreamWaitEvent(c->stream0, c->join_ev, 0));
+  c->b_pending = false;
+  return SWRT_OK;
+}
 
 bool is_pow2(int64_t v) { return v > 0 && (v & (v - 1)) == 0; }
 
@@ -549,6 +582,31 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
   c->tail_ev = stop;
 }
 
+// The LDS-tiled launch of TileArgs t: one launch over every tile, or (two
+// packet streams) two half launches of alternate band positions, the second
+// on stream2 after everything queued on the packet stream so far (this
+// call's re-binning, memsets and history growth).  A timed pair brackets
+// the first half's start and the second half's end.
+template <typename F>
+int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
+  const bool two = c->packet_streams == 2 && c->stream2 != nullptr && t.split == 0 && wgrid % 16 == 0 &&
+                   c->stream == c->stream0;
+  if (!two) {
+    t.spart = -1;
+    launch_k(c, kernel, dim3(wgrid), dim3(nt), t);
+    return SWRT_OK;
+  }
+  HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
+  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->fork_ev, 0));
+  t.spart = 0;
+  hipExtLaunchKernelGGL(kernel, dim3(wgrid / 2), dim3(nt), 0, c->stream, c->kev0, nullptr, 0, t);
+  t.spart = 1;
+  hipExtLaunchKernelGGL(kernel, dim3(wgrid / 2), dim3(nt), 0, c->stream2, nullptr, c->kev1, 0, t);
+  c->b_pending = true;
+  c->tail_ev = nullptr;  // slot uses are marked after the join (swrt_advance)
+  return SWRT_OK;
+}
+
 // Time every timing_every-th leapfrog launch with a pair of HIP events.
 int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next, const IvLaunch* iv = nullptr) {
   const bool timed = c->timing_every > 0 && (c->launch_count++ % c->timing_every) == 0;
@@ -565,6 +623,7 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next,
   }
   // timing events (pairs), grown on demand; fold into a running sum when full
   if (c->timing.used + 2 > kMaxEvents) {
+    if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (size_t i = 0; i + 1 < c->timing.used; i += 2) {
       float ms = 0.f;
@@ -653,6 +712,7 @@ int tile_cells(const swrt_ctx* c, int64_t nx) {
 // binned order (saves moving 36 B per packet twice).  Callers other than the
 // leapfrog loop need the packets moved (indirect = false).
 int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
+  if (int rc = join_b(c)) return rc;  // the second stream's half launches wrote packets this pass reads
   const Slot& s = c->slot[0];
   const FieldView v = view_of(s);
   BinGeom g;
@@ -719,6 +779,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   // half-tile workgroups at the end of each XCD band (swrt_tile.hpp wg_work)
   unsigned extra = 0;
   t.split = launch_shape(c, grid, &extra);
+  t.spart = -1;
   const unsigned wgrid = grid + extra;
   t.next_keys = nullptr;
   t.next_counts = nullptr;
@@ -742,13 +803,11 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     if (a.nslots != 2 || !(iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)))
       return fail(c, SWRT_ERR_STATE, "32-cell tiles need two divergence-free snapshots");
     if (c->gather_mode == 1)
-      launch_k(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true, true>, dim3(wgrid),
-               dim3(kBigTileThreads), t);
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true, true>, wgrid, kBigTileThreads, t));
     else
-      launch_k(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true>, dim3(wgrid),
-               dim3(kBigTileThreads), t);
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true>, wgrid, kBigTileThreads, t));
   } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
-    launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, dim3(wgrid), dim3(kTileThreads), t);
+    HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, wgrid, kTileThreads, t));
   } else if (a.nslots == 2) {
     if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)) {
       // paired lanes when the tiles hold few packets (a workgroup would have
@@ -756,29 +815,23 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
       const bool pair = c->lanes_per_packet == 2 ||
                         (c->lanes_per_packet == 0 && c->n < (int64_t)kPairBelow * (int64_t)grid);
       if (pair && c->gather_mode == 1)
-        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true, true>, dim3(wgrid),
-                 dim3(kTileThreads), t);
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true, true>, wgrid, kTileThreads, t));
       else if (pair)
-        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, false, true>, dim3(wgrid),
-                 dim3(kTileThreads), t);
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, false, true>, wgrid, kTileThreads, t));
       else if (c->gather_mode == 1)
-        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true>, dim3(wgrid),
-                 dim3(kTileThreads), t);
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true>, wgrid, kTileThreads, t));
       else
-        launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
-                 dim3(kTileThreads), t);
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, wgrid, kTileThreads, t));
     } else {
-      launch_k(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, dim3(wgrid), dim3(kTileThreads), t);
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, wgrid, kTileThreads, t));
     }
   } else {
     if (c->slot[0].div_free && c->gather_mode == 1)
-      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true, true>, dim3(wgrid),
-               dim3(kTileThreads), t);
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true, true>, wgrid, kTileThreads, t));
     else if (c->slot[0].div_free)
-      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true>, dim3(wgrid),
-               dim3(kTileThreads), t);
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true>, wgrid, kTileThreads, t));
     else
-      launch_k(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, dim3(wgrid), dim3(kTileThreads), t);
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, wgrid, kTileThreads, t));
   }
   HIPCHK(c, hipGetLastError());
   std::swap(c->dx, c->dx2);
@@ -911,6 +964,7 @@ int ensure_history(swrt_ctx* c, int64_t new_frames) {
   const int64_t per = 2 * c->n;
   const int64_t need = (c->hframes + new_frames) * per;
   if (new_frames <= 0 || need <= c->hcap) return SWRT_OK;
+  if (int rc = join_b(c)) return rc;  // the second stream may still write frames into the old buffers
   const int64_t ncap = std::max<int64_t>(need, 2 * c->hcap);
   double *nx_ = nullptr, *nk_ = nullptr;
   HIPCHK(c, hipMalloc(&nx_, sizeof(double) * ncap));
@@ -969,6 +1023,9 @@ int swrt_create(int device, swrt_ctx** out) {
     ok = ok && hipEventCreateWithFlags(&s->uev, hipEventDisableTiming) == hipSuccess &&
          hipEventCreateWithFlags(&s->wev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->use_ev, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
+       hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) == hipSuccess;
+  c->stream0 = c->stream;
   if (!ok) {
     swrt_destroy(c);
     return SWRT_ERR_HIP;
@@ -981,6 +1038,7 @@ void swrt_destroy(swrt_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
   if (c->qstream) (void)hipStreamSynchronize(c->qstream);
   auto free_slot = [](Slot& s) {
     if (s.nodes) (void)hipFree(s.nodes);
@@ -1022,7 +1080,10 @@ void swrt_destroy(swrt_ctx* c) {
                   (void*)c->o_ynk, (void*)c->o_dmax})
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
+  if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
   if (c->qstream) (void)hipStreamDestroy(c->qstream);
+  if (c->stream2) (void)hipStreamDestroy(c->stream2);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1466,6 +1527,16 @@ int swrt_set_tile_cells(swrt_ctx* c, int cells) {
   return SWRT_OK;
 }
 
+int swrt_set_packet_streams(swrt_ctx* c, int streams) {
+  if (!c) return SWRT_ERR_ARG;
+  if (streams != 1 && streams != 2) return fail(c, SWRT_ERR_ARG, "packet streams must be 1 or 2");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (int rc = join_b(c)) return rc;
+  if (streams == 2 && !c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+  c->packet_streams = streams;
+  return SWRT_OK;
+}
+
 int swrt_set_lanes_per_packet(swrt_ctx* c, int lanes) {
   if (!c) return SWRT_ERR_ARG;
   if (lanes < 0 || lanes > 2) return fail(c, SWRT_ERR_ARG, "lanes per packet must be 0 (auto), 1 or 2");
@@ -1530,7 +1601,7 @@ int64_t swrt_packets_count(const swrt_ctx* c) { return c ? c->n : -1; }
 int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int nslots,
                  double alpha0, double dalpha, double bump, int64_t save_every) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_SPLIT  // the half launches of the second packet stream stay unjoined across calls
   SlotUse slot_use(c);
   if (nsteps < 0) return fail(c, SWRT_ERR_ARG, "nsteps < 0");
   if (nslots != 1 && nslots != 2) return fail(c, SWRT_ERR_ARG, "nslots must be 1 or 2");
@@ -1551,6 +1622,8 @@ int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, in
   if (rc) return rc;
   c->hframes += new_frames;
   c->steps_done += nsteps;
+  // a QG stream renames slots by their use events: mark them after the second stream's launches too
+  if (slot_events(c)) HIPCHK_RC(join_b(c));
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -1558,7 +1631,7 @@ int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, in
 int swrt_advance_intervals(swrt_ctx* c, int nintervals, const double* dts, int64_t nsub, double f, double gH,
                            double alpha0, double dalpha, double bump, int64_t save_every) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_SPLIT  // the half launches of the second packet stream stay unjoined across calls
   SlotUse slot_use(c);
   if (nintervals < 1 || nintervals > SWRT_MAX_SLOTS - 1)
     return fail(c, SWRT_ERR_ARG, "nintervals must be 1..SWRT_MAX_SLOTS-1");
@@ -1582,6 +1655,8 @@ int swrt_advance_intervals(swrt_ctx* c, int nintervals, const double* dts, int64
   rc = run_advance_intervals(c, nintervals, dts, nsub, f, gH, alpha0, dalpha, bump, save_every);
   if (rc) return rc;
   c->steps_done += nintervals * nsub;
+  // a QG stream renames slots by their use events: mark them after the second stream's launches too
+  if (slot_events(c)) HIPCHK_RC(join_b(c));
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -2118,6 +2193,8 @@ int swrt_check_arith(swrt_ctx* c, int64_t n, uint64_t seed, int64_t* mismatches3
 int swrt_synchronize(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
+  if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));
+  c->b_pending = false;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipStreamSynchronize(c->qstream));
   return SWRT_OK;
@@ -2145,6 +2222,7 @@ int swrt_qg_set_stream(swrt_ctx* c, int separate) {
 
 int swrt_get_stream(swrt_ctx* c, void** out) {
   if (!c || !out) return SWRT_ERR_ARG;
+  if (int rc = join_b(c)) return rc;  // work queued on it by the caller sees every packet
   *out = (void*)c->stream;
   return SWRT_OK;
 }
@@ -2152,6 +2230,7 @@ int swrt_get_stream(swrt_ctx* c, void** out) {
 int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches) {
   if (!c) return SWRT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
+  if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));  // stop events of split launches
   HIPCHK(c, hipStreamSynchronize(c->stream));
   double tot = c->timing.folded_ms;
   for (size_t i = 0; i + 1 < c->timing.used; i += 2) {

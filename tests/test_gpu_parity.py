@@ -838,6 +838,57 @@ def test_fma_gather_mode_tolerance(ctx, oracle_lib, n_cells):
     assert not np.array_equal(xf, xo)  # the FMA path really ran
 
 
+def test_packet_streams_bit_identical(ctx, oracle_lib):
+    """swrt_set_packet_streams(2): tile launches as two half launches on two
+    streams, joined only when something reads the packets.  A call sequence
+    that mixes history frames, re-binnings inside and between calls, a field
+    rewrite, multi-interval launches, reads and ode23 gives the bits of one
+    stream — and the oracle's on a subset."""
+    import argparse
+    import bench
+    import swraytracing_amd as sw
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=300_000, world=1, rank=0, seed=146, mode="blend")
+    w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
+    p0, p1 = ctx.get_field_grid(0).copy(), ctx.get_field_grid(1).copy()
+    h = w["dt"] / 5
+    out = {}
+    for streams in (2, 1):
+        ctx.set_packet_streams(streams)
+        ctx.set_locality(20, 0)
+        try:
+            ctx.set_field_grid(0, p0, 512, w["L"], 1024)
+            ctx.set_field_grid(1, p1, 512, w["L"], 1024)
+            ctx.packets_set(w["x"], w["k"])
+            ctx.history_reset()
+            for _ in range(7):  # 35 steps: re-binnings at 20 and inside a call at 40 > 35
+                ctx.advance(h, 5, w["f"], w["gH"], nslots=2, alpha0=0.1, dalpha=0.2, bump=orc.BUMP_QG, save_every=5)
+            x1, k1 = ctx.packets_get()
+            hx, hk = ctx.history()
+            ctx.set_field_grid(1, p0, 512, w["L"], 1024)  # rewrite a slot the second stream read
+            ctx.set_field_grid(2, p1, 512, w["L"], 1024)
+            ctx.advance_intervals([h, 1.1 * h], 5, w["f"], w["gH"], alpha0=0.1, dalpha=0.2, bump=orc.BUMP_QG)
+            ctx.advance(h, 3, w["f"], w["gH"], nslots=2, alpha0=0.1, dalpha=0.2, bump=orc.BUMP_QG)
+            x2, k2 = ctx.packets_get()
+            ctx.set_field_grid(1, p1, 512, w["L"], 1024)
+            st = {}
+            sw.ode23_packets(ctx, (0.0, 5 * h), 5 * h, w["f"], 1.0, stats=st)
+            x3, k3 = ctx.packets_get()
+            out[streams] = (x1, k1, hx, hk, x2, k2, x3, k3)
+        finally:
+            ctx.set_packet_streams(1)
+            ctx.set_locality(4, 0)
+    for a, b in zip(out[1], out[2]):
+        assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    idx = np.sort(np.random.default_rng(4).choice(args.packets, 1500, replace=False))
+    xo, ko = w["x"][idx], w["k"][idx]
+    for _ in range(7):
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.2, 512, 1024, w["L"] / 512, orc.BUMP_QG, xo, ko, h, 5,
+                                           w["f"], w["gH"])
+    np.testing.assert_array_equal(out[2][0][idx], xo)
+    np.testing.assert_array_equal(out[2][1][idx], ko)
+
+
 @pytest.mark.parametrize("substeps,rebin_every,calls", [(5, 20, 10), (1, 4, 12)])
 def test_bench_configuration_subset_bitexact(ctx, oracle_lib, substeps, rebin_every, calls):
     """The headline bench configuration itself (bench.py: 2-layer 512^2 field,

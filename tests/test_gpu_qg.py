@@ -272,6 +272,26 @@ def _load_data_reads(d, nx, N, f, Cg, Ug):
     assert open(d / "run.log").read().rstrip("\n").split("\n")[-1].startswith("Real time elapsed: ")
 
 
+def test_qg2_driver_packet_streams_identical_files(tmp_path):
+    """The 2-layer driver (QG stream renaming snapshot slots beside the packet
+    launches) with the packet launches split over two streams writes the
+    same packet files, byte for byte, as with one."""
+    import swraytracing_amd as sw
+    files = {}
+    for streams in (1, 2):
+        c = sw.Context(0)
+        try:
+            c.set_packet_streams(streams)
+            d = tmp_path / f"s{streams}"
+            sw.qg2layersw_raytrace(128, 30_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=5, max_steps=60,
+                                   seed=5, ctx=c)
+            files[streams] = {n: (d / f"{n}.bin").read_bytes() for n in ("packet_x", "packet_k", "packet_time")}
+        finally:
+            c.close()
+    assert files[1] == files[2]
+    assert len(files[1]["packet_x"]) == 8 * 30_000 * 2 * (1 + 60 // 25)
+
+
 def test_golden_qg_fixture(ctx):
     import os
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_qg.npz"))
