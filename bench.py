@@ -201,7 +201,10 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     U0 = model.max_speed()
     loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
                            integrator=integrator)
-    for _ in range(4):  # AB1/AB2 start-up, first-use allocations
+    # AB1/AB2 start-up and first-use allocations: the snapshot renaming (qg.py
+    # TwoLayerLoop) allocates its spare slot buffers during the first steps, a
+    # hipMalloc each — outside the timed steps
+    for _ in range(args.driver_warmup):
         loop.step()
     loop.flush()
     ctx.synchronize()
@@ -350,6 +353,8 @@ def parse_args(argv=None):
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
     ap.add_argument("--driver-steps", type=int, default=20,
                     help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
+    ap.add_argument("--driver-warmup", type=int, default=16,
+                    help="untimed driver steps before the timed ones (start-up, spare snapshot buffers)")
     ap.add_argument("--ode23-steps", type=int, default=4,
                     help="then this many driver steps with the reference's ode23 packet integrator (0: skip)")
     ap.add_argument("--gather", action="store_true",
