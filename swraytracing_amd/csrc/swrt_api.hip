@@ -191,6 +191,8 @@ struct swrt_ctx {
   int64_t steps_since_bin = 0;
   bool bin_valid = false;
   bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
+  int64_t key_nx = 0;       // ... on slot 0's grid of that launch (the keys depend on nx and L only,
+  double key_L = 0.0;       //     not on the field values: new snapshots keep them valid)
   bool counts_zero = false;  // bins' count block is all zero (cleared by the last scan)
   int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
   bool sort_lead = SWRT_SORT_LEAD;  // in-tile sort keys lead by the group-velocity drift
@@ -724,7 +726,8 @@ int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
   if (nbins > kMaxBins) return fail(c, SWRT_ERR_ARG, "too many spatial bins (raise tile size)");
   const int64_t n = c->n;
   const unsigned grid = nblocks(n, 256 * kBinPerThread);
-  if (!(c->keys_fresh && c->bin_valid && nbins == c->nbins)) {
+  const bool keys_valid = c->keys_fresh && c->bin_valid && nbins == c->nbins && c->key_nx == s.nx && c->key_L == s.L;
+  if (!keys_valid) {
     HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * nbins, c->stream));
     hipLaunchKernelGGL(bin_count_kernel, dim3(grid), dim3(256), sizeof(int) * nbins, c->stream, g, c->dx, n,
                        nbins, c->keys, c->bins);
@@ -798,6 +801,8 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     c->counts_zero = false;
     t.next_keys = c->keys;
     t.next_counts = c->bins;
+    c->key_nx = c->slot[0].nx;
+    c->key_L = c->slot[0].L;
   }
   if (big) {  // leap_tile chose 32-cell tiles: two divergence-free snapshots (checked again here)
     if (a.nslots != 2 || !(iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)))
@@ -1121,7 +1126,6 @@ int swrt_set_field_grid(swrt_ctx* c, int slot, const double* fields6, int64_t nx
   s.ny_period = ny_period;
   s.has_psi = false;
   s.set = true;
-  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -1164,7 +1168,6 @@ int swrt_set_field_psi(swrt_ctx* c, int slot, const double* psi_grid, int64_t nx
   s.L = L;
   s.ny_period = nx;
   s.set = true;
-  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -1202,7 +1205,6 @@ int swrt_set_field_qk(swrt_ctx* c, int slot, const double* qk_interleaved, int64
   s.L = L;
   s.ny_period = ny_period;
   s.set = true;
-  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -1247,7 +1249,6 @@ int swrt_set_field_q(swrt_ctx* c, int slot, const double* q_grid, int64_t nx, do
   s.L = L;
   s.ny_period = ny_period;
   s.set = true;
-  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -2696,7 +2697,6 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
     HIPCHK(c, hipEventRecord(s.wev, c->stream));
     s.wpend = true;
   }
-  c->keys_fresh = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -2705,7 +2705,6 @@ int swrt_swap_slots(swrt_ctx* c, int a, int b) {
   if (!c) return SWRT_ERR_ARG;
   if (a < 0 || a >= SWRT_MAX_SLOTS || b < 0 || b >= SWRT_MAX_SLOTS) return fail(c, SWRT_ERR_ARG, "slot out of range");
   std::swap(c->slot[a], c->slot[b]);
-  c->keys_fresh = false;
   return SWRT_OK;
 }
 
