@@ -211,6 +211,7 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     torch.cuda.synchronize(dev)
     if distributed:
         dist.barrier()
+    nd0 = len(loop.dts)
     t0 = time.perf_counter()
     for _ in range(nsteps):
         loop.step()
@@ -225,7 +226,10 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
             + (f"{args.substeps} leapfrog substeps" if integrator == "leapfrog" else "ode23 over the interval "
                "(qg2layersw_raytrace.m:195: RelTol 1e-3, AbsTol 1e-6, MaxStep 0.1*dt)")
             + f" of {w['x'].shape[0]} packets/GPU (qg2layersw_raytrace.m:152-197)")
-    out = {"ms_per_pde_step": ms, "steps": nsteps, "what": what}
+    timed_dts = loop.dts[nd0:]
+    out = {"ms_per_pde_step": ms, "steps": nsteps, "what": what,
+           # the CFL rule (qg2layersw_raytrace.m:156-165) re-forms the exponential propagators when dt changes
+           "dt_changes": int(sum(1 for a, b in zip(loop.dts[nd0 - 1:], timed_dts) if a != b))}
     if integrator == "leapfrog":
         out["packet_steps_per_s"] = n_total * args.substeps / (ms / 1e3)
     else:
@@ -337,8 +341,9 @@ def parse_args(argv=None):
                     help="LDS-tiled launches: 0 auto (build threshold, off by default), 1, 2 (same bits)")
     ap.add_argument("--tile-cells", type=int, default=0,
                     help="LDS-tiled launches: cells per tile side, 0 auto (build threshold, off by default), 16, 32 (same bits)")
-    ap.add_argument("--packet-streams", type=int, default=1,
-                    help="LDS-tiled launches split over 1 or 2 streams (swrt_set_packet_streams; same bits)")
+    ap.add_argument("--packet-streams", type=int, default=0,
+                    help="LDS-tiled launches split over 1 or 2 streams (swrt_set_packet_streams; same bits); "
+                         "0: the library default (2)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--tail-split", type=int, default=-1,
@@ -492,7 +497,8 @@ def main(argv=None):
     ctx.set_blend_mode(args.blend_mode)
     ctx.set_lanes_per_packet(args.lanes_per_packet)
     ctx.set_tile_cells(args.tile_cells)
-    ctx.set_packet_streams(args.packet_streams)
+    if args.packet_streams:
+        ctx.set_packet_streams(args.packet_streams)
     if args.tail_split >= 0:
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
     if args.tile_order >= 0:

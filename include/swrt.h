@@ -230,7 +230,7 @@ int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
  * Results are bit-identical for any setting. */
 int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
 
-/* Packet streams of the LDS-tiled leapfrog: 1 (default) or 2.  With 2 every
+/* Packet streams of the LDS-tiled leapfrog: 2 (default) or 1.  With 2 every
  * launch runs as two half launches — alternate tiles of each XCD band — on
  * the context's packet stream and a second stream.  Between re-binnings the
  * halves advance disjoint packet ranges, so the second stream's launch k

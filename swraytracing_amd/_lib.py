@@ -356,8 +356,8 @@ class Context:
         """swrt_set_tile_cells: 0 auto (build threshold; off by default), 16, 32; same bits."""
         self._chk(self._L.swrt_set_tile_cells(self._h, int(cells)), "swrt_set_tile_cells")
 
-    def set_packet_streams(self, streams=1):
-        """swrt_set_packet_streams: 1, or 2 (tile launches split over two streams; same bits)."""
+    def set_packet_streams(self, streams=2):
+        """swrt_set_packet_streams: 2 (default: tile launches split over two streams) or 1; same bits."""
         self._chk(self._L.swrt_set_packet_streams(self._h, int(streams)), "swrt_set_packet_streams")
 
     def set_blend_mode(self, mode=0):

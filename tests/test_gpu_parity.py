@@ -876,7 +876,7 @@ def test_packet_streams_bit_identical(ctx, oracle_lib):
             x3, k3 = ctx.packets_get()
             out[streams] = (x1, k1, hx, hk, x2, k2, x3, k3)
         finally:
-            ctx.set_packet_streams(1)
+            ctx.set_packet_streams(2)  # the library default
             ctx.set_locality(4, 0)
     for a, b in zip(out[1], out[2]):
         assert np.array_equal(a.view(np.uint64), b.view(np.uint64))

@@ -6,7 +6,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$1
-BARGS=${2:-"--steps 12 --warmup 2 --no-cpu-baseline"}
+BARGS=${2:-"--steps 12 --warmup 2 --no-cpu-baseline --no-forecast --no-fma --driver-steps 0 --ode23-steps 0 --packet-streams 1"}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES"
