@@ -105,6 +105,9 @@ def build_workload(ctx, args, lo, hi, n_total):
         nt = max(1, nx // 16)
         t = np.arange(N) % (nt * nt)
         x = np.stack([(t // nt) * 16 + 16 * rng.random(N), (t % nt) * 16 + 16 * rng.random(N)], axis=1) * (L / nx)
+    elif getattr(args, "positions", "uniform") == "band":
+        x = (L * rng.random((n_total, 2)) - L / 2)[lo:hi]
+        x[:, 0] = (x[:, 0] + L / 2) / args.band_parts - L / 2
     else:
         x = (L * rng.random((n_total, 2)) - L / 2)[lo:hi]
     return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
@@ -324,8 +327,12 @@ def parse_args(argv=None):
                     help="PDE intervals per bench step, one call (swrt_advance_intervals; up to 4 per launch)")
     ap.add_argument("--mode", choices=["blend", "steady"], default="blend")
     ap.add_argument("--seed", type=int, default=146)
-    ap.add_argument("--positions", choices=["uniform", "stratified"], default="uniform",
-                    help="initial packet positions (stratified: equal packets per tile, a diagnostic)")
+    ap.add_argument("--positions", choices=["uniform", "stratified", "band"], default="uniform",
+                    help="initial packet positions (stratified: equal packets per tile; band: all packets in the "
+                         "first 1/--band-parts of the domain in x, a spatial-shard diagnostic)")
+    ap.add_argument("--band-parts", type=int, default=8)
+    ap.add_argument("--gather-mode", type=int, default=0, choices=[0, 1],
+                    help="headline stencil arithmetic: 0 bit-exact (default), 1 FMA (tolerance; PMC diagnostics)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fma", action="store_true",
@@ -341,9 +348,9 @@ def parse_args(argv=None):
                     help="LDS-tiled launches: 0 auto (build threshold, off by default), 1, 2 (same bits)")
     ap.add_argument("--tile-cells", type=int, default=0,
                     help="LDS-tiled launches: cells per tile side, 0 auto (build threshold, off by default), 16, 32 (same bits)")
-    ap.add_argument("--packet-streams", type=int, default=0,
-                    help="LDS-tiled launches split over 1 or 2 streams (swrt_set_packet_streams; same bits); "
-                         "0: the library default (2)")
+    ap.add_argument("--packet-streams", type=int, default=2, choices=[1, 2],
+                    help="LDS-tiled launches split over 1 or 2 streams (swrt_set_packet_streams; same bits; "
+                         "2 is the library default)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
     ap.add_argument("--tail-split", type=int, default=-1,
@@ -497,8 +504,8 @@ def main(argv=None):
     ctx.set_blend_mode(args.blend_mode)
     ctx.set_lanes_per_packet(args.lanes_per_packet)
     ctx.set_tile_cells(args.tile_cells)
-    if args.packet_streams:
-        ctx.set_packet_streams(args.packet_streams)
+    ctx.set_packet_streams(args.packet_streams)
+    ctx.set_gather_mode(args.gather_mode)
     if args.tail_split >= 0:
         ctx.set_tail_split(args.tail_split, args.tail_quarters)
     if args.tile_order >= 0:
@@ -529,10 +536,22 @@ def main(argv=None):
     # sampled HIP-event time of the packet kernel; without samples fall back to wall time per step
     avg_launch_s = (kms / 1e3) / launches if launches > 0 else elapsed / args.steps
     spl = steps_per_launch_of(args, ivs)
-    key = f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}" + (f"_iv{ivs}" if ivs > 1 else "")
+    key = (f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}" + (f"_iv{ivs}" if ivs > 1 else "")
+           + ("_fma" if args.gather_mode == 1 else ""))
     pmc, pmc_note = (load_pmc(key) if args.blend_mode == 0 and args.kernel in (0, 2)
                      else (None, "PMC only for the default bit-exact tile kernel"))
-    roof = roofline(pmc, N, args.nx, w["nslots"], spl, avg_launch_s, launches, args.timing_every)
+    # Two packet streams: each launch is two half launches whose spans overlap
+    # the neighbouring calls', so a launch's event span is not its share of
+    # the GPU; the roofline then uses the wall time per launch of the timed
+    # region (re-binning kernels and launch gaps included: a lower bound on
+    # the kernel's own rate).  One stream: the HIP-event launch time.
+    launches_per_step = max(1, -(-args.substeps * ivs // spl))
+    two = args.packet_streams == 2 and args.kernel in (0, 2)
+    basis_s = elapsed / (args.steps * launches_per_step) if two else avg_launch_s
+    roof = roofline(pmc, N, args.nx, w["nslots"], spl, basis_s, launches, args.timing_every)
+    roof["time_basis"] = ("wall time per launch of the timed region (two overlapping half launches per launch)"
+                          if two else "HIP-event time of the packet-kernel launches")
+    roof["launch_span_ms"] = avg_launch_s * 1e3
     roof["pmc_note"] = pmc_note
     workload = ("qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
                 f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, {args.nx}^2x2 field, {n_total} packets "
@@ -558,7 +577,7 @@ def main(argv=None):
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split,
                    "lanes_per_packet": args.lanes_per_packet, "tile_cells": args.tile_cells,
-                   "packet_streams": args.packet_streams,
+                   "packet_streams": args.packet_streams, "gather_mode": args.gather_mode,
                    "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,
@@ -566,7 +585,7 @@ def main(argv=None):
     }
     if gathered is not None:
         out["gathered_finite"] = gathered
-    if not args.no_fma and args.blend_mode == 0 and args.kernel in (0, 2):
+    if not args.no_fma and args.blend_mode == 0 and args.kernel in (0, 2) and args.gather_mode == 0:
         # the opt-in FMA gather (tolerance parity, tests/test_gpu_parity.py::test_fma_gather_mode_tolerance):
         # the same workload and packets, timed the same way; the headline stays bit-exact
         ctx.packets_set(w["x"], w["k"])

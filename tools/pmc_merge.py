@@ -26,7 +26,7 @@ def config_key(args):
         return args[args.index(name) + 1] if name in args else default
     key = f"{arg('--mode', 'blend')}_nx{arg('--nx', '512')}_N{arg('--packets', '1000000')}_sub{arg('--substeps', '5')}"
     iv = int(arg("--intervals", "1"))
-    return key + (f"_iv{iv}" if iv > 1 else "")
+    return key + (f"_iv{iv}" if iv > 1 else "") + ("_fma" if arg("--gather-mode", "0") == "1" else "")
 
 
 def main():
