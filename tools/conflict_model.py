@@ -19,12 +19,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle import cbind, swrt_oracle as orc  # noqa: E402
 
-T, M, WS = 16, 3, 28
+T, M, WS = 16, 3, 28  # tile cells, margin, window row stride (--tile 32: 32, 3, 44)
 
 
 def zorder(dx, dy):
     k = np.zeros_like(dx)
-    for b in range(4):
+    for b in range(5):
         k |= ((dy >> b) & 1) << (2 * b) | ((dx >> b) & 1) << (2 * b + 1)
     return k
 
@@ -57,7 +57,12 @@ def main():
     ap.add_argument("--cycle", type=int, default=20, help="steps between re-binnings (bench: 20)")
     ap.add_argument("--launch", type=int, default=5, help="steps per launch (bench: 5)")
     ap.add_argument("--packets", type=int, default=1_000_000, help="ensemble size (a strong-scaling shard: 125000)")
+    ap.add_argument("--tile", type=int, default=16, help="tile cells (16, or 32 with row stride 44)")
+    ap.add_argument("--only-deal", action="store_true", help="only the Z-order baseline and the class deal")
     args = ap.parse_args()
+    global T, WS
+    if args.tile == 32:
+        T, WS = 32, 44
     nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
     rng = np.random.default_rng(146)
     import bench
@@ -113,6 +118,8 @@ def main():
     lead = X[0] + 0.5 * R * dt * cg0
     policies["0.5 lead + in-wave re-sort per launch"] = ("wave", lead)
     policies["class deal per step (quad of x1, over the tile)"] = "deal"
+    if args.only_deal:
+        policies = {k: v for k, v in policies.items() if k.startswith("x0 + 0.5") or isinstance(v, str)}
     for name, keypos in policies.items():
         if isinstance(keypos, str):  # per step: deal the tile's packets to 16-lane groups by LDS slot class
             tot = np.zeros(R)
