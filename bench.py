@@ -105,9 +105,10 @@ def build_workload(ctx, args, lo, hi, n_total):
         nt = max(1, nx // 16)
         t = np.arange(N) % (nt * nt)
         x = np.stack([(t // nt) * 16 + 16 * rng.random(N), (t % nt) * 16 + 16 * rng.random(N)], axis=1) * (L / nx)
-    elif getattr(args, "positions", "uniform") == "band":
+    elif getattr(args, "positions", "uniform") in ("band", "yband"):
         x = (L * rng.random((n_total, 2)) - L / 2)[lo:hi]
-        x[:, 0] = (x[:, 0] + L / 2) / args.band_parts - L / 2
+        c = 0 if args.positions == "band" else 1
+        x[:, c] = (x[:, c] + L / 2) / args.band_parts - L / 2
     else:
         x = (L * rng.random((n_total, 2)) - L / 2)[lo:hi]
     return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
@@ -327,7 +328,7 @@ def parse_args(argv=None):
                     help="PDE intervals per bench step, one call (swrt_advance_intervals; up to 4 per launch)")
     ap.add_argument("--mode", choices=["blend", "steady"], default="blend")
     ap.add_argument("--seed", type=int, default=146)
-    ap.add_argument("--positions", choices=["uniform", "stratified", "band"], default="uniform",
+    ap.add_argument("--positions", choices=["uniform", "stratified", "band", "yband"], default="uniform",
                     help="initial packet positions (stratified: equal packets per tile; band: all packets in the "
                          "first 1/--band-parts of the domain in x, a spatial-shard diagnostic)")
     ap.add_argument("--band-parts", type=int, default=8)
