@@ -483,12 +483,23 @@ int pack_slot(swrt_ctx* c, int slot, const double* dplanes, double shear) {
 // layers (8-vector inverse + 1-vector forward 2-D transforms per step) the
 // one-buffer form takes the PDE step from 0.078 (radix 2, 256 lanes) / 0.077
 // (radix 4 ping-pong) to 0.073 ms (profiles/r02_v21_fft_mode_ab.log).
+// Vectors per workgroup of the one-buffer form: four (n lanes: the shape of
+// a packet workgroup's slot, so the PDE step's transforms fit where one
+// retired while packets run beside them; for the column pass also one
+// 64-B segment per row read) when the batch allows.
+int fft_group(int n, int nvec, bool tin) {
+  const int C = 4;
+  if (C * (n / 4) > 1024 || nvec % (tin ? 8 * C : C) != 0) return 1;
+  return C;
+}
+
 template <bool TIN>
 void launch_fft(swrt_ctx* c, const double2* in, double2* out, int n, int logn, int nvec, int inverse) {
-  if (n <= 1024)
-    hipLaunchKernelGGL((fft_vec_kernel<TIN, 2>), dim3((unsigned)nvec), dim3(n / 4), sizeof(double2) * n, c->stream,
-                       in, out, n, logn, c->tw, inverse, nvec);
-  else
+  if (n <= 1024) {
+    const int C = fft_group(n, nvec, TIN);
+    hipLaunchKernelGGL((fft_vec_kernel<TIN, 2>), dim3((unsigned)(nvec / C)), dim3(C * n / 4),
+                       sizeof(double2) * C * (n + 1), c->stream, in, out, n, logn, c->tw, inverse, nvec);
+  } else
     hipLaunchKernelGGL((fft_vec_kernel<TIN, 1>), dim3((unsigned)nvec), dim3(128), sizeof(double2) * 2 * n, c->stream,
                        in, out, n, logn, c->tw, inverse, nvec);
 }
@@ -2392,8 +2403,8 @@ int qg_post_inverse(swrt_ctx* c) {
     while ((1 << logn) < n) ++logn;
     const size_t lds = sizeof(double2) * nb * n;
     if (nl == 2)
-      hipLaunchKernelGGL(qg_post_rows_kernel<2>, dim3((unsigned)n), dim3(nb * n / 4), lds, c->stream,
-                         (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
+      hipLaunchKernelGGL(qg_post_rows_split_kernel, dim3(2 * (unsigned)n), dim3(n), sizeof(double2) * 4 * n,
+                         c->stream, (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
     else
       hipLaunchKernelGGL(qg_post_rows_kernel<1>, dim3((unsigned)n), dim3(nb * n / 4), lds, c->stream,
                          (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
@@ -2429,8 +2440,15 @@ int qg_post(swrt_ctx* c) {
     // values, same per-vector FFT as the separate kernel + transform_2d)
     int logn = 0;
     while ((1 << logn) < n) ++logn;
-    hipLaunchKernelGGL(fft_jacobian_rows_kernel, dim3((unsigned)n), dim3(n / 4), sizeof(double2) * n, c->stream,
-                       (const double2*)q.PT, nl, n, logn, uvT, q.g.shear, q.dmax, (const double2*)c->tw, q.PZ);
+    const int R = fft_group(n, n, false);  // rows per workgroup
+    const dim3 jg((unsigned)(n / R)), jb((unsigned)(R * n / 4));
+    const size_t jl = sizeof(double2) * R * n;
+    if (nl == 2)
+      hipLaunchKernelGGL(fft_jacobian_rows_kernel<2>, jg, jb, jl, c->stream, (const double2*)q.PT, n, logn, uvT,
+                         q.g.shear, q.dmax, (const double2*)c->tw, q.PZ);
+    else
+      hipLaunchKernelGGL(fft_jacobian_rows_kernel<1>, jg, jb, jl, c->stream, (const double2*)q.PT, n, logn, uvT,
+                         q.g.shear, q.dmax, (const double2*)c->tw, q.PZ);
     HIPCHK(c, hipGetLastError());
     launch_fft<true>(c, q.PZ, q.PT, n, logn, n, 0);
     HIPCHK(c, hipGetLastError());

@@ -29,8 +29,9 @@ namespace swrt {
 // One radix-4 Stockham butterfly (stride s = 4^(logs/2), quarter-length
 // m = n/(4s), b = q + s*p):  a_j = x[b + j*n/4],
 //   y_k = DFT4(a)_k * w^(k*p*s)  goes to  x'[q + s*(4p + k)];  returns q + 4sp.
-__device__ __forceinline__ int r4_butterfly(const double2* xa, int b, int quarter, int s, int logs,
-                                            const double2* tw, int inverse, double2 y[4]) {
+// w1..w3 = tw[k*p*s], conjugated for the inverse.
+__device__ __forceinline__ int r4_butterfly_w(const double2* xa, int b, int quarter, int s, int logs, double2 w1,
+                                              double2 w2, double2 w3, int inverse, double2 y[4]) {
   const int q = b & (s - 1);
   const int p = b >> logs;
   const double2 a0 = xa[b], a1 = xa[b + quarter], a2 = xa[b + 2 * quarter], a3 = xa[b + 3 * quarter];
@@ -38,9 +39,6 @@ __device__ __forceinline__ int r4_butterfly(const double2* xa, int b, int quarte
   const double2 t2 = make_double2(a1.x + a3.x, a1.y + a3.y), u = make_double2(a1.x - a3.x, a1.y - a3.y);
   // (a1 - a3) * (-i) forward, * (+i) inverse
   const double2 t3 = inverse ? make_double2(-u.y, u.x) : make_double2(u.y, -u.x);
-  const int e = p * s;
-  double2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
-  if (inverse) { w1.y = -w1.y; w2.y = -w2.y; w3.y = -w3.y; }
   const double2 b1 = make_double2(t1.x + t3.x, t1.y + t3.y), b2 = make_double2(t0.x - t2.x, t0.y - t2.y);
   const double2 b3 = make_double2(t1.x - t3.x, t1.y - t3.y);
   y[0] = make_double2(t0.x + t2.x, t0.y + t2.y);
@@ -49,19 +47,41 @@ __device__ __forceinline__ int r4_butterfly(const double2* xa, int b, int quarte
   y[3] = make_double2(b3.x * w3.x - b3.y * w3.y, b3.x * w3.y + b3.y * w3.x);
   return q + 4 * s * p;
 }
+__device__ __forceinline__ int r4_butterfly(const double2* xa, int b, int quarter, int s, int logs,
+                                            const double2* tw, int inverse, double2 y[4]) {
+  const int e = (b >> logs) * s;
+  double2 w1 = tw[e], w2 = tw[2 * e], w3 = tw[3 * e];
+  if (inverse) { w1.y = -w1.y; w2.y = -w2.y; w3.y = -w3.y; }
+  return r4_butterfly_w(xa, b, quarter, s, logs, w1, w2, w3, inverse, y);
+}
 
-// All stages of one length-n vector in ONE LDS buffer xa, blockDim == n/4:
-// each lane holds its butterfly's four values in registers between the read
-// and the write of a stage; b = the lane's butterfly (0..n/4-1).  The
-// barriers are the whole workgroup's: several vectors of one length may run
-// side by side.  Ends after a __syncthreads (xa holds the result).
+// All stages of one length-n vector in ONE LDS buffer xa, blockDim == n/4
+// per vector: each lane holds its butterfly's four values in registers
+// between the read and the write of a stage; b = the lane's butterfly
+// (0..n/4-1).  The barriers are the whole workgroup's: several vectors of one
+// length may run side by side.  Ends after a __syncthreads (xa holds the
+// result).  The twiddles are read from the global table (L2-resident): an
+// LDS copy of it made these kernels faster alone but the driver step slower,
+// its LDS footprint crowding the packet kernel they run beside
+// (profiles/r03_v4_qg/README.md).
 __device__ __forceinline__ void fft_stages_one_buffer(double2* xa, int b, int n, int logn, const double2* tw,
                                                       int inverse) {
   const int quarter = n >> 2, half = n >> 1;
+  // the next radix-4 stage's twiddles are loaded before this stage's LDS
+  // work, so their latency hides behind it (unconditional: e <= b < n/4
+  // keeps 3e inside the table for every stage)
+  int e = b;
+  double2 n1 = tw[e], n2 = tw[2 * e], n3 = tw[3 * e];
   int s = 1, logs = 0;
   for (; logs + 2 <= logn; logs += 2, s <<= 2) {
+    double2 w1 = n1, w2 = n2, w3 = n3;
+    e = (b >> (logs + 2)) << (logs + 2);
+    n1 = tw[e];
+    n2 = tw[2 * e];
+    n3 = tw[3 * e];
+    if (inverse) { w1.y = -w1.y; w2.y = -w2.y; w3.y = -w3.y; }
     double2 y[4];
-    const int o = r4_butterfly(xa, b, quarter, s, logs, tw, inverse, y);
+    const int o = r4_butterfly_w(xa, b, quarter, s, logs, w1, w2, w3, inverse, y);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) xa[o + k * s] = y[k];
@@ -79,14 +99,52 @@ __device__ __forceinline__ void fft_stages_one_buffer(double2* xa, int b, int n,
 }
 
 // MODE 1: radix-4 stages (+ one radix-2 stage for odd log2 n), ping-pong
-// LDS; 2: the same in one LDS buffer, blockDim = n/4 (n <= 1024).
+// LDS; 2: the same in one LDS buffer per vector, C vectors per workgroup of
+// C*n/4 lanes (n <= 1024), dynamic LDS C*(n+1) double2.
 template <bool TIN, int MODE>
-__global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2* data, int n, int logn,
+__global__ void __launch_bounds__(1024) fft_vec_kernel(const double2* in, double2* data, int n, int logn,
                                                       const double2* tw, int inverse, int nvec) {
   extern __shared__ double2 sbuf[];
   double2* xa = sbuf;
   double2* ya = MODE == 2 ? sbuf : sbuf + n;
   double2* v;
+  if constexpr (MODE == 2) {
+    // C = blockDim/(n/4) vectors per workgroup (1, 2 or 4; nvec % (8C) == 0
+    // for TIN), n/4 lanes each, four elements per lane; every load issued
+    // before the first wait.  LDS: C vectors at stride n + 1 (the C columns
+    // of one row land in distinct banks).
+    const int quarter = n >> 2, t = threadIdx.x, C = (int)blockDim.x / quarter;
+    const int ld = n + 1;
+    const int col = t / quarter, b = t - col * quarter;
+    double2 r[4];
+    int vec0;
+    if constexpr (TIN) {
+      // groups of C adjacent columns; consecutive groups on one XCD (above)
+      const int ng = nvec / C;
+      vec0 = ((int)(blockIdx.x & 7) * (ng >> 3) + (int)(blockIdx.x >> 3)) * C;
+      const int bb = vec0 >> logn, i0 = vec0 & (n - 1);
+      const double2* src = in + ((size_t)bb << (2 * logn)) + i0;
+      const int c = t % C, j0 = t / C;  // lanes C*j .. C*j + C-1 read row j's C columns
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = src[(size_t)(j0 + k * quarter) * n + c];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sbuf[c * ld + j0 + k * quarter] = r[k];
+    } else {
+      vec0 = (int)blockIdx.x * C;
+      const double2* src = data + (size_t)(vec0 + col) * n;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) r[k] = src[b + k * quarter];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sbuf[col * ld + b + k * quarter] = r[k];
+    }
+    __syncthreads();
+    double2* x = sbuf + col * ld;
+    fft_stages_one_buffer(x, b, n, logn, tw, inverse);
+    v = data + (size_t)(vec0 + col) * n;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[b + k * quarter] = x[b + k * quarter];
+    return;
+  }
   if constexpr (TIN) {
     const int vec = (int)(blockIdx.x & 7) * (nvec >> 3) + (int)(blockIdx.x >> 3);
     const int b = vec >> logn, i = vec & (n - 1);
@@ -99,10 +157,7 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2
   }
   __syncthreads();
   int s = 1, logs = 0;
-  if constexpr (MODE == 2) {
-    fft_stages_one_buffer(xa, threadIdx.x, n, logn, tw, inverse);
-    logs = logn;
-  } else {
+  {
     const int quarter = n >> 2;
     for (; logs + 2 <= logn; logs += 2, s <<= 2) {
       for (int b = threadIdx.x; b < quarter; b += blockDim.x) {
@@ -137,44 +192,60 @@ __global__ void __launch_bounds__(256) fft_vec_kernel(const double2* in, double2
 
 
 // The forward transform of J (qgsw_raytrace.m:282-283 / qg2layersw_raytrace.m:
-// 313-315) with the Jacobian computed in its first pass's load: vector y
-// (blockIdx.x) of J1 + i J2, J_l = psix.*qy - psiy.*qx from the inverse
-// transforms T[2l] = psi_x + i psi_y, T[2l+1] = q_x + i q_y (layout [x + n*y]),
+// 313-315) with the Jacobian computed in its first pass's load: vector y of
+// J1 + i J2, J_l = psix.*qy - psiy.*qx from the inverse transforms
+// T[2l] = psi_x + i psi_y, T[2l+1] = q_x + i q_y (layout [x + n*y]),
 // transformed along x into Zj's row y — the values qg_jacobian_max_kernel
 // writes, through the same per-vector FFT.  Also the CFL max of
 // (u + shear)^2 + v^2 over the nl u+iv planes at uv (one atomic per block).
-// blockDim == n/4 (n <= 1024).
-__global__ void __launch_bounds__(256) fft_jacobian_rows_kernel(const double2* T, int nl, int n, int logn,
-                                                                const double2* uv, double shear,
-                                                                unsigned long long* dmax, const double2* tw,
-                                                                double2* Zj) {
+// R = blockDim/(n/4) rows per workgroup (n <= 1024), dynamic LDS R*n double2;
+// every point load issued before the first wait.
+template <int NL>
+__global__ void __launch_bounds__(1024) fft_jacobian_rows_kernel(const double2* T, int n, int logn,
+                                                                 const double2* uv, double shear,
+                                                                 unsigned long long* dmax, const double2* tw,
+                                                                 double2* Zj) {
   extern __shared__ double2 sbuf[];
   __shared__ unsigned long long bmax;  // bits of a non-negative double: integer max == double max
-  if (threadIdx.x == 0) bmax = 0ull;
-  __syncthreads();
+  const int quarter = n >> 2, t = threadIdx.x, R = (int)blockDim.x / quarter;
+  const int rr = t / quarter, b = t - rr * quarter;
+  double2* x = sbuf + rr * n;
+  if (t == 0) bmax = 0ull;
   const int64_t nn = (int64_t)n * n;
-  const int64_t row = (int64_t)blockIdx.x * n;
-  double m = 0.0;
-  for (int j = threadIdx.x; j < n; j += blockDim.x) {
-    const int64_t i = row + j;
-    double J[2] = {0.0, 0.0};
-    for (int l = 0; l < nl; ++l) {
-      const double2 P = T[(2 * l) * nn + i], Q = T[(2 * l + 1) * nn + i];
-      J[l] = P.x * Q.y - P.y * Q.x;
+  const int64_t row = ((int64_t)blockIdx.x * R + rr) * n;
+  // the lane's four points, every load issued before the first wait
+  double2 P[4][NL], Q[4][NL], Z[4][NL];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = row + b + k * quarter;
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      P[k][l] = T[(2 * l) * nn + i];
+      Q[k][l] = T[(2 * l + 1) * nn + i];
+      Z[k][l] = uv[l * nn + i];
     }
-    sbuf[j] = make_double2(J[0], J[1]);
-    for (int l = 0; l < nl; ++l) {
-      const double2 z = uv[l * nn + i];
-      const double u = z.x + shear, v = z.y;
+  }
+  __syncthreads();  // bmax cleared
+  double m = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    double J[2] = {0.0, 0.0};
+#pragma unroll
+    for (int l = 0; l < NL; ++l) J[l] = P[k][l].x * Q[k][l].y - P[k][l].y * Q[k][l].x;
+    x[b + k * quarter] = make_double2(J[0], J[1]);
+#pragma unroll
+    for (int l = 0; l < NL; ++l) {
+      const double u = Z[k][l].x + shear, v = Z[k][l].y;
       const double s2 = u * u + v * v;
       m = s2 > m ? s2 : m;
     }
   }
   atomicMax(&bmax, (unsigned long long)__double_as_longlong(m));  // LDS atomic
   __syncthreads();
-  if (threadIdx.x == 0) atomicMax(dmax, bmax);
-  fft_stages_one_buffer(sbuf, threadIdx.x, n, logn, tw, 0);
-  for (int j = threadIdx.x; j < n; j += blockDim.x) Zj[row + j] = sbuf[j];
+  if (t == 0) atomicMax(dmax, bmax);
+  fft_stages_one_buffer(x, b, n, logn, tw, 0);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) Zj[row + b + k * quarter] = x[b + k * quarter];
 }
 
 // out[c + n*r] = in[r + n*c] for batch of nb n x n complex matrices.

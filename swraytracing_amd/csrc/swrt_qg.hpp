@@ -429,6 +429,36 @@ __global__ void __launch_bounds__(1024) qg_post_rows_kernel(const double2* qk, Q
     out[(int64_t)(e / n) * nn + (int64_t)r * n + (e % n)] = rows[e];
 }
 
+// The same for two layers, two workgroups per row (blockIdx = 2r + h): h = 0
+// builds and transforms the four Jacobian-input planes, h = 1 layer 1's
+// u+iv and layer 0's grid_U planes (output planes 4..7).  blockDim = n (four
+// vectors of n/4 lanes), dynamic LDS 4n double2: half the footprint of the
+// one-workgroup form (profiles/r03_v4_qg/README.md).
+__global__ void __launch_bounds__(1024) qg_post_rows_split_kernel(const double2* qk, QGDev g, int64_t nhalf,
+                                                                  int logn, const double2* tw, double2* out,
+                                                                  unsigned long long* dmax) {
+  extern __shared__ double2 rows[];
+  const int n = g.n;
+  const int64_t nn = (int64_t)n * n;
+  const int r = blockIdx.x >> 1, h = blockIdx.x & 1;
+  const int q = n >> 2, t = threadIdx.x;
+  if (blockIdx.x == 0 && t == 0) *dmax = 0ull;
+  const int64_t idx = (int64_t)t + (int64_t)n * r;
+  if (h == 0) {
+    qg_jac_spectra_to<2>(idx, qk, g, LdsRowPlanes{rows, n});
+  } else {
+    qg_vel_spectra_to<1>(idx, qk + nhalf, g, LdsRowPlanes{rows, n});
+    spectra_to(idx, qk, n, 1, g.K_d2, g.kscale, 0, LdsRowPlanes{rows + n, n}, n / 2, 1);
+  }
+  __syncthreads();
+  fft_stages_one_buffer(rows + (t / q) * n, t % q, n, logn, tw, 1);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int e = t + k * n;
+    out[(int64_t)(4 * h + k) * nn + (int64_t)r * n + t] = rows[e];
+  }
+}
+
 // qg_jacobian_kernel + qg_max_speed2_kernel over the same grid points:
 // J1 + i J2, and max (u + shear)^2 + v^2 over the nl u+iv planes at `uv`.
 // Grid-stride (kQgMaxPer points per thread), the max reduced by wave
