@@ -16,6 +16,9 @@ def main(out):
     for path in glob.glob(os.path.join(out, "q*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
             name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            grid = r.get("Grid_Size") or r.get("Grid_Size_X")
+            if grid:  # one kernel launched at several sizes (the 8-plane and the J column pass)
+                name += f" grid={grid}"
             per[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
             per[name]["ns"].append(float(r["End_Timestamp"]) - float(r["Start_Timestamp"]))
     res = {}
