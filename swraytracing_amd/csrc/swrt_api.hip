@@ -483,12 +483,14 @@ int pack_slot(swrt_ctx* c, int slot, const double* dplanes, double shear) {
 // layers (8-vector inverse + 1-vector forward 2-D transforms per step) the
 // one-buffer form takes the PDE step from 0.078 (radix 2, 256 lanes) / 0.077
 // (radix 4 ping-pong) to 0.073 ms (profiles/r02_v21_fft_mode_ab.log).
-// Vectors per workgroup of the one-buffer form: four (n lanes: the shape of
-// a packet workgroup's slot, so the PDE step's transforms fit where one
-// retired while packets run beside them; for the column pass also one
-// 64-B segment per row read) when the batch allows.
-int fft_group(int n, int nvec, bool tin) {
-  const int C = 4;
+// Vectors per workgroup of the one-buffer form (rows per workgroup of the
+// Jacobian pass): two when the transforms run alone (the PDE step 0.080 vs
+// 0.081 ms with four and 0.083 with one), one while packet launches run
+// beside them on their own stream (driver step 0.288 vs 0.293 ms with two and
+// 0.295 with four: small workgroups fit the slots packet workgroups free,
+// profiles/r03_v4_qg/README.md).  Batches that do not divide fall back to one.
+int fft_group(const swrt_ctx* c, int n, int nvec, bool tin) {
+  const int C = (c->qg_sep && c->n > 0) ? 1 : 2;
   if (C * (n / 4) > 1024 || nvec % (tin ? 8 * C : C) != 0) return 1;
   return C;
 }
@@ -496,7 +498,7 @@ int fft_group(int n, int nvec, bool tin) {
 template <bool TIN>
 void launch_fft(swrt_ctx* c, const double2* in, double2* out, int n, int logn, int nvec, int inverse) {
   if (n <= 1024) {
-    const int C = fft_group(n, nvec, TIN);
+    const int C = fft_group(c, n, nvec, TIN);
     hipLaunchKernelGGL((fft_vec_kernel<TIN, 2>), dim3((unsigned)(nvec / C)), dim3(C * n / 4),
                        sizeof(double2) * C * (n + 1), c->stream, in, out, n, logn, c->tw, inverse, nvec);
   } else
@@ -2440,7 +2442,7 @@ int qg_post(swrt_ctx* c) {
     // values, same per-vector FFT as the separate kernel + transform_2d)
     int logn = 0;
     while ((1 << logn) < n) ++logn;
-    const int R = fft_group(n, n, false);  // rows per workgroup
+    const int R = fft_group(c, n, n, false);  // rows per workgroup
     const dim3 jg((unsigned)(n / R)), jb((unsigned)(R * n / 4));
     const size_t jl = sizeof(double2) * R * n;
     if (nl == 2)
