@@ -414,6 +414,35 @@ def test_qg_fused_speed_and_snapshot_match_unfused(ctx, nx):
             assert np.array_equal(np.ascontiguousarray(u).view(np.uint64), np.ascontiguousarray(v).view(np.uint64))
 
 
+@pytest.mark.parametrize("nx", [64, 512])
+def test_qg_transform_grouping_bit_identical(nx):
+    """The post-step transforms take one vector per workgroup while a context
+    with packets runs its QG calls on the separate stream (the driver loop),
+    two otherwise (swrt_api.hip fft_group): the same per-vector FFTs, so U0,
+    the snapshots and qk agree bit for bit between a context without and one
+    with packets."""
+    out = []
+    for with_packets in (False, True):
+        c = sw.Context(0)
+        try:
+            if with_packets:
+                rng = np.random.default_rng(3)
+                c.packets_set(20.0 * rng.random((1000, 2)) - 10.0, rng.normal(0.0, 3.0, (1000, 2)))
+            m = sw.QGModel.two_layer(_two_layer_case(nx, seed=11), nx, 3.0, 1.0, L=20.0, ctx=c)
+            dt = 0.25 * (20.0 / nx) / m.max_speed()
+            for _ in range(4):
+                m.step(dt)
+            U0 = m.max_speed()
+            m.snapshot(0, which=0, ny_period=2 * nx)
+            out.append((U0, c.get_field_grid(0, nx).copy(), m.qk))
+        finally:
+            c.close()
+    (u_a, f_a, q_a), (u_b, f_b, q_b) = out
+    assert u_a == u_b
+    assert np.array_equal(f_a.view(np.uint64), f_b.view(np.uint64))
+    assert np.array_equal(np.ascontiguousarray(q_a).view(np.uint64), np.ascontiguousarray(q_b).view(np.uint64))
+
+
 def _ring_qk(nx, L, rng, Ug=0.2, kmin=10, kmax_ring=30):
     """Production-size 2-layer state (q1, -q1) on the driver's 10 < |k| <= 30
     ring (qg2layersw_raytrace.m:261-262) with random phases, scaled to
