@@ -349,8 +349,8 @@ def parse_args(argv=None):
                     help="LDS-tiled launches: 0 auto (build threshold, off by default), 1, 2 (same bits)")
     ap.add_argument("--tile-cells", type=int, default=0,
                     help="LDS-tiled launches: cells per tile side, 0 auto (build threshold, off by default), 16, 32 (same bits)")
-    ap.add_argument("--packet-streams", type=int, default=2, choices=[1, 2],
-                    help="LDS-tiled launches split over 1 or 2 streams (swrt_set_packet_streams; same bits; "
+    ap.add_argument("--packet-streams", type=int, default=2, choices=[1, 2, 4],
+                    help="LDS-tiled launches split over 1, 2 or 4 streams (swrt_set_packet_streams; same bits; "
                          "2 is the library default)")
     ap.add_argument("--cell-sort", type=int, default=0,
                     help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
@@ -547,10 +547,11 @@ def main(argv=None):
     # region (re-binning kernels and launch gaps included: a lower bound on
     # the kernel's own rate).  One stream: the HIP-event launch time.
     launches_per_step = max(1, -(-args.substeps * ivs // spl))
-    two = args.packet_streams == 2 and args.kernel in (0, 2)
+    two = args.packet_streams > 1 and args.kernel in (0, 2)
     basis_s = elapsed / (args.steps * launches_per_step) if two else avg_launch_s
     roof = roofline(pmc, N, args.nx, w["nslots"], spl, basis_s, launches, args.timing_every)
-    roof["time_basis"] = ("wall time per launch of the timed region (two overlapping half launches per launch)"
+    roof["time_basis"] = (f"wall time per launch of the timed region ({args.packet_streams} overlapping part "
+                          "launches per launch)"
                           if two else "HIP-event time of the packet-kernel launches")
     roof["launch_span_ms"] = avg_launch_s * 1e3
     roof["pmc_note"] = pmc_note

@@ -230,15 +230,18 @@ int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
  * Results are bit-identical for any setting. */
 int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
 
-/* Packet streams of the LDS-tiled leapfrog: 2 (default) or 1.  With 2 every
- * launch runs as two half launches — alternate tiles of each XCD band — on
- * the context's packet stream and a second stream.  Between re-binnings the
- * halves advance disjoint packet ranges, so the second stream's launch k
- * overlaps the first stream's launch k+1: one half's tail runs under the
- * other's body instead of leaving CUs idle at every launch boundary.  Any
- * call that reads the packets (or re-bins them) first orders the second
- * stream's work before its own; swrt_synchronize waits for both.  Results
- * are bit-identical for either setting. */
+/* Packet streams of the LDS-tiled leapfrog: 2 (default), 4 or 1.  With S > 1
+ * every launch runs as S part launches — every S-th tile of each XCD band —
+ * on the context's packet stream and S-1 more streams.  Between re-binnings
+ * the parts advance disjoint packet ranges, so one stream's launch k
+ * overlaps another's launch k+1: one part's tail runs under the other's
+ * body instead of leaving CUs idle at every launch boundary.  The launch
+ * after a re-binning's sort launch (which gathers its input from any slot)
+ * and any call that reads the packets (or re-bins them) first order the
+ * extra streams' work before their own; swrt_synchronize waits for all.
+ * Results are bit-identical for every setting.  4 measured slower than 2
+ * (1.65-1.69e10 vs 2.13-2.15e10 packet-steps/s: more streams than the
+ * process's hardware queues). */
 int swrt_set_packet_streams(swrt_ctx* ctx, int streams);
 
 /* Advance the device-resident packets by nsteps leapfrog steps

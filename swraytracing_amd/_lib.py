@@ -357,7 +357,7 @@ class Context:
         self._chk(self._L.swrt_set_tile_cells(self._h, int(cells)), "swrt_set_tile_cells")
 
     def set_packet_streams(self, streams=2):
-        """swrt_set_packet_streams: 2 (default: tile launches split over two streams) or 1; same bits."""
+        """swrt_set_packet_streams: 2 (default: tile launches split over two streams), 4 or 1; same bits."""
         self._chk(self._L.swrt_set_packet_streams(self._h, int(streams)), "swrt_set_packet_streams")
 
     def set_blend_mode(self, mode=0):

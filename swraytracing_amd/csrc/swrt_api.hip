@@ -204,17 +204,24 @@ struct swrt_ctx {
   int gather_mode = 0;      // 0: stencil sums mul then add (bit-exact); 1: fused multiply-add (tolerance)
   int lanes_per_packet = 0; // LDS-tiled two-snapshot launches: 1, 2 (paired lanes), 0 = by packets per tile
   int tile_mode = 0;        // leapfrog tile size: 0 auto (32 for small ensembles), 16, 32
-  // Two packet streams (swrt_set_packet_streams 2): each LDS-tiled leapfrog
-  // launch runs as two half launches — alternate band positions of every XCD
-  // band — on `stream` and `stream2`.  Within a re-binning cycle the halves
-  // touch disjoint packet ranges, so stream2's launch k overlaps stream's
-  // launch k+1 (one half's tail under the other's body).  stream2's work is
-  // joined back into `stream` (join_b) before anything else reads the packets.
+  // Several packet streams (swrt_set_packet_streams S = 2 or 4): each
+  // LDS-tiled leapfrog launch runs as S part launches — every S-th band
+  // position of every XCD band — on `stream` and the extra streams sx[].
+  // Within a re-binning cycle the parts touch disjoint packet ranges, so one
+  // part's launch k overlaps another's launch k+1 (one part's tail under the
+  // other's body).  The extra streams' work is joined back into `stream`
+  // (join_b) before anything else reads the packets.
+  static constexpr int kMaxPacketStreams = 4;
   int packet_streams = 2;           // default: two (measured +2-4 %, bit-identical); 1 = one launch per step
-  hipStream_t stream2 = nullptr;
+  hipStream_t sx[kMaxPacketStreams - 1] = {};  // the extra packet streams
+  hipEvent_t jx[kMaxPacketStreams - 1] = {};   // their join events
   hipStream_t stream0 = nullptr;  // the packet stream (`stream` outside OnQGStream)
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  bool b_pending = false;         // stream2 holds packet work not yet ordered before stream's
+  hipEvent_t fork_ev = nullptr;
+  int b_pending = 0;              // extra streams holding packet work not yet ordered before stream's
+  // The first launch after an indirect re-binning reads its input through
+  // src_idx at any slot of the old buffer, which the next launch's parts
+  // overwrite at their own tiles' slots: that launch joins first.
+  bool join_next = false;
   int bin_tile = 0;         // cells per tile side of the current binning
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -385,12 +392,22 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
     return fail(ctx, SWRT_ERR_STATE, "unexpected C++ exception");     \
   }
 
-// Order stream2's queued packet work before the packet stream's next work.
+// Order the extra streams' queued packet work before the packet stream's next work.
 int join_b(swrt_ctx* c) {
   if (!c || !c->b_pending) return SWRT_OK;
-  HIPCHK(c, hipEventRecord(c->join_ev, c->stream2));
-  HIPCHK(c, hipStreamWaitEvent(c->stream0, c->join_ev, 0));
-  c->b_pending = false;
+  for (int i = 0; i < c->b_pending; ++i) {
+    HIPCHK(c, hipEventRecord(c->jx[i], c->sx[i]));
+    HIPCHK(c, hipStreamWaitEvent(c->stream0, c->jx[i], 0));
+  }
+  c->b_pending = 0;
+  return SWRT_OK;
+}
+
+// Wait for the extra packet streams (host side).
+int sync_sx(swrt_ctx* c) {
+  for (hipStream_t s : c->sx)
+    if (s) HIPCHK(c, hipStreamSynchronize(s));
+  c->b_pending = 0;
   return SWRT_OK;
 }
 
@@ -597,27 +614,36 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
   c->tail_ev = stop;
 }
 
-// The LDS-tiled launch of TileArgs t: one launch over every tile, or (two
-// packet streams) two half launches of alternate band positions, the second
-// on stream2 after everything queued on the packet stream so far (this
-// call's re-binning, memsets and history growth).  A timed pair brackets
-// the first half's start and the second half's end.
+// The LDS-tiled launch of TileArgs t: one launch over every tile, or (S
+// packet streams) S part launches of every S-th band position, parts 1..S-1
+// on the extra streams after everything queued on the packet stream so far
+// (this call's re-binning, memsets and history growth).  A timed pair
+// brackets the first part's start and the last part's end.
 template <typename F>
 int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
-  const bool two = c->packet_streams == 2 && c->stream2 != nullptr && t.split == 0 && wgrid % 16 == 0 &&
-                   c->stream == c->stream0;
-  if (!two) {
+  if (c->join_next) {
+    if (int rc = join_b(c)) return rc;
+    c->join_next = false;
+  }
+  const int S = c->packet_streams;
+  bool multi = S > 1 && t.split == 0 && wgrid % (8 * S) == 0 && c->stream == c->stream0;
+  for (int i = 0; multi && i < S - 1; ++i) multi = c->sx[i] != nullptr;
+  t.sparts = S;
+  if (!multi) {
     t.spart = -1;
     launch_k(c, kernel, dim3(wgrid), dim3(nt), t);
     return SWRT_OK;
   }
   HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(c->stream2, c->fork_ev, 0));
+  for (int i = 0; i < S - 1; ++i) HIPCHK(c, hipStreamWaitEvent(c->sx[i], c->fork_ev, 0));
   t.spart = 0;
-  hipExtLaunchKernelGGL(kernel, dim3(wgrid / 2), dim3(nt), 0, c->stream, c->kev0, nullptr, 0, t);
-  t.spart = 1;
-  hipExtLaunchKernelGGL(kernel, dim3(wgrid / 2), dim3(nt), 0, c->stream2, nullptr, c->kev1, 0, t);
-  c->b_pending = true;
+  hipExtLaunchKernelGGL(kernel, dim3(wgrid / S), dim3(nt), 0, c->stream, c->kev0, nullptr, 0, t);
+  for (int i = 0; i < S - 1; ++i) {
+    t.spart = i + 1;
+    hipExtLaunchKernelGGL(kernel, dim3(wgrid / S), dim3(nt), 0, c->sx[i], nullptr, i == S - 2 ? c->kev1 : nullptr,
+                          0, t);
+  }
+  c->b_pending = S - 1;
   c->tail_ev = nullptr;  // slot uses are marked after the join (swrt_advance)
   return SWRT_OK;
 }
@@ -638,7 +664,7 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next,
   }
   // timing events (pairs), grown on demand; fold into a running sum when full
   if (c->timing.used + 2 > kMaxEvents) {
-    if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));
+    if (int rc = sync_sx(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     for (size_t i = 0; i + 1 < c->timing.used; i += 2) {
       float ms = 0.f;
@@ -796,6 +822,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   unsigned extra = 0;
   t.split = launch_shape(c, grid, &extra);
   t.spart = -1;
+  t.sparts = 1;
   const unsigned wgrid = grid + extra;
   t.next_keys = nullptr;
   t.next_counts = nullptr;
@@ -852,6 +879,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
       HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, wgrid, kTileThreads, t));
   }
   HIPCHK(c, hipGetLastError());
+  c->join_next = t.src != nullptr;  // (see swrt_ctx::join_next)
   std::swap(c->dx, c->dx2);
   std::swap(c->dk, c->dk2);
   std::swap(c->perm, c->perm2);
@@ -1042,8 +1070,8 @@ int swrt_create(int device, swrt_ctx** out) {
          hipEventCreateWithFlags(&s->wev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->use_ev, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
-       hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) == hipSuccess &&
-       hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) == hipSuccess;
+       hipStreamCreateWithFlags(&c->sx[0], hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t& e : c->jx) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   c->stream0 = c->stream;
   if (!ok) {
     swrt_destroy(c);
@@ -1057,7 +1085,8 @@ void swrt_destroy(swrt_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
-  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  for (hipStream_t s : c->sx)
+    if (s) (void)hipStreamSynchronize(s);
   if (c->qstream) (void)hipStreamSynchronize(c->qstream);
   auto free_slot = [](Slot& s) {
     if (s.nodes) (void)hipFree(s.nodes);
@@ -1100,9 +1129,11 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-  if (c->join_ev) (void)hipEventDestroy(c->join_ev);
+  for (hipEvent_t e : c->jx)
+    if (e) (void)hipEventDestroy(e);
   if (c->qstream) (void)hipStreamDestroy(c->qstream);
-  if (c->stream2) (void)hipStreamDestroy(c->stream2);
+  for (hipStream_t s : c->sx)
+    if (s) (void)hipStreamDestroy(s);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1544,10 +1575,11 @@ int swrt_set_tile_cells(swrt_ctx* c, int cells) {
 
 int swrt_set_packet_streams(swrt_ctx* c, int streams) {
   if (!c) return SWRT_ERR_ARG;
-  if (streams != 1 && streams != 2) return fail(c, SWRT_ERR_ARG, "packet streams must be 1 or 2");
+  if (streams != 1 && streams != 2 && streams != 4) return fail(c, SWRT_ERR_ARG, "packet streams must be 1, 2 or 4");
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = join_b(c)) return rc;
-  if (streams == 2 && !c->stream2) HIPCHK(c, hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+  for (int i = 0; i < streams - 1; ++i)
+    if (!c->sx[i]) HIPCHK(c, hipStreamCreateWithFlags(&c->sx[i], hipStreamNonBlocking));
   c->packet_streams = streams;
   return SWRT_OK;
 }
@@ -2208,8 +2240,7 @@ int swrt_check_arith(swrt_ctx* c, int64_t n, uint64_t seed, int64_t* mismatches3
 int swrt_synchronize(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));
-  c->b_pending = false;
+  if (int rc = sync_sx(c)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipStreamSynchronize(c->qstream));
   return SWRT_OK;
@@ -2245,7 +2276,8 @@ int swrt_get_stream(swrt_ctx* c, void** out) {
 int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches) {
   if (!c) return SWRT_ERR_ARG;
   HIPCHK(c, hipSetDevice(c->device));
-  if (c->stream2) HIPCHK(c, hipStreamSynchronize(c->stream2));  // stop events of split launches
+  for (hipStream_t s : c->sx)  // stop events of split launches
+    if (s) HIPCHK(c, hipStreamSynchronize(s));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   double tot = c->timing.folded_ms;
   for (size_t i = 0; i + 1 < c->timing.used; i += 2) {

@@ -43,10 +43,11 @@ struct TileArgs {
                          // src[p] (indirect re-binning); NULL: slot p holds packet p
   double sort_lead;      // in-tile sort key: position + sort_lead * (group velocity)
   int split;             // launch shape (wg_work_range): halves | quarters << 16 per XCD band
-  // Two-stream form (swrt_set_packet_streams 2): this launch takes every
-  // second band position of each XCD band (parity `spart`), the other launch
-  // on the second stream the rest; the grid is then ntiles / 2.
-  int spart;             // -1: one launch over every tile; 0 / 1: the band positions of that parity
+  // Multi-stream form (swrt_set_packet_streams S = 2 or 4): this launch takes
+  // every S-th band position of each XCD band (those = spart mod S), the
+  // launches on the other streams the rest; the grid is then ntiles / S.
+  int spart;             // -1: one launch over every tile; 0 .. sparts-1: this launch's band positions
+  int sparts;            // S
   // Multi-interval launch (ivmode, swrt_advance_intervals): nint consecutive
   // PDE intervals of s.nsteps steps each; interval i blends snapshots iv[i]
   // and iv[i+1] with alpha = alpha0 + st*dalpha (st = step within the
@@ -85,11 +86,11 @@ __device__ __forceinline__ double iv_dt(const TileArgs& ta, int i) {
 // the launch, which narrows the spread of CU finish times (the launch ends
 // with its slowest CU).  grid = ntiles + 8*(h + 3q).
 __device__ __forceinline__ int wg_work_range(const int* starts, const int* order, int split, int& pbeg,
-                                             int& pend, int spart = -1) {
+                                             int& pend, int spart = -1, int sparts = 1) {
   int b = (int)blockIdx.x, nb = (int)gridDim.x;
-  if (spart >= 0) {  // half of the tiles: band position 2j + spart of XCD band b % 8
-    b = (2 * (b / 8) + spart) * 8 + b % 8;
-    nb *= 2;
+  if (spart >= 0) {  // 1/S of the tiles: band position S*j + spart of XCD band b % 8
+    b = (sparts * (b / 8) + spart) * 8 + b % 8;
+    nb *= sparts;
   }
   int tile, part = 0, nparts = 1;
   if (split > 0) {
@@ -127,7 +128,7 @@ __device__ __forceinline__ int wg_work_range(const int* starts, const int* order
 }
 
 __device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend) {
-  return wg_work_range(ta.starts, ta.order, ta.split, pbeg, pend, ta.spart);
+  return wg_work_range(ta.starts, ta.order, ta.split, pbeg, pend, ta.spart, ta.sparts);
 }
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)

@@ -839,11 +839,11 @@ def test_fma_gather_mode_tolerance(ctx, oracle_lib, n_cells):
 
 
 def test_packet_streams_bit_identical(ctx, oracle_lib):
-    """swrt_set_packet_streams(2): tile launches as two half launches on two
-    streams, joined only when something reads the packets.  A call sequence
-    that mixes history frames, re-binnings inside and between calls, a field
-    rewrite, multi-interval launches, reads and ode23 gives the bits of one
-    stream — and the oracle's on a subset."""
+    """swrt_set_packet_streams(2 / 4): tile launches as two half (four
+    quarter) launches on two (four) streams, joined only when something reads
+    the packets.  A call sequence that mixes history frames, re-binnings
+    inside and between calls, a field rewrite, multi-interval launches, reads
+    and ode23 gives the bits of one stream — and the oracle's on a subset."""
     import argparse
     import bench
     import swraytracing_amd as sw
@@ -853,7 +853,7 @@ def test_packet_streams_bit_identical(ctx, oracle_lib):
     p0, p1 = ctx.get_field_grid(0).copy(), ctx.get_field_grid(1).copy()
     h = w["dt"] / 5
     out = {}
-    for streams in (2, 1):
+    for streams in (2, 4, 1):
         ctx.set_packet_streams(streams)
         ctx.set_locality(20, 0)
         try:
@@ -878,8 +878,9 @@ def test_packet_streams_bit_identical(ctx, oracle_lib):
         finally:
             ctx.set_packet_streams(2)  # the library default
             ctx.set_locality(4, 0)
-    for a, b in zip(out[1], out[2]):
-        assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
+    for streams in (2, 4):
+        for a, b in zip(out[1], out[streams]):
+            assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), streams
     idx = np.sort(np.random.default_rng(4).choice(args.packets, 1500, replace=False))
     xo, ko = w["x"][idx], w["k"][idx]
     for _ in range(7):
