@@ -178,6 +178,11 @@ struct swrt_ctx {
   double* dx2 = nullptr;  // scatter targets of the binning pass
   double* dk2 = nullptr;
   int* perm2 = nullptr;
+  // third packet buffers: the output of the launch after a source-gather
+  // sort launch split over several streams (see tile_launch)
+  double* dx3 = nullptr;
+  double* dk3 = nullptr;
+  int* perm3 = nullptr;
   int* keys = nullptr;   // N
   int* src_idx = nullptr;   // N: source slot of each binned slot (indirect re-binning)
   bool src_pending = false;  // the next tile launch reads its packets through src_idx
@@ -218,10 +223,7 @@ struct swrt_ctx {
   hipStream_t stream0 = nullptr;  // the packet stream (`stream` outside OnQGStream)
   hipEvent_t fork_ev = nullptr;
   int b_pending = 0;              // extra streams holding packet work not yet ordered before stream's
-  // The first launch after an indirect re-binning reads its input through
-  // src_idx at any slot of the old buffer, which the next launch's parts
-  // overwrite at their own tiles' slots: that launch joins first.
-  bool join_next = false;
+
   int bin_tile = 0;         // cells per tile side of the current binning
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -621,10 +623,6 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
 // brackets the first part's start and the last part's end.
 template <typename F>
 int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
-  if (c->join_next) {
-    if (int rc = join_b(c)) return rc;
-    c->join_next = false;
-  }
   const int S = c->packet_streams;
   bool multi = S > 1 && t.split == 0 && wgrid % (8 * S) == 0 && c->stream == c->stream0;
   for (int i = 0; multi && i < S - 1; ++i) multi = c->sx[i] != nullptr;
@@ -879,10 +877,22 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
       HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, wgrid, kTileThreads, t));
   }
   HIPCHK(c, hipGetLastError());
-  c->join_next = t.src != nullptr;  // (see swrt_ctx::join_next)
-  std::swap(c->dx, c->dx2);
-  std::swap(c->dk, c->dk2);
-  std::swap(c->perm, c->perm2);
+  if (t.src != nullptr && c->b_pending) {
+    // The first launch after an indirect re-binning reads its input through
+    // src_idx from any slot of dx while its parts run on several streams; the
+    // next launch's parts would overwrite dx at their own tiles' slots before
+    // the other parts have read them.  The next launches write the third
+    // buffers instead and dx is parked there until the next re-binning
+    // (which orders every stream's work first).
+    double* x = c->dx; double* k = c->dk; int* pm = c->perm;
+    c->dx = c->dx2; c->dk = c->dk2; c->perm = c->perm2;
+    c->dx2 = c->dx3; c->dk2 = c->dk3; c->perm2 = c->perm3;
+    c->dx3 = x; c->dk3 = k; c->perm3 = pm;
+  } else {
+    std::swap(c->dx, c->dx2);
+    std::swap(c->dk, c->dk2);
+    std::swap(c->perm, c->perm2);
+  }
   c->keys_fresh = t.next_keys != nullptr;
   c->cells_sorted = true;  // written in (the input's or this launch's) cell order
   return SWRT_OK;
@@ -1098,7 +1108,8 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->use_ev) (void)hipEventDestroy(c->use_ev);
   for (auto& s : c->spares) free_slot(s);
   for (void* p : {(void*)c->dx, (void*)c->dk, (void*)c->perm, (void*)c->dx2, (void*)c->dk2,
-                  (void*)c->perm2, (void*)c->keys, (void*)c->src_idx, (void*)c->bins})
+                  (void*)c->perm2, (void*)c->dx3, (void*)c->dk3, (void*)c->perm3, (void*)c->keys,
+                  (void*)c->src_idx, (void*)c->bins})
     if (p) (void)hipFree(p);
   if (c->hx) (void)hipFree(c->hx);
   if (c->hk) (void)hipFree(c->hk);
@@ -1475,7 +1486,8 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
   HIPCHK(c, hipSetDevice(c->device));
   if (n > c->cap) {
     for (void** p : {(void**)&c->dx, (void**)&c->dk, (void**)&c->perm, (void**)&c->dx2, (void**)&c->dk2,
-                     (void**)&c->perm2, (void**)&c->keys, (void**)&c->src_idx}) {
+                     (void**)&c->perm2, (void**)&c->dx3, (void**)&c->dk3, (void**)&c->perm3, (void**)&c->keys,
+                     (void**)&c->src_idx}) {
       if (*p) (void)hipFree(*p);
       *p = nullptr;
     }
@@ -1486,6 +1498,9 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
     HIPCHK(c, hipMalloc(&c->dk2, sizeof(double) * 2 * n));
     HIPCHK(c, hipMalloc(&c->perm, sizeof(int) * n));
     HIPCHK(c, hipMalloc(&c->perm2, sizeof(int) * n));
+    HIPCHK(c, hipMalloc(&c->dx3, sizeof(double) * 2 * n));
+    HIPCHK(c, hipMalloc(&c->dk3, sizeof(double) * 2 * n));
+    HIPCHK(c, hipMalloc(&c->perm3, sizeof(int) * n));
     HIPCHK(c, hipMalloc(&c->keys, sizeof(int) * n));
     HIPCHK(c, hipMalloc(&c->src_idx, sizeof(int) * n));
     c->cap = n;
