@@ -240,8 +240,8 @@ int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
  * and any call that reads the packets (or re-bins them) first order the
  * extra streams' work before their own; swrt_synchronize waits for all.
  * Results are bit-identical for every setting.  4 measured slower than 2
- * (1.65-1.69e10 vs 2.13-2.15e10 packet-steps/s: more streams than the
- * process's hardware queues). */
+ * (1.65-1.79e10 vs 2.13-2.18e10 packet-steps/s, with 4 or 8 hardware queues
+ * per process alike). */
 int swrt_set_packet_streams(swrt_ctx* ctx, int streams);
 
 /* Advance the device-resident packets by nsteps leapfrog steps
