@@ -547,7 +547,7 @@ def main(argv=None):
     # region (re-binning kernels and launch gaps included: a lower bound on
     # the kernel's own rate).  One stream: the HIP-event launch time.
     launches_per_step = max(1, -(-args.substeps * ivs // spl))
-    two = args.packet_streams > 1 and args.kernel in (0, 2)
+    two = args.packet_streams > 1 and args.kernel in (0, 2) and N >= 65536  # the library's kMultiStreamFrom
     basis_s = elapsed / (args.steps * launches_per_step) if two else avg_launch_s
     roof = roofline(pmc, N, args.nx, w["nslots"], spl, basis_s, launches, args.timing_every)
     roof["time_basis"] = (f"wall time per launch of the timed region ({args.packet_streams} overlapping part "

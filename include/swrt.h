@@ -241,7 +241,8 @@ int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
  * extra streams' work before their own; swrt_synchronize waits for all.
  * Results are bit-identical for every setting.  4 measured slower than 2
  * (1.65-1.79e10 vs 2.13-2.18e10 packet-steps/s, with 4 or 8 hardware queues
- * per process alike). */
+ * per process alike).  Ensembles under 65,536 packets always use one
+ * stream (the split costs more than it returns there). */
 int swrt_set_packet_streams(swrt_ctx* ctx, int streams);
 
 /* Advance the device-resident packets by nsteps leapfrog steps

@@ -621,9 +621,15 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
 // on the extra streams after everything queued on the packet stream so far
 // (this call's re-binning, memsets and history growth).  A timed pair
 // brackets the first part's start and the last part's end.
+// Ensembles below this run every tile launch on one stream: the split's
+// fork/join costs more than the overlap returns (profiles/r03_streams_ab:
+// 3e4 packets 3.0 vs 3.4e9, 1e4 at 256^2 1.8 vs 2.8e9; 6.25e4 even; 1.25e5
+// +3 %, 2.5e5 +6 %, 5e5 +4 %, 1e6 +3.7 %).
+constexpr int64_t kMultiStreamFrom = 65536;
+
 template <typename F>
 int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
-  const int S = c->packet_streams;
+  const int S = c->n >= kMultiStreamFrom ? c->packet_streams : 1;
   bool multi = S > 1 && t.split == 0 && wgrid % (8 * S) == 0 && c->stream == c->stream0;
   for (int i = 0; multi && i < S - 1; ++i) multi = c->sx[i] != nullptr;
   t.sparts = S;

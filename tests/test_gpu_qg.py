@@ -283,13 +283,14 @@ def test_qg2_driver_packet_streams_identical_files(tmp_path):
         try:
             c.set_packet_streams(streams)
             d = tmp_path / f"s{streams}"
-            sw.qg2layersw_raytrace(128, 30_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=5, max_steps=60,
+            # >= 65,536 packets: smaller ensembles always take one stream
+            sw.qg2layersw_raytrace(128, 70_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=5, max_steps=60,
                                    seed=5, ctx=c)
             files[streams] = {n: (d / f"{n}.bin").read_bytes() for n in ("packet_x", "packet_k", "packet_time")}
         finally:
             c.close()
     assert files[1] == files[2] == files[4]
-    assert len(files[1]["packet_x"]) == 8 * 30_000 * 2 * (1 + 60 // 25)
+    assert len(files[1]["packet_x"]) == 8 * 70_000 * 2 * (1 + 60 // 25)
 
 
 def test_golden_qg_fixture(ctx):
