@@ -223,7 +223,6 @@ struct swrt_ctx {
   hipStream_t stream0 = nullptr;  // the packet stream (`stream` outside OnQGStream)
   hipEvent_t fork_ev = nullptr;
   int b_pending = 0;              // extra streams holding packet work not yet ordered before stream's
-
   int bin_tile = 0;         // cells per tile side of the current binning
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
@@ -616,17 +615,17 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
   c->tail_ev = stop;
 }
 
-// The LDS-tiled launch of TileArgs t: one launch over every tile, or (S
-// packet streams) S part launches of every S-th band position, parts 1..S-1
-// on the extra streams after everything queued on the packet stream so far
-// (this call's re-binning, memsets and history growth).  A timed pair
-// brackets the first part's start and the last part's end.
 // Ensembles below this run every tile launch on one stream: the split's
 // fork/join costs more than the overlap returns (profiles/r03_streams_ab:
 // 3e4 packets 3.0 vs 3.4e9, 1e4 at 256^2 1.8 vs 2.8e9; 6.25e4 even; 1.25e5
 // +3 %, 2.5e5 +6 %, 5e5 +4 %, 1e6 +3.7 %).
 constexpr int64_t kMultiStreamFrom = 65536;
 
+// The LDS-tiled launch of TileArgs t: one launch over every tile, or (S
+// packet streams) S part launches of every S-th band position, parts 1..S-1
+// on the extra streams after everything queued on the packet stream so far
+// (this call's re-binning, memsets and history growth).  A timed pair
+// brackets the first part's start and the last part's end.
 template <typename F>
 int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
   const int S = c->n >= kMultiStreamFrom ? c->packet_streams : 1;
