@@ -890,6 +890,33 @@ def test_packet_streams_bit_identical(ctx, oracle_lib):
     np.testing.assert_array_equal(out[2][1][idx], ko)
 
 
+def test_packet_streams_long_run_bit_identical(ctx):
+    """The bench workload (1e6 packets, 5 substeps per call, re-binning every
+    20 steps) over 100 calls — 25 re-binnings, each followed by a sort launch
+    that gathers its input from any slot while the parts of the split launch
+    run on 2 or 4 streams — gives every packet's bits of one stream."""
+    import argparse
+    import bench
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=1_000_000, world=1, rank=0, seed=146, mode="blend")
+    w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
+    out = {}
+    try:
+        ctx.set_locality(20, 0)
+        for streams in (1, 2, 4):
+            ctx.set_packet_streams(streams)
+            ctx.packets_set(w["x"], w["k"])
+            for _ in range(100):
+                bench.step(ctx, w, 5)
+            out[streams] = ctx.packets_get()
+    finally:
+        ctx.set_packet_streams(2)
+        ctx.set_locality(4, 0)
+    for streams in (2, 4):
+        for a, b in zip(out[1], out[streams]):
+            assert np.array_equal(a.view(np.uint64), b.view(np.uint64)), streams
+
+
 @pytest.mark.parametrize("substeps,rebin_every,calls", [(5, 20, 10), (1, 4, 12)])
 def test_bench_configuration_subset_bitexact(ctx, oracle_lib, substeps, rebin_every, calls):
     """The headline bench configuration itself (bench.py: 2-layer 512^2 field,
