@@ -19,6 +19,9 @@
 //   swrt_mex('set_field_psi', h, slot, psi_grid, L)           % SpectralScheme ctor
 //   swrt_mex('set_field_qk', h, slot, qk, L, K_d2, shear, kscale, ny_period)   % grid_U
 //   swrt_mex('set_field_grid', h, slot, u, v, ux, uy, vx, vy, L, ny_period)
+//   swrt_mex('set_field_q', h, slot, q_grid, L, K_d2, shear, kscale, ny_period)   % grid_U(g2k(q)), read_field frame
+//   swrt_mex('advance_intervals', h, dts, nsub, f, gH, alpha0, dalpha, bump)       % slots 0..numel(dts)
+//   swrt_mex('set_locality', h, rebin_every, tile)
 //   F6  = swrt_mex('get_fields', h, slot, nx)                 % nx x nx x 6: u v u_x u_y v_x v_y
 //   psi = swrt_mex('get_psi', h, slot, nx)                    % k2g(g2k(psi)) of set_field_psi
 //   out = swrt_mex('eval', h, x, y, nslots, alpha, bump)      % n x 6 (U, grad U per column)
@@ -155,6 +158,15 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
           "swrt_set_field_qk");
     return;
   }
+  if (!strcmp(cmd, "set_field_q")) {  // (slot, q nx x nx, L, K_d2, shear, kscale, ny_period)
+    need(na, 8, cmd);
+    const int64_t nx = (int64_t)mxGetM(a[2]);
+    if ((int64_t)mxGetN(a[2]) != nx) mexErrMsgIdAndTxt("swrt:arg", "q must be an nx x nx frame");
+    check(c, swrt_set_field_q(c, (int)scalar(a[1]), reals(a[2], "q"), nx, scalar(a[3]), scalar(a[4]), scalar(a[5]),
+                              scalar(a[6]), (int64_t)scalar(a[7])),
+          "swrt_set_field_q");
+    return;
+  }
   if (!strcmp(cmd, "set_field_grid")) {  // (slot, u, v, ux, uy, vx, vy, L, ny_period)
     need(na, 10, cmd);
     const int64_t nx = (int64_t)mxGetM(a[2]);
@@ -263,6 +275,19 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     check(c, swrt_advance(c, scalar(a[1]), (int64_t)scalar(a[2]), scalar(a[3]), scalar(a[4]), (int)scalar(a[5]),
                           scalar(a[6]), scalar(a[7]), scalar(a[8]), 0),
           "swrt_advance");
+    return;
+  }
+  if (!strcmp(cmd, "advance_intervals")) {  // (dts, nsub, f, gH, alpha0, dalpha, bump)
+    need(na, 8, cmd);
+    const int nint = (int)mxGetNumberOfElements(a[1]);
+    check(c, swrt_advance_intervals(c, nint, reals(a[1], "dts"), (int64_t)scalar(a[2]), scalar(a[3]), scalar(a[4]),
+                                    scalar(a[5]), scalar(a[6]), scalar(a[7]), 0),
+          "swrt_advance_intervals");
+    return;
+  }
+  if (!strcmp(cmd, "set_locality")) {  // (rebin_every, tile)
+    need(na, 3, cmd);
+    check(c, swrt_set_locality(c, (int64_t)scalar(a[1]), (int64_t)scalar(a[2])), "swrt_set_locality");
     return;
   }
   if (!strcmp(cmd, "ode23_f1")) {  // (t, tmax, f, Cg, nslots, thr, bump) -> rh_raw

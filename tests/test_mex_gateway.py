@@ -391,3 +391,50 @@ def test_scheme_contexts_freed_with_last_reference(mex):
         copy.id()
     with pytest.raises(MexError, match="invalid or closed context handle"):
         mex("get_fields", h, 0.0, float(nx))
+
+
+@pytest.mark.gpu
+def test_trace_stored_gpu_m_matches_trace_stored(mex, ctx, tmp_path):
+    """matlab/trace_stored_gpu.m over the gateway (frames by read_field ->
+    set_field_q, intervals by advance_intervals at nsub substeps, four per
+    call, swap_slots between calls) gives the packets of the Python twin
+    swraytracing_amd.trace_stored on the same PV series, bit for bit."""
+    import swraytracing_amd as sw
+    nx, L, f, Cg, nsub = 64, 2 * np.pi, 3.0, 1.0, 5
+    rng = np.random.default_rng(21)
+    q1 = sw.qg.initial_q(nx, L, 0.2, f / Cg, 3, 8, rng)
+    for i in range(6):  # six frames: one call of four intervals, one of one
+        sw.write_field(q1 * (1 + 0.05 * i), str(tmp_path / "pv"))
+        sw.write_field(np.array([[0.3 * i + 0.01 * i * i]]), str(tmp_path / "pv_time"))
+    x0 = L * rng.random((3000, 2)) - L / 2
+    k0 = rng.normal(0.0, 5.0, (3000, 2))
+    xs, ks, t_end = sw.trace_stored(str(tmp_path / "pv"), nx, x0, k0, f, Cg, nsub=nsub, ctx=ctx)
+    # trace_stored_gpu.m line by line (MATLAB's 1-based frames / times)
+    times = sw.read_field(str(tmp_path / "pv_time"))[0]
+    frames = list(range(1, 7))
+    h = mex("create", 0.0)
+    try:
+        mex("packets_set", h, x0, k0)
+        mex("set_locality", h, 4.0 * nsub, 0.0)
+
+        def load_frame(slot, fr):
+            q = sw.read_frame(str(tmp_path / "pv"), nx, fr)
+            mex("set_field_q", h, float(slot), q, L, f / Cg, 0.0, 1.0, float(nx))
+
+        load_frame(0, frames[0])
+        i = 2
+        while i <= len(frames):
+            g = min(4, len(frames) - i + 1)
+            for j in range(g):
+                load_frame(1 + j, frames[i + j - 1])
+            mex("advance_intervals", h, np.diff(times[i - 2:i + g - 1]) / nsub, float(nsub), f, Cg ** 2,
+                0.5 / nsub, 1.0 / nsub, 1e-10)
+            mex("swap_slots", h, 0.0, float(g))
+            i += g
+        xm, km = mex("packets_get", h, nlhs=2)
+    finally:
+        mex("destroy", h)
+    assert t_end == times[-1]
+    np.testing.assert_array_equal(np.asarray(xm).view(np.uint64), np.ascontiguousarray(xs).view(np.uint64))
+    np.testing.assert_array_equal(np.asarray(km).view(np.uint64), np.ascontiguousarray(ks).view(np.uint64))
+    assert np.abs(xs - x0).max() > 1e-3  # the packets moved
