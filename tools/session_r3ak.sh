@@ -1,0 +1,8 @@
+#!/bin/bash
+# Kernel trace of the driver step on the final code (anatomy, diagnostic).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r3ak
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/prof -o run -- python3 bench.py --no-cpu-baseline --no-forecast --no-fma --ode23-steps 0 --steps 5 --driver-steps 40 > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
+python tools/driver_trace_summary.py $OUT/prof/run_kernel_trace.csv --steps 40 | tee $OUT/summary.txt
