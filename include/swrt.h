@@ -487,6 +487,30 @@ int swrt_set_timing(swrt_ctx* ctx, int every);
  * last reset (synchronizes). */
 int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launches);
 
+/* Debug knobs (test infrastructure; no reference counterpart).
+ * SWRT_DEBUG_HAZARD_CHECK 0/1: a host-side happens-before checker of the
+ *   packet buffers across the packet streams (swrt_set_packet_streams): every
+ *   re-binning, part launch, join and synchronisation is mirrored with one
+ *   vector clock per stream; a launch whose reads or writes of a packet
+ *   buffer are not ordered after a conflicting access on another stream is
+ *   refused before it is queued (SWRT_ERR_STATE, swrt_last_error names both
+ *   accesses).  Also on when the environment has SWRT_HAZARD_CHECK=1 at
+ *   swrt_create.  Turning it on synchronises the context.
+ * SWRT_DEBUG_SPIN_US n: each extra packet stream runs a ~n us sleep kernel
+ *   before every part launch of its own, so a call's extra-stream parts
+ *   overlap the next call's packet-stream part (adversarial schedule).
+ * SWRT_DEBUG_LEGACY_PARK 0/1: test-only; 1 restores the ordering before the
+ *   third packet buffers (the launch after a source-gather sort launch
+ *   overwrites the buffer that launch gathers from) — a known race the
+ *   checker must report.
+ * SWRT_DEBUG_HAZARD_CHECKS (get only): accesses the checker has compared. */
+#define SWRT_DEBUG_HAZARD_CHECK 1
+#define SWRT_DEBUG_SPIN_US 2
+#define SWRT_DEBUG_LEGACY_PARK 3
+#define SWRT_DEBUG_HAZARD_CHECKS 4
+int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
+int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
+
 #ifdef __cplusplus
 }
 #endif

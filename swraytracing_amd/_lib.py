@@ -113,7 +113,15 @@ SIGNATURES = {
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
     "swrt_kernel_time": (_INT, [_VP, _INT, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
+    "swrt_debug_set": (_INT, [_VP, _INT, _I]),
+    "swrt_debug_get": (_INT, [_VP, _INT, ctypes.POINTER(_I)]),
 }
+
+# swrt_debug_set / swrt_debug_get keys (include/swrt.h)
+DEBUG_HAZARD_CHECK = 1
+DEBUG_SPIN_US = 2
+DEBUG_LEGACY_PARK = 3
+DEBUG_HAZARD_CHECKS = 4
 
 _lib = None
 
@@ -603,6 +611,15 @@ class Context:
         self._chk(self._L.swrt_kernel_time(self._h, int(reset), ctypes.byref(ms), ctypes.byref(n)),
                   "swrt_kernel_time")
         return ms.value, n.value
+
+    def debug_set(self, key, value):
+        """swrt_debug_set: DEBUG_HAZARD_CHECK, DEBUG_SPIN_US, DEBUG_LEGACY_PARK (test infrastructure)."""
+        self._chk(self._L.swrt_debug_set(self._h, int(key), int(value)), "swrt_debug_set")
+
+    def debug_get(self, key):
+        v = _I()
+        self._chk(self._L.swrt_debug_get(self._h, int(key), ctypes.byref(v)), "swrt_debug_get")
+        return v.value
 
 
 def exported_symbols():

@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <climits>
@@ -25,6 +26,7 @@
 #include "swrt_xka.hpp"
 #include "swrt_rsw.hpp"
 #include "swrt_spectral.hpp"
+#include "swrt_hazard.hpp"
 #include "swrt_diag.hpp"
 
 using namespace swrt;
@@ -298,6 +300,14 @@ struct swrt_ctx {
   // between dependent packet launches (tools/gap_probe.py)
   hipEvent_t use_ev = nullptr;
   hipEvent_t tail_ev = nullptr;
+  // debug knobs (swrt_debug_set): the packet-buffer hazard checker
+  // (swrt_hazard.hpp), a spin kernel queued on every extra packet stream
+  // before each of its part launches (adversarial overlap of consecutive
+  // calls), and the pre-third-buffer ordering after a source-gather sort
+  // launch (test-only: reintroduces the race the checker must catch)
+  HazardChecker hz;
+  int debug_spin_us = 0;
+  bool debug_legacy_park = false;
 };
 
 namespace {
@@ -383,6 +393,7 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
     {                             \
       const int jrc_ = join_b(c); \
       if (jrc_) return jrc_;      \
+      hz_api(c);                  \
     }
 #define GUARD_END(ctx)                                                \
   }                                                                   \
@@ -399,15 +410,50 @@ int join_b(swrt_ctx* c) {
   for (int i = 0; i < c->b_pending; ++i) {
     HIPCHK(c, hipEventRecord(c->jx[i], c->sx[i]));
     HIPCHK(c, hipStreamWaitEvent(c->stream0, c->jx[i], 0));
+    if (c->hz.on) {
+      c->hz.record(c->jx[i], i + 1);
+      c->hz.wait(0, c->jx[i]);
+    }
   }
   c->b_pending = 0;
   return SWRT_OK;
 }
 
+// Hazard checker (swrt_hazard.hpp): the packet-state buffers of the context.
+template <typename F>
+void hz_each_buffer(swrt_ctx* c, F fn) {
+  for (const void* b : {(const void*)c->dx, (const void*)c->dk, (const void*)c->perm, (const void*)c->dx2,
+                        (const void*)c->dk2, (const void*)c->perm2, (const void*)c->dx3, (const void*)c->dk3,
+                        (const void*)c->perm3, (const void*)c->keys, (const void*)c->src_idx, (const void*)c->bins,
+                        (const void*)(c->bins ? c->bins + kMaxBins : nullptr),
+                        (const void*)(c->bins ? c->bins + 2 * kMaxBins : nullptr),
+                        (const void*)(c->bins ? c->bins + 3 * kMaxBins + 1 : nullptr), (const void*)c->hx,
+                        (const void*)c->hk})
+    if (b) fn(b);
+}
+
+// Every other API call runs on the packet stream after join_b: to the checker
+// it reads and writes every packet buffer there (conservative: a call that
+// lost its join is reported by the next part launch).
+void hz_api(swrt_ctx* c) {
+  if (!c || !c->hz.on) return;
+  const uint64_t t = c->hz.op(0);
+  hz_each_buffer(c, [&](const void* b) { (void)c->hz.access(0, t, b, kHzWrite, HzRegion::all(), "an API call"); });
+}
+
+// The host synchronised the packet stream after join_b: everything queued on
+// any packet stream before has completed.
+void hz_synced(swrt_ctx* c) {
+  if (c->hz.on) c->hz.sync(0);
+}
+
 // Wait for the extra packet streams (host side).
 int sync_sx(swrt_ctx* c) {
-  for (hipStream_t s : c->sx)
-    if (s) HIPCHK(c, hipStreamSynchronize(s));
+  for (int i = 0; i < swrt_ctx::kMaxPacketStreams - 1; ++i)
+    if (c->sx[i]) {
+      HIPCHK(c, hipStreamSynchronize(c->sx[i]));
+      if (c->hz.on) c->hz.sync(i + 1);
+    }
   c->b_pending = 0;
   return SWRT_OK;
 }
@@ -626,6 +672,44 @@ constexpr int64_t kMultiStreamFrom = 65536;
 // on the extra streams after everything queued on the packet stream so far
 // (this call's re-binning, memsets and history growth).  A timed pair
 // brackets the first part's start and the last part's end.
+// Hazard checker: the accesses of the tile launch t as nparts part launches
+// (part p on stream p: the packet stream, then the extra streams), forked from
+// the packet stream when nparts > 1.  Checked on a copy of the checker state,
+// committed only if every access is ordered: a hazard refuses the launch.
+int hz_tile_launch(swrt_ctx* c, const TileArgs& t, int nparts) {
+  HazardChecker h = c->hz;
+  if (nparts > 1) {
+    h.record(c->fork_ev, 0);
+    for (int i = 1; i < nparts; ++i) h.wait(i, c->fork_ev);
+  }
+  const StepArgs& a = t.s;
+  for (int p = 0; p < nparts; ++p) {
+    const uint64_t tp = h.op(p);
+    const HzRegion r = nparts > 1 ? HzRegion::of_part(h.epoch, p, nparts) : HzRegion::all();
+    const char* what = t.src ? "a part of the sort launch after a re-binning" : "a part launch";
+    // the sort launch after an indirect re-binning gathers its input through
+    // src_idx from any slot of the input buffers
+    const HzRegion rin = t.src ? HzRegion::all() : r;
+    bool ok = h.access(p, tp, a.x, kHzRead, rin, what) && h.access(p, tp, a.k, kHzRead, rin, what) &&
+              h.access(p, tp, a.perm, kHzRead, rin, what) && h.access(p, tp, t.src, kHzRead, r, what) &&
+              h.access(p, tp, t.starts, kHzRead, HzRegion::all(), what) &&
+              h.access(p, tp, t.order, kHzRead, HzRegion::all(), what) &&
+              h.access(p, tp, t.x_out, kHzWrite, r, what) && h.access(p, tp, t.k_out, kHzWrite, r, what) &&
+              h.access(p, tp, t.perm_out, kHzWrite, r, what) &&
+              h.access(p, tp, t.next_keys, kHzWrite, r, what) &&
+              h.access(p, tp, t.next_counts, kHzAtomic, HzRegion::all(), what) &&
+              h.access(p, tp, a.hist_x, kHzWrite, r, what) && h.access(p, tp, a.hist_k, kHzWrite, r, what);
+    if (!ok) return fail(c, SWRT_ERR_STATE, h.err);
+  }
+  c->hz = std::move(h);
+  return SWRT_OK;
+}
+
+// debug: a kernel that sleeps ~4 us per iteration (every wave returns)
+__global__ void debug_spin_kernel(int iters) {
+  for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
 template <typename F>
 int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
   const int S = c->n >= kMultiStreamFrom ? c->packet_streams : 1;
@@ -633,15 +717,23 @@ int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
   for (int i = 0; multi && i < S - 1; ++i) multi = c->sx[i] != nullptr;
   t.sparts = S;
   if (!multi) {
+    // one launch over every tile on the packet stream: it reads and writes
+    // packets that the extra streams' part launches of an earlier call may
+    // still be writing (swrt_set_tail_split > 0 takes this branch)
+    HIPCHK_RC(join_b(c));
+    if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, 1));
     t.spart = -1;
     launch_k(c, kernel, dim3(wgrid), dim3(nt), t);
     return SWRT_OK;
   }
+  if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, S));
   HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
   for (int i = 0; i < S - 1; ++i) HIPCHK(c, hipStreamWaitEvent(c->sx[i], c->fork_ev, 0));
   t.spart = 0;
   hipExtLaunchKernelGGL(kernel, dim3(wgrid / S), dim3(nt), 0, c->stream, c->kev0, nullptr, 0, t);
   for (int i = 0; i < S - 1; ++i) {
+    if (c->debug_spin_us > 0)
+      hipLaunchKernelGGL(debug_spin_kernel, dim3(1), dim3(64), 0, c->sx[i], (c->debug_spin_us + 3) / 4);
     t.spart = i + 1;
     hipExtLaunchKernelGGL(kernel, dim3(wgrid / S), dim3(nt), 0, c->sx[i], nullptr, i == S - 2 ? c->kev1 : nullptr,
                           0, t);
@@ -651,11 +743,30 @@ int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
   return SWRT_OK;
 }
 
+// Before a per-packet leapfrog launch (packets updated in place on the packet
+// stream): order the extra streams' part launches of an earlier call first
+// (swrt_set_locality(0, ..) after split launches lands here), and tell the
+// hazard checker.
+int leap_launch_prep(swrt_ctx* c, const StepArgs& a) {
+  HIPCHK_RC(join_b(c));
+  if (!c->hz.on) return SWRT_OK;
+  HazardChecker& h = c->hz;
+  const uint64_t t = h.op(0);
+  const char* what = "the per-packet leapfrog launch";
+  const bool ok = h.access(0, t, a.x, kHzWrite, HzRegion::all(), what) &&
+                  h.access(0, t, a.k, kHzWrite, HzRegion::all(), what) &&
+                  h.access(0, t, a.perm, kHzRead, HzRegion::all(), what) &&
+                  h.access(0, t, a.hist_x, kHzWrite, HzRegion::all(), what) &&
+                  h.access(0, t, a.hist_k, kHzWrite, HzRegion::all(), what);
+  return ok ? SWRT_OK : fail(c, SWRT_ERR_STATE, h.err);
+}
+
 // Time every timing_every-th leapfrog launch with a pair of HIP events.
 int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next, const IvLaunch* iv = nullptr) {
   const bool timed = c->timing_every > 0 && (c->launch_count++ % c->timing_every) == 0;
   if (!timed) {
     if (use_tile_kernel(c)) return tile_launch(c, a, count_next, iv);
+    HIPCHK_RC(leap_launch_prep(c, a));
     c->keys_fresh = false;
     if (a.nslots == 2)
       hipLaunchKernelGGL(leapfrog_kernel<true>, dim3(grid), dim3(256), 0, c->stream, a);
@@ -690,7 +801,7 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next,
   int rc = SWRT_OK;
   if (use_tile_kernel(c)) {
     rc = tile_launch(c, a, count_next, iv);
-  } else {
+  } else if ((rc = leap_launch_prep(c, a)) == SWRT_OK) {
     c->keys_fresh = false;
     if (a.nslots == 2)
       launch_k(c, leapfrog_kernel<true>, dim3(grid), dim3(256), a);
@@ -769,6 +880,25 @@ int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
   const int64_t n = c->n;
   const unsigned grid = nblocks(n, 256 * kBinPerThread);
   const bool keys_valid = c->keys_fresh && c->bin_valid && nbins == c->nbins && c->key_nx == s.nx && c->key_L == s.L;
+  if (c->hz.on) {  // count, scan and scatter on the packet stream
+    HazardChecker& h = c->hz;
+    const uint64_t t = h.op(0);
+    const char* what = "a re-binning";
+    const HzRegion all = HzRegion::all();
+    bool ok = h.access(0, t, c->dx, kHzRead, all, what) && h.access(0, t, c->dk, kHzRead, all, what) &&
+              h.access(0, t, c->perm, kHzRead, all, what) &&
+              h.access(0, t, c->keys, keys_valid ? kHzRead : kHzWrite, all, what) &&
+              h.access(0, t, c->bins, kHzWrite, all, what) && h.access(0, t, c->bins + kMaxBins, kHzWrite, all, what) &&
+              h.access(0, t, c->bins + 2 * kMaxBins, kHzWrite, all, what) &&
+              h.access(0, t, tile_order_of(c), kHzWrite, all, what);
+    if (indirect)
+      ok = ok && h.access(0, t, c->src_idx, kHzWrite, all, what);
+    else
+      ok = ok && h.access(0, t, c->dx2, kHzWrite, all, what) && h.access(0, t, c->dk2, kHzWrite, all, what) &&
+           h.access(0, t, c->perm2, kHzWrite, all, what);
+    if (!ok) return fail(c, SWRT_ERR_STATE, h.err);
+    ++h.epoch;  // a new partition of the packets into tiles
+  }
   if (!keys_valid) {
     HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * nbins, c->stream));
     hipLaunchKernelGGL(bin_count_kernel, dim3(grid), dim3(256), sizeof(int) * nbins, c->stream, g, c->dx, n,
@@ -840,6 +970,11 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     c->src_pending = false;
   }
   if (count_next && (int)grid == c->nbins) {
+    if (!c->counts_zero && c->hz.on) {
+      const uint64_t tm = c->hz.op(0);
+      if (!c->hz.access(0, tm, c->bins, kHzWrite, HzRegion::all(), "the next-binning counts' memset"))
+        return fail(c, SWRT_ERR_STATE, c->hz.err);
+    }
     if (!c->counts_zero) HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * grid, c->stream));
     c->counts_zero = false;
     t.next_keys = c->keys;
@@ -882,7 +1017,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
       HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, wgrid, kTileThreads, t));
   }
   HIPCHK(c, hipGetLastError());
-  if (t.src != nullptr && c->b_pending) {
+  if (t.src != nullptr && c->b_pending && !c->debug_legacy_park) {
     // The first launch after an indirect re-binning reads its input through
     // src_idx from any slot of dx while its parts run on several streams; the
     // next launch's parts would overwrite dx at their own tiles' slots before
@@ -1039,6 +1174,13 @@ int ensure_history(swrt_ctx* c, int64_t new_frames) {
   }
   // the old buffers may still be read or written by queued work
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  hz_synced(c);
+  if (c->hz.on) {
+    c->hz.bufs.erase(c->hx);
+    c->hz.bufs.erase(c->hk);
+    c->hz.name(nx_, "history x frames");
+    c->hz.name(nk_, "history k frames");
+  }
   if (c->hx) (void)hipFree(c->hx);
   if (c->hk) (void)hipFree(c->hk);
   c->hx = nx_;
@@ -1088,6 +1230,7 @@ int swrt_create(int device, swrt_ctx** out) {
        hipStreamCreateWithFlags(&c->sx[0], hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t& e : c->jx) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   c->stream0 = c->stream;
+  if (const char* e = getenv("SWRT_HAZARD_CHECK")) c->hz.on = atoi(e) != 0;
   if (!ok) {
     swrt_destroy(c);
     return SWRT_ERR_HIP;
@@ -1519,6 +1662,25 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
     HIPCHK(c, hipGetLastError());
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->hz.on) {  // every packet stream's work is complete (joined, then synchronised)
+    c->hz.quiesce();
+    ++c->hz.epoch;
+    const char* tags[] = {"A", "B", "C"};
+    double* xs[] = {c->dx, c->dx2, c->dx3};
+    double* ks[] = {c->dk, c->dk2, c->dk3};
+    int* ps[] = {c->perm, c->perm2, c->perm3};
+    for (int i = 0; i < 3; ++i) {
+      c->hz.name(xs[i], std::string("packet x buffer ") + tags[i]);
+      c->hz.name(ks[i], std::string("packet k buffer ") + tags[i]);
+      c->hz.name(ps[i], std::string("permutation buffer ") + tags[i]);
+    }
+    c->hz.name(c->keys, "binning keys");
+    c->hz.name(c->src_idx, "re-binning source index");
+    c->hz.name(c->bins, "bin counts");
+    c->hz.name(c->bins + kMaxBins, "bin cursors");
+    c->hz.name(c->bins + 2 * kMaxBins, "tile starts");
+    c->hz.name(c->bins + 3 * kMaxBins + 1, "tile order");
+  }
   // a new ensemble starts a new history and needs binning before the next step
   c->hframes = 0;
   c->steps_done = 0;
@@ -2263,7 +2425,44 @@ int swrt_synchronize(swrt_ctx* c) {
   if (int rc = sync_sx(c)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipStreamSynchronize(c->qstream));
+  if (c->hz.on) c->hz.sync_all();
   return SWRT_OK;
+}
+
+int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
+  if (!c) return SWRT_ERR_ARG;
+  switch (key) {
+    case SWRT_DEBUG_HAZARD_CHECK:
+      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "hazard check must be 0 or 1");
+      if (value && !c->hz.on) {
+        // start from a quiet device: nothing queued before is tracked
+        if (int rc = swrt_synchronize(c)) return rc;
+        c->hz = HazardChecker();
+      }
+      c->hz.on = value != 0;
+      return SWRT_OK;
+    case SWRT_DEBUG_SPIN_US:
+      if (value < 0 || value > 100000) return fail(c, SWRT_ERR_ARG, "spin must be 0..100000 us");
+      c->debug_spin_us = (int)value;
+      return SWRT_OK;
+    case SWRT_DEBUG_LEGACY_PARK:
+      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "legacy park must be 0 or 1");
+      c->debug_legacy_park = value != 0;
+      return SWRT_OK;
+    default:
+      return fail(c, SWRT_ERR_ARG, "unknown debug key");
+  }
+}
+
+int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
+  if (!c || !value_out) return SWRT_ERR_ARG;
+  switch (key) {
+    case SWRT_DEBUG_HAZARD_CHECK: *value_out = c->hz.on ? 1 : 0; return SWRT_OK;
+    case SWRT_DEBUG_SPIN_US: *value_out = c->debug_spin_us; return SWRT_OK;
+    case SWRT_DEBUG_LEGACY_PARK: *value_out = c->debug_legacy_park ? 1 : 0; return SWRT_OK;
+    case SWRT_DEBUG_HAZARD_CHECKS: *value_out = c->hz.checks; return SWRT_OK;
+    default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
+  }
 }
 
 int swrt_qg_set_fused(swrt_ctx* c, int on) {

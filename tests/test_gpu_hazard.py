@@ -1,0 +1,186 @@
+"""The multi-stream packet protocol made checkable (swrt_hazard.hpp).
+
+swrt_set_packet_streams(S) runs every LDS-tiled leapfrog launch as S part
+launches on S streams that stay unjoined across calls; its safety rests on
+"parts write disjoint tile ranges between joins".  These tests run the
+library's debug happens-before checker over the call sequences that exercise
+that protocol, force the worst overlap with a spin kernel on the extra
+streams, and reintroduce the known race of round 3 (the launch after a
+re-binning's source-gather sort launch overwriting the buffer it gathers
+from) to show the checker reports it before the racy launch is queued.
+
+Reference semantics the bits are pinned to: interpolate.m:43-49 (tap order)
+and ode_symplectic.m:23-28 (the step loop), through the C oracle.
+"""
+import argparse
+
+import numpy as np
+import pytest
+
+from oracle import swrt_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits_equal(a, b):
+    return np.array_equal(np.asarray(a).view(np.uint64), np.asarray(b).view(np.uint64))
+
+
+@pytest.fixture()
+def debug_ctx(ctx):
+    import swraytracing_amd._lib as L
+    yield ctx, L
+    ctx.debug_set(L.DEBUG_SPIN_US, 0)
+    ctx.debug_set(L.DEBUG_LEGACY_PARK, 0)
+    ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+    ctx.set_packet_streams(2)
+    ctx.set_locality(4, 0)
+    ctx.set_tail_split(0, 0)
+    ctx.synchronize()
+
+
+def _bench_workload(ctx, packets):
+    import bench
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=packets, world=1, rank=0, seed=146, mode="blend")
+    return bench, bench.build_workload(ctx, args, 0, packets, packets)
+
+
+def _run_calls(ctx, bench, w, calls, sub=5):
+    ctx.packets_set(w["x"], w["k"])
+    for _ in range(calls):
+        bench.step(ctx, w, sub)
+    return ctx.packets_get()
+
+
+@pytest.mark.parametrize("streams", [2, 4])
+def test_adversarial_overlap_bitexact_and_checker_silent(debug_ctx, oracle_lib, streams):
+    """A ~200 us sleep kernel before every extra-stream part launch: call k's
+    extra parts run entirely under call k+1's packet-stream part — and under
+    the sort launch that follows each re-binning, which gathers its input from
+    any slot.  12 calls of the bench step (5 substeps, re-binning every 20
+    steps: 3 re-binnings, each with its sort launch) give the bits of one
+    stream and of the C oracle, and the checker (on for the whole run) finds
+    every cross-stream access ordered."""
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 300_000)
+    ctx.set_locality(20, 0)
+    ctx.set_packet_streams(1)
+    x1, k1 = _run_calls(ctx, bench, w, 12)
+    ctx.set_packet_streams(streams)
+    ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1)
+    ctx.debug_set(L.DEBUG_SPIN_US, 200)
+    xs, ks = _run_calls(ctx, bench, w, 12)
+    checks = ctx.debug_get(L.DEBUG_HAZARD_CHECKS)
+    assert checks > 1000, checks  # the checker saw the part launches
+    assert _bits_equal(x1, xs) and _bits_equal(k1, ks), streams
+    p0, p1 = ctx.get_field_grid(0, 512), ctx.get_field_grid(1, 512)
+    idx = np.sort(np.random.default_rng(11).choice(300_000, 1200, replace=False))
+    xo, ko = w["x"][idx], w["k"][idx]
+    for _ in range(12):
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.2, 512, 1024, w["L"] / 512, orc.BUMP_QG, xo, ko,
+                                           w["dt"] / 5, 5, w["f"], w["gH"])
+    np.testing.assert_array_equal(xs[idx], xo)
+    np.testing.assert_array_equal(ks[idx], ko)
+
+
+def test_checker_catches_the_pre_third_buffer_race(debug_ctx):
+    """The ordering before the third packet buffers (test-only switch): the
+    launch after a sort launch writes the buffer that sort launch's extra-
+    stream parts gather from.  With the checker on, that launch is refused
+    (SWRT_ERR_STATE naming both accesses) before it is queued; with the
+    checker off and the spin schedule, the race really changes the result —
+    the adversarial schedule exposes it, and the fixed ordering (test above)
+    survives the same schedule."""
+    import swraytracing_amd as sw
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 300_000)
+    ctx.set_locality(20, 0)
+    ctx.set_packet_streams(1)
+    x1, k1 = _run_calls(ctx, bench, w, 6)
+    ctx.set_packet_streams(2)
+    ctx.debug_set(L.DEBUG_LEGACY_PARK, 1)
+    ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1)
+    ctx.packets_set(w["x"], w["k"])
+    bench.step(ctx, w, 5)  # re-binning + the sort launch (gathers through src_idx)
+    with pytest.raises(sw.SwrtError) as ei:
+        bench.step(ctx, w, 5)  # its output buffer is the one the sort launch reads
+    msg = str(ei.value)
+    assert "SWRT_ERR_STATE" in msg and "hazard" in msg and "sort launch" in msg, msg
+    ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+    ctx.synchronize()
+    # unchecked, under the spin schedule: the race corrupts the packets
+    ctx.debug_set(L.DEBUG_SPIN_US, 200)
+    xr, kr = _run_calls(ctx, bench, w, 6)
+    assert not (_bits_equal(x1, xr) and _bits_equal(k1, kr))
+    # the fixed ordering under the same schedule: the one-stream bits
+    ctx.debug_set(L.DEBUG_LEGACY_PARK, 0)
+    xf, kf = _run_calls(ctx, bench, w, 6)
+    assert _bits_equal(x1, xf) and _bits_equal(k1, kf)
+
+
+@pytest.mark.parametrize("switch", ["locality", "tail_split"])
+def test_single_launch_after_split_calls_joins_first(debug_ctx, switch):
+    """70,000 packets (above the one-stream threshold) advanced by split
+    launches, then a call whose launch runs on the packet stream alone — the
+    per-packet kernel after swrt_set_locality(0, 0), or one whole tile launch
+    after swrt_set_tail_split(1, 0) — then split launches again: that launch
+    orders the extra stream's parts of the previous call before it (the
+    checker stays silent) and the bits equal one stream's."""
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 70_000)
+    out = {}
+    for streams in (1, 2):
+        ctx.set_packet_streams(streams)
+        ctx.set_locality(20, 0)
+        ctx.set_tail_split(0, 0)
+        ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1 if streams > 1 else 0)
+        ctx.debug_set(L.DEBUG_SPIN_US, 100 if streams > 1 else 0)
+        ctx.packets_set(w["x"], w["k"])
+        for _ in range(3):
+            bench.step(ctx, w, 5)
+        if switch == "locality":
+            ctx.set_locality(0, 0)
+        else:
+            ctx.set_tail_split(1, 0)
+        bench.step(ctx, w, 5)
+        ctx.set_locality(20, 0)
+        ctx.set_tail_split(0, 0)
+        for _ in range(3):
+            bench.step(ctx, w, 5)
+        out[streams] = ctx.packets_get()
+        ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+    assert _bits_equal(out[1][0], out[2][0]) and _bits_equal(out[1][1], out[2][1])
+
+
+def test_checker_silent_over_the_mixed_call_sequence(debug_ctx):
+    """test_packet_streams_bit_identical's call sequence (history frames,
+    re-binnings inside and between calls, slot rewrites, multi-interval
+    launches, reads, ode23) on 2 and 4 streams with the checker on."""
+    import swraytracing_amd as sw
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 300_000)
+    p0, p1 = ctx.get_field_grid(0).copy(), ctx.get_field_grid(1).copy()
+    h = w["dt"] / 5
+    for streams in (2, 4):
+        ctx.set_packet_streams(streams)
+        ctx.set_locality(20, 0)
+        ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1)
+        ctx.set_field_grid(0, p0, 512, w["L"], 1024)
+        ctx.set_field_grid(1, p1, 512, w["L"], 1024)
+        ctx.packets_set(w["x"], w["k"])
+        ctx.history_reset()
+        for _ in range(7):
+            ctx.advance(h, 5, w["f"], w["gH"], nslots=2, alpha0=0.1, dalpha=0.2, bump=orc.BUMP_QG, save_every=5)
+        ctx.packets_get()
+        ctx.history()
+        ctx.set_field_grid(1, p0, 512, w["L"], 1024)
+        ctx.set_field_grid(2, p1, 512, w["L"], 1024)
+        ctx.advance_intervals([h, 1.1 * h], 5, w["f"], w["gH"], alpha0=0.1, dalpha=0.2, bump=orc.BUMP_QG)
+        ctx.advance(h, 3, w["f"], w["gH"], nslots=2, alpha0=0.1, dalpha=0.2, bump=orc.BUMP_QG)
+        ctx.packets_get()
+        ctx.set_field_grid(1, p1, 512, w["L"], 1024)
+        sw.ode23_packets(ctx, (0.0, 5 * h), 5 * h, w["f"], 1.0, stats={})
+        ctx.packets_get()
+        assert ctx.debug_get(L.DEBUG_HAZARD_CHECKS) > 0
+        ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
