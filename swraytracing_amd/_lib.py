@@ -511,7 +511,10 @@ class Context:
 
     def ode23_run(self, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_cap=100_000):
         """swrt_ode23_run: the whole ode23 call with the controller in the
-        library.  Returns (accepted times, {steps, failed, attempts})."""
+        library.  Returns (accepted times, {steps, failed, attempts,
+        accepted}); `accepted` counts every accepted time, and a warning is
+        raised when more than ts_cap were accepted (the list then holds the
+        first ts_cap only)."""
         ts = np.empty(ts_cap)
         nts = _I()
         st = (_I * 3)()
@@ -519,7 +522,12 @@ class Context:
                                          int(nslots), float(rtol), float(atol), float(bump), _p(ts), int(ts_cap),
                                          ctypes.byref(nts), st), "swrt_ode23_run")
         # ts_cap bounds the recorded times only (the interval always completes)
-        return ts[:min(nts.value, ts_cap)].copy(), {"steps": st[0], "failed": st[1], "attempts": st[2]}
+        if nts.value > ts_cap:
+            import warnings
+            warnings.warn(f"swrt_ode23_run accepted {nts.value} times; only the first ts_cap={ts_cap} are returned",
+                          RuntimeWarning, stacklevel=2)
+        return ts[:min(nts.value, ts_cap)].copy(), {"steps": st[0], "failed": st[1], "attempts": st[2],
+                                                    "accepted": nts.value}
 
     # ---- QG PDE stepper (swrt_qg_*) ---------------------------------------
     def qg_init(self, params: QGParams, nx, qk):

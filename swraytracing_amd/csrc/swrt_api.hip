@@ -198,8 +198,8 @@ struct swrt_ctx {
   int64_t steps_since_bin = 0;
   bool bin_valid = false;
   bool keys_fresh = false;  // keys/counts of the current state came from the last tile launch
-  int64_t key_nx = 0;       // ... on slot 0's grid of that launch (the keys depend on nx and L only,
-  double key_L = 0.0;       //     not on the field values: new snapshots keep them valid)
+  int64_t key_nx = 0;       // ... on the grid the launch read (its first snapshot's nx and dx: the keys
+  double key_dx = 0.0;      //     depend on those only, not on the field values — new snapshots keep them valid)
   bool counts_zero = false;  // bins' count block is all zero (cleared by the last scan)
   int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
   bool sort_lead = SWRT_SORT_LEAD;  // in-tile sort keys lead by the group-velocity drift
@@ -879,7 +879,7 @@ int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
   if (nbins > kMaxBins) return fail(c, SWRT_ERR_ARG, "too many spatial bins (raise tile size)");
   const int64_t n = c->n;
   const unsigned grid = nblocks(n, 256 * kBinPerThread);
-  const bool keys_valid = c->keys_fresh && c->bin_valid && nbins == c->nbins && c->key_nx == s.nx && c->key_L == s.L;
+  const bool keys_valid = c->keys_fresh && c->bin_valid && nbins == c->nbins && c->key_nx == v.nx && c->key_dx == v.dx;
   if (c->hz.on) {  // count, scan and scatter on the packet stream
     HazardChecker& h = c->hz;
     const uint64_t t = h.op(0);
@@ -979,8 +979,8 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     c->counts_zero = false;
     t.next_keys = c->keys;
     t.next_counts = c->bins;
-    c->key_nx = c->slot[0].nx;
-    c->key_L = c->slot[0].L;
+    c->key_nx = a.f0.nx;  // the view this launch bins by (a multi-interval launch: slot i0's)
+    c->key_dx = a.f0.dx;
   }
   if (big) {  // leap_tile chose 32-cell tiles: two divergence-free snapshots (checked again here)
     if (a.nslots != 2 || !(iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)))

@@ -356,11 +356,6 @@ __device__ __forceinline__ void gather5_half(const double2* lds, int node0, int 
   }
 }
 
-// pair_rank: the packet (0..31) of lane t (0..31) within the wave's run of 32
-// cell-sorted packets, so each ds_read_b128 lane group (b128_lane_rank's
-// 16-lane groups, the upper half mirroring the lower) takes 16 consecutive
-// packets.
-
 // Stage tile (ox, oy)'s window into LDS, chunk-major (chunk c of node e at
 // win[c*WN + e]): node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx.
 // Register staging: each lane copies whole 48-B records, 3 or 6 loads back
@@ -617,6 +612,9 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
       const int h = (tid >> 5) & 1;  // this lane's half: x weights + snapshot 0, or y weights + snapshot 1
       const double cper = h ? a.f0.py : a.f0.px, inv_cper = h ? a.f0.inv_py : a.f0.inv_px;
       const int icper = h ? a.f0.ipy : a.f0.ipx;
+      // lane_rank & 31: the packet (0..31) of this lane within the wave's run of
+      // 32 cell-sorted packets, so each ds_read_b128 lane group takes 16
+      // consecutive packets (the upper half mirrors the lower)
       for (int r0 = (tid >> 6) * 32; r0 < nb; r0 += NT / 2) {
         const int r = r0 + (lane_rank & 31);
         if (r >= nb) continue;

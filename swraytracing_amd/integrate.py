@@ -158,7 +158,7 @@ def ode23_packets(ctx: Context, tspan, tmax, f, Cg, nslots=2, rtol=1e-3, atol=1e
             temp = 1.25 * (err / rtol) ** pw
             absh = absh / temp if temp > 0.2 else 5.0 * absh
     if stats is not None:
-        stats.update(steps=len(ts) - 1, failed=nfailed, attempts=attempts)
+        stats.update(steps=len(ts) - 1, failed=nfailed, attempts=attempts, accepted=len(ts))
     return np.array(ts)
 
 

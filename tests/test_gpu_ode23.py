@@ -88,10 +88,14 @@ def test_ode23_run_ts_cap_bounds_times_only(ctx, qg_case):
     out = []
     for cap in (100_000, 3):
         ctx.packets_set(x, k)
-        ts, st = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG, ts_cap=cap)
+        if cap < 100:  # fewer slots than accepted times: the caller is told
+            with pytest.warns(RuntimeWarning, match="accepted"):
+                ts, st = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG, ts_cap=cap)
+        else:
+            ts, st = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG, ts_cap=cap)
         out.append((ts, st, *ctx.packets_get()))
     (ts_a, st_a, xa, ka), (ts_b, st_b, xb, kb) = out
-    assert st_a == st_b and st_a["steps"] > 3
+    assert st_a == st_b and st_a["steps"] > 3 and st_a["accepted"] == len(ts_a) > 3
     np.testing.assert_array_equal(ts_b, ts_a[:3])
     np.testing.assert_array_equal(xb, xa)
     np.testing.assert_array_equal(kb, ka)
