@@ -86,12 +86,7 @@ def build_workload(ctx, args, lo, hi, n_total):
     ctx.set_field_qk(0, qk1, nx, L, K_d2, shear, ks, 2 * nx)
     if nslots == 2:
         ctx.set_field_qk(1, qk2, nx, L, K_d2, shear, ks, 2 * nx)
-        # --intervals K: the later snapshots of K consecutive PDE intervals, each
-        # a further small phase rotation of the previous one
-        qk = qk2
-        for s in range(2, getattr(args, "intervals", 1) + 1):
-            qk = qk * np.exp(1j * rng2.normal(0, 0.05, qk.shape))
-            ctx.set_field_qk(s, qk, nx, L, K_d2, shear, ks, 2 * nx)
+        set_interval_snapshots(ctx, qk2, rng2, nx, L, K_d2, shear, ks, getattr(args, "intervals", 1))
     p = ctx.get_field_grid(0, nx)
     U0 = math.sqrt(float((p[0] ** 2 + p[1] ** 2).max()))
     dt = 0.25 * (L / nx) / U0  # qg2layersw_raytrace.m:31,78
@@ -112,7 +107,30 @@ def build_workload(ctx, args, lo, hi, n_total):
     else:
         x = (L * rng.random((n_total, 2)) - L / 2)[lo:hi]
     return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
-                K_d2=K_d2, ks=ks, shear=shear, intervals=getattr(args, "intervals", 1) if nslots == 2 else 1)
+                K_d2=K_d2, ks=ks, shear=shear, intervals=getattr(args, "intervals", 1) if nslots == 2 else 1,
+                seed=args.seed)
+
+
+def set_interval_snapshots(ctx, qk2, rng2, nx, L, K_d2, shear, ks, intervals):
+    """Slots 2..intervals: the later snapshots of `intervals` consecutive PDE
+    intervals (--intervals), each a further small phase rotation of the
+    previous one (rng2 continues the stream that made qk2)."""
+    qk = qk2
+    for s in range(2, intervals + 1):
+        qk = qk * np.exp(1j * rng2.normal(0, 0.05, qk.shape))
+        ctx.set_field_qk(s, qk, nx, L, K_d2, shear, ks, 2 * nx)
+
+
+def with_intervals(ctx, w, K):
+    """The workload `w` advanced K PDE intervals per call (one
+    swrt_advance_intervals call, 5K steps per launch): slots 2..K get the
+    snapshots build_workload makes for --intervals K (the same seed stream)."""
+    if w["nslots"] != 2 or K <= w["intervals"]:
+        return dict(w, intervals=K if w["nslots"] == 2 else 1)
+    rng2 = np.random.default_rng(w["seed"] + 1)
+    rng2.normal(0, 0.05, w["qk1"].shape)  # the draw that made qk2
+    set_interval_snapshots(ctx, w["qk2"], rng2, w["nx"], w["L"], w["K_d2"], w["shear"], w["ks"], K)
+    return dict(w, intervals=K)
 
 
 def step(ctx, w, sub):
@@ -241,8 +259,68 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     return out
 
 
+def pde_alone(ctx, w, args, dev, nsteps=None):
+    """The driver loop without packets (TwoLayerLoop with no ensemble): CFL
+    rule, 2-layer PDE step and the U0 read-back (qg2layersw_raytrace.m:152-181),
+    i.e. the replicated part of every rank's driver step."""
+    nx, L, f, Cg = w["nx"], w["L"], w["f"], math.sqrt(w["gH"])
+    nsteps = nsteps or args.driver_steps
+    qk = np.stack([w["qk1"], -w["qk1"]], axis=2)
+    model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
+    U0 = model.max_speed()
+    loop = sw.TwoLayerLoop(model, None, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps)
+    for _ in range(args.driver_warmup):
+        loop.step()
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(nsteps):
+        loop.step()
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / nsteps * 1e3
+
+
+def driver_forecast(ctx, w, args, dev, n_total, full):
+    """End-to-end strong-scaling forecast of the 2-layer driver: `driver_step`
+    timed on one GPU with rank 0's shard of a G-GPU run (the first
+    ceil(n_total/G) packets) beside the full replicated PDE, G = 2, 4, 8;
+    efficiency = rate(shard) / rate(all n_total on one GPU).  With the PDE
+    alone and the packets alone (strong_scaling_forecast) beside it, `bound`
+    names the term that sets the step: the PDE when its own step time exceeds
+    the packets'."""
+    pde_ms = pde_alone(ctx, w, args, dev)
+    out = {"pde_alone_ms": pde_ms,
+           "what": "TwoLayerLoop.step with 1e6/G packets on one GPU (full replicated 2-layer PDE + snapshot + "
+                   f"{args.substeps} leapfrog substeps); pde_alone_ms: the same loop without packets"}
+    rate_full = full["packet_steps_per_s"]
+    for G in (2, 4, 8):
+        n = -(-n_total // G)
+        ws = dict(w, x=w["x"][:n], k=w["k"][:n])
+        d = driver_step(ctx, ws, args, dev, False, n)
+        r = {"packets_per_gpu": n, "ms_per_pde_step": d["ms_per_pde_step"],
+             "value_1gpu": d["packet_steps_per_s"], "forecast_value": G * d["packet_steps_per_s"],
+             "efficiency": d["packet_steps_per_s"] / rate_full}
+        out[str(G)] = r
+    return out
+
+
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s (78.6 TFLOP/s spec counts an FMA as 2)
 LDS_CYCLES_PEAK = 256 * 2.4e9               # LDS-array cycles/s over the chip (one array per CU, 2.4 GHz)
+# fp64 operations one packet-step of the reference arithmetic needs (each +, -, *, /, sqrt, floor one op;
+# the six Lagrange weights per direction and the 36 products wx_i*wy_j computed once per step and shared
+# by every field, as any implementation may; v_y = -u_x on streamfunction fields):
+#   cell + fractional offset (interpolate.m:21-30): x/dx, mod (div, floor, mul, sub), 1 + floor,
+#     1 + xl - i0; 2 directions x 9                                            18
+#   Lagrange weights (:32-40): 6 factors (a - j + bump) x 2 ops + 30 mul + 30 div, x 2 directions  144
+#   tap products wx_i*wy_j (:45-48)                                           36
+#   10 stencil sums (5 fields x 2 snapshots) x (36 mul + 35 add)             710
+#   blend (interpolate_U.m:19-23): (1 - alpha) + 5 fields x (2 mul, add)      16
+#   leapfrog (ode_symplectic.m:10-21): omega (k*k, l*l, add, gH*, f^2 +, sqrt) 6, gH*k/omega and
+#     gH*l/omega 4, half-step scaling 2, two drifts applied 4; kick: x 2 x (mul, add),
+#     k 2 x (3 mul, add, sub)                                                  30
+ALG_OPS_PER_PACKET_STEP = 18 + 144 + 36 + 710 + 16 + 30  # = 954 (two-snapshot blend)
+ALG_OPS_STEADY = 18 + 144 + 36 + 5 * 71 + 30             # = 583 (one snapshot)
 
 
 def load_pmc(config_key):
@@ -273,10 +351,16 @@ def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timin
     array are reported beside it as fractions of their own peaks."""
     ps = N * steps_per_launch
     B = BYTES_BLEND if nslots == 2 else BYTES_STEADY
+    ops = ALG_OPS_PER_PACKET_STEP if nslots == 2 else ALG_OPS_STEADY
     r = {"bound": "valu-fp64-issue", "achieved": None, "peak": FP64_LANE_OPS_PEAK / 1e12, "unit": "Tlane-op/s",
          "frac": None, "traffic": None,
          "avg_launch_ms": avg_launch_s * 1e3, "timed_launches": launches, "timing_every": timing_every,
          "packet_steps_per_launch": ps,
+         # the reference arithmetic's own fp64 operations (ALG_OPS_PER_PACKET_STEP) over the same time and
+         # peak: instruction overhead (index math, exact-division sequences, loads' address arithmetic)
+         # does not count here, so this fraction cannot be raised by issuing more instructions
+         "algorithmic_ops_per_packet_step": ops,
+         "algorithmic_frac": ops * ps / avg_launch_s / FP64_LANE_OPS_PEAK,
          # SURVEY §8d's algorithmic bytes (taps counted as if each were read from HBM; they are
          # re-read from LDS): an effective gather bandwidth, not an HBM fraction
          "effective_gather_gbs": ps * B / avg_launch_s / 1e9, "gather_bytes_per_packet_step": B}
@@ -305,6 +389,7 @@ def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timin
         clk = pmc["GRBM_GUI_ACTIVE"] / 8.0 / pmc_s
         r.update({"clock_ghz_measured": clk / 1e9,
                   "frac_at_measured_clock": ach / (FP64_LANE_OPS_PEAK * clk / 2.4e9),
+                  "algorithmic_frac_at_measured_clock": r["algorithmic_frac"] * 2.4e9 / clk,
                   "lds_frac_at_measured_clock": pmc["SQ_LDS_IDX_ACTIVE"] / (256 * clk * pmc_s)})
     return r
 
@@ -340,11 +425,16 @@ def parse_args(argv=None):
                     help="skip the extra line of the opt-in FMA gather mode (swrt_set_gather_mode 1, tolerance parity)")
     ap.add_argument("--no-forecast", action="store_true",
                     help="at N = 1, skip the strong-scaling forecast (the workload at 2/4/8-GPU shard sizes)")
+    ap.add_argument("--forecast-intervals", type=int, default=4,
+                    help="at N = 1, also forecast with this many PDE intervals per call (1: skip)")
     ap.add_argument("--rebin-every", type=int, default=20, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
     ap.add_argument("--blend-mode", type=int, default=0,
                     help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
+    ap.add_argument("--sparse-tiles", type=int, default=0, choices=[0, 1, 2],
+                    help="LDS-tiled launches: sparse-tile shape (256 threads, reads 3 taps ahead) 0 auto, 1 never, "
+                         "2 always (same bits)")
     ap.add_argument("--lanes-per-packet", type=int, default=0,
                     help="LDS-tiled launches: 0 auto (build threshold, off by default), 1, 2 (same bits)")
     ap.add_argument("--tile-cells", type=int, default=0,
@@ -457,22 +547,42 @@ def timed(ctx, w, args, dev, steps, warmup, barrier=None):
     return t1 - t0, kms, launches
 
 
-def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu):
+def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu, sizes=(2, 4, 8), steps=None):
     """One GPU timed on the packets rank 0 of a G-GPU strong-scaling run
     holds (the first ceil(n_total/G) of the same ensemble) for G = 2, 4, 8:
     forecast value = G x that rate (the field is replicated and the timed path
-    has no collective), efficiency = rate(shard) / rate(n_total)."""
+    has no collective), efficiency = rate(shard) / rate_1gpu (the rate of all
+    n_total packets on one GPU; G = 1 in `sizes` times that too)."""
     out = {}
     x, k = w["x"], w["k"]
-    for G in (2, 4, 8):
+    steps = steps or args.steps
+    for G in sizes:
         n = -(-n_total // G)
         ctx.packets_set(x[:n], k[:n])
-        el, kms, launches = timed(ctx, w, args, dev, args.steps, args.warmup)
-        rate = n * args.substeps * w["intervals"] * args.steps / el
+        el, kms, launches = timed(ctx, w, args, dev, steps, args.warmup)
+        rate = n * args.substeps * w["intervals"] * steps / el
         out[str(G)] = {"packets_per_gpu": n, "value_1gpu": rate, "forecast_value": G * rate,
-                       "efficiency": rate / rate_1gpu, "ms_per_step": el / args.steps * 1e3,
+                       "efficiency": rate / rate_1gpu if rate_1gpu else None, "ms_per_step": el / steps * 1e3,
                        "avg_launch_ms": (kms / launches) if launches else None}
     ctx.packets_set(x, k)
+    return out
+
+
+def intervals_forecast(ctx, w, args, dev, n_total, rate_1gpu, K):
+    """The strong-scaling forecast with K PDE intervals per call (swrt_advance_
+    intervals, 5K steps per tile launch: the window staging, in-tile sort and
+    launch tail paid once per K intervals; each interval blends its own pair of
+    K + 1 distinct snapshots, as a driver running the PDE K steps ahead or
+    trace_stored does).  Efficiencies against the metric's one-interval 1e6
+    rate (`efficiency`) and against this form's own 1e6 rate."""
+    wk = with_intervals(ctx, w, K)
+    steps = max(1, args.steps // K)  # the same packet-steps per timed region
+    out = strong_scaling_forecast(ctx, wk, args, dev, n_total, rate_1gpu, sizes=(1, 2, 4, 8), steps=steps)
+    own = out["1"]["value_1gpu"]
+    for G, r in out.items():
+        r["efficiency_vs_own_1gpu"] = r["value_1gpu"] / own
+    out["intervals_per_call"] = K
+    out["steps_per_launch"] = args.substeps * min(K, 4)
     return out
 
 
@@ -505,6 +615,7 @@ def main(argv=None):
     ctx.set_blend_mode(args.blend_mode)
     ctx.set_lanes_per_packet(args.lanes_per_packet)
     ctx.set_tile_cells(args.tile_cells)
+    ctx.set_sparse_tiles(args.sparse_tiles)
     ctx.set_packet_streams(args.packet_streams)
     ctx.set_gather_mode(args.gather_mode)
     if args.tail_split >= 0:
@@ -579,6 +690,7 @@ def main(argv=None):
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split,
                    "lanes_per_packet": args.lanes_per_packet, "tile_cells": args.tile_cells,
+                   "sparse_tiles": args.sparse_tiles,
                    "packet_streams": args.packet_streams, "gather_mode": args.gather_mode,
                    "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
@@ -601,8 +713,11 @@ def main(argv=None):
                              "avg_launch_ms": (kms2 / l2) if l2 else None, "vs_exact": elapsed / el2,
                              "parity": "tolerance: stencil sums and blend by fused multiply-add, "
                                        "<= 1e-13 relative per step vs the bit-exact path"}
-    if world == 1 and not args.no_forecast and args.scaling == "strong" and args.intervals == 1:
+    if world == 1 and not args.no_forecast and args.scaling == "strong":
         out["strong_scaling_forecast"] = strong_scaling_forecast(ctx, w, args, dev, n_total, value)
+        if args.forecast_intervals > 1 and w["nslots"] == 2 and args.kernel in (0, 2):
+            out["strong_scaling_forecast_intervals"] = intervals_forecast(ctx, w, args, dev, n_total, value,
+                                                                          args.forecast_intervals)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the GPU box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there)
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
@@ -623,6 +738,14 @@ def main(argv=None):
         out["cpu_baseline"] = None
     if args.driver_steps > 0 and args.mode == "blend":
         out["driver_step"] = driver_step(ctx, w, args, dev, distributed, n_total)
+        if world == 1 and not args.no_forecast and args.scaling == "strong":
+            fc = driver_forecast(ctx, w, args, dev, n_total, out["driver_step"])
+            pk = out.get("strong_scaling_forecast", {})
+            for G in ("2", "4", "8"):
+                if G in pk:  # packets alone at this shard (the metric's form) vs the PDE alone
+                    fc[G]["packets_alone_ms"] = pk[G]["ms_per_step"]
+                    fc[G]["bound"] = "pde" if fc["pde_alone_ms"] > pk[G]["ms_per_step"] else "packets"
+            out["driver_step_forecast"] = fc
     if args.ode23_steps > 0 and args.mode == "blend" and world == 1:
         # (single rank: a sharded ode23 needs the error norm's allreduce, PacketEnsemble(shard=...))
         out["driver_step_ode23"] = driver_step(ctx, w, args, dev, distributed, n_total, integrator="ode23",

@@ -230,6 +230,15 @@ int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
  * Results are bit-identical for any setting. */
 int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
 
+/* Launch shape of the LDS-tiled two-snapshot launches (fields with v_y ==
+ * -u_x) when tiles hold few packets: 256-thread workgroups with a 256-VGPR
+ * budget whose stencil gather issues each tap's LDS reads three taps ahead
+ * (instead of 512 threads, 128 VGPRs, one tap ahead), so the one busy wave a
+ * SIMD has at ~120 packets per tile waits less on the LDS.  0 (default) =
+ * below SWRT_SPARSE_BELOW packets per 16x16 tile on average, 1 = never, 2 =
+ * always.  Same arithmetic in the same order: bit-identical for any setting. */
+int swrt_set_sparse_tiles(swrt_ctx* ctx, int mode);
+
 /* Packet streams of the LDS-tiled leapfrog: 2 (default), 4 or 1.  With S > 1
  * every launch runs as S part launches — every S-th tile of each XCD band —
  * on the context's packet stream and S-1 more streams.  Between re-binnings

@@ -72,6 +72,7 @@ SIGNATURES = {
     "swrt_set_blend_mode": (_INT, [_VP, _INT]),
     "swrt_set_gather_mode": (_INT, [_VP, _INT]),
     "swrt_set_lanes_per_packet": (_INT, [_VP, _INT]),
+    "swrt_set_sparse_tiles": (_INT, [_VP, _INT]),
     "swrt_set_tile_cells": (_INT, [_VP, _INT]),
     "swrt_set_packet_streams": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
@@ -355,6 +356,10 @@ class Context:
         """swrt_set_gather_mode: 0 bit-exact mul-then-add stencil sums (default),
         1 fused multiply-add (tolerance parity, fewer VALU instructions)."""
         self._chk(self._L.swrt_set_gather_mode(self._h, int(mode)), "swrt_set_gather_mode")
+
+    def set_sparse_tiles(self, mode=0):
+        """swrt_set_sparse_tiles: 0 auto (below SWRT_SPARSE_BELOW packets per tile), 1 never, 2 always; same bits."""
+        self._chk(self._L.swrt_set_sparse_tiles(self._h, int(mode)), "swrt_set_sparse_tiles")
 
     def set_lanes_per_packet(self, lanes=0):
         """swrt_set_lanes_per_packet: 0 auto (build threshold; off by default), 1, 2; same bits."""

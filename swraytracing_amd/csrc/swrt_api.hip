@@ -80,6 +80,19 @@ constexpr int kPairBelow = SWRT_PAIR_BELOW;
 #ifndef SWRT_BIG_TILE_BELOW
 #define SWRT_BIG_TILE_BELOW 0
 #endif
+// Sparse-tile launches: below SWRT_SPARSE_BELOW packets per 16x16 tile on
+// average (a strong-scaling shard: ~120 at 1.25e5 packets on 512^2) a
+// 512-thread workgroup has one or two busy waves, one per SIMD, each capped
+// at 128 VGPRs by the dense launch's 4-waves-per-SIMD budget and waiting on
+// LDS reads issued one tap earlier.  The sparse form is the same kernel with
+// 256 threads per workgroup, a 256-VGPR budget and the gather's reads issued
+// three taps ahead (gather5_lds PF): same arithmetic, same bits.
+#ifndef SWRT_SPARSE_BELOW
+#define SWRT_SPARSE_BELOW 192
+#endif
+constexpr int kSparseBelow = SWRT_SPARSE_BELOW;
+constexpr int kSparseThreads = 256;
+constexpr int kSparsePrefetch = 3;
 constexpr int kBigTile = 32;
 constexpr int kBigTileThreads = 1024;
 constexpr int kBigTileBelow = SWRT_BIG_TILE_BELOW;
@@ -211,6 +224,7 @@ struct swrt_ctx {
   int gather_mode = 0;      // 0: stencil sums mul then add (bit-exact); 1: fused multiply-add (tolerance)
   int lanes_per_packet = 0; // LDS-tiled two-snapshot launches: 1, 2 (paired lanes), 0 = by packets per tile
   int tile_mode = 0;        // leapfrog tile size: 0 auto (32 for small ensembles), 16, 32
+  int sparse_mode = 0;      // sparse-tile launches: 0 auto (below kSparseBelow packets per tile), 1 never, 2 always
   // Several packet streams (swrt_set_packet_streams S = 2 or 4): each
   // LDS-tiled leapfrog launch runs as S part launches — every S-th band
   // position of every XCD band — on `stream` and the extra streams sx[].
@@ -837,6 +851,14 @@ bool use_tile_kernel(const swrt_ctx* c) {
   return c->kernel == 0 && c->slot[0].nx >= 2 * kTile;
 }
 
+// The sparse-tile launch shape (kSparseThreads threads, prefetch depth
+// kSparsePrefetch) for the two-snapshot five-sum launches over `ntiles` tiles.
+bool sparse_tiles(const swrt_ctx* c, int64_t ntiles) {
+  if (c->sparse_mode == 1) return false;
+  if (c->sparse_mode == 2) return true;
+  return c->n < (int64_t)kSparseBelow * ntiles;
+}
+
 // Tile side of the LDS-tiled leapfrog for this call: 32 for small ensembles
 // on two divergence-free snapshots (the kernel's only 32-cell instantiation),
 // else kTile.  slot0..slot0+nslots-1 are the snapshots the call reads.
@@ -908,7 +930,7 @@ int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
   c->keys_fresh = false;
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins,
                      c->bins + 2 * kMaxBins, c->tile_order ? tile_order_of(c) : nullptr,
-                     g.tile == kBigTile ? kBigTileThreads : kTileThreads);
+                     g.tile == kBigTile ? kBigTileThreads : (sparse_tiles(c, nbins) ? kSparseThreads : kTileThreads));
   HIPCHK(c, hipGetLastError());
   c->counts_zero = true;
   c->bin_tile = g.tile;
@@ -997,7 +1019,12 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
       // one or two busy waves): two waves per packet run instead of one
       const bool pair = c->lanes_per_packet == 2 ||
                         (c->lanes_per_packet == 0 && c->n < (int64_t)kPairBelow * (int64_t)grid);
-      if (pair && c->gather_mode == 1)
+      const bool sparse = !pair && sparse_tiles(c, grid);
+      if (sparse && c->gather_mode == 1)
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, false, true, true, false, kSparsePrefetch, 2>, wgrid, kSparseThreads, t));
+      else if (sparse)
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, false, true, false, false, kSparsePrefetch, 2>, wgrid, kSparseThreads, t));
+      else if (pair && c->gather_mode == 1)
         HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true, true>, wgrid, kTileThreads, t));
       else if (pair)
         HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, false, true>, wgrid, kTileThreads, t));
@@ -1770,6 +1797,16 @@ int swrt_set_lanes_per_packet(swrt_ctx* c, int lanes) {
   if (!c) return SWRT_ERR_ARG;
   if (lanes < 0 || lanes > 2) return fail(c, SWRT_ERR_ARG, "lanes per packet must be 0 (auto), 1 or 2");
   c->lanes_per_packet = lanes;
+  return SWRT_OK;
+}
+
+int swrt_set_sparse_tiles(swrt_ctx* c, int mode) {
+  if (!c) return SWRT_ERR_ARG;
+  if (mode < 0 || mode > 2) return fail(c, SWRT_ERR_ARG, "sparse tiles must be 0 (auto), 1 (never) or 2 (always)");
+  c->sparse_mode = mode;
+  c->bin_valid = false;  // the tile order of the next binning is sized for the launch shape
+  c->keys_fresh = false;
+  c->src_pending = false;
   return SWRT_OK;
 }
 

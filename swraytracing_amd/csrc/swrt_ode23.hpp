@@ -291,14 +291,22 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
       double s4[4], fe[4];
 #pragma unroll 1
       for (int sg = 0; sg < 3; ++sg) {
+        // The packet's index re-materialised per stage: without the barrier
+        // the compiler hoisted the per-packet 64-bit addresses (y, F1, F4,
+        // ynew) out of the loop and kept them live across the gather — 76 B
+        // per lane spilled to scratch and re-loaded every stage, most of the
+        // launch's HBM writes (profiles/r04_ode23_pmc).  Recomputing them
+        // costs a few integer instructions per stage.
+        int64_t q = p;
+        asm volatile("" : "+v"(q));
         double ts;
         // y is re-read per stage (an L2 hit) rather than held across the
         // gather: 8 VGPRs fewer at the loop's peak
-        const double yv[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
+        const double yv[4] = {a.yx[q], a.yx[n + q], a.yk[q], a.yk[n + q]};
         if (sg == 0) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const double f1 = a.F[0][c * n + p];
+            const double f1 = a.F[0][c * n + q];
             ys[c] = yv[c] + f1 * a.c[0];
             s4[c] = f1 * a.c4[0];
             fe[c] = f1 * E1;
@@ -311,8 +319,8 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
         } else {
 #pragma unroll
           for (int c = 0; c < 4; ++c) ys[c] = yv[c] + (s4[c] + fo[c] * a.c4[2]);
-          a.ynx[p] = ys[0]; a.ynx[n + p] = ys[1];
-          a.ynk[p] = ys[2]; a.ynk[n + p] = ys[3];
+          a.ynx[q] = ys[0]; a.ynx[n + q] = ys[1];
+          a.ynk[q] = ys[2]; a.ynk[n + q] = ys[3];
           ts = a.ts4;
         }
         tile_rhs<TWO, T, M, WS, WNP, V5>(a, win, ox, oy, nx, alpha_of(a, ts), ys, fo);
@@ -327,9 +335,11 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
           for (int c = 0; c < 4; ++c) fe[c] = fe[c] + fo[c] * E3;
         }
       }
+      int64_t q = p;
+      asm volatile("" : "+v"(q));
 #pragma unroll
-      for (int c = 0; c < 4; ++c) a.F[3][c * n + p] = fo[c];
-      const double yv[4] = {a.yx[p], a.yx[n + p], a.yk[p], a.yk[n + p]};
+      for (int c = 0; c < 4; ++c) a.F[3][c * n + q] = fo[c];
+      const double yv[4] = {a.yx[q], a.yx[n + q], a.yk[q], a.yk[n + q]};
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
         const double e = fe[c] + fo[c] * E4;

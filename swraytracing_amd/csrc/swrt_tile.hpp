@@ -256,9 +256,17 @@ __device__ __forceinline__ void tap5_read(const double2* p, int e, Tap5<TWO>& t)
     t.c.x = reinterpret_cast<const double*>(p + 2 * WN + e)[0];
   }
 }
-template <bool TWO, int W, int WN, bool FMA = false>
+//
+// PF (prefetch depth, default 1): tap t+PF's reads are issued before tap t's
+// arithmetic, from a ring of PF+1 tap buffers (fully unrolled: registers).
+// The sparse-tile launches (few packets per tile, at most two waves per SIMD,
+// 256 VGPRs per wave) run PF = 3: a lone wave per SIMD then waits on reads
+// issued three taps earlier instead of one.  Same operations, same bits.
+template <bool TWO, int W, int WN, bool FMA = false, int PF = 1>
 __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const Stencil& s,
                                             double o0[kRec], double o1[kRec]) {
+  static_assert(PF >= 1 && PF <= 4, "prefetch depth");
+  constexpr int NTAP = kNT * kNT;
 #pragma unroll
   for (int f = 0; f < 5; ++f) { o0[f] = -0.0; o1[f] = -0.0; }
   const double2* p = lds + node0;
@@ -270,13 +278,15 @@ __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const
     asm volatile("" : "+v"(wx[q]));
     asm volatile("" : "+v"(wy[q]));
   }
-  Tap5<TWO> cur, nxt;
-  tap5_read<TWO, WN>(p, 0, cur);
+  Tap5<TWO> ring[PF + 1];
 #pragma unroll
-  for (int t = 0; t < kNT * kNT; ++t) {
+  for (int t = 0; t < PF; ++t) tap5_read<TWO, WN>(p, (t / kNT) * W + t % kNT, ring[t]);
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t) {
     const int i = t / kNT, j = t % kNT;
-    if (t + 1 < kNT * kNT) tap5_read<TWO, WN>(p, ((t + 1) / kNT) * W + (t + 1) % kNT, nxt);
+    if (t + PF < NTAP) tap5_read<TWO, WN>(p, ((t + PF) / kNT) * W + (t + PF) % kNT, ring[(t + PF) % (PF + 1)]);
     __builtin_amdgcn_sched_barrier(0);
+    const Tap5<TWO>& cur = ring[t % (PF + 1)];
     const double wij = wx[i] * wy[j];
     o0[0] = madd<FMA>(o0[0], wij, cur.a0.x); o0[1] = madd<FMA>(o0[1], wij, cur.a0.y);
     o0[2] = madd<FMA>(o0[2], wij, cur.a1.x); o0[3] = madd<FMA>(o0[3], wij, cur.a1.y);
@@ -287,7 +297,6 @@ __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const
       o1[4] = madd<FMA>(o1[4], wij, cur.c.y);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < kNT * kNT) cur = nxt;
   }
   o0[5] = -o0[2];
   o1[5] = -o1[2];
@@ -448,8 +457,12 @@ __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 // snapshot blend as fused multiply-adds — tolerance parity, not bits.
 // PAIR (small ensembles): two lanes per packet (paired lanes, above); the
 // two-snapshot five-sum window only.
-template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false, bool FMA = false, bool PAIR = false>
-__global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(TileArgs ta) {
+// PF: the five-sum gather's prefetch depth (gather5_lds); MINW: the waves per
+// SIMD the register budget is sized for (4: 128 VGPRs; the sparse-tile
+// instantiation, 256 threads with PF 3, takes 2: 256 VGPRs).
+template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false, bool FMA = false, bool PAIR = false,
+          int PF = 1, int MINW = SWRT_TILE_MIN_WAVES>
+__global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
   static_assert(!FMA || (V5 && !WBLEND), "the FMA gather exists for the five-sum window only");
   static_assert(!PAIR || (TWO && V5 && !WBLEND), "paired lanes split the two snapshots of the five-sum window");
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
@@ -753,7 +766,7 @@ __global__ void __launch_bounds__(NT, SWRT_TILE_MIN_WAVES) tile_leapfrog_kernel(
         } else {
           if (inwin) {
             if constexpr (V5)
-              gather5_lds<TWO, WS, WNP, FMA>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+              gather5_lds<TWO, WS, WNP, FMA, PF>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
             else
               gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
           } else {

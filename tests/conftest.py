@@ -29,6 +29,20 @@ def ctx():
     c.close()
 
 
+@pytest.fixture()
+def fresh_ctx():
+    """A device context of its own for one test.  The session context may
+    carry a QG stream from an earlier driver test; while one is initialised
+    every advance call joins the extra packet streams at its end
+    (slot_events), so split launches never overlap across calls there — the
+    packet-stream tests and the bench-configuration tests need the bench's own
+    state (no QG stream)."""
+    import swraytracing_amd as sw
+    c = sw.Context(0)
+    yield c
+    c.close()
+
+
 def periodic_grid(nx, L=2 * np.pi):
     xs = np.arange(nx) * (L / nx)
     return np.meshgrid(xs, xs, indexing="ij")

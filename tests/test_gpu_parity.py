@@ -517,6 +517,84 @@ def test_small_shard_bench_field_bitexact(ctx, oracle_lib, N, lanes, cells):
     np.testing.assert_array_equal(kg[idx], ko)
 
 
+@pytest.mark.parametrize("sparse", [1, 2])
+@pytest.mark.parametrize("dt_scale,cell_sort", [(1.0, 0), (40.0, 1)])
+def test_sparse_tiles_bitexact(ctx, oracle_lib, qg_case, sparse, dt_scale, cell_sort):
+    """The two-snapshot tile launch in the dense shape (512 threads, reads
+    one tap ahead) and the sparse shape (256 threads, 256 VGPRs, reads three
+    taps ahead: swrt_set_sparse_tiles 2): the oracle's bits, history frames
+    included; dt x 40 drives packets onto the global fallback gather."""
+    c = qg_case
+    nx, L = c["nx"], c["L"]
+    p0 = _planes(c["flow"])
+    p1 = _planes({n: np.asarray(v) * 0.8 for n, v in c["flow"].items()})
+    p0[5], p1[5] = -p0[2], -p1[2]  # five-sum window
+    ctx.set_field_grid(0, p0, nx, L, 2 * nx)
+    ctx.set_field_grid(1, p1, nx, L, 2 * nx)
+    rng = np.random.default_rng(37)
+    N = 3001
+    x = (rng.random((N, 2)) - 0.5) * L
+    th = rng.random(N) * 2 * np.pi
+    k = 3.0 * np.stack([np.cos(th), np.sin(th)], axis=1)
+    dt = c["dt"] * dt_scale
+    ctx.set_kernel(2)
+    ctx.set_cell_sort(cell_sort)
+    ctx.set_locality(5, 0)
+    ctx.set_sparse_tiles(sparse)
+    try:
+        xg, kg, hxg, hkg = ctx.leapfrog(x, k, dt, 12, c["f"], 1.0, nslots=2, alpha0=0.1, dalpha=0.07,
+                                        bump=orc.BUMP_QG, save_every=3)
+    finally:
+        ctx.set_sparse_tiles(0)
+        ctx.set_cell_sort(0)
+        ctx.set_kernel(0)
+        ctx.set_locality(4, 0)
+    xo, ko, hxo, hko = oracle_lib.leapfrog(p0, p1, 0.1, 0.07, nx, 2 * nx, L / nx, orc.BUMP_QG, x, k, dt, 12,
+                                           c["f"], 1.0, save_every=3)
+    np.testing.assert_array_equal(xg, xo)
+    np.testing.assert_array_equal(kg, ko)
+    np.testing.assert_array_equal(hxg, hxo)
+    np.testing.assert_array_equal(hkg, hko)
+
+
+@pytest.mark.parametrize("N,sparse", [(125_000, 0), (125_000, 1), (400_000, 2)])
+def test_sparse_tiles_bench_field_bitexact(fresh_ctx, oracle_lib, N, sparse):
+    """Strong-scaling shards of the bench ensemble on its device-derived 512^2
+    fields, 5 substeps per call, re-binning every 20 steps, two packet
+    streams: 1.25e5 packets in the automatic (sparse) and the dense shape, and
+    4e5 forced sparse (~390 packets per tile: every lane of a 256-thread
+    workgroup takes two packets) — one shape's bits equal the other's, and a
+    random subset the C oracle's."""
+    import argparse
+    import bench
+    ctx = fresh_ctx
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=1_000_000, world=8, rank=0, seed=146, mode="blend")
+    w = bench.build_workload(ctx, args, 0, N, args.packets)
+    ctx.set_locality(20, 0)
+    ctx.set_sparse_tiles(sparse)
+    ctx.packets_set(w["x"], w["k"])
+    for _ in range(6):
+        bench.step(ctx, w, 5)
+    xg, kg = ctx.packets_get()
+    p0, p1 = ctx.get_field_grid(0), ctx.get_field_grid(1)
+    idx = np.sort(np.random.default_rng(5).choice(N, 2000, replace=False))
+    xo, ko = w["x"][idx], w["k"][idx]
+    for _ in range(6):
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.2, 512, 1024, w["L"] / 512, orc.BUMP_QG, xo, ko,
+                                           w["dt"] / 5, 5, w["f"], w["gH"])
+    np.testing.assert_array_equal(xg[idx], xo)
+    np.testing.assert_array_equal(kg[idx], ko)
+    # the other shape, same calls: the same bits for every packet
+    ctx.set_sparse_tiles(1 if sparse != 1 else 2)
+    ctx.packets_set(w["x"], w["k"])
+    for _ in range(6):
+        bench.step(ctx, w, 5)
+    x2, k2 = ctx.packets_get()
+    assert np.array_equal(xg.view(np.uint64), x2.view(np.uint64))
+    assert np.array_equal(kg.view(np.uint64), k2.view(np.uint64))
+
+
 @pytest.mark.parametrize("variant,tail_split,order", [(2, (0, 0), 1), (2, (32, 0), 1), (2, (1000, 0), 1),
                                                       (2, (16, 16), 1), (2, (0, 1000), 1), (2, (0, 0), 0),
                                                       (2, (16, 0), 0)])
@@ -838,12 +916,13 @@ def test_fma_gather_mode_tolerance(ctx, oracle_lib, n_cells):
     assert not np.array_equal(xf, xo)  # the FMA path really ran
 
 
-def test_packet_streams_bit_identical(ctx, oracle_lib):
+def test_packet_streams_bit_identical(fresh_ctx, oracle_lib):
     """swrt_set_packet_streams(2 / 4): tile launches as two half (four
     quarter) launches on two (four) streams, joined only when something reads
     the packets.  A call sequence that mixes history frames, re-binnings
     inside and between calls, a field rewrite, multi-interval launches, reads
     and ode23 gives the bits of one stream — and the oracle's on a subset."""
+    ctx = fresh_ctx
     import argparse
     import bench
     import swraytracing_amd as sw
@@ -890,11 +969,12 @@ def test_packet_streams_bit_identical(ctx, oracle_lib):
     np.testing.assert_array_equal(out[2][1][idx], ko)
 
 
-def test_packet_streams_long_run_bit_identical(ctx):
+def test_packet_streams_long_run_bit_identical(fresh_ctx):
     """The bench workload (1e6 packets, 5 substeps per call, re-binning every
     20 steps) over 100 calls — 25 re-binnings, each followed by a sort launch
     that gathers its input from any slot while the parts of the split launch
     run on 2 or 4 streams — gives every packet's bits of one stream."""
+    ctx = fresh_ctx
     import argparse
     import bench
     bench._imports()
@@ -918,13 +998,14 @@ def test_packet_streams_long_run_bit_identical(ctx):
 
 
 @pytest.mark.parametrize("substeps,rebin_every,calls", [(5, 20, 10), (1, 4, 12)])
-def test_bench_configuration_subset_bitexact(ctx, oracle_lib, substeps, rebin_every, calls):
+def test_bench_configuration_subset_bitexact(fresh_ctx, oracle_lib, substeps, rebin_every, calls):
     """The headline bench configuration itself (bench.py: 2-layer 512^2 field,
     L = 20, shear 0.5, two snapshots, 1e6 packets, one advance call per PDE
     interval of `substeps` leapfrog steps — the default 5 steps of
     0.05*dx/U0 with re-binning every 20, and the single-step 0.25*dx/U0 form
     with re-binning every 4 — the default kernel): a random subset of 3000
     packets bit-identical to the C oracle on the same device-prepared fields."""
+    ctx = fresh_ctx
     import argparse
     import bench
     bench._imports()

@@ -12,6 +12,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--timeline", type=int, default=0,
+                    help="also print every kernel of the last N steps: start/end (us from the step's update), stream")
     args = ap.parse_args()
     rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
     upd = [i for i, r in enumerate(rows) if "qg_update_kernel" in r["Kernel_Name"]]
@@ -37,6 +39,14 @@ def main():
     chain.sort()
     if chain:
         print(f"  QG chain update -> U0 copy: median {chain[len(chain) // 2]:.1f} us")
+    if args.timeline:
+        tl = rows[upd[-args.timeline - 1]:upd[-1]]
+        z = int(tl[0]["Start_Timestamp"])
+        busy = 0
+        for r in tl:
+            a, b = (int(r["Start_Timestamp"]) - z) / 1e3, (int(r["End_Timestamp"]) - z) / 1e3
+            print(f"  {a:8.1f} {b:8.1f} {b - a:7.1f}  q{r['Queue_Id']:>3s} s{r['Stream_Id']:>3s}  "
+                  f"{r['Kernel_Name'].split('(')[0].replace('void ', '')[:60]}")
 
 
 if __name__ == "__main__":

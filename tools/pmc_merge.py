@@ -15,10 +15,12 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "tile_leapfrog_kernel"
+# PMC_KERNEL: a substring of the kernel name to merge (default: the bench's packet kernel)
+KERNEL = os.environ.get("PMC_KERNEL", "tile_leapfrog_kernel")
 
 
 def config_key(args):
@@ -61,7 +63,10 @@ def main():
     sys.path.insert(0, ROOT)
     from swraytracing_amd._lib import device_code_sha256
     rec["code_object_sha256"] = device_code_sha256()
-    out = {config_key(args): rec}
+    key = config_key(args)
+    if KERNEL != "tile_leapfrog_kernel":
+        key = re.sub(r"\W+", "_", KERNEL).strip("_") + "__" + key
+    out = {key: rec}
     json.dump(out, open(os.path.join(d, "pmc.json"), "w"), indent=1, sort_keys=True)
     print(json.dumps(out))
 
