@@ -426,6 +426,22 @@ int swrt_qg_init(swrt_ctx* ctx, const swrt_qg_params* params, int64_t nx, const 
  * :167-181 with expLdt/expL2dt recomputed on the device whenever dt changes.
  * Before each step the previous qk is kept (prev_qk, :122 / :167). */
 int swrt_qg_step(swrt_ctx* ctx, double dt, int64_t nsteps);
+/* Speculative PDE step (qg2layersw_raytrace.m:152-181 with the CFL rule of
+ * :156-165 decided late): queue the next step with `dt` — the step size the
+ * rule will keep unless U0 of the current qk says otherwise — together with
+ * its post-step transforms and its CFL read-back, before the host has read
+ * the current U0 (swrt_qg_max_speed_result pops read-backs oldest first).
+ * The step is computed into spare buffers; the committed state (qk, history,
+ * t, steps — what swrt_qg_get reports) is untouched until swrt_qg_resolve:
+ * accept (1) makes it the current step, reject (0) drops it and its read-back,
+ * after which the caller steps with the rule's new dt.  An accepted step is
+ * the same computation as swrt_qg_step(dt): bit-identical.  Needs the fused
+ * post-step transforms and, for two layers, dt equal to the dt of the last
+ * step (the exponential propagators are not recomputed).  While one is
+ * pending, swrt_qg_step / _snapshot / _max_speed(_async) fail with
+ * SWRT_ERR_STATE. */
+int swrt_qg_step_speculative(swrt_ctx* ctx, double dt);
+int swrt_qg_resolve(swrt_ctx* ctx, int accept);
 /* 1: steady AB3 steps are replayed from hipGraphs of the step's 9 launches
  * (one per qk buffer parity and dt; re-captured when dt changes).  0
  * (default): plain launches, measured faster on ROCm 7 (73.5 vs 67.5 us per

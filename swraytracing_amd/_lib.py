@@ -97,6 +97,8 @@ SIGNATURES = {
                               ctypes.POINTER(_I)]),
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
+    "swrt_qg_step_speculative": (_INT, [_VP, _D]),
+    "swrt_qg_resolve": (_INT, [_VP, _INT]),
     "swrt_qg_set_graphs": (_INT, [_VP, _INT]),
     "swrt_qg_set_stream": (_INT, [_VP, _INT]),
     "swrt_qg_set_fused": (_INT, [_VP, _INT]),
@@ -550,6 +552,15 @@ class Context:
     def qg_step(self, dt, nsteps=1):
         self._chk(self._L.swrt_qg_step(self._h, float(dt), int(nsteps)), "swrt_qg_step")
 
+    def qg_step_speculative(self, dt):
+        """swrt_qg_step_speculative: the next step with dt, its transforms and CFL read-back queued into
+        spare buffers; the committed state is kept until qg_resolve."""
+        self._chk(self._L.swrt_qg_step_speculative(self._h, float(dt)), "swrt_qg_step_speculative")
+
+    def qg_resolve(self, accept):
+        """swrt_qg_resolve: accept (the speculative step becomes current) or drop it."""
+        self._chk(self._L.swrt_qg_resolve(self._h, int(bool(accept))), "swrt_qg_resolve")
+
     def qg_set_graphs(self, on=False):
         """hipGraph replay of steady AB3 steps (swrt_qg_set_graphs); results identical."""
         self._chk(self._L.swrt_qg_set_graphs(self._h, int(bool(on))), "swrt_qg_set_graphs")
@@ -561,6 +572,7 @@ class Context:
     def qg_set_fused(self, on=True):
         """One batched transform per qk for the step, CFL speed and snapshot (swrt_qg_set_fused)."""
         self._chk(self._L.swrt_qg_set_fused(self._h, int(bool(on))), "swrt_qg_set_fused")
+        self.qg_fused = bool(on)
 
     def qg_max_speed(self):
         u = _D()

@@ -130,17 +130,31 @@ struct QGState {
   double2* Z = nullptr;        // max(2*nl, 3) * nn transform scratch
   double2* T = nullptr;
   unsigned long long* dmax = nullptr;
-  double* hmax = nullptr;      // pinned host copy of dmax (async CFL read-back)
-  hipEvent_t ev = nullptr;     // recorded after that copy
-  bool speed_pending = false;
+  // The CFL read-back (dmax -> pinned host memory + an event): a FIFO of two,
+  // so a speculative step's speed can be queued behind the committed one's.
+  double* hmax = nullptr;      // pinned host copies of dmax, two slots
+  hipEvent_t ev = nullptr;     // recorded after the copy into hmax[0]
+  hipEvent_t ev_b = nullptr;   // ... into hmax[1]
+  int sp_head = 0;             // slot of the next read-back
+  int sp_count = 0;            // read-backs pending (0..2), the oldest at (sp_head - sp_count) & 1
+  // Speculative step (swrt_qg_step_speculative): computed into the spare
+  // buffers from the committed state, which stays untouched until
+  // swrt_qg_resolve accepts it (pointer swaps) or drops it.
+  double2* qk_spare = nullptr;
+  double2* Qm1_spare = nullptr;
+  double2* Qm2_spare = nullptr;
+  bool spec = false;
+  double spec_dt = 0.0, spec_t = 0.0;
+  int64_t spec_steps = 0;
+  const double2* post_of = nullptr;  // the qk whose post-step transforms PZ/PT hold
   // fused mode: the post-step transforms of the current qk — the next step's
   // Jacobian spectrum (PT[0, nn) after its forward FFT), the CFL speed
   // (dmax) and layer 0's grid_U (the snapshot) — from ONE batched inverse
   // 2-D FFT, computed once per qk on first use
   double2* PZ = nullptr;
   double2* PT = nullptr;
-  bool post_valid = false;      // both phases of qg_post done for the current qk
-  bool post_inv_valid = false;  // its first phase (the inverse transforms)
+  bool post_valid = false;      // both phases of qg_post done for post_of (valid for the current qk when
+  bool post_inv_valid = false;  // post_of == qk); post_inv_valid: its first phase (the inverse transforms)
   double exp_dt = -1.0;        // dt of the current E1/E2
   // replayable AB3 steps (hipGraph), one per qk buffer parity, for one dt
   hipGraphExec_t gexec[2] = {nullptr, nullptr};
@@ -286,6 +300,8 @@ struct swrt_ctx {
   int* o_order = nullptr;      // ode23 tile kernel: in-tile cell order of the binned slots
   int64_t o_order_cap = 0;
   bool o_order_valid = false;  // computed for the current binning
+  bool o_sorted = false;       // the packets themselves are in the in-tile cell order of the current binning
+                               // (swrt_ode23_f1's tile_cell_sort_kernel): the stages take them in slot order
   int o_order_split = 0;       // ... and launch shape
   double* o_ynx = nullptr;
   double* o_ynk = nullptr;
@@ -352,16 +368,25 @@ struct OnQGStream {
 // launch boundary, tools/gap_probe.py).
 bool slot_events(const swrt_ctx* c) { return c->qg_sep && c->qg.init; }
 
+// The packet stream waits for the QG stream's pending snapshot writes before
+// the first kernel that reads a slot.  Deferred (swrt_advance / _intervals):
+// the wait is placed by slot_writes_wait() just before the first packet
+// launch, so a re-binning at the start of the call (packet buffers only)
+// runs while the PDE chain is still producing the snapshot.
+void slot_writes_wait(swrt_ctx* c) {
+  if (!c->qg_sep) return;
+  for (Slot& s : c->slot)
+    if (s.wpend) {
+      (void)hipStreamWaitEvent(c->stream, s.wev, 0);
+      s.wpend = false;
+    }
+}
+
 struct SlotUse {
   swrt_ctx* c;
-  explicit SlotUse(swrt_ctx* c_) : c(c_) {
+  explicit SlotUse(swrt_ctx* c_, bool defer_writes = false) : c(c_) {
     c->tail_ev = nullptr;
-    if (!c->qg_sep) return;
-    for (Slot& s : c->slot)
-      if (s.wpend) {
-        (void)hipStreamWaitEvent(c->stream, s.wev, 0);
-        s.wpend = false;
-      }
+    if (!defer_writes) slot_writes_wait(c);
   }
   ~SlotUse() {
     if (!slot_events(c)) return;
@@ -949,6 +974,7 @@ int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
   HIPCHK(c, hipGetLastError());
   c->src_pending = indirect;
   c->o_order_valid = false;
+  c->o_sorted = false;
   c->steps_since_bin = 0;
   c->bin_valid = true;
   c->cells_sorted = false;
@@ -1104,6 +1130,7 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
     a.nsteps = (int)chunk;
     // the launch that ends at a re-binning point also counts the next bins
     const bool count_next = c->rebin_every > 0 && c->steps_since_bin + chunk >= c->rebin_every;
+    slot_writes_wait(c);  // after the re-binning: it reads no slot
     int rc = timed_launch(c, a, grid, count_next);
     if (rc) return rc;
     c->steps_since_bin += chunk;
@@ -1170,6 +1197,7 @@ int run_advance_intervals(swrt_ctx* c, int nint, const double* hs, int64_t nsub,
     a.s0 = 0;
     a.nsteps = (int)nsub;
     const bool count_next = c->steps_since_bin + k * nsub >= c->rebin_every;
+    slot_writes_wait(c);  // after the re-binning: it reads no slot
     int rc = timed_launch(c, a, nblocks(c->n, 256), count_next, &iv);
     if (rc) return rc;
     c->steps_since_bin += k * nsub;
@@ -1299,13 +1327,14 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->qg.qk, (void*)c->qg.qk_prev, (void*)c->qg.Qm1, (void*)c->qg.Qm2, (void*)c->qg.E1,
                   (void*)c->qg.E2, (void*)c->qg.Z, (void*)c->qg.T, (void*)c->qg.dmax, (void*)c->qg.PZ,
-                  (void*)c->qg.PT})
+                  (void*)c->qg.PT, (void*)c->qg.qk_spare, (void*)c->qg.Qm1_spare, (void*)c->qg.Qm2_spare})
     if (p) (void)hipFree(p);
   if (c->qg.hmax) (void)hipHostFree(c->qg.hmax);
   if (c->o_hmax) (void)hipHostFree(c->o_hmax);
   for (hipEvent_t e : c->o_ev)
     if (e) (void)hipEventDestroy(e);
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
+  if (c->qg.ev_b) (void)hipEventDestroy(c->qg.ev_b);
   qg_drop_graphs(c->qg);
   if (c->o_order) (void)hipFree(c->o_order);
   for (void* p : {(void*)c->o_spx, (void*)c->o_spk, (void*)c->o_spF})
@@ -1819,6 +1848,7 @@ int swrt_set_cell_sort(swrt_ctx* c, int every_launch) {
 
 int swrt_qg_set_graphs(swrt_ctx* c, int on) {
   if (!c) return SWRT_ERR_ARG;
+  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   if (on != 0 && on != 1) return fail(c, SWRT_ERR_ARG, "on must be 0 or 1");
   c->qg_graphs = on != 0;
   return SWRT_OK;
@@ -1868,7 +1898,7 @@ int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, in
                  double alpha0, double dalpha, double bump, int64_t save_every) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN_KEEP_SPLIT  // the half launches of the second packet stream stay unjoined across calls
-  SlotUse slot_use(c);
+  SlotUse slot_use(c, true);  // snapshot writes waited for before the first launch (run_advance)
   if (nsteps < 0) return fail(c, SWRT_ERR_ARG, "nsteps < 0");
   if (nslots != 1 && nslots != 2) return fail(c, SWRT_ERR_ARG, "nslots must be 1 or 2");
   if (save_every < 0) return fail(c, SWRT_ERR_ARG, "save_every < 0");
@@ -1898,7 +1928,7 @@ int swrt_advance_intervals(swrt_ctx* c, int nintervals, const double* dts, int64
                            double alpha0, double dalpha, double bump, int64_t save_every) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN_KEEP_SPLIT  // the half launches of the second packet stream stay unjoined across calls
-  SlotUse slot_use(c);
+  SlotUse slot_use(c, true);  // snapshot writes waited for before the first launch (run_advance*)
   if (nintervals < 1 || nintervals > SWRT_MAX_SLOTS - 1)
     return fail(c, SWRT_ERR_ARG, "nintervals must be 1..SWRT_MAX_SLOTS-1");
   if (!dts) return fail(c, SWRT_ERR_ARG, "dts is NULL");
@@ -2504,6 +2534,7 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
 
 int swrt_qg_set_fused(swrt_ctx* c, int on) {
   if (!c) return SWRT_ERR_ARG;
+  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   if (on != 0 && on != 1) return fail(c, SWRT_ERR_ARG, "on must be 0 or 1");
   int rc = swrt_synchronize(c);
   if (rc) return rc;
@@ -2515,6 +2546,7 @@ int swrt_qg_set_fused(swrt_ctx* c, int on) {
 
 int swrt_qg_set_stream(swrt_ctx* c, int separate) {
   if (!c) return SWRT_ERR_ARG;
+  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   if (separate != 0 && separate != 1) return fail(c, SWRT_ERR_ARG, "separate must be 0 or 1");
   int rc = swrt_synchronize(c);
   if (rc) return rc;
@@ -2565,10 +2597,12 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
   HIPCHK(c, hipSetDevice(c->device));
   QGState& q = c->qg;
   for (void* ptr : {(void*)q.qk, (void*)q.qk_prev, (void*)q.Qm1, (void*)q.Qm2, (void*)q.E1, (void*)q.E2,
-                    (void*)q.Z, (void*)q.T, (void*)q.dmax, (void*)q.PZ, (void*)q.PT})
+                    (void*)q.Z, (void*)q.T, (void*)q.dmax, (void*)q.PZ, (void*)q.PT, (void*)q.qk_spare,
+                    (void*)q.Qm1_spare, (void*)q.Qm2_spare})
     if (ptr) (void)hipFree(ptr);
   if (q.hmax) (void)hipHostFree(q.hmax);
   if (q.ev) (void)hipEventDestroy(q.ev);
+  if (q.ev_b) (void)hipEventDestroy(q.ev_b);
   qg_drop_graphs(q);
   q = QGState{};
   const int n = (int)nx, kmax = n / 2 - 1;
@@ -2600,8 +2634,9 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
   HIPCHK(c, hipMalloc(&q.Z, zb));
   HIPCHK(c, hipMalloc(&q.T, zb));
   HIPCHK(c, hipMalloc(&q.dmax, sizeof(unsigned long long)));
-  HIPCHK(c, hipHostMalloc(&q.hmax, sizeof(double)));
+  HIPCHK(c, hipHostMalloc(&q.hmax, 2 * sizeof(double)));
   HIPCHK(c, hipEventCreateWithFlags(&q.ev, hipEventDisableTiming));
+  HIPCHK(c, hipEventCreateWithFlags(&q.ev_b, hipEventDisableTiming));
   if (g.nl == 2) {
     HIPCHK(c, hipMalloc(&q.E1, sizeof(double2) * 4 * q.nhalf));
     HIPCHK(c, hipMalloc(&q.E2, sizeof(double2) * 4 * q.nhalf));
@@ -2632,14 +2667,19 @@ namespace {
 // fused g2k crop + AB3 update from the forward-transformed Jacobian F into
 // qk_prev (out of place: the new qk goes to the other buffer, the old one
 // becomes prev_qk)
-int qg_update_launch(swrt_ctx* c, double dt, int abstep, const double2* F) {
+// The AB3 update of the current qk into qk_out, the tendency history into
+// Qm1_out/Qm2_out (the committed buffers, or a speculative step's spares).
+int qg_update_launch(swrt_ctx* c, double dt, int abstep, const double2* F, double2* qk_out, double2* Qm1_out,
+                     double2* Qm2_out) {
   QGState& q = c->qg;
   if (q.g.nl == 2)
     hipLaunchKernelGGL(qg_update_kernel<2>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, F, q.g, dt,
-                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+                       abstep, q.E1, q.E2, (const double2*)q.qk, qk_out, (const double2*)q.Qm1,
+                       (const double2*)q.Qm2, Qm1_out, Qm2_out);
   else
     hipLaunchKernelGGL(qg_update_kernel<1>, dim3(nblocks(q.nhalf, 256)), dim3(256), 0, c->stream, F, q.g, dt,
-                       abstep, q.E1, q.E2, (const double2*)q.qk, q.qk_prev, q.Qm1, q.Qm2);
+                       abstep, q.E1, q.E2, (const double2*)q.qk, qk_out, (const double2*)q.Qm1,
+                       (const double2*)q.Qm2, Qm1_out, Qm2_out);
   HIPCHK(c, hipGetLastError());
   return SWRT_OK;
 }
@@ -2661,7 +2701,7 @@ int qg_step_launches(swrt_ctx* c, double dt, int abstep) {
   hipLaunchKernelGGL(qg_jacobian_kernel, dim3(nblocks(q.nn, 256)), dim3(256), 0, c->stream, q.T, nl, q.nn, Zj);
   HIPCHK(c, hipGetLastError());
   if ((rc = transform_2d(c, Zj, q.T, n, 1, 0))) return rc;  // along x, then y: [ky + n*kx]
-  return qg_update_launch(c, dt, abstep, q.T);
+  return qg_update_launch(c, dt, abstep, q.T, q.qk_prev, q.Qm1, q.Qm2);
 }
 
 // Post-step transforms of the current qk (fused mode), see QGState::PZ.
@@ -2673,7 +2713,9 @@ int qg_step_launches(swrt_ctx* c, double dt, int abstep) {
 // behind the second phase.
 int qg_post_inverse(swrt_ctx* c) {
   QGState& q = c->qg;
-  if (q.post_inv_valid) return SWRT_OK;
+  if (q.post_inv_valid && q.post_of == q.qk) return SWRT_OK;
+  q.post_valid = false;
+  q.post_of = q.qk;
   const int n = q.g.n, nl = q.g.nl;
   const int nb = 2 * nl + (nl - 1) + 3;  // Jacobian inputs | layer-1 u+iv | layer-0 grid_U (u+iv first)
   if (!q.PZ) {
@@ -2717,7 +2759,7 @@ int qg_post_inverse(swrt_ctx* c) {
 
 int qg_post(swrt_ctx* c) {
   QGState& q = c->qg;
-  if (q.post_valid) return SWRT_OK;
+  if (q.post_valid && q.post_of == q.qk) return SWRT_OK;
   int rc;
   if ((rc = qg_post_inverse(c))) return rc;
   const int n = q.g.n, nl = q.g.nl;
@@ -2794,6 +2836,7 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   if (!(dt > 0) || nsteps < 0) return fail(c, SWRT_ERR_ARG, "dt must be > 0, nsteps >= 0");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
@@ -2808,7 +2851,7 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
     const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
     if (c->qg_fused) {
       if ((rc = qg_post(c))) return rc;
-      rc = qg_update_launch(c, dt, abstep, q.PT);
+      rc = qg_update_launch(c, dt, abstep, q.PT, q.qk_prev, q.Qm1, q.Qm2);
     } else if (abstep == 3 && c->qg_graphs) {
       rc = qg_step_graphed(c, dt);
     } else {
@@ -2827,17 +2870,94 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
 }
 
 namespace {
+int qg_speed_launch(swrt_ctx* c);
+}  // namespace
+
+int swrt_qg_step_speculative(swrt_ctx* c, double dt) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  OnQGStream on_qg(c);
+  QGState& q = c->qg;
+  if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (q.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is already pending");
+  if (!c->qg_fused) return fail(c, SWRT_ERR_STATE, "speculative steps need the fused post-step transforms");
+  if (!(dt > 0)) return fail(c, SWRT_ERR_ARG, "dt must be > 0");
+  if (q.g.nl == 2 && dt != q.exp_dt)
+    return fail(c, SWRT_ERR_STATE, "a speculative step takes the dt of the exponential propagators in place");
+  if (q.sp_count >= 2) return fail(c, SWRT_ERR_STATE, "two CFL read-backs already pending");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_twiddles(c, q.g.n))) return rc;
+  const size_t hb = sizeof(double2) * (size_t)q.g.nl * (size_t)q.nhalf;
+  for (double2** b : {&q.qk_spare, &q.Qm1_spare, &q.Qm2_spare})
+    if (!*b) HIPCHK(c, hipMalloc(b, hb));
+  const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
+  if ((rc = qg_post(c))) return rc;  // of the committed qk (valid when the caller read its speed)
+  if ((rc = qg_update_launch(c, dt, abstep, q.PT, q.qk_spare, q.Qm1_spare, q.Qm2_spare))) return rc;
+  // the post-step transforms and CFL read-back of the speculative qk
+  double2* committed = q.qk;
+  q.qk = q.qk_spare;
+  rc = qg_speed_launch(c);
+  q.qk = committed;
+  if (rc) return rc;
+  q.spec = true;
+  q.spec_dt = dt;
+  q.spec_steps = q.steps + 1;
+  q.spec_t = q.t + dt;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_qg_resolve(swrt_ctx* c, int accept) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  OnQGStream on_qg(c);
+  QGState& q = c->qg;
+  if (!q.spec) return fail(c, SWRT_ERR_STATE, "no speculative QG step pending");
+  if (accept) {
+    // the committed qk becomes the previous one, the speculative one current
+    double2* old_prev = q.qk_prev;
+    q.qk_prev = q.qk;
+    q.qk = q.qk_spare;
+    q.qk_spare = old_prev;
+    std::swap(q.Qm1, q.Qm1_spare);
+    std::swap(q.Qm2, q.Qm2_spare);
+    q.steps = q.spec_steps;
+    q.t = q.spec_t;
+    q.has_prev = true;
+    qg_drop_graphs(q);  // captured for the committed buffers
+  } else {
+    // its CFL read-back (the newest pending) is dropped; PZ/PT hold its
+    // post-step transforms, so the committed qk's are recomputed on use
+    q.sp_head ^= 1;
+    q.sp_count -= 1;
+  }
+  q.spec = false;
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+namespace {
+// dmax -> the next FIFO slot of pinned host memory, and its event
+int qg_speed_copy(swrt_ctx* c) {
+  QGState& q = c->qg;
+  const int slot = q.sp_head;
+  HIPCHK(c, hipMemcpyAsync(q.hmax + slot, q.dmax, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipEventRecord(slot ? q.ev_b : q.ev, c->stream));
+  q.sp_head ^= 1;
+  q.sp_count += 1;
+  return SWRT_OK;
+}
+
 // grid_U speed of the current qk -> device max -> pinned host copy + event
 int qg_speed_launch(swrt_ctx* c) {
   QGState& q = c->qg;
   int rc;
   const int n = q.g.n, nl = q.g.nl;
+  if (q.sp_count >= 2) return fail(c, SWRT_ERR_STATE, "two CFL read-backs already pending");
   if (c->qg_fused) {  // the speed comes with the post-step transforms
     if ((rc = qg_post(c))) return rc;
-    HIPCHK(c, hipMemcpyAsync(q.hmax, q.dmax, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipEventRecord(q.ev, c->stream));
-    q.speed_pending = true;
-    return SWRT_OK;
+    return qg_speed_copy(c);
   }
   if ((rc = ensure_twiddles(c, n))) return rc;
   if (nl == 2)
@@ -2851,17 +2971,16 @@ int qg_speed_launch(swrt_ctx* c) {
   HIPCHK(c, hipMemsetAsync(q.dmax, 0, sizeof(unsigned long long), c->stream));
   hipLaunchKernelGGL(qg_max_speed2_kernel, dim3(256), dim3(256), 0, c->stream, q.T, q.nn * nl, q.g.shear, q.dmax);
   HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipMemcpyAsync(q.hmax, q.dmax, sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipEventRecord(q.ev, c->stream));
-  q.speed_pending = true;
-  return SWRT_OK;
+  return qg_speed_copy(c);
 }
 
+// the oldest pending read-back (FIFO)
 int qg_speed_wait(swrt_ctx* c, double* U0_out) {
   QGState& q = c->qg;
-  HIPCHK(c, hipEventSynchronize(q.ev));
-  q.speed_pending = false;
-  *U0_out = std::sqrt(*q.hmax);  // bits of a non-negative double: the max of (u+shear)^2 + v^2
+  const int slot = (q.sp_head - q.sp_count) & 1;
+  HIPCHK(c, hipEventSynchronize(slot ? q.ev_b : q.ev));
+  q.sp_count -= 1;
+  *U0_out = std::sqrt(q.hmax[slot]);  // bits of a non-negative double: the max of (u+shear)^2 + v^2
   return SWRT_OK;
 }
 }  // namespace
@@ -2873,10 +2992,13 @@ int swrt_qg_max_speed(swrt_ctx* c, double* U0_out) {
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   if (!U0_out) return fail(c, SWRT_ERR_ARG, "NULL output");
+  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   if ((rc = qg_speed_launch(c))) return rc;
-  return qg_speed_wait(c, U0_out);
+  while (q.sp_count > 0)  // the last one popped is this call's (earlier pending ones are superseded)
+    if ((rc = qg_speed_wait(c, U0_out))) return rc;
+  return SWRT_OK;
   GUARD_END(c)
 }
 
@@ -2885,6 +3007,7 @@ int swrt_qg_max_speed_async(swrt_ctx* c) {
   GUARD_BEGIN
   OnQGStream on_qg(c);
   if (!c->qg.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   HIPCHK(c, hipSetDevice(c->device));
   return qg_speed_launch(c);
   GUARD_END(c)
@@ -2894,7 +3017,7 @@ int swrt_qg_max_speed_result(swrt_ctx* c, double* U0_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
   OnQGStream on_qg(c);
-  if (!c->qg.speed_pending) return fail(c, SWRT_ERR_STATE, "no swrt_qg_max_speed_async pending");
+  if (c->qg.sp_count == 0) return fail(c, SWRT_ERR_STATE, "no swrt_qg_max_speed_async pending");
   if (!U0_out) return fail(c, SWRT_ERR_ARG, "NULL output");
   return qg_speed_wait(c, U0_out);
   GUARD_END(c)
@@ -2955,6 +3078,7 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (current) or 1 (previous)");
   if (which == 1 && !q.has_prev) return fail(c, SWRT_ERR_STATE, "no previous qk before the first step");
   if (layer < 0 || layer >= q.g.nl) return fail(c, SWRT_ERR_ARG, "layer out of range");
@@ -3125,8 +3249,11 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
     unsigned extra = 0;
     a.split = launch_shape(c, ntiles, &extra);
     const unsigned grid = ntiles + extra;
-    // in-tile cell order of this binning, once (swrt_ode23.hpp)
-    if (!c->o_order_valid || c->o_order_split != a.split) {
+    // in-tile cell order of this binning, once (swrt_ode23.hpp): the packets'
+    // own order after swrt_ode23_f1's sort, else an order array
+    if (c->o_sorted && c->o_order_split == a.split) {
+      a.order = nullptr;
+    } else if (!c->o_order_valid || c->o_order_split != a.split) {
       if (c->o_order_cap < c->cap) {
         if (c->o_order) (void)hipFree(c->o_order);
         c->o_order = nullptr;
@@ -3139,8 +3266,10 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
       HIPCHK(c, hipGetLastError());
       c->o_order_valid = true;
       c->o_order_split = a.split;
+      a.order = c->o_order;
+    } else {
+      a.order = c->o_order;
     }
-    a.order = c->o_order;
     const bool v5 = c->slot[0].div_free && (a.nslots == 1 || c->slot[1].div_free);
     if (a.nslots == 2) {
       if (v5) ode23_tile_launch<STAGE, true, true>(c, a, grid, starts, ntx);
@@ -3179,6 +3308,23 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
   // error norm is a max over all components)
   if (c->rebin_every > 0 && c->slot[0].set) {
     if ((rc = rebin(c, false, use_tile_kernel(c) ? kTile : 0))) return rc;  // the ode23 tile kernel's 16x16 tiles
+    const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
+    if (use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx * ntx) {
+      // the in-tile cell order applied to the packets (swrt_ode23.hpp tile_cell_sort_kernel)
+      unsigned extra = 0;
+      const int split = launch_shape(c, (unsigned)(ntx * ntx), &extra);
+      const FieldView v = view_of(c->slot[0]);
+      hipLaunchKernelGGL((tile_cell_sort_kernel<kTile, kTileThreads>), dim3((unsigned)(ntx * ntx) + extra),
+                         dim3(kTileThreads), 0, c->stream, (const double*)c->dx, (const double*)c->dk,
+                         (const int*)c->perm, c->n, (const int*)(c->bins + 2 * kMaxBins), split, ntx, v.inv_dx,
+                         (int)v.nx, c->dx2, c->dk2, c->perm2);
+      HIPCHK(c, hipGetLastError());
+      std::swap(c->dx, c->dx2);
+      std::swap(c->dk, c->dk2);
+      std::swap(c->perm, c->perm2);
+      c->o_sorted = true;
+      c->o_order_split = split;
+    }
   }
   Ode23Args a;
   if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;

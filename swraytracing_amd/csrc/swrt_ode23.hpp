@@ -193,6 +193,79 @@ __global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, in
   }
 }
 
+// The ode23 calls' in-tile cell order applied to the packets themselves:
+// tile_cell_order_kernel's counting sort, with each packet's state (x, k and
+// its original index) copied to its sorted slot of the spare buffers instead
+// of writing an order array.  The stages then read y and F1 and write ynew
+// and F4 at contiguous slots (through order[] every 8-byte access was
+// scattered: 250 MB of writes per 1e6-packet attempt for 64 MB of outputs,
+// profiles/r04_ode23).  Order only: results do not depend on it.
+template <int T, int NT>
+__global__ void __launch_bounds__(NT) tile_cell_sort_kernel(const double* x, const double* k, const int* perm,
+                                                            int64_t n, const int* starts, int split, int ntx,
+                                                            double inv_dx, int nx, double* x_out, double* k_out,
+                                                            int* perm_out) {
+  constexpr int NB = T * T;
+  constexpr int MAXB = 2 * NT;
+  __shared__ int hist[NB];
+  __shared__ int kr[MAXB];
+  int pbeg, pend;
+  const int tile = wg_work_range(starts, nullptr, split, pbeg, pend);
+  const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
+  const int tid = threadIdx.x;
+  for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
+    const int nb = min(MAXB, pend - b0);
+    for (int h = tid; h < NB; h += NT) hist[h] = 0;
+    __syncthreads();
+    for (int i = tid; i < nb; i += NT) {
+      const int64_t p = b0 + i;
+      const int dx_ = min(max(ring_diff(fast_cell(x[p], inv_dx, nx), ox, nx), 0), T - 1);
+      const int dy_ = min(max(ring_diff(fast_cell(x[n + p], inv_dx, nx), oy, nx), 0), T - 1);
+      int key = 0;
+#pragma unroll
+      for (int bit = 0; (1 << bit) < T; ++bit)
+        key |= ((dy_ >> bit) & 1) << (2 * bit) | ((dx_ >> bit) & 1) << (2 * bit + 1);
+      kr[i] = (key << 16) | atomicAdd(&hist[key], 1);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the NB bins by one wavefront
+      constexpr int PER = (NB + 63) / 64;
+      int loc[PER];
+      int sum = 0;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int h = tid * PER + q;
+        loc[q] = h < NB ? hist[h] : 0;
+        sum += loc[q];
+      }
+      int incl = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int v = __shfl_up(incl, off, 64);
+        if (tid >= off) incl += v;
+      }
+      int run = incl - sum;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int h = tid * PER + q;
+        if (h < NB) hist[h] = run;
+        run += loc[q];
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < nb; i += NT) {
+      const int v = kr[i];
+      const int64_t src = b0 + i, dst = b0 + hist[v >> 16] + (v & 0xffff);
+      x_out[dst] = x[src];
+      x_out[n + dst] = x[n + src];
+      k_out[dst] = k[src];
+      k_out[n + dst] = k[n + src];
+      perm_out[dst] = perm[src];
+    }
+    __syncthreads();
+  }
+}
+
 // The same four stages over spatially binned packets, one workgroup per
 // T x T-cell tile (half-tile workgroups at the end of each XCD band) with the
 // field window of both snapshots in LDS — the leapfrog tile kernel's window:
@@ -348,7 +421,7 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
       continue;
     }
     tile_rhs<TWO, T, M, WS, WNP, V5>(a, win, ox, oy, nx, alpha, ys, fo);
-    double* Fo = a.F[STAGE - 1];
+    double* Fo = a.F[STAGE > 0 ? STAGE - 1 : 0];  // (STAGE 0 returned above)
 #pragma unroll
     for (int c = 0; c < 4; ++c) Fo[c * n + p] = fo[c];
     if constexpr (STAGE == 1) {

@@ -242,9 +242,13 @@ __device__ __forceinline__ void mmul2(const double2* E, int64_t idx, const cd x[
 //   dq = dt*Qn | dt/2*(3Qn - X1) | dt/12*(23Qn - 16X1 + 5X2), X = Qm (1 layer)
 //   or mmult3(expL(2)dt, Qm) (2 layers); then Qm2 = Qm1, Qm1 = Qn.
 template <int NL>
+// Qm1/Qm2 are read, and the shifted history (Qm2 <- Qm1, Qm1 <- Qn) written
+// to Qm1_out/Qm2_out: the same buffers for a committed step, spare ones for
+// a speculative step (swrt_qg_step_speculative), which must leave the
+// committed state intact until it is accepted.
 __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev g, double dt, int abstep, const double2* E1,
-                                 const double2* E2, const double2* qk, double2* qk_out, double2* Qm1,
-                                 double2* Qm2) {
+                                 const double2* E2, const double2* qk, double2* qk_out, const double2* Qm1,
+                                 const double2* Qm2, double2* Qm1_out, double2* Qm2_out) {
   const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t nhalf = (int64_t)nkx * (kmax + 1);
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -313,8 +317,8 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
   }
   _Pragma("unroll") for (int l = 0; l < NL; ++l) {
     st(qk_out, l * nhalf + idx, out[l]);
-    st(Qm2, l * nhalf + idx, m1[l]);
-    st(Qm1, l * nhalf + idx, Qn[l]);
+    st(Qm2_out, l * nhalf + idx, m1[l]);
+    st(Qm1_out, l * nhalf + idx, Qn[l]);
   }
 }
 

@@ -61,6 +61,14 @@ class QGModel:
     def step(self, dt, nsteps=1):
         self.ctx.qg_step(dt, nsteps)
 
+    def step_speculative(self, dt):
+        """Queue the next step with dt and its CFL read-back before the current
+        U0 is known; the committed state stays until resolve()."""
+        self.ctx.qg_step_speculative(dt)
+
+    def resolve(self, accept):
+        self.ctx.qg_resolve(accept)
+
     def max_speed(self):
         """U0 = sqrt(max(u.^2 + v.^2)) of grid_U(qk) (all layers, u + shear)."""
         return self.ctx.qg_max_speed()
@@ -206,8 +214,15 @@ class TwoLayerLoop:
     end-to-end driver-step figure."""
 
     def __init__(self, model, ens, dt, U0, cfl_fraction=0.25, packet_delay=0.0, nsub=5, packet_intervals=1,
-                 integrator="leapfrog", log=None):
+                 integrator="leapfrog", log=None, speculate=True):
         self.model, self.ens, self.dt, self.U0 = model, ens, dt, U0
+        # speculate: each step also queues the NEXT PDE step with this step's
+        # dt (swrt_qg_step_speculative) before waiting for this step's U0, so
+        # the QG stream never idles through the host's read-back and CFL rule;
+        # the rule then accepts it, or drops it and steps with its new dt —
+        # the same computation either way (bit-identical files)
+        self.speculate = speculate
+        self._spec = False
         self.cfl_fraction, self.packet_delay = cfl_fraction, packet_delay
         self.nx = model.nx
         self.t = 0.0
@@ -224,9 +239,17 @@ class TwoLayerLoop:
         if changed and self.log is not None:
             self.log(f"CFL condition not met, max|u|={self.U0:f}, new dt={self.dt:f}\n")
         self.dts.append(self.dt)
-        self.model.step(self.dt)
+        if self._spec:
+            # the step queued by the previous call with the previous dt
+            self.model.resolve(not changed)
+            self._spec = False
+            if changed:
+                self.model.step(self.dt)
+                self.model.max_speed_async()
+        else:
+            self.model.step(self.dt)
+            self.model.max_speed_async()
         self.t = self.t + self.dt
-        self.model.max_speed_async()
         active = self.ens is not None and self.t > self.packet_delay
         if active:
             ny = 2 * self.nx
@@ -237,12 +260,22 @@ class TwoLayerLoop:
             self.group.add(self.dt)
         else:
             self.have_cur = False
-        self.U0 = self.model.max_speed_result()
+        if self.speculate and self.model.params.nlayers == 2 and getattr(self.model.ctx, "qg_fused", True):
+            self.model.step_speculative(self.dt)
+            self._spec = True
+        self.U0 = self.model.max_speed_result()  # this step's (read-backs pop oldest first)
         return active
 
     def flush(self):
         if self.group is not None:
             self.group.flush()
+
+    def settle(self):
+        """Drop a pending speculative step: the model stays at the committed
+        step (for PDE calls outside the loop after it)."""
+        if self._spec:
+            self.model.resolve(False)
+            self._spec = False
 
 
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
@@ -391,6 +424,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
             frames += 1
         log.progress(loop.steps, Nsteps)
     loop.flush()
+    loop.settle()
     ctx.synchronize()
     log.finish()
     log.close()
