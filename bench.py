@@ -222,7 +222,7 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
                             bump=sw.BUMP_QG, ctx=ctx)
     U0 = model.max_speed()
     loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
-                           integrator=integrator)
+                           integrator=integrator, speculate=bool(args.speculate))
     # AB1/AB2 start-up and first-use allocations: the snapshot renaming (qg.py
     # TwoLayerLoop) allocates its spare slot buffers during the first steps, a
     # hipMalloc each — outside the timed steps
@@ -268,7 +268,8 @@ def pde_alone(ctx, w, args, dev, nsteps=None):
     qk = np.stack([w["qk1"], -w["qk1"]], axis=2)
     model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
     U0 = model.max_speed()
-    loop = sw.TwoLayerLoop(model, None, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps)
+    loop = sw.TwoLayerLoop(model, None, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
+                           speculate=bool(args.speculate))
     for _ in range(args.driver_warmup):
         loop.step()
     ctx.synchronize()
@@ -289,7 +290,7 @@ def driver_forecast(ctx, w, args, dev, n_total, full):
     alone and the packets alone (strong_scaling_forecast) beside it, `bound`
     names the term that sets the step: the PDE when its own step time exceeds
     the packets'."""
-    pde_ms = pde_alone(ctx, w, args, dev)
+    pde_ms = pde_alone(ctx, w, args, dev, nsteps=args.forecast_driver_steps)
     out = {"pde_alone_ms": pde_ms,
            "what": "TwoLayerLoop.step with 1e6/G packets on one GPU (full replicated 2-layer PDE + snapshot + "
                    f"{args.substeps} leapfrog substeps); pde_alone_ms: the same loop without packets"}
@@ -297,7 +298,7 @@ def driver_forecast(ctx, w, args, dev, n_total, full):
     for G in (2, 4, 8):
         n = -(-n_total // G)
         ws = dict(w, x=w["x"][:n], k=w["k"][:n])
-        d = driver_step(ctx, ws, args, dev, False, n)
+        d = driver_step(ctx, ws, args, dev, False, n, nsteps=args.forecast_driver_steps)
         r = {"packets_per_gpu": n, "ms_per_pde_step": d["ms_per_pde_step"],
              "value_1gpu": d["packet_steps_per_s"], "forecast_value": G * d["packet_steps_per_s"],
              "efficiency": d["packet_steps_per_s"] / rate_full}
@@ -454,8 +455,12 @@ def parse_args(argv=None):
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
-    ap.add_argument("--driver-steps", type=int, default=20,
+    ap.add_argument("--driver-steps", type=int, default=50,
                     help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
+    ap.add_argument("--speculate", type=int, default=1, choices=[0, 1],
+                    help="driver steps: queue the next PDE step before reading U0 (TwoLayerLoop speculate)")
+    ap.add_argument("--forecast-driver-steps", type=int, default=100,
+                    help="timed driver steps per shard size in driver_step_forecast")
     ap.add_argument("--driver-warmup", type=int, default=16,
                     help="untimed driver steps before the timed ones (start-up, spare snapshot buffers)")
     ap.add_argument("--ode23-steps", type=int, default=4,

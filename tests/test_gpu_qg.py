@@ -614,5 +614,5 @@ def test_qg2_speculative_steps_bit_identical(fresh_ctx):
     assert a[4] == b[4] and len(set(a[4])) >= 2  # dts, with a change
     assert a[5] == b[5]  # U0 per step
     for u, v in zip(a[:4], b[:4]):
-        assert np.array_equal(np.asarray(u).view(np.uint64), np.asarray(v).view(np.uint64))
+        assert np.ascontiguousarray(u).tobytes() == np.ascontiguousarray(v).tobytes()
     assert a[6] == b[6] and a[7] == b[7] == 12
