@@ -457,6 +457,8 @@ def parse_args(argv=None):
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
     ap.add_argument("--driver-steps", type=int, default=50,
                     help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
+    ap.add_argument("--qg-jfuse", type=int, default=1, choices=[0, 1],
+                    help="2-layer PDE: inverse column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE; same bits)")
     ap.add_argument("--speculate", type=int, default=1, choices=[0, 1],
                     help="driver steps: queue the next PDE step before reading U0 (TwoLayerLoop speculate)")
     ap.add_argument("--forecast-driver-steps", type=int, default=100,
@@ -621,6 +623,7 @@ def main(argv=None):
     ctx.set_lanes_per_packet(args.lanes_per_packet)
     ctx.set_tile_cells(args.tile_cells)
     ctx.set_sparse_tiles(args.sparse_tiles)
+    ctx.debug_set(sw._lib.DEBUG_QG_JFUSE, args.qg_jfuse)
     ctx.set_packet_streams(args.packet_streams)
     ctx.set_gather_mode(args.gather_mode)
     if args.tail_split >= 0:

@@ -528,11 +528,16 @@ int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launch
  *   third packet buffers (the launch after a source-gather sort launch
  *   overwrites the buffer that launch gathers from) — a known race the
  *   checker must report.
- * SWRT_DEBUG_HAZARD_CHECKS (get only): accesses the checker has compared. */
+ * SWRT_DEBUG_HAZARD_CHECKS (get only): accesses the checker has compared.
+ * SWRT_DEBUG_QG_JFUSE 0/1 (default 1): two-layer fused mode runs the inverse
+ *   column pass fused with the Jacobian, the CFL max and J's first forward
+ *   pass (one kernel); 0 = the separate column pass + Jacobian-rows kernel —
+ *   the same values, kept so tests can compare them bit for bit. */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3
 #define SWRT_DEBUG_HAZARD_CHECKS 4
+#define SWRT_DEBUG_QG_JFUSE 5
 int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
 int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
 

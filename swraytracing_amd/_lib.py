@@ -125,6 +125,7 @@ DEBUG_HAZARD_CHECK = 1
 DEBUG_SPIN_US = 2
 DEBUG_LEGACY_PARK = 3
 DEBUG_HAZARD_CHECKS = 4
+DEBUG_QG_JFUSE = 5
 
 _lib = None
 

@@ -147,6 +147,8 @@ struct QGState {
   double spec_dt = 0.0, spec_t = 0.0;
   int64_t spec_steps = 0;
   const double2* post_of = nullptr;  // the qk whose post-step transforms PZ/PT hold
+  bool post_jrows = false;     // phase 1 ran fft_cols_jacobian2_kernel: J's first forward pass is in PT[0, nn)
+  const double2* Fj = nullptr; // where qg_post left the spectrum of J (the update's input)
   // fused mode: the post-step transforms of the current qk — the next step's
   // Jacobian spectrum (PT[0, nn) after its forward FFT), the CFL speed
   // (dmax) and layer 0's grid_U (the snapshot) — from ONE batched inverse
@@ -199,6 +201,7 @@ struct swrt_ctx {
   hipStream_t qstream = nullptr;
   bool qg_sep = true;
   bool qg_fused = true;  // swrt_qg_set_fused
+  bool qg_jfuse = true;  // fused mode, 2 layers: the column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE)
   std::vector<Slot> spares;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
@@ -2516,6 +2519,13 @@ int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
       if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "legacy park must be 0 or 1");
       c->debug_legacy_park = value != 0;
       return SWRT_OK;
+    case SWRT_DEBUG_QG_JFUSE:
+      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG column/Jacobian fusion must be 0 or 1");
+      if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
+      c->qg_jfuse = value != 0;
+      c->qg.post_valid = false;
+      c->qg.post_inv_valid = false;
+      return SWRT_OK;
     default:
       return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
@@ -2528,6 +2538,7 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_SPIN_US: *value_out = c->debug_spin_us; return SWRT_OK;
     case SWRT_DEBUG_LEGACY_PARK: *value_out = c->debug_legacy_park ? 1 : 0; return SWRT_OK;
     case SWRT_DEBUG_HAZARD_CHECKS: *value_out = c->hz.checks; return SWRT_OK;
+    case SWRT_DEBUG_QG_JFUSE: *value_out = c->qg_jfuse ? 1 : 0; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
 }
@@ -2741,7 +2752,17 @@ int qg_post_inverse(swrt_ctx* c) {
       hipLaunchKernelGGL(qg_post_rows_kernel<1>, dim3((unsigned)n), dim3(nb * n / 4), lds, c->stream,
                          (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
     HIPCHK(c, hipGetLastError());
-    launch_fft<true>(c, q.PZ, q.PT, n, logn, nb * n, 1);
+    if (nl == 2 && n % 8 == 0 && c->qg_jfuse) {
+      // the column pass fused with the Jacobian, the CFL max and J's first
+      // forward pass (swrt_fft.hpp): planes 0-4 stay on chip; J -> PT[0, nn)
+      hipLaunchKernelGGL(fft_cols_jacobian2_kernel, dim3(2 * (unsigned)n), dim3(n), sizeof(double2) * 4 * (n + 1),
+                         c->stream, (const double2*)q.PZ, q.PT, q.PT, n, logn, q.g.shear, q.dmax,
+                         (const double2*)c->tw);
+      q.post_jrows = true;
+    } else {
+      launch_fft<true>(c, q.PZ, q.PT, n, logn, nb * n, 1);
+      q.post_jrows = false;
+    }
     HIPCHK(c, hipGetLastError());
   } else {
     if (nl == 2)
@@ -2752,6 +2773,7 @@ int qg_post_inverse(swrt_ctx* c) {
                          q.PZ, uv, uv, q.dmax);
     HIPCHK(c, hipGetLastError());
     if ((rc = inverse_2d(c, q.PZ, q.PT, n, nb))) return rc;
+    q.post_jrows = false;
   }
   q.post_inv_valid = true;
   return SWRT_OK;
@@ -2767,7 +2789,15 @@ int qg_post(swrt_ctx* c) {
   // Jacobian and the CFL speed over every layer's u + i v (layer 1, then
   // layer 0: contiguous); the spectrum of J then lands in PT[0, nn)
   const double2* uvT = q.PT + 2 * nl * q.nn;
-  if (n <= 1024) {
+  q.Fj = q.PT;
+  if (q.post_jrows) {
+    // J's first pass came with the inverse column pass: its second pass only
+    int logn = 0;
+    while ((1 << logn) < n) ++logn;
+    launch_fft<true>(c, q.PT, q.PZ, n, logn, n, 0);
+    HIPCHK(c, hipGetLastError());
+    q.Fj = q.PZ;
+  } else if (n <= 1024) {
     // J computed in the load of the forward transform's first pass (same
     // values, same per-vector FFT as the separate kernel + transform_2d)
     int logn = 0;
@@ -2851,7 +2881,7 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
     const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
     if (c->qg_fused) {
       if ((rc = qg_post(c))) return rc;
-      rc = qg_update_launch(c, dt, abstep, q.PT, q.qk_prev, q.Qm1, q.Qm2);
+      rc = qg_update_launch(c, dt, abstep, q.Fj, q.qk_prev, q.Qm1, q.Qm2);
     } else if (abstep == 3 && c->qg_graphs) {
       rc = qg_step_graphed(c, dt);
     } else {
@@ -2893,7 +2923,7 @@ int swrt_qg_step_speculative(swrt_ctx* c, double dt) {
     if (!*b) HIPCHK(c, hipMalloc(b, hb));
   const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
   if ((rc = qg_post(c))) return rc;  // of the committed qk (valid when the caller read its speed)
-  if ((rc = qg_update_launch(c, dt, abstep, q.PT, q.qk_spare, q.Qm1_spare, q.Qm2_spare))) return rc;
+  if ((rc = qg_update_launch(c, dt, abstep, q.Fj, q.qk_spare, q.Qm1_spare, q.Qm2_spare))) return rc;
   // the post-step transforms and CFL read-back of the speculative qk
   double2* committed = q.qk;
   q.qk = q.qk_spare;

@@ -248,6 +248,90 @@ __global__ void __launch_bounds__(1024) fft_jacobian_rows_kernel(const double2* 
   for (int k = 0; k < 4; ++k) Zj[row + b + k * quarter] = x[b + k * quarter];
 }
 
+// Two-layer fused mode: the second pass of the post-step inverse transforms
+// fused with what reads its first five planes (n <= 1024).  Workgroup (y, h):
+//   h = 0: the column pass (along x) of the four Jacobian-input planes 0-3 at
+//          y, J1 + i J2 from them (the values fft_jacobian_rows_kernel
+//          forms from the pass's output) and the forward pass of J along x
+//          into Zj's row y;
+//   h = 1: the column pass of planes 4-7 at y, the CFL max of
+//          (u + shear)^2 + v^2 over planes 4, 5 (layer 1's and layer 0's
+//          u + iv) and planes 5-7 (layer 0's grid_U, the snapshot) written
+//          to `out` in the pass's layout [x + n*y].
+// Planes 0-4 of the inverse transform never go to memory (20 MB at 512^2,
+// and the Jacobian pass's 25 MB of reads).  Same per-vector FFTs and element
+// operations in the same order as the column pass + fft_jacobian_rows_kernel:
+// the same bits.  Block b: XCD b % 8 walks a contiguous range of y, both
+// halves of one y adjacent, so the 8 columns of each 128-B line are read by
+// workgroups of one XCD (one L2).  blockDim = n (4 vectors of n/4 lanes),
+// dynamic LDS 4*(n+1) double2.  Zj must not alias `in` (other workgroups are
+// still reading their columns).
+__global__ void __launch_bounds__(1024) fft_cols_jacobian2_kernel(const double2* in, double2* out, double2* Zj,
+                                                                  int n, int logn, double shear,
+                                                                  unsigned long long* dmax, const double2* tw) {
+  extern __shared__ double2 sbuf[];
+  __shared__ unsigned long long bmax;
+  const int quarter = n >> 2, t = threadIdx.x;
+  const int ld = n + 1;
+  const int64_t nn = (int64_t)n * n;
+  const int xcd = (int)(blockIdx.x & 7), j = (int)(blockIdx.x >> 3);
+  const int y = xcd * (n >> 3) + (j >> 1), h = j & 1;
+  if (t == 0) bmax = 0ull;
+  // lanes 4*jr .. 4*jr + 3 read row jr's four planes (4 loads per lane per row block)
+  {
+    const int c = t & 3, j0 = t >> 2;
+    const double2* src = in + (int64_t)(4 * h + c) * nn + y;
+    double2 r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = src[(int64_t)(j0 + k * quarter) * n];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sbuf[c * ld + j0 + k * quarter] = r[k];
+  }
+  __syncthreads();
+  const int col = t / quarter, b = t - col * quarter;
+  fft_stages_one_buffer(sbuf + col * ld, b, n, logn, tw, 1);
+  if (h == 0) {
+    // J at the lane's four x of vector 0 (in place: each x read and written by one lane)
+    double2* x0 = sbuf;
+    if (col == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = b + k * quarter;
+        const double2 P0 = sbuf[i], Q0 = sbuf[ld + i], P1 = sbuf[2 * ld + i], Q1 = sbuf[3 * ld + i];
+        x0[i] = make_double2(P0.x * Q0.y - P0.y * Q0.x, P1.x * Q1.y - P1.y * Q1.x);
+      }
+    }
+    __syncthreads();
+    // every vector runs the forward stages (the barriers are the workgroup's);
+    // only vector 0 — J — is kept
+    fft_stages_one_buffer(sbuf + col * ld, b, n, logn, tw, 0);
+    if (col == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) Zj[(int64_t)y * n + b + k * quarter] = x0[b + k * quarter];
+    }
+    return;
+  }
+  double m = 0.0;
+  if (col < 2) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double2 z = sbuf[col * ld + b + k * quarter];
+      const double u = z.x + shear, v = z.y;
+      const double s2 = u * u + v * v;
+      m = s2 > m ? s2 : m;
+    }
+  }
+  if (col >= 1) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      out[(int64_t)(4 + col) * nn + (int64_t)y * n + b + k * quarter] = sbuf[col * ld + b + k * quarter];
+  }
+  for (int off = 32; off > 0; off >>= 1) m = fmax(m, __shfl_xor(m, off, 64));
+  if ((t & 63) == 0) atomicMax(&bmax, (unsigned long long)__double_as_longlong(m));  // LDS atomic
+  __syncthreads();
+  if (t == 0) atomicMax(dmax, bmax);
+}
+
 // out[c + n*r] = in[r + n*c] for batch of nb n x n complex matrices.
 __global__ void transpose_kernel(const double2* in, double2* out, int n) {
   __shared__ double2 tile[32][33];

@@ -616,3 +616,32 @@ def test_qg2_speculative_steps_bit_identical(fresh_ctx):
     for u, v in zip(a[:4], b[:4]):
         assert np.ascontiguousarray(u).tobytes() == np.ascontiguousarray(v).tobytes()
     assert a[6] == b[6] and a[7] == b[7] == 12
+
+
+@pytest.mark.parametrize("nx", [64, 512])
+def test_qg2_column_jacobian_fusion_bit_identical(fresh_ctx, nx):
+    """Two-layer fused mode: the inverse column pass fused with the Jacobian,
+    the CFL max and J's first forward pass (fft_cols_jacobian2_kernel, the
+    default) against the separate column pass + Jacobian-rows kernel
+    (SWRT_DEBUG_QG_JFUSE 0): the same qk after 8 AB3 steps, the same U0 at
+    every step and the same packet snapshot, bit for bit
+    (qg2layersw_raytrace.m:309-323, grid_U.m)."""
+    import swraytracing_amd._lib as L
+    ctx = fresh_ctx
+    L_ = 20.0
+    qk0 = _two_layer_case(nx) if nx == 64 else _ring_qk(nx, L_, np.random.default_rng(9))
+    out = {}
+    for fuse in (0, 1):
+        ctx.debug_set(L.DEBUG_QG_JFUSE, fuse)
+        m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, L=L_, ctx=ctx)
+        U = [m.max_speed()]
+        dt = 0.25 * (L_ / nx) / U[0]
+        for _ in range(8):
+            m.step(dt)
+            U.append(m.max_speed())
+        m.snapshot(0, which=0, layer=0, ny_period=2 * nx)
+        out[fuse] = (np.ascontiguousarray(m.qk).tobytes(), U, ctx.get_field_grid(0, nx).tobytes())
+    ctx.debug_set(L.DEBUG_QG_JFUSE, 1)
+    assert out[0][1] == out[1][1]
+    assert out[0][0] == out[1][0]
+    assert out[0][2] == out[1][2]
