@@ -459,6 +459,8 @@ def parse_args(argv=None):
                     help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
     ap.add_argument("--qg-jfuse", type=int, default=1, choices=[0, 1],
                     help="2-layer PDE: inverse column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE; same bits)")
+    ap.add_argument("--qg-rows-vecs", type=int, default=0, choices=[0, 1, 2, 4],
+                    help="2-layer PDE beside packets: planes per first inverse-pass workgroup (0: library default)")
     ap.add_argument("--speculate", type=int, default=1, choices=[0, 1],
                     help="driver steps: queue the next PDE step before reading U0 (TwoLayerLoop speculate)")
     ap.add_argument("--forecast-driver-steps", type=int, default=100,
@@ -624,6 +626,7 @@ def main(argv=None):
     ctx.set_tile_cells(args.tile_cells)
     ctx.set_sparse_tiles(args.sparse_tiles)
     ctx.debug_set(sw._lib.DEBUG_QG_JFUSE, args.qg_jfuse)
+    ctx.debug_set(sw._lib.DEBUG_QG_ROWS_VECS, args.qg_rows_vecs)
     ctx.set_packet_streams(args.packet_streams)
     ctx.set_gather_mode(args.gather_mode)
     if args.tail_split >= 0:

@@ -532,12 +532,18 @@ int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launch
  * SWRT_DEBUG_QG_JFUSE 0/1 (default 1): two-layer fused mode runs the inverse
  *   column pass fused with the Jacobian, the CFL max and J's first forward
  *   pass (one kernel); 0 = the separate column pass + Jacobian-rows kernel —
- *   the same values, kept so tests can compare them bit for bit. */
+ *   the same values, kept so tests can compare them bit for bit.  Applies
+ *   when no packets share the context (beside packet launches the separate
+ *   passes' smaller workgroups run faster).
+ * SWRT_DEBUG_QG_ROWS_VECS 0/1/2/4: two-layer fused mode beside packets: the
+ *   planes each workgroup of the first inverse pass builds and transforms
+ *   (0 = 4); the same values for any setting. */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3
 #define SWRT_DEBUG_HAZARD_CHECKS 4
 #define SWRT_DEBUG_QG_JFUSE 5
+#define SWRT_DEBUG_QG_ROWS_VECS 6
 int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
 int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
 

@@ -126,6 +126,7 @@ DEBUG_SPIN_US = 2
 DEBUG_LEGACY_PARK = 3
 DEBUG_HAZARD_CHECKS = 4
 DEBUG_QG_JFUSE = 5
+DEBUG_QG_ROWS_VECS = 6
 
 _lib = None
 

@@ -202,6 +202,7 @@ struct swrt_ctx {
   bool qg_sep = true;
   bool qg_fused = true;  // swrt_qg_set_fused
   bool qg_jfuse = true;  // fused mode, 2 layers: the column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE)
+  int qg_rows_vecs = 0;  // fused mode, 2 layers beside packets: planes per first-pass workgroup (0: 4)
   std::vector<Slot> spares;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
@@ -2519,6 +2520,14 @@ int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
       if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "legacy park must be 0 or 1");
       c->debug_legacy_park = value != 0;
       return SWRT_OK;
+    case SWRT_DEBUG_QG_ROWS_VECS:
+      if (value != 0 && value != 1 && value != 2 && value != 4)
+        return fail(c, SWRT_ERR_ARG, "QG first-pass planes per workgroup must be 0, 1, 2 or 4");
+      if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
+      c->qg_rows_vecs = (int)value;
+      c->qg.post_valid = false;
+      c->qg.post_inv_valid = false;
+      return SWRT_OK;
     case SWRT_DEBUG_QG_JFUSE:
       if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG column/Jacobian fusion must be 0 or 1");
       if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
@@ -2539,6 +2548,7 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_LEGACY_PARK: *value_out = c->debug_legacy_park ? 1 : 0; return SWRT_OK;
     case SWRT_DEBUG_HAZARD_CHECKS: *value_out = c->hz.checks; return SWRT_OK;
     case SWRT_DEBUG_QG_JFUSE: *value_out = c->qg_jfuse ? 1 : 0; return SWRT_OK;
+    case SWRT_DEBUG_QG_ROWS_VECS: *value_out = c->qg_rows_vecs; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
 }
@@ -2745,14 +2755,26 @@ int qg_post_inverse(swrt_ctx* c) {
     int logn = 0;
     while ((1 << logn) < n) ++logn;
     const size_t lds = sizeof(double2) * nb * n;
-    if (nl == 2)
+    // planes per first-pass workgroup beside packets (SWRT_DEBUG_QG_ROWS_VECS; 0: 4)
+    const int rv = (c->qg_sep && c->n > 0 && c->qg_rows_vecs > 0) ? c->qg_rows_vecs : 4;
+    if (nl == 2 && rv == 1)
+      hipLaunchKernelGGL(qg_post_rows_v_kernel<1>, dim3(8 * (unsigned)n), dim3(n / 4), sizeof(double2) * n,
+                         c->stream, (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
+    else if (nl == 2 && rv == 2)
+      hipLaunchKernelGGL(qg_post_rows_v_kernel<2>, dim3(4 * (unsigned)n), dim3(n / 2), sizeof(double2) * 2 * n,
+                         c->stream, (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
+    else if (nl == 2)
       hipLaunchKernelGGL(qg_post_rows_split_kernel, dim3(2 * (unsigned)n), dim3(n), sizeof(double2) * 4 * n,
                          c->stream, (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
     else
       hipLaunchKernelGGL(qg_post_rows_kernel<1>, dim3((unsigned)n), dim3(nb * n / 4), lds, c->stream,
                          (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
     HIPCHK(c, hipGetLastError());
-    if (nl == 2 && n % 8 == 0 && c->qg_jfuse) {
+    // (not beside packets: its four-plane 512-lane workgroups then wait for
+    // packet workgroups to retire — driver step +2 %, 8-GPU shard +10 %,
+    // profiles/r04_qg_ab — where the separate column pass runs one plane per
+    // 128-lane workgroup)
+    if (nl == 2 && n % 8 == 0 && c->qg_jfuse && !(c->qg_sep && c->n > 0)) {
       // the column pass fused with the Jacobian, the CFL max and J's first
       // forward pass (swrt_fft.hpp): planes 0-4 stay on chip; J -> PT[0, nn)
       hipLaunchKernelGGL(fft_cols_jacobian2_kernel, dim3(2 * (unsigned)n), dim3(n), sizeof(double2) * 4 * (n + 1),

@@ -645,3 +645,23 @@ def test_qg2_column_jacobian_fusion_bit_identical(fresh_ctx, nx):
     assert out[0][1] == out[1][1]
     assert out[0][0] == out[1][0]
     assert out[0][2] == out[1][2]
+
+
+def test_qg2_rows_planes_per_workgroup_identical_files(tmp_path):
+    """The 2-layer driver with packets on the context, the first inverse pass
+    of the post-step transforms run with 4, 2 or 1 planes per workgroup
+    (SWRT_DEBUG_QG_ROWS_VECS): the same packet files, byte for byte."""
+    import swraytracing_amd as sw
+    import swraytracing_amd._lib as L
+    files = {}
+    for rv in (4, 2, 1):
+        c = sw.Context(0)
+        try:
+            c.debug_set(L.DEBUG_QG_ROWS_VECS, rv)
+            d = tmp_path / f"rv{rv}"
+            sw.qg2layersw_raytrace(128, 20_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), nsub=5, max_steps=50,
+                                   seed=5, ctx=c)
+            files[rv] = {n: (d / f"{n}.bin").read_bytes() for n in ("packet_x", "packet_k", "packet_time")}
+        finally:
+            c.close()
+    assert files[4] == files[2] == files[1]
