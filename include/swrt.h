@@ -235,8 +235,9 @@ int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
  * budget whose stencil gather issues each tap's LDS reads three taps ahead
  * (instead of 512 threads, 128 VGPRs, one tap ahead), so the one busy wave a
  * SIMD has at ~120 packets per tile waits less on the LDS.  0 (default) =
- * below SWRT_SPARSE_BELOW packets per 16x16 tile on average, 1 = never, 2 =
- * always.  Same arithmetic in the same order: bit-identical for any setting. */
+ * below SWRT_SPARSE_BELOW packets per 16x16 tile on average (build default
+ * 0: measured no faster), 1 = never, 2 = always.  Same arithmetic in the same
+ * order: bit-identical for any setting. */
 int swrt_set_sparse_tiles(swrt_ctx* ctx, int mode);
 
 /* Packet streams of the LDS-tiled leapfrog: 2 (default), 4 or 1.  With S > 1

@@ -86,9 +86,12 @@ constexpr int kPairBelow = SWRT_PAIR_BELOW;
 // at 128 VGPRs by the dense launch's 4-waves-per-SIMD budget and waiting on
 // LDS reads issued one tap earlier.  The sparse form is the same kernel with
 // 256 threads per workgroup, a 256-VGPR budget and the gather's reads issued
-// three taps ahead (gather5_lds PF): same arithmetic, same bits.
+// three taps ahead (gather5_lds PF): same arithmetic, same bits.  Measured
+// the same as the dense shape at 1.25e5 and 2.5e5 packets and 4 % slower at
+// 5e5 (profiles/r04_v1/ab_*.json): off by default (threshold 0), kept
+// selectable (swrt_set_sparse_tiles).
 #ifndef SWRT_SPARSE_BELOW
-#define SWRT_SPARSE_BELOW 192
+#define SWRT_SPARSE_BELOW 0
 #endif
 constexpr int kSparseBelow = SWRT_SPARSE_BELOW;
 constexpr int kSparseThreads = 256;
