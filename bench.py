@@ -461,6 +461,10 @@ def parse_args(argv=None):
                     help="2-layer PDE: inverse column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE; same bits)")
     ap.add_argument("--qg-rows-vecs", type=int, default=0, choices=[0, 1, 2, 4],
                     help="2-layer PDE beside packets: planes per first inverse-pass workgroup (0: library default)")
+    ap.add_argument("--qg-update-cols", type=int, default=1, choices=[0, 1],
+                    help="PDE: J's last forward pass fused into the AB3 update (SWRT_DEBUG_QG_UPDATE_COLS; same bits)")
+    ap.add_argument("--qg-stream", type=int, default=1, choices=[0, 1],
+                    help="driver steps: the PDE on its own stream beside the packets (1) or on the packet stream (0)")
     ap.add_argument("--speculate", type=int, default=1, choices=[0, 1],
                     help="driver steps: queue the next PDE step before reading U0 (TwoLayerLoop speculate)")
     ap.add_argument("--forecast-driver-steps", type=int, default=100,
@@ -627,6 +631,8 @@ def main(argv=None):
     ctx.set_sparse_tiles(args.sparse_tiles)
     ctx.debug_set(sw._lib.DEBUG_QG_JFUSE, args.qg_jfuse)
     ctx.debug_set(sw._lib.DEBUG_QG_ROWS_VECS, args.qg_rows_vecs)
+    ctx.debug_set(sw._lib.DEBUG_QG_UPDATE_COLS, args.qg_update_cols)
+    ctx.qg_set_stream(bool(args.qg_stream))
     ctx.set_packet_streams(args.packet_streams)
     ctx.set_gather_mode(args.gather_mode)
     if args.tail_split >= 0:

@@ -538,13 +538,20 @@ int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launch
  *   passes' smaller workgroups run faster).
  * SWRT_DEBUG_QG_ROWS_VECS 0/1/2/4: two-layer fused mode beside packets: the
  *   planes each workgroup of the first inverse pass builds and transforms
- *   (0 = 4); the same values for any setting. */
+ *   (0 = 4); the same values for any setting.
+ * SWRT_DEBUG_QG_UPDATE_COLS 0/1 (default 1): fused mode runs the last pass of
+ *   J's forward transform inside the AB3 update (one kernel; the spectrum
+ *   never goes to memory); 0 = the separate column pass + update — the same
+ *   values, kept so tests can compare them bit for bit.  Applies, like
+ *   SWRT_DEBUG_QG_JFUSE, unless packet launches share the context beside a
+ *   separate QG stream. */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3
 #define SWRT_DEBUG_HAZARD_CHECKS 4
 #define SWRT_DEBUG_QG_JFUSE 5
 #define SWRT_DEBUG_QG_ROWS_VECS 6
+#define SWRT_DEBUG_QG_UPDATE_COLS 7
 int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
 int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
 

@@ -127,6 +127,7 @@ DEBUG_LEGACY_PARK = 3
 DEBUG_HAZARD_CHECKS = 4
 DEBUG_QG_JFUSE = 5
 DEBUG_QG_ROWS_VECS = 6
+DEBUG_QG_UPDATE_COLS = 7
 
 _lib = None
 

@@ -152,6 +152,9 @@ struct QGState {
   const double2* post_of = nullptr;  // the qk whose post-step transforms PZ/PT hold
   bool post_jrows = false;     // phase 1 ran fft_cols_jacobian2_kernel: J's first forward pass is in PT[0, nn)
   const double2* Fj = nullptr; // where qg_post left the spectrum of J (the update's input)
+  bool Fj_rows = false;        // Fj is J after its first forward pass only: the update runs the last
+                               // (qg_update_cols_kernel) and renames the tendency history
+  bool spec_rot = false;       // the pending speculative step stored only its tendency (Qm1_spare)
   // fused mode: the post-step transforms of the current qk — the next step's
   // Jacobian spectrum (PT[0, nn) after its forward FFT), the CFL speed
   // (dmax) and layer 0's grid_U (the snapshot) — from ONE batched inverse
@@ -206,6 +209,7 @@ struct swrt_ctx {
   bool qg_fused = true;  // swrt_qg_set_fused
   bool qg_jfuse = true;  // fused mode, 2 layers: the column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE)
   int qg_rows_vecs = 0;  // fused mode, 2 layers beside packets: planes per first-pass workgroup (0: 4)
+  bool qg_update_cols = true;  // fused mode: J's last forward pass inside the update (SWRT_DEBUG_QG_UPDATE_COLS)
   std::vector<Slot> spares;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
@@ -2531,6 +2535,12 @@ int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
       c->qg.post_valid = false;
       c->qg.post_inv_valid = false;
       return SWRT_OK;
+    case SWRT_DEBUG_QG_UPDATE_COLS:
+      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG update/column-pass fusion must be 0 or 1");
+      if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
+      c->qg_update_cols = value != 0;
+      c->qg.post_valid = false;
+      return SWRT_OK;
     case SWRT_DEBUG_QG_JFUSE:
       if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG column/Jacobian fusion must be 0 or 1");
       if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
@@ -2552,6 +2562,7 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_HAZARD_CHECKS: *value_out = c->hz.checks; return SWRT_OK;
     case SWRT_DEBUG_QG_JFUSE: *value_out = c->qg_jfuse ? 1 : 0; return SWRT_OK;
     case SWRT_DEBUG_QG_ROWS_VECS: *value_out = c->qg_rows_vecs; return SWRT_OK;
+    case SWRT_DEBUG_QG_UPDATE_COLS: *value_out = c->qg_update_cols ? 1 : 0; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
 }
@@ -2565,6 +2576,7 @@ int swrt_qg_set_fused(swrt_ctx* c, int on) {
   c->qg_fused = on != 0;
   c->qg.post_valid = false;
   c->qg.post_inv_valid = false;
+  qg_drop_graphs(c->qg);  // fused steps rename the tendency buffers a captured step has baked in
   return SWRT_OK;
 }
 
@@ -2708,6 +2720,28 @@ int qg_update_launch(swrt_ctx* c, double dt, int abstep, const double2* F, doubl
   return SWRT_OK;
 }
 
+// Fused mode: J's last forward pass and the update in one launch from J after
+// its first pass (Zr); the new tendency goes to Qn_out only (the caller
+// renames the history buffers).
+int qg_update_cols_launch(swrt_ctx* c, double dt, int abstep, const double2* Zr, double2* qk_out,
+                          double2* Qn_out) {
+  QGState& q = c->qg;
+  const int n = q.g.n;
+  int logn = 0;
+  while ((1 << logn) < n) ++logn;
+  const size_t lds = sizeof(double2) * 2 * (size_t)(n + 1);
+  if (q.g.nl == 2)
+    hipLaunchKernelGGL(qg_update_cols_kernel<2>, dim3((unsigned)(n / 2)), dim3((unsigned)(n / 2)), lds, c->stream,
+                       Zr, q.g, logn, (const double2*)c->tw, dt, abstep, q.E1, q.E2, (const double2*)q.qk, qk_out,
+                       (const double2*)q.Qm1, (const double2*)q.Qm2, Qn_out);
+  else
+    hipLaunchKernelGGL(qg_update_cols_kernel<1>, dim3((unsigned)(n / 2)), dim3((unsigned)(n / 2)), lds, c->stream,
+                       Zr, q.g, logn, (const double2*)c->tw, dt, abstep, q.E1, q.E2, (const double2*)q.qk, qk_out,
+                       (const double2*)q.Qm1, (const double2*)q.Qm2, Qn_out);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+}
+
 // The kernel sequence of one QG step (update of qgsw_raytrace.m:270-286 /
 // qg2layersw_raytrace.m:309-323 + the AB3 step): spectra -> inverse 2-D FFT ->
 // Jacobian -> forward 2-D FFT -> fused g2k crop + AB3 update into qk_prev.
@@ -2815,13 +2849,23 @@ int qg_post(swrt_ctx* c) {
   // layer 0: contiguous); the spectrum of J then lands in PT[0, nn)
   const double2* uvT = q.PT + 2 * nl * q.nn;
   q.Fj = q.PT;
+  q.Fj_rows = false;
+  // J's last forward pass is left to the update (qg_update_cols_kernel) —
+  // not beside packets: PDE alone -7 %, but the driver step +1.3 % with the
+  // QG stream beside packet launches (profiles/r04_update_cols), as for
+  // fft_cols_jacobian2_kernel
+  const bool cols = c->qg_update_cols && n >= 16 && !(c->qg_sep && c->n > 0);
   if (q.post_jrows) {
     // J's first pass came with the inverse column pass: its second pass only
-    int logn = 0;
-    while ((1 << logn) < n) ++logn;
-    launch_fft<true>(c, q.PT, q.PZ, n, logn, n, 0);
-    HIPCHK(c, hipGetLastError());
-    q.Fj = q.PZ;
+    if (cols) {
+      q.Fj_rows = true;  // J's first pass is in PT[0, nn)
+    } else {
+      int logn = 0;
+      while ((1 << logn) < n) ++logn;
+      launch_fft<true>(c, q.PT, q.PZ, n, logn, n, 0);
+      HIPCHK(c, hipGetLastError());
+      q.Fj = q.PZ;
+    }
   } else if (n <= 1024) {
     // J computed in the load of the forward transform's first pass (same
     // values, same per-vector FFT as the separate kernel + transform_2d)
@@ -2837,8 +2881,13 @@ int qg_post(swrt_ctx* c) {
       hipLaunchKernelGGL(fft_jacobian_rows_kernel<1>, jg, jb, jl, c->stream, (const double2*)q.PT, n, logn, uvT,
                          q.g.shear, q.dmax, (const double2*)c->tw, q.PZ);
     HIPCHK(c, hipGetLastError());
-    launch_fft<true>(c, q.PZ, q.PT, n, logn, n, 0);
-    HIPCHK(c, hipGetLastError());
+    if (cols) {
+      q.Fj = q.PZ;
+      q.Fj_rows = true;
+    } else {
+      launch_fft<true>(c, q.PZ, q.PT, n, logn, n, 0);
+      HIPCHK(c, hipGetLastError());
+    }
   } else {
     const dim3 jgrid((unsigned)nblocks(q.nn, 256 * kQgMaxPer));
     hipLaunchKernelGGL(qg_jacobian_max_kernel, jgrid, block, 0, c->stream, (const double2*)q.PT, nl, q.nn, q.PZ,
@@ -2906,7 +2955,14 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
     const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
     if (c->qg_fused) {
       if ((rc = qg_post(c))) return rc;
-      rc = qg_update_launch(c, dt, abstep, q.Fj, q.qk_prev, q.Qm1, q.Qm2);
+      if (q.Fj_rows) {
+        // the tendency over Qm2 (read first by the same lane), then renamed:
+        // Qm2 <- Qm1, Qm1 <- Qn
+        if ((rc = qg_update_cols_launch(c, dt, abstep, q.Fj, q.qk_prev, q.Qm2))) return rc;
+        std::swap(q.Qm1, q.Qm2);
+      } else {
+        rc = qg_update_launch(c, dt, abstep, q.Fj, q.qk_prev, q.Qm1, q.Qm2);
+      }
     } else if (abstep == 3 && c->qg_graphs) {
       rc = qg_step_graphed(c, dt);
     } else {
@@ -2948,7 +3004,12 @@ int swrt_qg_step_speculative(swrt_ctx* c, double dt) {
     if (!*b) HIPCHK(c, hipMalloc(b, hb));
   const int abstep = q.steps == 0 ? 1 : (q.steps == 1 ? 2 : 3);
   if ((rc = qg_post(c))) return rc;  // of the committed qk (valid when the caller read its speed)
-  if ((rc = qg_update_launch(c, dt, abstep, q.Fj, q.qk_spare, q.Qm1_spare, q.Qm2_spare))) return rc;
+  q.spec_rot = q.Fj_rows;
+  if (q.spec_rot)  // the tendency only; the committed Qm1 becomes Qm2 on acceptance
+    rc = qg_update_cols_launch(c, dt, abstep, q.Fj, q.qk_spare, q.Qm1_spare);
+  else
+    rc = qg_update_launch(c, dt, abstep, q.Fj, q.qk_spare, q.Qm1_spare, q.Qm2_spare);
+  if (rc) return rc;
   // the post-step transforms and CFL read-back of the speculative qk
   double2* committed = q.qk;
   q.qk = q.qk_spare;
@@ -2975,8 +3036,17 @@ int swrt_qg_resolve(swrt_ctx* c, int accept) {
     q.qk_prev = q.qk;
     q.qk = q.qk_spare;
     q.qk_spare = old_prev;
-    std::swap(q.Qm1, q.Qm1_spare);
-    std::swap(q.Qm2, q.Qm2_spare);
+    if (q.spec_rot) {
+      // Qm2 <- the committed Qm1, Qm1 <- the speculative tendency; the old
+      // Qm2 is the next spare
+      double2* old_m2 = q.Qm2;
+      q.Qm2 = q.Qm1;
+      q.Qm1 = q.Qm1_spare;
+      q.Qm1_spare = old_m2;
+    } else {
+      std::swap(q.Qm1, q.Qm1_spare);
+      std::swap(q.Qm2, q.Qm2_spare);
+    }
     q.steps = q.spec_steps;
     q.t = q.spec_t;
     q.has_prev = true;

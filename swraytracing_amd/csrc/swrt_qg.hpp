@@ -235,37 +235,29 @@ __device__ __forceinline__ void mmul2(const double2* E, int64_t idx, const cd x[
 }
 
 // g2k crop of the (packed) forward spectrum, the tendency, and the AB3 update
-// of qk, fused per half-plane wavenumber (both layers together for mmult3).
+// of qk at one half-plane wavenumber idx = (kx+kmax)*(kmax+1) + ky (both
+// layers together for mmult3), from the packed spectrum Z = F1 + i F2 at k
+// (Fk) and at -k (Fm):
 //   1 layer:  Qn = g2k(J) - beta*psikx + r_drag*K2 + surface_forces
 //             qk = Ef.*(qk + dq)                       (qgsw_raytrace.m:121-137)
 //   2 layers: Qn = g2k(J);  qk = mmult3(expLdt, qk + dq)   (:168-181)
 //   dq = dt*Qn | dt/2*(3Qn - X1) | dt/12*(23Qn - 16X1 + 5X2), X = Qm (1 layer)
-//   or mmult3(expL(2)dt, Qm) (2 layers); then Qm2 = Qm1, Qm1 = Qn.
+//   or mmult3(expL(2)dt, Qm) (2 layers).  Returns the new qk (out), the
+// tendency Qn and the previous one m1 (the history shifts Qm2 <- m1,
+// Qm1 <- Qn; the callers store what their buffer scheme needs).
 template <int NL>
-// Qm1/Qm2 are read, and the shifted history (Qm2 <- Qm1, Qm1 <- Qn) written
-// to Qm1_out/Qm2_out: the same buffers for a committed step, spare ones for
-// a speculative step (swrt_qg_step_speculative), which must leave the
-// committed state intact until it is accepted.
-__global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev g, double dt, int abstep, const double2* E1,
-                                 const double2* E2, const double2* qk, double2* qk_out, const double2* Qm1,
-                                 const double2* Qm2, double2* Qm1_out, double2* Qm2_out) {
+__device__ __forceinline__ void qg_update_at(int64_t idx, int kx, int ky, double2 Fk, double2 Fm, const QGDev& g,
+                                             double dt, int abstep, const double2* E1, const double2* E2,
+                                             const double2* qk, const double2* Qm1, const double2* Qm2, cd out[NL],
+                                             cd Qn[NL], cd m1[NL]) {
   const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
   const int64_t nhalf = (int64_t)nkx * (kmax + 1);
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= nhalf) return;
-  const int shh_ = __ffs(n) - 2;  // kmax + 1 = n/2, a power of two
-  const int col = (int)idx & (kmax), row = (int)idx >> shh_;
-  const int kx = row - kmax, ky = col;
   const double kxs = (double)kx * g.kscale, kys = (double)ky * g.kscale;
   const double K2 = kxs * kxs + kys * kys;
   const double nn = (double)n * (double)n;
-  // packed forward spectrum Z = F1 + i F2 at k and -k (FFT indices)
-  const int r = kx < 0 ? kx + n : kx, c = ky;
-  const int rm = kx > 0 ? n - kx : -kx, cm = ky > 0 ? n - ky : 0;
-  const double2 Fk = Fj[c + (int64_t)n * r], Fm = Fj[cm + (int64_t)n * rm];
-  cd Qn[2];
   if constexpr (NL == 1) {
     // g2k(J) = fftshift(fft2(J))/nx^2 of a real J: the packed imaginary part is 0
+    (void)Fm;
     Qn[0] = cmk(Fk.x / nn, Fk.y / nn);
   } else {
     const cd F1 = cmk(0.5 * (Fk.x + Fm.x), 0.5 * (Fk.y - Fm.y));
@@ -273,7 +265,7 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
     Qn[0] = cdivr(F1, nn);
     Qn[1] = cdivr(F2, nn);
   }
-  cd q[2];
+  cd q[NL];
   _Pragma("unroll") for (int l = 0; l < NL; ++l) q[l] = ld(qk, l * nhalf + idx);
   if constexpr (NL == 1) {
     const double den = g.K_d2 + K2;
@@ -285,7 +277,7 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
     Qn[0].x = Qn[0].x + g.r_drag * K2;
     Qn[0].x = Qn[0].x + force;
   }
-  cd X1[2], X2[2], m1[2], m2[2];
+  cd X1[NL], X2[NL], m2[NL];
   _Pragma("unroll") for (int l = 0; l < NL; ++l) {
     m1[l] = ld(Qm1, l * nhalf + idx);
     m2[l] = ld(Qm2, l * nhalf + idx);
@@ -297,7 +289,7 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
     mmul2(E1, idx, m1, X1);
     mmul2(E2, idx, m2, X2);
   }
-  cd dq[2];
+  cd dq[NL];
   _Pragma("unroll") for (int l = 0; l < NL; ++l) {
     if (abstep == 1) {
       dq[l] = crs(dt, Qn[l]);
@@ -307,7 +299,6 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
       dq[l] = crs(dt / 12, cadd(csub(crs(23.0, Qn[l]), crs(16.0, X1[l])), crs(5.0, X2[l])));
     }
   }
-  cd out[2];
   if constexpr (NL == 1) {
     const double Ef = g.filter ? qg_filter_at(kxs, kys, g.dx) : 1.0;
     out[0] = crs(Ef, cadd(q[0], dq[0]));
@@ -315,10 +306,96 @@ __global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev
     cd s[2] = {cadd(q[0], dq[0]), cadd(q[1], dq[1])};
     mmul2(E1, idx, s, out);
   }
+}
+
+// The update over the half plane from the full forward spectrum Fj (layout
+// [ky + n*kx], FFT indices).  Qm1/Qm2 are read, and the shifted history
+// (Qm2 <- Qm1, Qm1 <- Qn) written to Qm1_out/Qm2_out: the same buffers for a
+// committed step, spare ones for a speculative step
+// (swrt_qg_step_speculative), which must leave the committed state intact
+// until it is accepted.
+template <int NL>
+__global__ void __launch_bounds__(256) qg_update_kernel(const double2* Fj, QGDev g, double dt, int abstep, const double2* E1,
+                                 const double2* E2, const double2* qk, double2* qk_out, const double2* Qm1,
+                                 const double2* Qm2, double2* Qm1_out, double2* Qm2_out) {
+  const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int64_t nhalf = (int64_t)nkx * (kmax + 1);
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= nhalf) return;
+  const int shh_ = __ffs(n) - 2;  // kmax + 1 = n/2, a power of two
+  const int col = (int)idx & (kmax), row = (int)idx >> shh_;
+  const int kx = row - kmax, ky = col;
+  // packed forward spectrum Z = F1 + i F2 at k and -k (FFT indices)
+  const int r = kx < 0 ? kx + n : kx, c = ky;
+  const int rm = kx > 0 ? n - kx : -kx, cm = ky > 0 ? n - ky : 0;
+  const double2 Fk = Fj[c + (int64_t)n * r], Fm = Fj[cm + (int64_t)n * rm];
+  cd out[NL], Qn[NL], m1[NL];
+  qg_update_at<NL>(idx, kx, ky, Fk, Fm, g, dt, abstep, E1, E2, qk, Qm1, Qm2, out, Qn, m1);
   _Pragma("unroll") for (int l = 0; l < NL; ++l) {
     st(qk_out, l * nhalf + idx, out[l]);
     st(Qm2_out, l * nhalf + idx, m1[l]);
     st(Qm1_out, l * nhalf + idx, Qn[l]);
+  }
+}
+
+// The last pass of J's forward transform fused with the update (fused mode,
+// n <= 2048): Zr holds J1 + i J2 after its first pass (along x, layout
+// [kx + n*y], FFT index kx), workgroup w transforms the two columns kx = r
+// and kx = n - r along y — the per-vector FFT of fft_vec_kernel<true,...>'s
+// column pass, so the same spectrum bits — and, with both in LDS, updates
+// every half-plane wavenumber (+-r, ky), ky = 0..kmax, whose k and -k they
+// hold (r = 0 pairs with the Nyquist column, which no wavenumber reads).
+// The spectrum never goes to memory (the column pass's write and the update's
+// k / -k reads) and the state is read and written along ky, contiguously.
+// Only the new tendency is stored, to Qn_out (which may alias Qm2: each
+// wavenumber is read and written by one lane); the caller renames the
+// history buffers (Qm2 <- Qm1, Qm1 <- Qn_out).  blockDim = n/2 (two vectors
+// of n/4 lanes, lane t = ky for the update), dynamic LDS 2*(n+1) double2.
+// Block b: XCD b % 8 walks a contiguous range of r, so the columns of each
+// 128-B line are read by workgroups of one XCD (one L2).
+template <int NL>
+__global__ void __launch_bounds__(1024) qg_update_cols_kernel(const double2* Zr, QGDev g, int logn,
+                                                               const double2* tw, double dt, int abstep,
+                                                               const double2* E1, const double2* E2,
+                                                               const double2* qk, double2* qk_out, const double2* Qm1,
+                                                               const double2* Qm2, double2* Qn_out) {
+  extern __shared__ double2 sbuf[];
+  const int n = g.n, kmax = n / 2 - 1, nkx = 2 * kmax + 1;
+  const int64_t nhalf = (int64_t)nkx * (kmax + 1);
+  const int quarter = n >> 2, t = threadIdx.x, ld = n + 1;
+  const int r = (int)(blockIdx.x & 7) * (n >> 4) + (int)(blockIdx.x >> 3);  // 0 .. n/2-1
+  const int rb = r == 0 ? n / 2 : n - r;                                     // the partner column
+  {
+    // lanes 2j, 2j+1 read row j's two columns, every load issued before the first wait
+    const int c = t & 1, j0 = t >> 1;
+    const double2* src = Zr + (c ? rb : r);
+    double2 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = src[(int64_t)(j0 + k * quarter) * n];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sbuf[c * ld + j0 + k * quarter] = v[k];
+  }
+  __syncthreads();
+  {
+    const int col = t / quarter, b = t - col * quarter;
+    fft_stages_one_buffer(sbuf + col * ld, b, n, logn, tw, 0);
+  }
+  const double2* A = sbuf;       // FFT row r:  kx = r
+  const double2* B = sbuf + ld;  // FFT row rb: kx = -r (r > 0)
+  const int ky = t, cm = ky > 0 ? n - ky : 0;
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    if (side == 1 && r == 0) break;
+    const int kx = side ? -r : r;
+    const double2 Fk = side ? B[ky] : A[ky];
+    const double2 Fm = r == 0 ? A[cm] : (side ? A[cm] : B[cm]);
+    const int64_t idx = (int64_t)(kx + kmax) * (kmax + 1) + ky;
+    cd out[NL], Qn[NL], m1[NL];
+    qg_update_at<NL>(idx, kx, ky, Fk, Fm, g, dt, abstep, E1, E2, qk, Qm1, Qm2, out, Qn, m1);
+    _Pragma("unroll") for (int l = 0; l < NL; ++l) {
+      st(qk_out, l * nhalf + idx, out[l]);
+      st(Qn_out, l * nhalf + idx, Qn[l]);
+    }
   }
 }
 

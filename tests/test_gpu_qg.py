@@ -665,3 +665,54 @@ def test_qg2_rows_planes_per_workgroup_identical_files(tmp_path):
         finally:
             c.close()
     assert files[4] == files[2] == files[1]
+
+
+@pytest.mark.parametrize("layers,nx", [(1, 32), (1, 256), (2, 16), (2, 64), (2, 512)])
+def test_qg_update_column_fusion_bit_identical(fresh_ctx, layers, nx):
+    """Fused mode: the last pass of J's forward transform inside the AB3
+    update (qg_update_cols_kernel, the default: each workgroup transforms
+    the FFT columns kx = +-r and updates every wavenumber (+-r, ky) from
+    LDS, storing only the new tendency and renaming the history buffers)
+    against the separate column pass + update (SWRT_DEBUG_QG_UPDATE_COLS 0):
+    the same qk and U0 after every step, bit for bit, through the Euler and
+    AB2 start steps, AB3 steps, a rejected and an accepted speculative step
+    (swrt_qg_resolve's buffer renaming), and steps after them that read the
+    renamed history (qgsw_raytrace.m:121-137, qg2layersw_raytrace.m:168-181,
+    309-323)."""
+    import swraytracing_amd._lib as L
+    ctx = fresh_ctx
+    out = {}
+    try:
+        for cols in (0, 1):
+            ctx.debug_set(L.DEBUG_QG_UPDATE_COLS, cols)
+            if layers == 1:
+                # (r_drag as written forces every mode: at 256^2 the run overflows
+                # within these steps, and NaN payloads carry no parity)
+                m = sw.QGModel.one_layer(_one_layer_case(nx), nx, 3.0, 1.0, r_drag=0.1 if nx < 64 else 0.0, ctx=ctx)
+                Lx = 2 * np.pi
+            else:
+                qk0 = _two_layer_case(nx) if nx < 512 else _ring_qk(nx, 20.0, np.random.default_rng(9))
+                m = sw.QGModel.two_layer(qk0, nx, 3.0, 1.0, L=20.0, ctx=ctx)
+                Lx = 20.0
+            U = [m.max_speed()]
+            dt = 0.25 * (Lx / nx) / U[0]
+            trace = []
+            for s in range(9):
+                if s == 3:
+                    m.step_speculative(dt)
+                    m.resolve(False)
+                if s == 5:
+                    m.step_speculative(dt)
+                    m.resolve(True)
+                else:
+                    m.step(dt)
+                U.append(m.max_speed())
+                trace.append(np.ascontiguousarray(m.qk).tobytes())
+            out[cols] = (U, trace, m.steps)
+    finally:
+        ctx.debug_set(L.DEBUG_QG_UPDATE_COLS, 1)
+    assert out[0][2] == out[1][2] == 9
+    assert np.isfinite(out[1][0]).all()
+    assert out[0][0] == out[1][0]
+    for s, (a, b) in enumerate(zip(out[0][1], out[1][1])):
+        assert a == b, s
