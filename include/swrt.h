@@ -236,7 +236,8 @@ int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
  * (instead of 512 threads, 128 VGPRs, one tap ahead), so the one busy wave a
  * SIMD has at ~120 packets per tile waits less on the LDS.  0 (default) =
  * below SWRT_SPARSE_BELOW packets per 16x16 tile on average (build default
- * 0: measured no faster), 1 = never, 2 = always.  Same arithmetic in the same
+ * 192: the 8-GPU shard of the 1e6 bench, whose driver step it shortens by
+ * 2.5 % beside the PDE), 1 = never, 2 = always.  Same arithmetic in the same
  * order: bit-identical for any setting. */
 int swrt_set_sparse_tiles(swrt_ctx* ctx, int mode);
 

@@ -84,14 +84,18 @@ constexpr int kPairBelow = SWRT_PAIR_BELOW;
 // average (a strong-scaling shard: ~120 at 1.25e5 packets on 512^2) a
 // 512-thread workgroup has one or two busy waves, one per SIMD, each capped
 // at 128 VGPRs by the dense launch's 4-waves-per-SIMD budget and waiting on
-// LDS reads issued one tap earlier.  The sparse form is the same kernel with
-// 256 threads per workgroup, a 256-VGPR budget and the gather's reads issued
-// three taps ahead (gather5_lds PF): same arithmetic, same bits.  Measured
-// the same as the dense shape at 1.25e5 and 2.5e5 packets and 4 % slower at
-// 5e5 (profiles/r04_v1/ab_*.json): off by default (threshold 0), kept
-// selectable (swrt_set_sparse_tiles).
+// LDS reads issued one tap earlier, and its idle waves hold their registers
+// until the workgroup ends.  The sparse form is the same kernel with 256
+// threads per workgroup, a 256-VGPR budget and the gather's reads issued
+// three taps ahead (gather5_lds PF): same arithmetic, same bits.  Packets
+// alone it measured the same as the dense shape at 1.25e5 and 2.5e5 and 4 %
+// slower at 5e5 (profiles/r04_v1/ab_*.json); beside the replicated PDE at
+// the 8-GPU shard (1.25e5) the driver step is 2.5 % shorter, the PDE's
+// kernels finding the slots the idle waves no longer hold
+// (profiles/r04_sparse_driver): on below 192 packets per tile (1.25e5 on
+// 512^2, not 2.5e5).
 #ifndef SWRT_SPARSE_BELOW
-#define SWRT_SPARSE_BELOW 0
+#define SWRT_SPARSE_BELOW 192
 #endif
 constexpr int kSparseBelow = SWRT_SPARSE_BELOW;
 constexpr int kSparseThreads = 256;
