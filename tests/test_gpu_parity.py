@@ -1114,3 +1114,57 @@ def test_maximum_size_ensemble_subset():
                                       dt / sub, sub, 3.0, 1.0)
     np.testing.assert_array_equal(xg[idx], xo)
     np.testing.assert_array_equal(kg[idx], ko)
+
+
+@pytest.mark.parametrize("sparse", [0, 1])
+def test_tile_path_non_finite_and_far_packets(fresh_ctx, oracle_lib, sparse):
+    """Bad inputs on the LDS-tiled hot path (the bench field, 70,000 packets,
+    two packet streams, 8 calls of 5 steps with re-binning every 20; the
+    automatic launch shape at ~68 packets per tile is the sparse one, 1 forces
+    the dense one): packets
+    at NaN / +-Inf positions or with a NaN wavevector are binned, sorted and
+    advanced without a fault and stay non-finite; packets far outside the
+    periodic domain (|x| ~ 1e6 L, interpolate.m's mod wraps them) and exactly
+    on its edges match the C oracle bit for bit; every other packet is
+    bit-identical to the run without the bad ones (packets never interact,
+    ode_symplectic.m:18-21)."""
+    import argparse
+    import bench
+    ctx = fresh_ctx
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=70_000, world=1, rank=0, seed=146, mode="blend")
+    w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
+    x, k = w["x"].copy(), w["k"].copy()
+    L = w["L"]
+    bad = {10: (np.nan, 0.0), 20: (np.inf, 1.0), 30: (0.0, -np.inf)}
+    far = {40: (1e6 * L + 0.3, -2.5e6 * L), 50: (-L / 2, -L / 2), 60: (L / 2, L / 2 - 1e-13)}
+    for i, v in {**bad, **far}.items():
+        x[i] = v
+    k[70] = (np.nan, 1.0)
+    ctx.set_locality(20, 0)
+    ctx.set_sparse_tiles(sparse)
+    out = {}
+    try:
+        for name, xs in (("mixed", x), ("clean", w["x"])):
+            ks = k if name == "mixed" else w["k"]
+            ctx.packets_set(xs, ks)
+            for _ in range(8):
+                bench.step(ctx, w, 5)
+            out[name] = ctx.packets_get()
+        p0, p1 = ctx.get_field_grid(0, 512), ctx.get_field_grid(1, 512)
+    finally:
+        ctx.set_locality(4, 0)
+    xg, kg = out["mixed"]
+    for i in (10, 20, 30, 70):
+        assert not (np.isfinite(xg[i]).all() and np.isfinite(kg[i]).all()), i
+    special = [10, 20, 30, 40, 50, 60, 70]
+    keep = np.setdiff1d(np.arange(args.packets), special)
+    assert xg[keep].tobytes() == out["clean"][0][keep].tobytes()
+    assert kg[keep].tobytes() == out["clean"][1][keep].tobytes()
+    idx = np.array(sorted(far))
+    xo, ko = x[idx], k[idx]
+    for _ in range(8):
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.2, 512, 1024, L / 512, orc.BUMP_QG, xo, ko,
+                                           w["dt"] / 5, 5, w["f"], w["gH"])
+    np.testing.assert_array_equal(xg[idx], xo)
+    np.testing.assert_array_equal(kg[idx], ko)
