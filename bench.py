@@ -457,11 +457,11 @@ def parse_args(argv=None):
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
     ap.add_argument("--driver-steps", type=int, default=50,
                     help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
-    ap.add_argument("--qg-jfuse", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--qg-jfuse", type=int, default=1, choices=[0, 1, 2],
                     help="2-layer PDE: inverse column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE; same bits)")
     ap.add_argument("--qg-rows-vecs", type=int, default=0, choices=[0, 1, 2, 4],
                     help="2-layer PDE beside packets: planes per first inverse-pass workgroup (0: library default)")
-    ap.add_argument("--qg-update-cols", type=int, default=1, choices=[0, 1],
+    ap.add_argument("--qg-update-cols", type=int, default=1, choices=[0, 1, 2],
                     help="PDE: J's last forward pass fused into the AB3 update (SWRT_DEBUG_QG_UPDATE_COLS; same bits)")
     ap.add_argument("--qg-stream", type=int, default=1, choices=[0, 1],
                     help="driver steps: the PDE on its own stream beside the packets (1) or on the packet stream (0)")

@@ -536,7 +536,7 @@ int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launch
  *   pass (one kernel); 0 = the separate column pass + Jacobian-rows kernel —
  *   the same values, kept so tests can compare them bit for bit.  Applies
  *   when no packets share the context (beside packet launches the separate
- *   passes' smaller workgroups run faster).
+ *   passes' smaller workgroups run faster); 2 = beside packets too.
  * SWRT_DEBUG_QG_ROWS_VECS 0/1/2/4: two-layer fused mode beside packets: the
  *   planes each workgroup of the first inverse pass builds and transforms
  *   (0 = 4); the same values for any setting.
@@ -545,7 +545,7 @@ int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launch
  *   never goes to memory); 0 = the separate column pass + update — the same
  *   values, kept so tests can compare them bit for bit.  Applies, like
  *   SWRT_DEBUG_QG_JFUSE, unless packet launches share the context beside a
- *   separate QG stream. */
+ *   separate QG stream; 2 = beside packets too. */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3

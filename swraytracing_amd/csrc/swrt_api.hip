@@ -211,9 +211,9 @@ struct swrt_ctx {
   hipStream_t qstream = nullptr;
   bool qg_sep = true;
   bool qg_fused = true;  // swrt_qg_set_fused
-  bool qg_jfuse = true;  // fused mode, 2 layers: the column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE)
+  int qg_jfuse = 1;  // fused mode, 2 layers: the column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE; 2: beside packets too)
   int qg_rows_vecs = 0;  // fused mode, 2 layers beside packets: planes per first-pass workgroup (0: 4)
-  bool qg_update_cols = true;  // fused mode: J's last forward pass inside the update (SWRT_DEBUG_QG_UPDATE_COLS)
+  int qg_update_cols = 1;  // fused mode: J's last forward pass inside the update (SWRT_DEBUG_QG_UPDATE_COLS; 2: beside packets too)
   std::vector<Slot> spares;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
@@ -2540,15 +2540,15 @@ int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
       c->qg.post_inv_valid = false;
       return SWRT_OK;
     case SWRT_DEBUG_QG_UPDATE_COLS:
-      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG update/column-pass fusion must be 0 or 1");
+      if (value < 0 || value > 2) return fail(c, SWRT_ERR_ARG, "QG update/column-pass fusion must be 0, 1 or 2");
       if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
-      c->qg_update_cols = value != 0;
+      c->qg_update_cols = (int)value;
       c->qg.post_valid = false;
       return SWRT_OK;
     case SWRT_DEBUG_QG_JFUSE:
-      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG column/Jacobian fusion must be 0 or 1");
+      if (value < 0 || value > 2) return fail(c, SWRT_ERR_ARG, "QG column/Jacobian fusion must be 0, 1 or 2");
       if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
-      c->qg_jfuse = value != 0;
+      c->qg_jfuse = (int)value;
       c->qg.post_valid = false;
       c->qg.post_inv_valid = false;
       return SWRT_OK;
@@ -2564,9 +2564,9 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_SPIN_US: *value_out = c->debug_spin_us; return SWRT_OK;
     case SWRT_DEBUG_LEGACY_PARK: *value_out = c->debug_legacy_park ? 1 : 0; return SWRT_OK;
     case SWRT_DEBUG_HAZARD_CHECKS: *value_out = c->hz.checks; return SWRT_OK;
-    case SWRT_DEBUG_QG_JFUSE: *value_out = c->qg_jfuse ? 1 : 0; return SWRT_OK;
+    case SWRT_DEBUG_QG_JFUSE: *value_out = c->qg_jfuse; return SWRT_OK;
     case SWRT_DEBUG_QG_ROWS_VECS: *value_out = c->qg_rows_vecs; return SWRT_OK;
-    case SWRT_DEBUG_QG_UPDATE_COLS: *value_out = c->qg_update_cols ? 1 : 0; return SWRT_OK;
+    case SWRT_DEBUG_QG_UPDATE_COLS: *value_out = c->qg_update_cols; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
 }
@@ -2815,7 +2815,7 @@ int qg_post_inverse(swrt_ctx* c) {
     // packet workgroups to retire — driver step +2 %, 8-GPU shard +10 %,
     // profiles/r04_qg_ab — where the separate column pass runs one plane per
     // 128-lane workgroup)
-    if (nl == 2 && n % 8 == 0 && c->qg_jfuse && !(c->qg_sep && c->n > 0)) {
+    if (nl == 2 && n % 8 == 0 && (c->qg_jfuse == 2 || (c->qg_jfuse == 1 && !(c->qg_sep && c->n > 0)))) {
       // the column pass fused with the Jacobian, the CFL max and J's first
       // forward pass (swrt_fft.hpp): planes 0-4 stay on chip; J -> PT[0, nn)
       hipLaunchKernelGGL(fft_cols_jacobian2_kernel, dim3(2 * (unsigned)n), dim3(n), sizeof(double2) * 4 * (n + 1),
@@ -2858,7 +2858,8 @@ int qg_post(swrt_ctx* c) {
   // not beside packets: PDE alone -7 %, but the driver step +1.3 % with the
   // QG stream beside packet launches (profiles/r04_update_cols), as for
   // fft_cols_jacobian2_kernel
-  const bool cols = c->qg_update_cols && n >= 16 && !(c->qg_sep && c->n > 0);
+  const bool cols =
+      n >= 16 && (c->qg_update_cols == 2 || (c->qg_update_cols == 1 && !(c->qg_sep && c->n > 0)));
   if (q.post_jrows) {
     // J's first pass came with the inverse column pass: its second pass only
     if (cols) {
