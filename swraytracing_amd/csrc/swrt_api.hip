@@ -781,6 +781,12 @@ int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
     return SWRT_OK;
   }
   if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, S));
+  // Part i always takes the band positions = i (mod S): a stream's
+  // consecutive part launches own the same tiles, so stream order alone
+  // orders them, and stream 0's next launch may start while stream 1's
+  // previous one still runs.  A launch with another tile-to-stream mapping
+  // would race it without a join first (measured: a hang,
+  // profiles/r04_stream_split).
   HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
   for (int i = 0; i < S - 1; ++i) HIPCHK(c, hipStreamWaitEvent(c->sx[i], c->fork_ev, 0));
   t.spart = 0;
