@@ -395,6 +395,23 @@ def roofline(pmc, N, nx, nslots, steps_per_launch, avg_launch_s, launches, timin
     return r
 
 
+def add_observed_clock(r, ghz, spread):
+    """The clock the timed region actually ran at (swrt_clock_stamp probes,
+    rank 0's GPU) and the fractions re-based to it: peak x ghz / 2.4 (the
+    chip lowers its clock under load, and boxes differ — this is what makes
+    a throughput change attributable to code rather than to the box)."""
+    r["clock_ghz_observed"] = ghz
+    r["clock_probe_spread"] = spread
+    r["clock_note"] = ("median over same-XCD (start, end) probe pairs of s_memtime cycles / s_memrealtime seconds "
+                       "across the timed region; *_at_observed_clock = the fraction against the peak at that clock")
+    if ghz and ghz > 0:
+        s = 2.4 / ghz
+        if r.get("frac") is not None:
+            r["frac_at_observed_clock"] = r["frac"] * s
+        r["algorithmic_frac_at_observed_clock"] = r["algorithmic_frac"] * s
+    return r
+
+
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -431,37 +448,21 @@ def parse_args(argv=None):
     ap.add_argument("--rebin-every", type=int, default=20, help="steps between spatial re-binning (0: off)")
     ap.add_argument("--tile", type=int, default=0, help="binning tile (cells); 0: automatic")
     ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 per-packet, 2 LDS tile")
-    ap.add_argument("--blend-mode", type=int, default=0,
-                    help="0 bit-exact interpolate-then-blend (default), 1 blend in the LDS window (tolerance parity)")
     ap.add_argument("--sparse-tiles", type=int, default=0, choices=[0, 1, 2],
                     help="LDS-tiled launches: sparse-tile shape (256 threads, reads 3 taps ahead) 0 auto, 1 never, "
                          "2 always (same bits)")
-    ap.add_argument("--lanes-per-packet", type=int, default=0,
-                    help="LDS-tiled launches: 0 auto (build threshold, off by default), 1, 2 (same bits)")
-    ap.add_argument("--tile-cells", type=int, default=0,
-                    help="LDS-tiled launches: cells per tile side, 0 auto (build threshold, off by default), 16, 32 (same bits)")
-    ap.add_argument("--packet-streams", type=int, default=2, choices=[1, 2, 4],
-                    help="LDS-tiled launches split over 1, 2 or 4 streams (swrt_set_packet_streams; same bits; "
+    ap.add_argument("--packet-streams", type=int, default=2, choices=[1, 2],
+                    help="LDS-tiled launches split over 1 or 2 streams (swrt_set_packet_streams; same bits; "
                          "2 is the library default)")
-    ap.add_argument("--cell-sort", type=int, default=0,
-                    help="in-tile cell sort: 0 after each re-binning only, 1 every launch")
-    ap.add_argument("--tail-split", type=int, default=-1,
-                    help="tiles per XCD band run as two half-tile workgroups (-1: library default)")
-    ap.add_argument("--tail-quarters", type=int, default=0,
-                    help="then tiles per XCD band run as four quarter-tile workgroups (with --tail-split)")
-    ap.add_argument("--tile-order", type=int, default=-1,
-                    help="LDS-tiled launches: 1 longest tiles first per XCD band, 0 spatial (-1: library default)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="process-group backend (nccl = RCCL over xGMI); gloo lets ranks share a GPU")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="HIP-event-time every k-th packet-kernel launch (sampled, inside the timed region)")
     ap.add_argument("--driver-steps", type=int, default=50,
                     help="after the metric, time this many end-to-end driver steps (PDE + snapshot + packets; 0: skip)")
-    ap.add_argument("--qg-jfuse", type=int, default=1, choices=[0, 1, 2],
+    ap.add_argument("--qg-jfuse", type=int, default=1, choices=[0, 1],
                     help="2-layer PDE: inverse column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE; same bits)")
-    ap.add_argument("--qg-rows-vecs", type=int, default=0, choices=[0, 1, 2, 4],
-                    help="2-layer PDE beside packets: planes per first inverse-pass workgroup (0: library default)")
-    ap.add_argument("--qg-update-cols", type=int, default=1, choices=[0, 1, 2],
+    ap.add_argument("--qg-update-cols", type=int, default=1, choices=[0, 1],
                     help="PDE: J's last forward pass fused into the AB3 update (SWRT_DEBUG_QG_UPDATE_COLS; same bits)")
     ap.add_argument("--qg-stream", type=int, default=1, choices=[0, 1],
                     help="driver steps: the PDE on its own stream beside the packets (1) or on the packet stream (0)")
@@ -538,7 +539,10 @@ def steps_per_launch_of(args, ivs):
 
 def timed(ctx, w, args, dev, steps, warmup, barrier=None):
     """warmup untimed steps, then `steps` timed ones bracketed by a device
-    sync (and the caller's barrier); returns (elapsed s, sampled kernel ms, launches)."""
+    sync (and the caller's barrier); returns (elapsed s, sampled kernel ms,
+    launches, observed shader clock: (GHz, spread) from swrt_clock_stamp's
+    one-wave probes enqueued on the packet stream before the first and after
+    the last timed launch)."""
     for _ in range(warmup):
         step(ctx, w, args.substeps)
     ctx.synchronize()
@@ -547,9 +551,11 @@ def timed(ctx, w, args, dev, steps, warmup, barrier=None):
         barrier()
     ctx.set_timing(args.timing_every)
     ctx.kernel_time(reset=True)
+    ctx.clock_stamp(0)
     t0 = time.perf_counter()
     for _ in range(steps):
         step(ctx, w, args.substeps)
+    ctx.clock_stamp(1)
     ctx.synchronize()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
@@ -557,7 +563,7 @@ def timed(ctx, w, args, dev, steps, warmup, barrier=None):
         barrier()
     kms, launches = ctx.kernel_time(reset=True)
     ctx.set_timing(0)
-    return t1 - t0, kms, launches
+    return t1 - t0, kms, launches, ctx.clock_ghz()
 
 
 def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu, sizes=(2, 4, 8), steps=None):
@@ -572,11 +578,11 @@ def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu, sizes=(2, 4, 
     for G in sizes:
         n = -(-n_total // G)
         ctx.packets_set(x[:n], k[:n])
-        el, kms, launches = timed(ctx, w, args, dev, steps, args.warmup)
+        el, kms, launches, (clk, _) = timed(ctx, w, args, dev, steps, args.warmup)
         rate = n * args.substeps * w["intervals"] * steps / el
         out[str(G)] = {"packets_per_gpu": n, "value_1gpu": rate, "forecast_value": G * rate,
                        "efficiency": rate / rate_1gpu if rate_1gpu else None, "ms_per_step": el / steps * 1e3,
-                       "avg_launch_ms": (kms / launches) if launches else None}
+                       "avg_launch_ms": (kms / launches) if launches else None, "clock_ghz_observed": clk}
     ctx.packets_set(x, k)
     return out
 
@@ -624,21 +630,12 @@ def main(argv=None):
     ctx = sw.Context(device)
     ctx.set_locality(args.rebin_every, args.tile)
     ctx.set_kernel(args.kernel)
-    ctx.set_cell_sort(args.cell_sort)
-    ctx.set_blend_mode(args.blend_mode)
-    ctx.set_lanes_per_packet(args.lanes_per_packet)
-    ctx.set_tile_cells(args.tile_cells)
     ctx.set_sparse_tiles(args.sparse_tiles)
     ctx.debug_set(sw._lib.DEBUG_QG_JFUSE, args.qg_jfuse)
-    ctx.debug_set(sw._lib.DEBUG_QG_ROWS_VECS, args.qg_rows_vecs)
     ctx.debug_set(sw._lib.DEBUG_QG_UPDATE_COLS, args.qg_update_cols)
     ctx.qg_set_stream(bool(args.qg_stream))
     ctx.set_packet_streams(args.packet_streams)
     ctx.set_gather_mode(args.gather_mode)
-    if args.tail_split >= 0:
-        ctx.set_tail_split(args.tail_split, args.tail_quarters)
-    if args.tile_order >= 0:
-        ctx.set_tile_order(args.tile_order)
     w = build_workload(ctx, args, lo, hi, n_total)
     ctx.packets_set(w["x"], w["k"])
 
@@ -646,7 +643,7 @@ def main(argv=None):
         if distributed:
             dist.barrier()
 
-    elapsed, kms, launches = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
+    elapsed, kms, launches, (clock_ghz, clock_spread) = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
     if distributed:
         elapsed = max_over_ranks(elapsed, backend=args.dist_backend)
     xg, kg = ctx.packets_get()
@@ -667,7 +664,7 @@ def main(argv=None):
     spl = steps_per_launch_of(args, ivs)
     key = (f"{args.mode}_nx{args.nx}_N{N}_sub{args.substeps}" + (f"_iv{ivs}" if ivs > 1 else "")
            + ("_fma" if args.gather_mode == 1 else ""))
-    pmc, pmc_note = (load_pmc(key) if args.blend_mode == 0 and args.kernel in (0, 2)
+    pmc, pmc_note = (load_pmc(key) if args.kernel in (0, 2)
                      else (None, "PMC only for the default bit-exact tile kernel"))
     # Two packet streams: each launch is two half launches whose spans overlap
     # the neighbouring calls', so a launch's event span is not its share of
@@ -683,6 +680,7 @@ def main(argv=None):
                           if two else "HIP-event time of the packet-kernel launches")
     roof["launch_span_ms"] = avg_launch_s * 1e3
     roof["pmc_note"] = pmc_note
+    add_observed_clock(roof, clock_ghz, clock_spread)
     workload = ("qg2layersw_raytrace packet loop (configs[3]): 2-layer QG, layer 1, "
                 f"{'two-snapshot blend' if w['nslots'] == 2 else 'steady'}, {args.nx}^2x2 field, {n_total} packets "
                 f"({args.scaling} scaling, {N} on rank 0's GPU), leapfrog dt {0.25 / args.substeps:g}*dx/U0 "
@@ -705,29 +703,28 @@ def main(argv=None):
                    "pde_dt": "0.25*dx/U0", "leapfrog_dt": f"{0.25 / args.substeps:g}*dx/U0",
                    "steps_per_launch": spl, "intervals_per_step": ivs,
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
-                   "cell_sort": args.cell_sort, "blend_mode": args.blend_mode, "tail_split": args.tail_split,
-                   "lanes_per_packet": args.lanes_per_packet, "tile_cells": args.tile_cells,
                    "sparse_tiles": args.sparse_tiles,
                    "packet_streams": args.packet_streams, "gather_mode": args.gather_mode,
-                   "tail_quarters": args.tail_quarters, "tile_order": args.tile_order, "positions": args.positions,
+                   "positions": args.positions,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,
         "finite": finite,
     }
     if gathered is not None:
         out["gathered_finite"] = gathered
-    if not args.no_fma and args.blend_mode == 0 and args.kernel in (0, 2) and args.gather_mode == 0:
+    if not args.no_fma and args.kernel in (0, 2) and args.gather_mode == 0:
         # the opt-in FMA gather (tolerance parity, tests/test_gpu_parity.py::test_fma_gather_mode_tolerance):
         # the same workload and packets, timed the same way; the headline stays bit-exact
         ctx.packets_set(w["x"], w["k"])
         ctx.set_gather_mode(1)
-        el2, kms2, l2 = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
+        el2, kms2, l2, (clk2, _) = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
         ctx.set_gather_mode(0)
         if distributed:
             el2 = max_over_ranks(el2, backend=args.dist_backend)
         ctx.packets_set(w["x"], w["k"])
         out["fma_gather"] = {"value": total_ps / el2, "ms_per_step": el2 / args.steps * 1e3,
                              "avg_launch_ms": (kms2 / l2) if l2 else None, "vs_exact": elapsed / el2,
+                             "clock_ghz_observed": clk2,
                              "parity": "tolerance: stencil sums and blend by fused multiply-add, "
                                        "<= 1e-13 relative per step vs the bit-exact path"}
     if world == 1 and not args.no_forecast and args.scaling == "strong":

@@ -164,38 +164,6 @@ int swrt_set_locality(swrt_ctx* ctx, int64_t rebin_every, int64_t tile);
  * cell tiles, field window staged in LDS, in-tile cell sort). */
 int swrt_set_kernel(swrt_ctx* ctx, int variant);
 
-/* In-tile cell sort of the LDS-tiled kernel (performance only; results are
- * identical): 0 = sort on the first launch after each re-binning, later
- * launches read the packets in the cell order the previous launch wrote
- * (default); 1 = sort on every launch. */
-int swrt_set_cell_sort(swrt_ctx* ctx, int every_launch);
-
-/* Launch shape of the LDS-tiled kernels (performance only; results are
- * identical): each XCD's band of tiles ends with `halves_per_xcd` tiles run
- * as two workgroups of half the tile's packets and then `quarters_per_xcd`
- * tiles run as four workgroups of a quarter each, so the end of a launch is
- * made of smaller work items and the CUs finish closer together.
- * 0, 0 = one workgroup per tile (the default: with the longest-first tile
- * order, swrt_set_tile_order, the split measured no faster). */
-int swrt_set_tail_split(swrt_ctx* ctx, int halves_per_xcd, int quarters_per_xcd);
-
-/* Tile order of the LDS-tiled kernels (performance only; results are
- * identical): 1 (default) = each XCD band's tiles longest first (by the
- * rounds of 512 packets their workgroup runs, spatial order among equals),
- * so the long tiles start first and the launch ends with short ones;
- * 0 = spatial order.  Takes effect at the next re-binning (forced). */
-int swrt_set_tile_order(swrt_ctx* ctx, int longest_first);
-
-/* Two-snapshot blend of the LDS-tiled kernel.  0 (default): interpolate each
- * snapshot, then blend (1-alpha)*U1 + alpha*U2 — interpolate_U.m:19-23 in its
- * own operation order, bit-identical to the reference arithmetic.  1: blend
- * the snapshots' node values once per step in the LDS window, then
- * interpolate once — the same linear function (interpolate_U is linear in
- * the fields) with a different rounding order: half the gather work, results
- * agree to ~1e-16 relative per step (tolerance parity, not bits); launches
- * advance one step each. */
-int swrt_set_blend_mode(swrt_ctx* ctx, int mode);
-
 /* Opt-in stencil arithmetic of the LDS-tiled packet kernel for fields with
  * v_y == -u_x (every field the library derives from psi / qk): 1 = each
  * tap's wij*F added by one fused multiply-add (and the snapshot blend as
@@ -208,28 +176,6 @@ int swrt_set_blend_mode(swrt_ctx* ctx, int mode);
  * xka) always use mul then add. */
 int swrt_set_gather_mode(swrt_ctx* ctx, int mode);
 
-/* Lanes per packet of the LDS-tiled two-snapshot launch (fields with v_y ==
- * -u_x): 1 = one lane advances a packet; 2 = two lanes of one wave share it
- * (one computes the x weights and snapshot 1's five stencil sums, the other
- * the y weights and snapshot 2's; cross-lane swaps combine them), so a tile
- * with few packets still keeps two waves per SIMD busy — small shards of a
- * strongly scaled ensemble.  0 (default) = 2 below SWRT_PAIR_BELOW packets
- * per tile on average (build default 0: measured no faster, see
- * swrt_api.hip), else 1.  Every sum keeps the reference's order: results are
- * bit-identical for any setting. */
-int swrt_set_lanes_per_packet(swrt_ctx* ctx, int lanes);
-
-/* Cells per tile side of the LDS-tiled leapfrog launches (the spatial
- * binning and each workgroup's window): 16, or 32 — one 1024-thread
- * workgroup per CU whose 151 KB two-snapshot window fills the LDS, for
- * ensembles too small to keep 16x16-cell workgroups busy (a strong-scaling
- * shard: ~120 packets per 16x16 tile at 1.25e5 packets on 512^2).  32 applies
- * to two divergence-free snapshots in the bit-exact blend order; other
- * launches keep 16.  0 (default) = 32 below SWRT_BIG_TILE_BELOW packets per
- * 16x16 tile on average (build default 0: measured no faster), else 16.
- * Results are bit-identical for any setting. */
-int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
-
 /* Launch shape of the LDS-tiled two-snapshot launches (fields with v_y ==
  * -u_x) when tiles hold few packets: 256-thread workgroups with a 256-VGPR
  * budget whose stencil gather issues each tap's LDS reads three taps ahead
@@ -241,19 +187,19 @@ int swrt_set_tile_cells(swrt_ctx* ctx, int cells);
  * order: bit-identical for any setting. */
 int swrt_set_sparse_tiles(swrt_ctx* ctx, int mode);
 
-/* Packet streams of the LDS-tiled leapfrog: 2 (default), 4 or 1.  With S > 1
- * every launch runs as S part launches — every S-th tile of each XCD band —
- * on the context's packet stream and S-1 more streams.  Between re-binnings
- * the parts advance disjoint packet ranges, so one stream's launch k
- * overlaps another's launch k+1: one part's tail runs under the other's
- * body instead of leaving CUs idle at every launch boundary.  The launch
- * after a re-binning's sort launch (which gathers its input from any slot)
- * and any call that reads the packets (or re-bins them) first order the
- * extra streams' work before their own; swrt_synchronize waits for all.
- * Results are bit-identical for every setting.  4 measured slower than 2
- * (1.65-1.79e10 vs 2.13-2.18e10 packet-steps/s, with 4 or 8 hardware queues
- * per process alike).  Ensembles under 65,536 packets always use one
- * stream (the split costs more than it returns there). */
+/* Packet streams of the LDS-tiled leapfrog: 2 (default) or 1.  With 2 every
+ * launch runs as two part launches — the even and the odd band positions of
+ * each XCD band's tiles (the mapping: swraytracing_amd/csrc/swrt_share.hpp)
+ * — on the context's packet stream and a second stream.
+ * Between re-binnings the parts advance disjoint packet ranges, so one
+ * stream's launch k overlaps the other's launch k+1: one part's tail runs
+ * under the other's body instead of leaving CUs idle at every launch
+ * boundary.  The launch after a re-binning's sort launch (which gathers its
+ * input from any slot) and any call that reads the packets (or re-bins them)
+ * first order the second stream's work before their own; swrt_synchronize
+ * waits for both.  Results are bit-identical for either setting.  Ensembles
+ * under 65,536 packets always use one stream (the split costs more than it
+ * returns there). */
 int swrt_set_packet_streams(swrt_ctx* ctx, int streams);
 
 /* Advance the device-resident packets by nsteps leapfrog steps
@@ -444,11 +390,6 @@ int swrt_qg_step(swrt_ctx* ctx, double dt, int64_t nsteps);
  * SWRT_ERR_STATE. */
 int swrt_qg_step_speculative(swrt_ctx* ctx, double dt);
 int swrt_qg_resolve(swrt_ctx* ctx, int accept);
-/* 1: steady AB3 steps are replayed from hipGraphs of the step's 9 launches
- * (one per qk buffer parity and dt; re-captured when dt changes).  0
- * (default): plain launches, measured faster on ROCm 7 (73.5 vs 67.5 us per
- * 512^2 two-layer step).  Performance only: results are identical. */
-int swrt_qg_set_graphs(swrt_ctx* ctx, int on);
 /* 1 (default): the swrt_qg_* calls run on a second HIP stream of the
  * context, so the next PDE step, its CFL speed and snapshot overlap the
  * packet launch that reads the previous snapshots.  Slot reads and writes
@@ -513,15 +454,26 @@ int swrt_set_timing(swrt_ctx* ctx, int every);
 /* Sum of HIP-event-measured durations of the packet kernel launches since the
  * last reset (synchronizes). */
 int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launches);
+/* Observed shader clock over a region of the packet stream: swrt_clock_stamp
+ * (ctx, 0) before it and (ctx, 1) after it each enqueue (after every queued
+ * packet launch) one-wave workgroups on every XCD that record the shader-cycle
+ * counter (s_memtime) and the 100 MHz real-time counter (s_memrealtime);
+ * swrt_clock_ghz synchronises and returns the median over same-XCD
+ * (start, end) pairs of cycles / seconds, and (spread_out, may be NULL) the
+ * pairs' (max - min) / median.  Normalises a throughput measured on one box to
+ * the clock it actually ran at (the chip lowers its clock under load). */
+int swrt_clock_stamp(swrt_ctx* ctx, int which);
+int swrt_clock_ghz(swrt_ctx* ctx, double* ghz_out, double* spread_out);
 
 /* Debug knobs (test infrastructure; no reference counterpart).
  * SWRT_DEBUG_HAZARD_CHECK 0/1: a host-side happens-before checker of the
  *   packet buffers across the packet streams (swrt_set_packet_streams): every
  *   re-binning, part launch, join and synchronisation is mirrored with one
- *   vector clock per stream; a launch whose reads or writes of a packet
- *   buffer are not ordered after a conflicting access on another stream is
- *   refused before it is queued (SWRT_ERR_STATE, swrt_last_error names both
- *   accesses).  Also on when the environment has SWRT_HAZARD_CHECK=1 at
+ *   vector clock per stream, each part launch's accesses covering the tiles
+ *   its workgroups actually take (the device's own mapping); a launch whose
+ *   reads or writes of a packet buffer are not ordered after a conflicting
+ *   access on another stream is refused before it is queued (SWRT_ERR_STATE,
+ *   swrt_last_error names both accesses).  Also on when the environment has SWRT_HAZARD_CHECK=1 at
  *   swrt_create.  Turning it on synchronises the context.
  * SWRT_DEBUG_SPIN_US n: each extra packet stream runs a ~n us sleep kernel
  *   before every part launch of its own, so a call's extra-stream parts
@@ -536,23 +488,33 @@ int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launch
  *   pass (one kernel); 0 = the separate column pass + Jacobian-rows kernel —
  *   the same values, kept so tests can compare them bit for bit.  Applies
  *   when no packets share the context (beside packet launches the separate
- *   passes' smaller workgroups run faster); 2 = beside packets too.
- * SWRT_DEBUG_QG_ROWS_VECS 0/1/2/4: two-layer fused mode beside packets: the
- *   planes each workgroup of the first inverse pass builds and transforms
- *   (0 = 4); the same values for any setting.
+ *   passes' smaller workgroups run faster).
  * SWRT_DEBUG_QG_UPDATE_COLS 0/1 (default 1): fused mode runs the last pass of
  *   J's forward transform inside the AB3 update (one kernel; the spectrum
  *   never goes to memory); 0 = the separate column pass + update — the same
  *   values, kept so tests can compare them bit for bit.  Applies, like
  *   SWRT_DEBUG_QG_JFUSE, unless packet launches share the context beside a
- *   separate QG stream; 2 = beside packets too. */
+ *   separate QG stream.
+ * SWRT_DEBUG_SHARE_SKEW 0/1: test-only; 1 makes the launch that ends each
+ *   re-binning cycle split its tiles unevenly between the two packet streams
+ *   (2/3 : 1/3) — a tile-to-stream mapping that differs from the previous
+ *   launch's, the race of round 4.  Accepted only while the hazard checker is
+ *   on, which models the tiles each part launch takes and refuses such a
+ *   launch (SWRT_ERR_STATE) before it is queued.
+ * SWRT_DEBUG_CORRUPT_COUNT d: test-only; the next re-binning adds d to one
+ *   tile's count before its scan.  The scan's own check (counts >= 0, summing
+ *   to the packets) then leaves an empty binning — no kernel runs over a bad
+ *   range — and the next host synchronisation (swrt_synchronize,
+ *   swrt_packets_get, ...) returns SWRT_ERR_STATE; the packet state is lost
+ *   until swrt_packets_set. */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3
 #define SWRT_DEBUG_HAZARD_CHECKS 4
 #define SWRT_DEBUG_QG_JFUSE 5
-#define SWRT_DEBUG_QG_ROWS_VECS 6
 #define SWRT_DEBUG_QG_UPDATE_COLS 7
+#define SWRT_DEBUG_SHARE_SKEW 8
+#define SWRT_DEBUG_CORRUPT_COUNT 9
 int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
 int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
 

@@ -26,8 +26,6 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SWRT_LIB_PATH") or os.path.join(_HERE, "libswrt.so")
 
 SWRT_OK = 0
-# swrt_set_tail_split defaults of the library build (SWRT_TAIL_SPLIT / _QUARTERS in swrt_api.hip)
-DEFAULT_TAIL_SPLIT = (0, 0)
 ERRORS = {1: "SWRT_ERR_ARG", 2: "SWRT_ERR_HIP", 3: "SWRT_ERR_STATE", 4: "SWRT_ERR_ALLOC"}
 
 _D = ctypes.c_double
@@ -65,15 +63,9 @@ SIGNATURES = {
     "swrt_packets_get_device": (_INT, [_VP, _VP, _VP, ctypes.c_int64]),
     "swrt_packets_count": (_I, [_VP]),
     "swrt_set_locality": (_INT, [_VP, _I, _I]),
-    "swrt_set_tile_order": (_INT, [_VP, _INT]),
     "swrt_set_kernel": (_INT, [_VP, _INT]),
-    "swrt_set_cell_sort": (_INT, [_VP, _INT]),
-    "swrt_set_tail_split": (_INT, [_VP, _INT, _INT]),
-    "swrt_set_blend_mode": (_INT, [_VP, _INT]),
     "swrt_set_gather_mode": (_INT, [_VP, _INT]),
-    "swrt_set_lanes_per_packet": (_INT, [_VP, _INT]),
     "swrt_set_sparse_tiles": (_INT, [_VP, _INT]),
-    "swrt_set_tile_cells": (_INT, [_VP, _INT]),
     "swrt_set_packet_streams": (_INT, [_VP, _INT]),
     "swrt_advance": (_INT, [_VP, _D, _I, _D, _D, _INT, _D, _D, _D, _I]),
     "swrt_advance_intervals": (_INT, [_VP, _INT, _VP, _I, _D, _D, _D, _D, _D, _I]),
@@ -99,7 +91,6 @@ SIGNATURES = {
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_step_speculative": (_INT, [_VP, _D]),
     "swrt_qg_resolve": (_INT, [_VP, _INT]),
-    "swrt_qg_set_graphs": (_INT, [_VP, _INT]),
     "swrt_qg_set_stream": (_INT, [_VP, _INT]),
     "swrt_qg_set_fused": (_INT, [_VP, _INT]),
     "swrt_qg_max_speed": (_INT, [_VP, ctypes.POINTER(_D)]),
@@ -116,6 +107,8 @@ SIGNATURES = {
     "swrt_get_stream": (_INT, [_VP, ctypes.POINTER(_VP)]),
     "swrt_set_timing": (_INT, [_VP, _INT]),
     "swrt_kernel_time": (_INT, [_VP, _INT, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
+    "swrt_clock_stamp": (_INT, [_VP, _INT]),
+    "swrt_clock_ghz": (_INT, [_VP, ctypes.POINTER(_D), ctypes.POINTER(_D)]),
     "swrt_debug_set": (_INT, [_VP, _INT, _I]),
     "swrt_debug_get": (_INT, [_VP, _INT, ctypes.POINTER(_I)]),
 }
@@ -126,8 +119,9 @@ DEBUG_SPIN_US = 2
 DEBUG_LEGACY_PARK = 3
 DEBUG_HAZARD_CHECKS = 4
 DEBUG_QG_JFUSE = 5
-DEBUG_QG_ROWS_VECS = 6
 DEBUG_QG_UPDATE_COLS = 7
+DEBUG_SHARE_SKEW = 8
+DEBUG_CORRUPT_COUNT = 9
 
 _lib = None
 
@@ -349,11 +343,6 @@ class Context:
     def set_locality(self, rebin_every=4, tile=0):
         self._chk(self._L.swrt_set_locality(self._h, int(rebin_every), int(tile)), "swrt_set_locality")
 
-    def set_tile_order(self, longest_first=1):
-        """swrt_set_tile_order: LDS-tiled launches take each XCD band's tiles
-        longest first (1, default) or in spatial order (0); same results."""
-        self._chk(self._L.swrt_set_tile_order(self._h, int(longest_first)), "swrt_set_tile_order")
-
     def set_kernel(self, variant=0):
         self._chk(self._L.swrt_set_kernel(self._h, int(variant)), "swrt_set_kernel")
 
@@ -366,29 +355,9 @@ class Context:
         """swrt_set_sparse_tiles: 0 auto (below SWRT_SPARSE_BELOW packets per tile), 1 never, 2 always; same bits."""
         self._chk(self._L.swrt_set_sparse_tiles(self._h, int(mode)), "swrt_set_sparse_tiles")
 
-    def set_lanes_per_packet(self, lanes=0):
-        """swrt_set_lanes_per_packet: 0 auto (build threshold; off by default), 1, 2; same bits."""
-        self._chk(self._L.swrt_set_lanes_per_packet(self._h, int(lanes)), "swrt_set_lanes_per_packet")
-
-    def set_tile_cells(self, cells=0):
-        """swrt_set_tile_cells: 0 auto (build threshold; off by default), 16, 32; same bits."""
-        self._chk(self._L.swrt_set_tile_cells(self._h, int(cells)), "swrt_set_tile_cells")
-
     def set_packet_streams(self, streams=2):
-        """swrt_set_packet_streams: 2 (default: tile launches split over two streams), 4 or 1; same bits."""
+        """swrt_set_packet_streams: 2 (default: tile launches split over two streams) or 1; same bits."""
         self._chk(self._L.swrt_set_packet_streams(self._h, int(streams)), "swrt_set_packet_streams")
-
-    def set_blend_mode(self, mode=0):
-        """0: bit-exact interpolate-then-blend; 1: blend in the LDS window (tolerance parity)."""
-        self._chk(self._L.swrt_set_blend_mode(self._h, int(mode)), "swrt_set_blend_mode")
-
-    def set_cell_sort(self, every_launch=0):
-        self._chk(self._L.swrt_set_cell_sort(self._h, int(every_launch)), "swrt_set_cell_sort")
-
-    def set_tail_split(self, halves_per_xcd=0, quarters_per_xcd=0):
-        """Half- then quarter-tile workgroups for the last tiles of each XCD band (launch shape only)."""
-        self._chk(self._L.swrt_set_tail_split(self._h, int(halves_per_xcd), int(quarters_per_xcd)),
-                  "swrt_set_tail_split")
 
     def advance(self, dt, nsteps, f, gH, nslots=1, alpha0=0.0, dalpha=0.0, bump=1e-13, save_every=0):
         self._chk(self._L.swrt_advance(self._h, float(dt), int(nsteps), float(f), float(gH), int(nslots),
@@ -564,10 +533,6 @@ class Context:
         """swrt_qg_resolve: accept (the speculative step becomes current) or drop it."""
         self._chk(self._L.swrt_qg_resolve(self._h, int(bool(accept))), "swrt_qg_resolve")
 
-    def qg_set_graphs(self, on=False):
-        """hipGraph replay of steady AB3 steps (swrt_qg_set_graphs); results identical."""
-        self._chk(self._L.swrt_qg_set_graphs(self._h, int(bool(on))), "swrt_qg_set_graphs")
-
     def qg_set_stream(self, separate=True):
         """QG PDE on its own stream, overlapping the packet launches (swrt_qg_set_stream)."""
         self._chk(self._L.swrt_qg_set_stream(self._h, int(bool(separate))), "swrt_qg_set_stream")
@@ -639,6 +604,16 @@ class Context:
         self._chk(self._L.swrt_kernel_time(self._h, int(reset), ctypes.byref(ms), ctypes.byref(n)),
                   "swrt_kernel_time")
         return ms.value, n.value
+
+    def clock_stamp(self, which):
+        """swrt_clock_stamp: 0 before, 1 after a region of packet-stream work."""
+        self._chk(self._L.swrt_clock_stamp(self._h, int(which)), "swrt_clock_stamp")
+
+    def clock_ghz(self):
+        """swrt_clock_ghz: (median observed shader clock in GHz, relative spread) between the stamps."""
+        g, s = _D(), _D()
+        self._chk(self._L.swrt_clock_ghz(self._h, ctypes.byref(g), ctypes.byref(s)), "swrt_clock_ghz")
+        return g.value, s.value
 
     def debug_set(self, key, value):
         """swrt_debug_set: DEBUG_HAZARD_CHECK, DEBUG_SPIN_US, DEBUG_LEGACY_PARK (test infrastructure)."""

@@ -44,42 +44,12 @@ constexpr int kXkaMargin = 3;           // xka_tile_kernel: drift margin (cells)
 #ifndef SWRT_SORT_LEAD
 #define SWRT_SORT_LEAD 1
 #endif
-#ifndef SWRT_QG_GRAPHS
-#define SWRT_QG_GRAPHS 0
-#endif
-#ifndef SWRT_TILE_ORDER
-#define SWRT_TILE_ORDER 1
-#endif
-#ifndef SWRT_TAIL_QUARTERS
-#define SWRT_TAIL_QUARTERS 0
-#endif
-#ifndef SWRT_TAIL_SPLIT
-#define SWRT_TAIL_SPLIT 0
-#endif
 #ifndef SWRT_TILE_THREADS
 #define SWRT_TILE_THREADS 512
 #endif
 constexpr int kTile = SWRT_TILE;                // LDS tile kernel: cells per tile side
 constexpr int kMargin = SWRT_MARGIN;            // LDS tile kernel: drift margin (cells)
 constexpr int kTileThreads = SWRT_TILE_THREADS;
-// Paired-lane tile launches (swrt_tile.hpp PAIR) below this many packets per
-// tile, and 32x32-cell tiles (one 1024-thread workgroup per CU, its 151 KB
-// window filling the LDS) below SWRT_BIG_TILE_BELOW packets per 16x16 tile.
-// Both target small shards (~120 packets per 16x16 tile at 1.25e5 packets on
-// 512^2: one busy wave per SIMD) and both are bit-identical, but neither was
-// faster on the hardware (1.25e5: 60.0 / 62.0 vs 58.1-61.2 us per 5-step
-// launch; 32x32 at 5e5: 171 vs 129 us; profiles/r03_small_shard.md): at that
-// density the 16 lanes of a ds_read_b128 group read 16 distinct nodes and the
-// LDS bank conflicts double (2.0-2.3 vs 1.22 cycles per access), which more
-// busy waves cannot hide.  Auto-selection is therefore off (0); both stay
-// available through swrt_set_lanes_per_packet / swrt_set_tile_cells.
-#ifndef SWRT_PAIR_BELOW
-#define SWRT_PAIR_BELOW 0
-#endif
-constexpr int kPairBelow = SWRT_PAIR_BELOW;
-#ifndef SWRT_BIG_TILE_BELOW
-#define SWRT_BIG_TILE_BELOW 0
-#endif
 // Sparse-tile launches: below SWRT_SPARSE_BELOW packets per 16x16 tile on
 // average (a strong-scaling shard: ~120 at 1.25e5 packets on 512^2) a
 // 512-thread workgroup has one or two busy waves, one per SIMD, each capped
@@ -100,9 +70,6 @@ constexpr int kPairBelow = SWRT_PAIR_BELOW;
 constexpr int kSparseBelow = SWRT_SPARSE_BELOW;
 constexpr int kSparseThreads = 256;
 constexpr int kSparsePrefetch = 3;
-constexpr int kBigTile = 32;
-constexpr int kBigTileThreads = 1024;
-constexpr int kBigTileBelow = SWRT_BIG_TILE_BELOW;
 
 struct Slot {
   double* nodes = nullptr;  // padded interleaved records
@@ -159,6 +126,9 @@ struct QGState {
   bool Fj_rows = false;        // Fj is J after its first forward pass only: the update runs the last
                                // (qg_update_cols_kernel) and renames the tendency history
   bool spec_rot = false;       // the pending speculative step stored only its tendency (Qm1_spare)
+  bool spec_rb = false;        // the pending speculative step's CFL read-back is still queued (not popped by
+                               // swrt_qg_max_speed_result): a reject drops it only then
+  int spec_rb_slot = 0;        // ... its FIFO slot
   // fused mode: the post-step transforms of the current qk — the next step's
   // Jacobian spectrum (PT[0, nn) after its forward FFT), the CFL speed
   // (dmax) and layer 0's grid_U (the snapshot) — from ONE batched inverse
@@ -168,24 +138,10 @@ struct QGState {
   bool post_valid = false;      // both phases of qg_post done for post_of (valid for the current qk when
   bool post_inv_valid = false;  // post_of == qk); post_inv_valid: its first phase (the inverse transforms)
   double exp_dt = -1.0;        // dt of the current E1/E2
-  // replayable AB3 steps (hipGraph), one per qk buffer parity, for one dt
-  hipGraphExec_t gexec[2] = {nullptr, nullptr};
-  const double2* gqk[2] = {nullptr, nullptr};
-  double gdt[2] = {0.0, 0.0};
-  const double2* gtw[2] = {nullptr, nullptr};  // twiddles baked into each graph
   int64_t steps = 0;
   double t = 0.0;
   bool has_prev = false;
 };
-
-static void qg_drop_graphs(QGState& q) {
-  for (int i = 0; i < 2; ++i) {
-    if (q.gexec[i]) (void)hipGraphExecDestroy(q.gexec[i]);
-    q.gexec[i] = nullptr;
-    q.gqk[i] = nullptr;
-  }
-}
-
 
 struct Timing {
   std::vector<hipEvent_t> ev;  // pairs
@@ -211,9 +167,8 @@ struct swrt_ctx {
   hipStream_t qstream = nullptr;
   bool qg_sep = true;
   bool qg_fused = true;  // swrt_qg_set_fused
-  int qg_jfuse = 1;  // fused mode, 2 layers: the column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE; 2: beside packets too)
-  int qg_rows_vecs = 0;  // fused mode, 2 layers beside packets: planes per first-pass workgroup (0: 4)
-  int qg_update_cols = 1;  // fused mode: J's last forward pass inside the update (SWRT_DEBUG_QG_UPDATE_COLS; 2: beside packets too)
+  int qg_jfuse = 1;  // fused mode, 2 layers, no packets beside: the column pass fused with the Jacobian (SWRT_DEBUG_QG_JFUSE)
+  int qg_update_cols = 1;  // fused mode, no packets beside: J's last forward pass inside the update (SWRT_DEBUG_QG_UPDATE_COLS)
   std::vector<Slot> spares;
   // packets (device order = spatially binned; perm maps to the original index)
   double* dx = nullptr;  // 2N
@@ -243,25 +198,17 @@ struct swrt_ctx {
   int64_t key_nx = 0;       // ... on the grid the launch read (its first snapshot's nx and dx: the keys
   double key_dx = 0.0;      //     depend on those only, not on the field values — new snapshots keep them valid)
   bool counts_zero = false;  // bins' count block is all zero (cleared by the last scan)
-  int cell_sort = 0;        // 0: in-tile cell sort only on the first launch after a re-binning; 1: every launch
   bool sort_lead = SWRT_SORT_LEAD;  // in-tile sort keys lead by the group-velocity drift
-  int tail_split = SWRT_TAIL_SPLIT;  // tiles per XCD band run as two half-tile workgroups (swrt_tile.hpp)
-  int tail_quarters = SWRT_TAIL_QUARTERS;  // ... then as four quarter-tile workgroups
-  bool tile_order = SWRT_TILE_ORDER;  // LDS-tiled launches take each XCD band's tiles longest first
-  bool qg_graphs = SWRT_QG_GRAPHS;         // replay steady QG steps as hipGraphs
-  int blend_mode = 0;       // 0: interpolate each snapshot, then blend (bit-exact); 1: blend in the LDS window
   int gather_mode = 0;      // 0: stencil sums mul then add (bit-exact); 1: fused multiply-add (tolerance)
-  int lanes_per_packet = 0; // LDS-tiled two-snapshot launches: 1, 2 (paired lanes), 0 = by packets per tile
-  int tile_mode = 0;        // leapfrog tile size: 0 auto (32 for small ensembles), 16, 32
   int sparse_mode = 0;      // sparse-tile launches: 0 auto (below kSparseBelow packets per tile), 1 never, 2 always
-  // Several packet streams (swrt_set_packet_streams S = 2 or 4): each
-  // LDS-tiled leapfrog launch runs as S part launches — every S-th band
-  // position of every XCD band — on `stream` and the extra streams sx[].
-  // Within a re-binning cycle the parts touch disjoint packet ranges, so one
-  // part's launch k overlaps another's launch k+1 (one part's tail under the
-  // other's body).  The extra streams' work is joined back into `stream`
-  // (join_b) before anything else reads the packets.
-  static constexpr int kMaxPacketStreams = 4;
+  // Two packet streams (swrt_set_packet_streams 2, the default): each
+  // LDS-tiled leapfrog launch runs as 2 part launches — the even and the odd
+  // band positions of every XCD band — on `stream` and the extra stream
+  // sx[0].  Within a re-binning cycle the parts touch disjoint packet ranges,
+  // so one part's launch k overlaps the other's launch k+1 (one part's tail
+  // under the other's body).  The extra stream's work is joined back into
+  // `stream` (join_b) before anything else reads the packets.
+  static constexpr int kMaxPacketStreams = 2;
   int packet_streams = 2;           // default: two (measured +2-4 %, bit-identical); 1 = one launch per step
   hipStream_t sx[kMaxPacketStreams - 1] = {};  // the extra packet streams
   hipEvent_t jx[kMaxPacketStreams - 1] = {};   // their join events
@@ -269,6 +216,7 @@ struct swrt_ctx {
   hipEvent_t fork_ev = nullptr;
   int b_pending = 0;              // extra streams holding packet work not yet ordered before stream's
   int bin_tile = 0;         // cells per tile side of the current binning
+  int bin_lanes = 0;        // ... and the workgroup width its tile order was ranked for (tile_threads)
   bool cells_sorted = false;  // packets of every tile are in cell order (a tile launch wrote them)
   // history
   double* hx = nullptr;
@@ -317,7 +265,6 @@ struct swrt_ctx {
   bool o_order_valid = false;  // computed for the current binning
   bool o_sorted = false;       // the packets themselves are in the in-tile cell order of the current binning
                                // (swrt_ode23_f1's tile_cell_sort_kernel): the stages take them in slot order
-  int o_order_split = 0;       // ... and launch shape
   double* o_ynx = nullptr;
   double* o_ynk = nullptr;
   // a third state set (x, k, F) for swrt_ode23_run's speculative attempt
@@ -353,6 +300,16 @@ struct swrt_ctx {
   HazardChecker hz;
   int debug_spin_us = 0;
   bool debug_legacy_park = false;
+  bool debug_share_skew = false;  // test-only: the cycle-ending launch takes an uneven share (checker on only)
+  int debug_corrupt_count = 0;    // test-only: added to one tile count before the next scan (once)
+  // device-raised errors (host-visible pinned memory): [0] the binning scan's
+  // count check failed (bin_scan_kernel) — read after host synchronisations
+  int* dev_err = nullptr;
+  int* dev_err_d = nullptr;
+  bool packets_lost = false;  // a failed binning left the packet state undefined (until swrt_packets_set)
+  // shader-clock probe (swrt_clock_stamp): 2 stamps x kClockWaves waves x
+  // {s_memtime, s_memrealtime, XCC id}
+  unsigned long long* clk = nullptr;
 };
 
 namespace {
@@ -499,6 +456,25 @@ void hz_api(swrt_ctx* c) {
 // any packet stream before has completed.
 void hz_synced(swrt_ctx* c) {
   if (c->hz.on) c->hz.sync(0);
+}
+
+// After a host synchronisation with the packet stream: an error the device
+// raised since (bin_scan_kernel's count check) becomes SWRT_ERR_STATE here,
+// and the packet state — advanced by launches over an empty binning — is
+// marked lost until the next swrt_packets_set.
+int dev_err_check(swrt_ctx* c) {
+  if (!c->dev_err || !c->dev_err[0]) return SWRT_OK;
+  c->dev_err[0] = 0;
+  c->packets_lost = true;
+  c->bin_valid = false;
+  c->keys_fresh = false;
+  c->src_pending = false;
+  c->o_order_valid = false;
+  c->o_sorted = false;
+  return fail(c, SWRT_ERR_STATE,
+              "packet binning corrupted: the tile counts do not sum to the packets (device check in "
+              "bin_scan_kernel); no packet kernel ran over the bad ranges, but the packet state is lost — "
+              "swrt_packets_set again");
 }
 
 // Wait for the extra packet streams (host side).
@@ -721,17 +697,27 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
 // +3 %, 2.5e5 +6 %, 5e5 +4 %, 1e6 +3.7 %).
 constexpr int64_t kMultiStreamFrom = 65536;
 
-// The LDS-tiled launch of TileArgs t: one launch over every tile, or (S
-// packet streams) S part launches of every S-th band position, parts 1..S-1
-// on the extra streams after everything queued on the packet stream so far
-// (this call's re-binning, memsets and history growth).  A timed pair
-// brackets the first part's start and the last part's end.
-// Hazard checker: the accesses of the tile launch t as nparts part launches
-// (part p on stream p: the packet stream, then the extra streams), forked from
-// the packet stream when nparts > 1.  Checked on a copy of the checker state,
-// committed only if every access is ordered: a hazard refuses the launch.
-int hz_tile_launch(swrt_ctx* c, const TileArgs& t, int nparts) {
+// The LDS-tiled launch of TileArgs t: one launch over every tile, or (two
+// packet streams) two part launches, each a share of every XCD band's tiles
+// (swrt_share.hpp), the second on the extra stream after everything queued
+// on the packet stream so far (this call's re-binning, memsets and history
+// growth).  A timed pair brackets the first part's start and the last
+// part's end.
+//
+// Hazard checker: the accesses of the launch's parts (part p on stream p),
+// forked from the packet stream when split, each over the band slots its
+// workgroups take — enumerated with the device's own mapping (share_slot),
+// so a launch whose tile-to-stream mapping differs from the previous
+// launch's is seen to touch the other stream's tiles.  Checked on a copy of
+// the checker state, committed only if every access is ordered: a hazard
+// refuses the launch before anything is queued.
+int hz_tile_launch(swrt_ctx* c, const TileArgs& t, const TileShare* parts, int nparts, bool zero_counts) {
   HazardChecker h = c->hz;
+  if (zero_counts) {  // the next-binning counts' memset, on the packet stream before the parts
+    const uint64_t tm = h.op(0);
+    if (!h.access(0, tm, t.next_counts, kHzWrite, HzRegion::all(), "the next-binning counts' memset"))
+      return fail(c, SWRT_ERR_STATE, h.err);
+  }
   if (nparts > 1) {
     h.record(c->fork_ev, 0);
     for (int i = 1; i < nparts; ++i) h.wait(i, c->fork_ev);
@@ -739,7 +725,7 @@ int hz_tile_launch(swrt_ctx* c, const TileArgs& t, int nparts) {
   const StepArgs& a = t.s;
   for (int p = 0; p < nparts; ++p) {
     const uint64_t tp = h.op(p);
-    const HzRegion r = nparts > 1 ? HzRegion::of_part(h.epoch, p, nparts) : HzRegion::all();
+    const HzRegion r = HzRegion::of_share(h.epoch, parts[p]);
     const char* what = t.src ? "a part of the sort launch after a re-binning" : "a part launch";
     // the sort launch after an indirect re-binning gathers its input through
     // src_idx from any slot of the input buffers
@@ -764,47 +750,82 @@ __global__ void debug_spin_kernel(int iters) {
   for (int i = 0; i < iters; ++i) __builtin_amdgcn_s_sleep(127);
 }
 
+// debug (SWRT_DEBUG_CORRUPT_COUNT): add `delta` to one tile's count before a
+// scan, as a corrupted binning would
+__global__ void debug_corrupt_count_kernel(int* counts, int tile, int delta) {
+  if (threadIdx.x == 0) counts[tile] += delta;
+}
+
+// Shader-clock probe (swrt_clock_stamp): kClockWaves one-wave workgroups
+// (dispatched round-robin over the 8 XCDs) each record the shader-cycle
+// counter (s_memtime), the 100 MHz real-time counter (s_memrealtime) and
+// their XCD.  Start and end stamps of one XCD bracket a timed region:
+// cycles / seconds = the clock the chip ran at over it (MI355X_MICROARCH.md,
+// "DVFS give-back" item 6).  Plain vector stores, a buffer of its own.
+constexpr int kClockWaves = 32;
+constexpr double kRealTimeHz = 100e6;
+__global__ void clock_stamp_kernel(unsigned long long* out) {
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const unsigned long long t = __builtin_amdgcn_s_memtime();
+  const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    out[3 * blockIdx.x + 0] = t;
+    out[3 * blockIdx.x + 1] = r;
+    out[3 * blockIdx.x + 2] = xcc & 0xf;
+  }
+}
+
+// zero_counts: clear t.next_counts (the next binning's counts) first, on the
+// packet stream — after the hazard check, so a refused launch queues nothing.
 template <typename F>
-int launch_tiles(swrt_ctx* c, F kernel, unsigned wgrid, int nt, TileArgs t) {
+int launch_tiles(swrt_ctx* c, F kernel, int nt, TileArgs t, bool zero_counts) {
+  const int ntiles = t.ntx * t.ntx;
   const int S = c->n >= kMultiStreamFrom ? c->packet_streams : 1;
-  bool multi = S > 1 && t.split == 0 && wgrid % (8 * S) == 0 && c->stream == c->stream0;
-  for (int i = 0; multi && i < S - 1; ++i) multi = c->sx[i] != nullptr;
-  t.sparts = S;
+  // test-only (SWRT_DEBUG_SHARE_SKEW): the launch that ends a re-binning
+  // cycle takes an uneven share — a mapping that differs from the previous
+  // launch's, round 4's race; only ever run with the checker on, which
+  // refuses it (swrt_debug_set enforces that)
+  const bool skew = c->debug_share_skew && t.next_keys != nullptr;
+  if (skew && !c->hz.on) return fail(c, SWRT_ERR_STATE, "the skewed share runs only under the hazard checker");
+  const bool multi = S == 2 && c->stream == c->stream0 && c->sx[0] != nullptr &&
+                     (skew ? ntiles % 8 == 0 && ntiles / 8 >= 3 : ntiles % 16 == 0);
   if (!multi) {
     // one launch over every tile on the packet stream: it reads and writes
-    // packets that the extra streams' part launches of an earlier call may
-    // still be writing (swrt_set_tail_split > 0 takes this branch)
+    // packets that the extra stream's part launch of an earlier call may
+    // still be writing
+    t.sh = TileShare{ntiles, -1, 1, kShareEven};
     HIPCHK_RC(join_b(c));
-    if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, 1));
-    t.spart = -1;
-    launch_k(c, kernel, dim3(wgrid), dim3(nt), t);
+    if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, &t.sh, 1, zero_counts));
+    if (zero_counts) HIPCHK(c, hipMemsetAsync(t.next_counts, 0, sizeof(int) * ntiles, c->stream));
+    launch_k(c, kernel, dim3((unsigned)share_grid(t.sh)), dim3(nt), t);
     return SWRT_OK;
   }
-  if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, S));
-  // Part i always takes the band positions = i (mod S): a stream's
-  // consecutive part launches own the same tiles, so stream order alone
-  // orders them, and stream 0's next launch may start while stream 1's
-  // previous one still runs.  A launch with another tile-to-stream mapping
-  // would race it without a join first (measured: a hang,
-  // profiles/r04_stream_split).
+  const TileShare sh[2] = {TileShare{ntiles, 0, 2, skew ? kShareSkew : kShareEven},
+                           TileShare{ntiles, 1, 2, skew ? kShareSkew : kShareEven}};
+  if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, sh, 2, zero_counts));
+  if (zero_counts) HIPCHK(c, hipMemsetAsync(t.next_counts, 0, sizeof(int) * ntiles, c->stream));
+  // Part p takes the same slots at every launch of a binning (the product
+  // rule, kShareEven): a stream's consecutive part launches own the same
+  // tiles, so stream order alone orders them, and stream 0's next launch may
+  // start while stream 1's previous one still runs.  A launch with another
+  // mapping races it unless joined first — the checker, which enumerates the
+  // slots each part takes, refuses it (round 4's hang, profiles/r04_stream_split).
   HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
-  for (int i = 0; i < S - 1; ++i) HIPCHK(c, hipStreamWaitEvent(c->sx[i], c->fork_ev, 0));
-  t.spart = 0;
-  hipExtLaunchKernelGGL(kernel, dim3(wgrid / S), dim3(nt), 0, c->stream, c->kev0, nullptr, 0, t);
-  for (int i = 0; i < S - 1; ++i) {
-    if (c->debug_spin_us > 0)
-      hipLaunchKernelGGL(debug_spin_kernel, dim3(1), dim3(64), 0, c->sx[i], (c->debug_spin_us + 3) / 4);
-    t.spart = i + 1;
-    hipExtLaunchKernelGGL(kernel, dim3(wgrid / S), dim3(nt), 0, c->sx[i], nullptr, i == S - 2 ? c->kev1 : nullptr,
-                          0, t);
-  }
-  c->b_pending = S - 1;
+  HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->fork_ev, 0));
+  t.sh = sh[0];
+  hipExtLaunchKernelGGL(kernel, dim3((unsigned)share_grid(sh[0])), dim3(nt), 0, c->stream, c->kev0, nullptr, 0, t);
+  if (c->debug_spin_us > 0)
+    hipLaunchKernelGGL(debug_spin_kernel, dim3(1), dim3(64), 0, c->sx[0], (c->debug_spin_us + 3) / 4);
+  t.sh = sh[1];
+  hipExtLaunchKernelGGL(kernel, dim3((unsigned)share_grid(sh[1])), dim3(nt), 0, c->sx[0], nullptr, c->kev1, 0, t);
+  c->b_pending = 1;
   c->tail_ev = nullptr;  // slot uses are marked after the join (swrt_advance)
   return SWRT_OK;
 }
 
 // Before a per-packet leapfrog launch (packets updated in place on the packet
-// stream): order the extra streams' part launches of an earlier call first
+// stream): order the extra stream's part launches of an earlier call first
 // (swrt_set_locality(0, ..) after split launches lands here), and tell the
 // hazard checker.
 int leap_launch_prep(swrt_ctx* c, const StepArgs& a) {
@@ -874,19 +895,6 @@ int timed_launch(swrt_ctx* c, const StepArgs& a, unsigned grid, bool count_next,
   return SWRT_OK;
 }
 
-// Tail shape of a tile launch over `ntiles` tiles (swrt_tile.hpp
-// wg_work_range): the split code and the extra workgroups it adds.
-int launch_shape(const swrt_ctx* c, unsigned ntiles, unsigned* extra) {
-  *extra = 0;
-  if (ntiles % 8 != 0 || (c->tail_split <= 0 && c->tail_quarters <= 0)) return 0;
-  const unsigned tpx = ntiles / 8;
-  const unsigned h = std::min<unsigned>((unsigned)std::max(c->tail_split, 0), tpx);
-  const unsigned q = std::min<unsigned>((unsigned)std::max(c->tail_quarters, 0), tpx - h);
-  if (h + q == 0) return 0;
-  *extra = 8u * (h + 3u * q);
-  return (int)(h | (q << 16));
-}
-
 // Longest-first tile order of the LDS-tiled launches, written by every
 // re-binning's scan (bin_scan_kernel) beside the tile starts.
 int* tile_order_of(swrt_ctx* c) { return c->bins + 3 * kMaxBins + 1; }
@@ -905,19 +913,19 @@ bool sparse_tiles(const swrt_ctx* c, int64_t ntiles) {
   return c->n < (int64_t)kSparseBelow * ntiles;
 }
 
-// Tile side of the LDS-tiled leapfrog for this call: 32 for small ensembles
-// on two divergence-free snapshots (the kernel's only 32-cell instantiation),
-// else kTile.  slot0..slot0+nslots-1 are the snapshots the call reads.
-int leap_tile(const swrt_ctx* c, int nslots, int slot0 = 0) {
-  if (!use_tile_kernel(c) || c->tile_mode == 16) return kTile;
+// Threads per workgroup of the LDS-tiled leapfrog launch over `ntiles` tiles
+// of snapshots that are (v5) two divergence-free slots: ONE decision for the
+// launch (tile_launch) and for the re-binning's longest-first tile order,
+// which ranks tiles by the rounds of this many lanes their workgroup runs.
+int tile_threads(const swrt_ctx* c, bool v5_two, int64_t ntiles) {
+  return v5_two && sparse_tiles(c, ntiles) ? kSparseThreads : kTileThreads;
+}
+
+// slots sa .. sa+nslots-1 are two divergence-free snapshots (the five-sum kernels)
+bool two_v5(const swrt_ctx* c, int nslots, int sa) {
   bool v5 = nslots >= 2;
-  for (int i = 0; i < nslots; ++i) v5 = v5 && c->slot[slot0 + i].div_free;
-  const int64_t nx = c->slot[slot0].nx;
-  if (!v5 || c->blend_mode != 0 || c->lanes_per_packet == 2 || nx % kBigTile != 0 || nx / kBigTile < 2)
-    return kTile;
-  if (c->tile_mode == 32) return kBigTile;
-  const int64_t tiles16 = (nx / kTile) * (nx / kTile);
-  return c->n < (int64_t)kBigTileBelow * tiles16 ? kBigTile : kTile;
+  for (int i = 0; i < nslots && v5; ++i) v5 = c->slot[sa + i].div_free;
+  return v5;
 }
 
 int tile_cells(const swrt_ctx* c, int64_t nx) {
@@ -933,8 +941,10 @@ int tile_cells(const swrt_ctx* c, int64_t nx) {
 // indirect: only build the source index of the binned order (c->src_idx);
 // the tile launch that follows reads through it and writes the packets in
 // binned order (saves moving 36 B per packet twice).  Callers other than the
-// leapfrog loop need the packets moved (indirect = false).
-int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
+// leapfrog loop need the packets moved (indirect = false).  lanes: the
+// workgroup width of the launches this binning serves (tile_threads), by
+// which the scan ranks the tile order.
+int rebin(swrt_ctx* c, bool indirect, int tile = 0, int lanes = kTileThreads) {
   if (int rc = join_b(c)) return rc;  // the second stream's half launches wrote packets this pass reads
   const Slot& s = c->slot[0];
   const FieldView v = view_of(s);
@@ -974,12 +984,17 @@ int rebin(swrt_ctx* c, bool indirect, int tile = 0) {
     HIPCHK(c, hipGetLastError());
   }
   c->keys_fresh = false;
+  if (c->debug_corrupt_count != 0) {  // test-only: one corrupted count, once
+    hipLaunchKernelGGL(debug_corrupt_count_kernel, dim3(1), dim3(64), 0, c->stream, c->bins, nbins / 2,
+                       c->debug_corrupt_count);
+    c->debug_corrupt_count = 0;
+  }
   hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->bins, nbins, c->bins + kMaxBins,
-                     c->bins + 2 * kMaxBins, c->tile_order ? tile_order_of(c) : nullptr,
-                     g.tile == kBigTile ? kBigTileThreads : (sparse_tiles(c, nbins) ? kSparseThreads : kTileThreads));
+                     c->bins + 2 * kMaxBins, n, c->dev_err_d, tile_order_of(c), lanes);
   HIPCHK(c, hipGetLastError());
   c->counts_zero = true;
   c->bin_tile = g.tile;
+  c->bin_lanes = lanes;
   if (indirect) {
     hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3(grid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
                        c->dx, c->dk, c->perm, c->keys, n, nbins, c->bins + kMaxBins, c->dx2, c->dk2, c->perm2,
@@ -1016,86 +1031,62 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   t.k_out = c->dk2;
   t.perm_out = c->perm2;
   t.starts = c->bins + 2 * kMaxBins;
-  t.order = c->tile_order ? tile_order_of(c) : nullptr;
-  const bool big = c->bin_tile == kBigTile;
-  t.ntx = (int)((a.f0.nx + c->bin_tile - 1) / c->bin_tile);
-  const unsigned grid = (unsigned)(t.ntx * t.ntx);
-  // half-tile workgroups at the end of each XCD band (swrt_tile.hpp wg_work)
-  unsigned extra = 0;
-  t.split = launch_shape(c, grid, &extra);
-  t.spart = -1;
-  t.sparts = 1;
-  const unsigned wgrid = grid + extra;
+  t.order = tile_order_of(c);
+  if (c->bin_tile != kTile) return fail(c, SWRT_ERR_STATE, "the binning is not the LDS-tiled kernel's");
+  t.ntx = (int)((a.f0.nx + kTile - 1) / kTile);
+  const int ntiles = t.ntx * t.ntx;
   t.next_keys = nullptr;
   t.next_counts = nullptr;
-  t.sort_cells = (c->cell_sort == 1 || !c->cells_sorted) ? 1 : 0;
+  t.sort_cells = c->cells_sorted ? 0 : 1;
   t.src = nullptr;
   // sort keys lead by half the steps until the next sort (swrt_tile.hpp)
-  t.sort_lead = 0.0;
-  if (c->sort_lead) t.sort_lead = 0.5 * a.dt * (c->cell_sort == 1 ? (double)a.nsteps : (double)std::max<int64_t>(1, c->rebin_every));
+  t.sort_lead = c->sort_lead ? 0.5 * a.dt * (double)std::max<int64_t>(1, c->rebin_every) : 0.0;
   if (c->src_pending) {  // first launch after an indirect re-binning (always a sort launch)
     t.src = c->src_idx;
     t.sort_cells = 1;
-    c->src_pending = false;
   }
-  if (count_next && (int)grid == c->nbins) {
-    if (!c->counts_zero && c->hz.on) {
-      const uint64_t tm = c->hz.op(0);
-      if (!c->hz.access(0, tm, c->bins, kHzWrite, HzRegion::all(), "the next-binning counts' memset"))
-        return fail(c, SWRT_ERR_STATE, c->hz.err);
-    }
-    if (!c->counts_zero) HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * grid, c->stream));
-    c->counts_zero = false;
+  bool zero = false;  // the counts' memset, queued by launch_tiles after its hazard check
+  if (count_next && ntiles == c->nbins) {
+    zero = !c->counts_zero;
     t.next_keys = c->keys;
     t.next_counts = c->bins;
+  }
+  const bool fma = c->gather_mode == 1;
+  if (a.nslots == 2) {
+    if (iv ? iv->div_free : two_v5(c, 2, 0)) {
+      if (tile_threads(c, true, ntiles) == kSparseThreads) {
+        if (fma)
+          HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, true, true, kSparsePrefetch, 2>, kSparseThreads, t, zero));
+        else
+          HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, true, false, kSparsePrefetch, 2>, kSparseThreads, t, zero));
+      } else if (fma) {
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true, true>, kTileThreads, t, zero));
+      } else {
+        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, kTileThreads, t, zero));
+      }
+    } else {
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, kTileThreads, t, zero));
+    }
+  } else {
+    if (c->slot[0].div_free && fma)
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, true, true>, kTileThreads, t, zero));
+    else if (c->slot[0].div_free)
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, true>, kTileThreads, t, zero));
+    else
+      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, kTileThreads, t, zero));
+  }
+  HIPCHK(c, hipGetLastError());
+  c->src_pending = false;
+  if (t.next_keys != nullptr) {
+    c->counts_zero = false;
     c->key_nx = a.f0.nx;  // the view this launch bins by (a multi-interval launch: slot i0's)
     c->key_dx = a.f0.dx;
   }
-  if (big) {  // leap_tile chose 32-cell tiles: two divergence-free snapshots (checked again here)
-    if (a.nslots != 2 || !(iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)))
-      return fail(c, SWRT_ERR_STATE, "32-cell tiles need two divergence-free snapshots");
-    if (c->gather_mode == 1)
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true, true>, wgrid, kBigTileThreads, t));
-    else
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kBigTile, kMargin, kBigTileThreads, false, true>, wgrid, kBigTileThreads, t));
-  } else if (a.nslots == 2 && c->blend_mode == 1 && a.nsteps == 1) {
-    HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true>, wgrid, kTileThreads, t));
-  } else if (a.nslots == 2) {
-    if (iv ? iv->div_free : (c->slot[0].div_free && c->slot[1].div_free)) {
-      // paired lanes when the tiles hold few packets (a workgroup would have
-      // one or two busy waves): two waves per packet run instead of one
-      const bool pair = c->lanes_per_packet == 2 ||
-                        (c->lanes_per_packet == 0 && c->n < (int64_t)kPairBelow * (int64_t)grid);
-      const bool sparse = !pair && sparse_tiles(c, grid);
-      if (sparse && c->gather_mode == 1)
-        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, false, true, true, false, kSparsePrefetch, 2>, wgrid, kSparseThreads, t));
-      else if (sparse)
-        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, false, true, false, false, kSparsePrefetch, 2>, wgrid, kSparseThreads, t));
-      else if (pair && c->gather_mode == 1)
-        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true, true>, wgrid, kTileThreads, t));
-      else if (pair)
-        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, false, true>, wgrid, kTileThreads, t));
-      else if (c->gather_mode == 1)
-        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true, true>, wgrid, kTileThreads, t));
-      else
-        HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, false, true>, wgrid, kTileThreads, t));
-    } else {
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads>, wgrid, kTileThreads, t));
-    }
-  } else {
-    if (c->slot[0].div_free && c->gather_mode == 1)
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true, true>, wgrid, kTileThreads, t));
-    else if (c->slot[0].div_free)
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads, false, true>, wgrid, kTileThreads, t));
-    else
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<false, kTile, kMargin, kTileThreads>, wgrid, kTileThreads, t));
-  }
-  HIPCHK(c, hipGetLastError());
   if (t.src != nullptr && c->b_pending && !c->debug_legacy_park) {
     // The first launch after an indirect re-binning reads its input through
-    // src_idx from any slot of dx while its parts run on several streams; the
+    // src_idx from any slot of dx while its parts run on two streams; the
     // next launch's parts would overwrite dx at their own tiles' slots before
-    // the other parts have read them.  The next launches write the third
+    // the other part has read them.  The next launches write the third
     // buffers instead and dx is parked there until the next re-binning
     // (which orders every stream's work first).
     double* x = c->dx; double* k = c->dk; int* pm = c->perm;
@@ -1109,6 +1100,18 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   }
   c->keys_fresh = t.next_keys != nullptr;
   c->cells_sorted = true;  // written in (the input's or this launch's) cell order
+  return SWRT_OK;
+}
+
+// the re-binning of a leapfrog call over slots sa .. sa+nslots-1, when due
+int leap_rebin_if_due(swrt_ctx* c, int nslots, int sa) {
+  if (c->rebin_every <= 0) return SWRT_OK;
+  const bool tiled = use_tile_kernel(c);
+  const int64_t ntiles = tiled ? ((c->slot[sa].nx + kTile - 1) / kTile) * ((c->slot[sa].nx + kTile - 1) / kTile) : 0;
+  const int lanes = tiled ? tile_threads(c, two_v5(c, nslots, sa), ntiles) : kTileThreads;
+  if (!c->bin_valid || c->steps_since_bin >= c->rebin_every ||
+      (tiled && (c->bin_tile != kTile || c->bin_lanes != lanes)))
+    return rebin(c, tiled, tiled ? kTile : 0, lanes);
   return SWRT_OK;
 }
 
@@ -1135,13 +1138,8 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
   int64_t s0 = 0;
   while (s0 < nsteps) {
     int64_t chunk = std::min<int64_t>(kMaxStepsPerLaunch, nsteps - s0);
-    if (c->blend_mode == 1 && nslots == 2 && use_tile_kernel(c)) chunk = 1;  // alpha fixed per launch
     if (c->rebin_every > 0) {
-      const int want = leap_tile(c, nslots, sa);
-      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every || (use_tile_kernel(c) && c->bin_tile != want)) {
-        int rc = rebin(c, use_tile_kernel(c), use_tile_kernel(c) ? want : 0);
-        if (rc) return rc;
-      }
+      if (int rc = leap_rebin_if_due(c, nslots, sa)) return rc;
       chunk = std::min<int64_t>(chunk, c->rebin_every - c->steps_since_bin);
     }
     a.x = c->dx;
@@ -1165,18 +1163,14 @@ int run_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, int
 // across a re-binning), else one interval at a time through run_advance.
 int run_advance_intervals(swrt_ctx* c, int nint, const double* hs, int64_t nsub, double f, double gH,
                           double alpha0, double dalpha, double bump, int64_t save_every) {
-  const bool fused = use_tile_kernel(c) && c->blend_mode == 0 && c->rebin_every > 0 &&
-                     c->rebin_every % nsub == 0 && nsub <= kMaxStepsPerLaunch;
+  const bool fused = use_tile_kernel(c) && c->rebin_every > 0 && c->rebin_every % nsub == 0 &&
+                     nsub <= kMaxStepsPerLaunch;
   const int64_t fpi = save_every > 0 ? nsub / save_every : 0;  // frames per interval
   int i0 = 0;
   while (i0 < nint) {
     int k = 0;
     if (fused) {
-      const int want = leap_tile(c, std::min(nint - i0, kMaxIntervals) + 1, i0);
-      if (!c->bin_valid || c->steps_since_bin >= c->rebin_every || c->bin_tile != want) {
-        int rc = rebin(c, true, want);
-        if (rc) return rc;
-      }
+      if (int rc = leap_rebin_if_due(c, std::min(nint - i0, kMaxIntervals) + 1, i0)) return rc;
       k = (int)std::min<int64_t>({(int64_t)(nint - i0), (c->rebin_every - c->steps_since_bin) / nsub,
                                   (int64_t)kMaxIntervals});
     }
@@ -1305,6 +1299,9 @@ int swrt_create(int device, swrt_ctx** out) {
   ok = ok && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
        hipStreamCreateWithFlags(&c->sx[0], hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t& e : c->jx) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  ok = ok && hipHostMalloc((void**)&c->dev_err, sizeof(int) * 4, hipHostMallocMapped) == hipSuccess &&
+       hipHostGetDevicePointer((void**)&c->dev_err_d, c->dev_err, 0) == hipSuccess;
+  if (c->dev_err) std::memset(c->dev_err, 0, sizeof(int) * 4);
   c->stream0 = c->stream;
   if (const char* e = getenv("SWRT_HAZARD_CHECK")) c->hz.on = atoi(e) != 0;
   if (!ok) {
@@ -1337,6 +1334,8 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->hx) (void)hipFree(c->hx);
   if (c->hk) (void)hipFree(c->hk);
+  if (c->clk) (void)hipFree(c->clk);
+  if (c->dev_err) (void)hipHostFree(c->dev_err);
   if (c->scratch) (void)hipFree(c->scratch);
   if (c->tw) (void)hipFree(c->tw);
   for (void* p : {(void*)c->xka_state2, (void*)c->xka_keys, (void*)c->xka_src, (void*)c->xka_bins,
@@ -1356,7 +1355,6 @@ void swrt_destroy(swrt_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
   if (c->qg.ev_b) (void)hipEventDestroy(c->qg.ev_b);
-  qg_drop_graphs(c->qg);
   if (c->o_order) (void)hipFree(c->o_order);
   for (void* p : {(void*)c->o_spx, (void*)c->o_spk, (void*)c->o_spF})
     if (p) (void)hipFree(p);
@@ -1759,6 +1757,8 @@ int swrt_packets_set(swrt_ctx* c, const double* x, const double* k, int64_t n) {
     c->hz.name(c->bins + 3 * kMaxBins + 1, "tile order");
   }
   // a new ensemble starts a new history and needs binning before the next step
+  if (c->dev_err) c->dev_err[0] = 0;  // (an error raised over the old ensemble is superseded)
+  c->packets_lost = false;
   c->hframes = 0;
   c->steps_done = 0;
   c->bin_valid = false;
@@ -1774,6 +1774,7 @@ int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
   GUARD_BEGIN
   if (c->n == 0) return SWRT_OK;
   if (!x || !k) return fail(c, SWRT_ERR_ARG, "NULL buffer");
+  if (c->packets_lost) return fail(c, SWRT_ERR_STATE, "the packet state was lost to a corrupted binning");
   HIPCHK(c, hipSetDevice(c->device));
   // un-permute into the scatter buffers, then download in original order
   hipLaunchKernelGGL(unpermute_kernel, dim3(nblocks(c->n, 256)), dim3(256), 0, c->stream, c->dx, c->dk,
@@ -1782,7 +1783,7 @@ int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
   HIPCHK(c, hipMemcpyAsync(x, c->dx2, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(k, c->dk2, sizeof(double) * 2 * c->n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return SWRT_OK;
+  return dev_err_check(c);
   GUARD_END(c)
 }
 
@@ -1808,13 +1809,6 @@ int swrt_set_timing(swrt_ctx* c, int every) {
   return SWRT_OK;
 }
 
-int swrt_set_blend_mode(swrt_ctx* c, int mode) {
-  if (!c) return SWRT_ERR_ARG;
-  if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "blend mode must be 0 or 1");
-  c->blend_mode = mode;
-  return SWRT_OK;
-}
-
 int swrt_set_gather_mode(swrt_ctx* c, int mode) {
   if (!c) return SWRT_ERR_ARG;
   if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "gather mode must be 0 or 1");
@@ -1822,31 +1816,14 @@ int swrt_set_gather_mode(swrt_ctx* c, int mode) {
   return SWRT_OK;
 }
 
-int swrt_set_tile_cells(swrt_ctx* c, int cells) {
-  if (!c) return SWRT_ERR_ARG;
-  if (cells != 0 && cells != kTile && cells != kBigTile) return fail(c, SWRT_ERR_ARG, "tile cells must be 0, 16 or 32");
-  c->tile_mode = cells;
-  c->bin_valid = false;
-  c->keys_fresh = false;
-  c->src_pending = false;
-  return SWRT_OK;
-}
-
 int swrt_set_packet_streams(swrt_ctx* c, int streams) {
   if (!c) return SWRT_ERR_ARG;
-  if (streams != 1 && streams != 2 && streams != 4) return fail(c, SWRT_ERR_ARG, "packet streams must be 1, 2 or 4");
+  if (streams != 1 && streams != 2) return fail(c, SWRT_ERR_ARG, "packet streams must be 1 or 2");
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = join_b(c)) return rc;
   for (int i = 0; i < streams - 1; ++i)
     if (!c->sx[i]) HIPCHK(c, hipStreamCreateWithFlags(&c->sx[i], hipStreamNonBlocking));
   c->packet_streams = streams;
-  return SWRT_OK;
-}
-
-int swrt_set_lanes_per_packet(swrt_ctx* c, int lanes) {
-  if (!c) return SWRT_ERR_ARG;
-  if (lanes < 0 || lanes > 2) return fail(c, SWRT_ERR_ARG, "lanes per packet must be 0 (auto), 1 or 2");
-  c->lanes_per_packet = lanes;
   return SWRT_OK;
 }
 
@@ -1857,38 +1834,6 @@ int swrt_set_sparse_tiles(swrt_ctx* c, int mode) {
   c->bin_valid = false;  // the tile order of the next binning is sized for the launch shape
   c->keys_fresh = false;
   c->src_pending = false;
-  return SWRT_OK;
-}
-
-int swrt_set_cell_sort(swrt_ctx* c, int every_launch) {
-  if (!c) return SWRT_ERR_ARG;
-  if (every_launch != 0 && every_launch != 1) return fail(c, SWRT_ERR_ARG, "every_launch must be 0 or 1");
-  c->cell_sort = every_launch;
-  return SWRT_OK;
-}
-
-int swrt_qg_set_graphs(swrt_ctx* c, int on) {
-  if (!c) return SWRT_ERR_ARG;
-  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
-  if (on != 0 && on != 1) return fail(c, SWRT_ERR_ARG, "on must be 0 or 1");
-  c->qg_graphs = on != 0;
-  return SWRT_OK;
-}
-
-int swrt_set_tail_split(swrt_ctx* c, int halves_per_xcd, int quarters_per_xcd) {
-  if (!c) return SWRT_ERR_ARG;
-  if (halves_per_xcd < 0 || quarters_per_xcd < 0) return fail(c, SWRT_ERR_ARG, "tail split counts must be >= 0");
-  if (halves_per_xcd > 0xffff || quarters_per_xcd > 0x7fff) return fail(c, SWRT_ERR_ARG, "tail split counts too large");
-  c->tail_split = halves_per_xcd;
-  c->tail_quarters = quarters_per_xcd;
-  return SWRT_OK;
-}
-
-int swrt_set_tile_order(swrt_ctx* c, int longest_first) {
-  if (!c) return SWRT_ERR_ARG;
-  if (longest_first != 0 && longest_first != 1) return fail(c, SWRT_ERR_ARG, "tile order must be 0 or 1");
-  c->tile_order = longest_first != 0;
-  c->bin_valid = false;  // the next launch re-bins, which writes the order
   return SWRT_OK;
 }
 
@@ -1920,6 +1865,7 @@ int swrt_advance(swrt_ctx* c, double dt, int64_t nsteps, double f, double gH, in
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN_KEEP_SPLIT  // the half launches of the second packet stream stay unjoined across calls
   SlotUse slot_use(c, true);  // snapshot writes waited for before the first launch (run_advance)
+  if (c->packets_lost) return fail(c, SWRT_ERR_STATE, "the packet state was lost to a corrupted binning");
   if (nsteps < 0) return fail(c, SWRT_ERR_ARG, "nsteps < 0");
   if (nslots != 1 && nslots != 2) return fail(c, SWRT_ERR_ARG, "nslots must be 1 or 2");
   if (save_every < 0) return fail(c, SWRT_ERR_ARG, "save_every < 0");
@@ -1950,6 +1896,7 @@ int swrt_advance_intervals(swrt_ctx* c, int nintervals, const double* dts, int64
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN_KEEP_SPLIT  // the half launches of the second packet stream stay unjoined across calls
   SlotUse slot_use(c, true);  // snapshot writes waited for before the first launch (run_advance*)
+  if (c->packets_lost) return fail(c, SWRT_ERR_STATE, "the packet state was lost to a corrupted binning");
   if (nintervals < 1 || nintervals > SWRT_MAX_SLOTS - 1)
     return fail(c, SWRT_ERR_ARG, "nintervals must be 1..SWRT_MAX_SLOTS-1");
   if (!dts) return fail(c, SWRT_ERR_ARG, "dts is NULL");
@@ -1992,7 +1939,7 @@ int swrt_history_get(swrt_ctx* c, int64_t first, int64_t count, double* hist_x, 
   HIPCHK(c, hipMemcpyAsync(hist_x, (char*)c->hx + fb * first, fb * count, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(hist_k, (char*)c->hk + fb * first, fb * count, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  return SWRT_OK;
+  return dev_err_check(c);
   GUARD_END(c)
 }
 
@@ -2224,7 +2171,8 @@ int swrt_xka_step(swrt_ctx* c, double* state5, int64_t n, double C0, double f, d
     hipLaunchKernelGGL(bin_count_kernel, dim3(bgrid), dim3(256), sizeof(int) * nbins, c->stream, g, cur, n, nbins,
                        c->xka_keys, c->xka_bins);
     hipLaunchKernelGGL(bin_scan_kernel, dim3(1), dim3(1024), 0, c->stream, c->xka_bins, nbins,
-                       c->xka_bins + kMaxBins, c->xka_bins + 2 * kMaxBins, nullptr, kTileThreads);
+                       c->xka_bins + kMaxBins, c->xka_bins + 2 * kMaxBins, n, c->dev_err_d, nullptr,
+                       kTileThreads);
     hipLaunchKernelGGL(bin_scatter_kernel<true>, dim3(bgrid), dim3(256), 2 * sizeof(int) * nbins, c->stream,
                        cur, cur, nullptr, c->xka_keys, n, nbins, c->xka_bins + kMaxBins, nullptr, nullptr, nullptr,
                        c->xka_src2);
@@ -2514,7 +2462,7 @@ int swrt_synchronize(swrt_ctx* c) {
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipStreamSynchronize(c->qstream));
   if (c->hz.on) c->hz.sync_all();
-  return SWRT_OK;
+  return dev_err_check(c);
 }
 
 int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
@@ -2528,6 +2476,7 @@ int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
         c->hz = HazardChecker();
       }
       c->hz.on = value != 0;
+      if (!c->hz.on) c->debug_share_skew = false;
       return SWRT_OK;
     case SWRT_DEBUG_SPIN_US:
       if (value < 0 || value > 100000) return fail(c, SWRT_ERR_ARG, "spin must be 0..100000 us");
@@ -2537,22 +2486,25 @@ int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
       if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "legacy park must be 0 or 1");
       c->debug_legacy_park = value != 0;
       return SWRT_OK;
-    case SWRT_DEBUG_QG_ROWS_VECS:
-      if (value != 0 && value != 1 && value != 2 && value != 4)
-        return fail(c, SWRT_ERR_ARG, "QG first-pass planes per workgroup must be 0, 1, 2 or 4");
-      if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
-      c->qg_rows_vecs = (int)value;
-      c->qg.post_valid = false;
-      c->qg.post_inv_valid = false;
+    case SWRT_DEBUG_SHARE_SKEW:
+      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "share skew must be 0 or 1");
+      if (value && !c->hz.on) return fail(c, SWRT_ERR_STATE, "the skewed share runs only under the hazard checker");
+      c->debug_share_skew = value != 0;
+      return SWRT_OK;
+    case SWRT_DEBUG_CORRUPT_COUNT:
+      if (value < -1000000 || value > 1000000) return fail(c, SWRT_ERR_ARG, "count corruption out of range");
+      c->debug_corrupt_count = (int)value;
+      c->keys_fresh = false;
+      c->bin_valid = false;  // the next call re-bins (and meets the corrupted count)
       return SWRT_OK;
     case SWRT_DEBUG_QG_UPDATE_COLS:
-      if (value < 0 || value > 2) return fail(c, SWRT_ERR_ARG, "QG update/column-pass fusion must be 0, 1 or 2");
+      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG update/column-pass fusion must be 0 or 1");
       if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
       c->qg_update_cols = (int)value;
       c->qg.post_valid = false;
       return SWRT_OK;
     case SWRT_DEBUG_QG_JFUSE:
-      if (value < 0 || value > 2) return fail(c, SWRT_ERR_ARG, "QG column/Jacobian fusion must be 0, 1 or 2");
+      if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "QG column/Jacobian fusion must be 0 or 1");
       if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
       c->qg_jfuse = (int)value;
       c->qg.post_valid = false;
@@ -2571,7 +2523,8 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_LEGACY_PARK: *value_out = c->debug_legacy_park ? 1 : 0; return SWRT_OK;
     case SWRT_DEBUG_HAZARD_CHECKS: *value_out = c->hz.checks; return SWRT_OK;
     case SWRT_DEBUG_QG_JFUSE: *value_out = c->qg_jfuse; return SWRT_OK;
-    case SWRT_DEBUG_QG_ROWS_VECS: *value_out = c->qg_rows_vecs; return SWRT_OK;
+    case SWRT_DEBUG_SHARE_SKEW: *value_out = c->debug_share_skew ? 1 : 0; return SWRT_OK;
+    case SWRT_DEBUG_CORRUPT_COUNT: *value_out = c->debug_corrupt_count; return SWRT_OK;
     case SWRT_DEBUG_QG_UPDATE_COLS: *value_out = c->qg_update_cols; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
@@ -2586,7 +2539,6 @@ int swrt_qg_set_fused(swrt_ctx* c, int on) {
   c->qg_fused = on != 0;
   c->qg.post_valid = false;
   c->qg.post_inv_valid = false;
-  qg_drop_graphs(c->qg);  // fused steps rename the tendency buffers a captured step has baked in
   return SWRT_OK;
 }
 
@@ -2619,6 +2571,7 @@ int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches
     HIPCHK(c, hipEventElapsedTime(&ms, c->timing.ev[i], c->timing.ev[i + 1]));
     tot += ms;
   }
+  HIPCHK_RC(dev_err_check(c));
   if (total_ms) *total_ms = tot;
   if (launches) *launches = c->timing.folded_n + (int64_t)(c->timing.used / 2);
   if (reset) {
@@ -2627,6 +2580,46 @@ int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches
     c->timing.folded_n = 0;
   }
   return SWRT_OK;
+}
+
+int swrt_clock_stamp(swrt_ctx* c, int which) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN  // join_b: the stamp follows every packet launch queued on any packet stream
+  if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (start) or 1 (end)");
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!c->clk) HIPCHK(c, hipMalloc(&c->clk, sizeof(unsigned long long) * 2 * kClockWaves * 3));
+  hipLaunchKernelGGL(clock_stamp_kernel, dim3(kClockWaves), dim3(64), 0, c->stream, c->clk + which * kClockWaves * 3);
+  HIPCHK(c, hipGetLastError());
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_clock_ghz(swrt_ctx* c, double* ghz_out, double* spread_out) {
+  if (!c || !ghz_out) return SWRT_ERR_ARG;
+  if (!c->clk) return fail(c, SWRT_ERR_STATE, "no clock stamps (swrt_clock_stamp 0 and 1 first)");
+  GUARD_BEGIN
+  HIPCHK(c, hipSetDevice(c->device));
+  unsigned long long h[2 * kClockWaves * 3];
+  HIPCHK(c, hipMemcpyAsync(h, c->clk, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  hz_synced(c);
+  // every (start, end) pair of waves on one XCD: shader cycles / real time
+  std::vector<double> ghz;
+  const unsigned long long* s = h;
+  const unsigned long long* e = h + kClockWaves * 3;
+  for (int i = 0; i < kClockWaves; ++i)
+    for (int j = 0; j < kClockWaves; ++j) {
+      if (s[3 * i + 2] != e[3 * j + 2] || e[3 * j + 1] <= s[3 * i + 1] || e[3 * j] <= s[3 * i]) continue;
+      const double sec = (double)(e[3 * j + 1] - s[3 * i + 1]) / kRealTimeHz;
+      ghz.push_back((double)(e[3 * j] - s[3 * i]) / sec / 1e9);
+    }
+  if (ghz.empty()) return fail(c, SWRT_ERR_STATE, "no start/end stamp pair on one XCD");
+  std::sort(ghz.begin(), ghz.end());
+  const double med = ghz[ghz.size() / 2];
+  *ghz_out = med;
+  if (spread_out) *spread_out = (ghz.back() - ghz.front()) / med;
+  return SWRT_OK;
+  GUARD_END(c)
 }
 
 // ---------------------------------------------------------------------------
@@ -2649,7 +2642,6 @@ int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double*
   if (q.hmax) (void)hipHostFree(q.hmax);
   if (q.ev) (void)hipEventDestroy(q.ev);
   if (q.ev_b) (void)hipEventDestroy(q.ev_b);
-  qg_drop_graphs(q);
   q = QGState{};
   const int n = (int)nx, kmax = n / 2 - 1;
   q.nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
@@ -2802,15 +2794,7 @@ int qg_post_inverse(swrt_ctx* c) {
     int logn = 0;
     while ((1 << logn) < n) ++logn;
     const size_t lds = sizeof(double2) * nb * n;
-    // planes per first-pass workgroup beside packets (SWRT_DEBUG_QG_ROWS_VECS; 0: 4)
-    const int rv = (c->qg_sep && c->n > 0 && c->qg_rows_vecs > 0) ? c->qg_rows_vecs : 4;
-    if (nl == 2 && rv == 1)
-      hipLaunchKernelGGL(qg_post_rows_v_kernel<1>, dim3(8 * (unsigned)n), dim3(n / 4), sizeof(double2) * n,
-                         c->stream, (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
-    else if (nl == 2 && rv == 2)
-      hipLaunchKernelGGL(qg_post_rows_v_kernel<2>, dim3(4 * (unsigned)n), dim3(n / 2), sizeof(double2) * 2 * n,
-                         c->stream, (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
-    else if (nl == 2)
+    if (nl == 2)
       hipLaunchKernelGGL(qg_post_rows_split_kernel, dim3(2 * (unsigned)n), dim3(n), sizeof(double2) * 4 * n,
                          c->stream, (const double2*)q.qk, q.g, q.nhalf, logn, (const double2*)c->tw, q.PZ, q.dmax);
     else
@@ -2821,7 +2805,7 @@ int qg_post_inverse(swrt_ctx* c) {
     // packet workgroups to retire — driver step +2 %, 8-GPU shard +10 %,
     // profiles/r04_qg_ab — where the separate column pass runs one plane per
     // 128-lane workgroup)
-    if (nl == 2 && n % 8 == 0 && (c->qg_jfuse == 2 || (c->qg_jfuse == 1 && !(c->qg_sep && c->n > 0)))) {
+    if (nl == 2 && n % 8 == 0 && c->qg_jfuse == 1 && !(c->qg_sep && c->n > 0)) {
       // the column pass fused with the Jacobian, the CFL max and J's first
       // forward pass (swrt_fft.hpp): planes 0-4 stay on chip; J -> PT[0, nn)
       hipLaunchKernelGGL(fft_cols_jacobian2_kernel, dim3(2 * (unsigned)n), dim3(n), sizeof(double2) * 4 * (n + 1),
@@ -2865,7 +2849,7 @@ int qg_post(swrt_ctx* c) {
   // QG stream beside packet launches (profiles/r04_update_cols), as for
   // fft_cols_jacobian2_kernel
   const bool cols =
-      n >= 16 && (c->qg_update_cols == 2 || (c->qg_update_cols == 1 && !(c->qg_sep && c->n > 0)));
+      n >= 16 && c->qg_update_cols == 1 && !(c->qg_sep && c->n > 0);
   if (q.post_jrows) {
     // J's first pass came with the inverse column pass: its second pass only
     if (cols) {
@@ -2910,39 +2894,6 @@ int qg_post(swrt_ctx* c) {
   return SWRT_OK;
 }
 
-// Steady AB3 steps replay a captured graph of the launch sequence (kernel
-// arguments are baked in: one graph per qk buffer parity and dt; the drivers'
-// dt changes only when the CFL rule fires).  Measured slower than the plain
-// launches on ROCm 7 at 512^2 (73.5 vs 67.5 us per step), so
-// off by default (swrt_qg_set_graphs).
-int qg_step_graphed(swrt_ctx* c, double dt) {
-  QGState& q = c->qg;
-  int g = -1;
-  for (int i = 0; i < 2; ++i)
-    if (q.gexec[i] && q.gqk[i] == q.qk && q.gdt[i] == dt && q.gtw[i] == c->tw) g = i;
-  if (g < 0) {
-    g = (q.gexec[0] && q.gqk[0] != q.qk && q.gdt[0] == dt && q.gtw[0] == c->tw) ? 1 : 0;  // keep the other parity
-    if (q.gexec[g]) (void)hipGraphExecDestroy(q.gexec[g]);
-    q.gexec[g] = nullptr;
-    hipGraph_t graph = nullptr;
-    HIPCHK(c, hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    const int rc = qg_step_launches(c, dt, 3);
-    const hipError_t e = hipStreamEndCapture(c->stream, &graph);
-    if (rc) {
-      if (graph) (void)hipGraphDestroy(graph);
-      return rc;
-    }
-    HIPCHK(c, e);
-    const hipError_t ei = hipGraphInstantiate(&q.gexec[g], graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    HIPCHK(c, ei);
-    q.gqk[g] = q.qk;
-    q.gdt[g] = dt;
-    q.gtw[g] = c->tw;
-  }
-  HIPCHK(c, hipGraphLaunch(q.gexec[g], c->stream));
-  return SWRT_OK;
-}
 }  // namespace
 
 int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
@@ -2974,8 +2925,6 @@ int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
       } else {
         rc = qg_update_launch(c, dt, abstep, q.Fj, q.qk_prev, q.Qm1, q.Qm2);
       }
-    } else if (abstep == 3 && c->qg_graphs) {
-      rc = qg_step_graphed(c, dt);
     } else {
       rc = qg_step_launches(c, dt, abstep);
     }
@@ -3024,9 +2973,12 @@ int swrt_qg_step_speculative(swrt_ctx* c, double dt) {
   // the post-step transforms and CFL read-back of the speculative qk
   double2* committed = q.qk;
   q.qk = q.qk_spare;
+  const int rb_slot = q.sp_head;
   rc = qg_speed_launch(c);
   q.qk = committed;
   if (rc) return rc;
+  q.spec_rb = true;
+  q.spec_rb_slot = rb_slot;
   q.spec = true;
   q.spec_dt = dt;
   q.spec_steps = q.steps + 1;
@@ -3061,14 +3013,17 @@ int swrt_qg_resolve(swrt_ctx* c, int accept) {
     q.steps = q.spec_steps;
     q.t = q.spec_t;
     q.has_prev = true;
-    qg_drop_graphs(q);  // captured for the committed buffers
   } else {
-    // its CFL read-back (the newest pending) is dropped; PZ/PT hold its
-    // post-step transforms, so the committed qk's are recomputed on use
-    q.sp_head ^= 1;
-    q.sp_count -= 1;
+    // its CFL read-back (the newest pending) is dropped unless the caller
+    // already popped it; PZ/PT hold its post-step transforms, so the
+    // committed qk's are recomputed on use
+    if (q.spec_rb) {
+      q.sp_head ^= 1;
+      q.sp_count -= 1;
+    }
   }
   q.spec = false;
+  q.spec_rb = false;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -3116,6 +3071,7 @@ int qg_speed_wait(swrt_ctx* c, double* U0_out) {
   const int slot = (q.sp_head - q.sp_count) & 1;
   HIPCHK(c, hipEventSynchronize(slot ? q.ev_b : q.ev));
   q.sp_count -= 1;
+  if (q.spec && q.spec_rb && slot == q.spec_rb_slot) q.spec_rb = false;  // the speculative step's, consumed
   *U0_out = std::sqrt(q.hmax[slot]);  // bits of a non-negative double: the max of (u+shear)^2 + v^2
   return SWRT_OK;
 }
@@ -3333,7 +3289,6 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   a.gate_scale = 0.0;
   a.gate_limit = 0.0;
   a.order = nullptr;
-  a.split = 0;
   return SWRT_OK;
 }
 
@@ -3361,7 +3316,7 @@ int read_max(swrt_ctx* c, double* out) {
   // (spinning on an event instead measured within noise: 2.55-2.59 vs 2.60-2.62 ms)
   HIPCHK(c, hipStreamSynchronize(c->stream));
   std::memcpy(out, c->o_hmax + slot, sizeof(double));
-  return SWRT_OK;
+  return dev_err_check(c);
 }
 }  // namespace
 
@@ -3382,14 +3337,12 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
     const int* starts = c->bins + 2 * kMaxBins;
     const unsigned ntiles = (unsigned)(ntx * ntx);
     Ode23Args a = a0;
-    unsigned extra = 0;
-    a.split = launch_shape(c, ntiles, &extra);
-    const unsigned grid = ntiles + extra;
+    const unsigned grid = ntiles;
     // in-tile cell order of this binning, once (swrt_ode23.hpp): the packets'
     // own order after swrt_ode23_f1's sort, else an order array
-    if (c->o_sorted && c->o_order_split == a.split) {
+    if (c->o_sorted) {
       a.order = nullptr;
-    } else if (!c->o_order_valid || c->o_order_split != a.split) {
+    } else if (!c->o_order_valid) {
       if (c->o_order_cap < c->cap) {
         if (c->o_order) (void)hipFree(c->o_order);
         c->o_order = nullptr;
@@ -3398,10 +3351,9 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
       }
       const FieldView v = view_of(c->slot[0]);
       hipLaunchKernelGGL((tile_cell_order_kernel<kTile, kTileThreads>), dim3(grid), dim3(kTileThreads), 0,
-                         c->stream, c->dx, c->n, starts, a.split, ntx, v.inv_dx, v.nx, c->o_order);
+                         c->stream, c->dx, c->n, starts, ntx, v.inv_dx, v.nx, c->o_order);
       HIPCHK(c, hipGetLastError());
       c->o_order_valid = true;
-      c->o_order_split = a.split;
       a.order = c->o_order;
     } else {
       a.order = c->o_order;
@@ -3447,19 +3399,16 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
     const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
     if (use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx * ntx) {
       // the in-tile cell order applied to the packets (swrt_ode23.hpp tile_cell_sort_kernel)
-      unsigned extra = 0;
-      const int split = launch_shape(c, (unsigned)(ntx * ntx), &extra);
       const FieldView v = view_of(c->slot[0]);
-      hipLaunchKernelGGL((tile_cell_sort_kernel<kTile, kTileThreads>), dim3((unsigned)(ntx * ntx) + extra),
+      hipLaunchKernelGGL((tile_cell_sort_kernel<kTile, kTileThreads>), dim3((unsigned)(ntx * ntx)),
                          dim3(kTileThreads), 0, c->stream, (const double*)c->dx, (const double*)c->dk,
-                         (const int*)c->perm, c->n, (const int*)(c->bins + 2 * kMaxBins), split, ntx, v.inv_dx,
+                         (const int*)c->perm, c->n, (const int*)(c->bins + 2 * kMaxBins), ntx, v.inv_dx,
                          (int)v.nx, c->dx2, c->dk2, c->perm2);
       HIPCHK(c, hipGetLastError());
       std::swap(c->dx, c->dx2);
       std::swap(c->dk, c->dk2);
       std::swap(c->perm, c->perm2);
       c->o_sorted = true;
-      c->o_order_split = split;
     }
   }
   Ode23Args a;

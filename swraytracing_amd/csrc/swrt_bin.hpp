@@ -60,6 +60,12 @@ constexpr int kOrderBuckets = 16;  // workgroup rounds told apart by the tile or
 // Pass 2: exclusive scan of counts -> cursor (single workgroup, nbins <= 16384).
 // Also clears counts (each thread its own bins, after reading them) so the next
 // fused count in the tile kernel starts from zero without a memset launch.
+// Guard: the counts must be >= 0 and sum to n (the packets binned).  If not
+// — a corrupted count — the scan writes an empty binning (every start 0, every
+// cursor n: the scatter skips every packet, the tile launches get empty
+// ranges) and raises *err (host-visible memory), which the host turns into
+// SWRT_ERR_STATE at its next synchronisation.  So a bad binning is an error,
+// never a launch over foreign packet ranges.
 // order != NULL (nbins % 8 == 0): the tile order of the LDS-tiled launches
 // (tile_order_of).  Each of the 8 XCD bands of nbins/8 consecutive tiles is
 // listed longest first — by the rounds ceil(count / lanes) its workgroup of
@@ -68,23 +74,43 @@ constexpr int kOrderBuckets = 16;  // workgroup rounds told apart by the tile or
 // the short ones (longest-processing-time-first list scheduling).  A stable
 // counting sort per band by one wavefront (ballots).
 __global__ void __launch_bounds__(1024) bin_scan_kernel(int* counts, int nbins, int* cursor,
-                                                        int* starts, int* order = nullptr, int lanes = 512) {
+                                                        int* starts, int64_t n, int* err, int* order = nullptr,
+                                                        int lanes = 512) {
   __shared__ int part[1024];
   const int per = (nbins + 1023) / 1024;
   const int b0 = threadIdx.x * per;
   int s = 0;
+  int neg = 0;
   for (int i = 0; i < per; ++i) {
     const int b = b0 + i;
-    if (b < nbins) s += counts[b];
+    if (b < nbins) {
+      const int c = counts[b];
+      neg |= c < 0;
+      s += c;
+    }
   }
   part[threadIdx.x] = s;
-  __syncthreads();
+  neg = __syncthreads_or(neg);
   // Hillis-Steele inclusive scan over the 1024 partials
   for (int off = 1; off < 1024; off <<= 1) {
     const int v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
     __syncthreads();
     part[threadIdx.x] += v;
     __syncthreads();
+  }
+  if (neg || (int64_t)part[1023] != n) {
+    for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
+      cursor[b] = (int)n;
+      starts[b] = 0;
+      counts[b] = 0;
+    }
+    if (threadIdx.x == 0) {
+      starts[nbins] = 0;
+      *err = 1;
+    }
+    if (order != nullptr)
+      for (int b = threadIdx.x; b < nbins; b += blockDim.x) order[b] = b;
+    return;
   }
   int run = threadIdx.x ? part[threadIdx.x - 1] : 0;
   for (int i = 0; i < per; ++i) {
@@ -173,6 +199,7 @@ __global__ void __launch_bounds__(256) bin_scatter_kernel(const double* x, const
     const int64_t p = b0 + (int64_t)q * blockDim.x + threadIdx.x;
     if (p < n) {
       const int64_t d = (int64_t)base[key[q]] + local[q];
+      if (d < 0 || d >= n) continue;  // an empty binning after a failed scan check (bin_scan_kernel)
       if constexpr (INDEX) {
         src[d] = (int)p;
         continue;

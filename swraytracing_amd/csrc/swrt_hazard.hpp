@@ -2,8 +2,8 @@
 // (host code; swrt_debug_set(ctx, SWRT_DEBUG_HAZARD_CHECK, 1) or the
 // environment variable SWRT_HAZARD_CHECK=1 turns it on).
 //
-// The LDS-tiled leapfrog runs each launch as S part launches on S streams
-// (swrt_set_packet_streams): the packet stream and up to three extra ones.
+// The LDS-tiled leapfrog runs each launch as S = 2 part launches on two
+// streams (swrt_set_packet_streams): the packet stream and an extra one.
 // Between re-binnings the parts touch disjoint packet ranges, and the extra
 // streams' work is joined back into the packet stream only where something
 // reads every packet (join_b).  That protocol lives in comments in
@@ -16,11 +16,13 @@
 //     stream's clock into the host clock, which every later operation
 //     inherits;
 //   * each access names a buffer, a kind (read / write / atomic add) and a
-//     region: the whole buffer, or part p of S of binning epoch e (the
-//     packets of the tiles at band positions = p mod S of the binning made at
-//     epoch e — the slots a part launch reads and writes, and the history
-//     frames' entries of those packets).  Two regions overlap unless both are
-//     parts of the same epoch and S with p != q.
+//     region: the whole buffer, or a set of band slots of binning epoch e —
+//     the slots the launch's workgroups actually take, enumerated with the
+//     device's own mapping (swrt_share.hpp share_slot), i.e. the packets of
+//     those tiles of the binning made at epoch e (and the history frames'
+//     entries of those packets).  Two regions overlap unless both belong to
+//     the same epoch and their slot sets are disjoint: whatever share rule a
+//     launch uses, only slots proven disjoint count as disjoint.
 // An access conflicts with an earlier one on an overlapping region unless
 // both read (or both add atomically); a conflicting pair must be ordered:
 // the earlier access's stream clock at that access <= the later stream's
@@ -32,12 +34,15 @@
 #include <stdio.h>
 
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
+#include "swrt_share.hpp"
+
 namespace swrt {
 
-constexpr int kHzStreams = 5;  // 0 = packet stream, 1..3 = extra packet streams, 4 = any other stream
+constexpr int kHzStreams = 3;  // 0 = packet stream, 1 = the extra packet stream, 2 = any other stream
 
 struct HzClock {
   uint64_t v[kHzStreams] = {};
@@ -48,29 +53,43 @@ struct HzClock {
 
 struct HzRegion {
   int64_t epoch = 0;
-  int part = 0;
-  int nparts = 0;  // 0: the whole buffer
+  std::shared_ptr<const std::vector<uint64_t>> slots;  // bit s: band slot s; null: the whole buffer
+  std::string desc;
   static HzRegion all() { return HzRegion{}; }
-  static HzRegion of_part(int64_t e, int p, int s) {
+  // the band slots of the launch `sh` (every workgroup b < share_grid(sh))
+  static HzRegion of_share(int64_t e, const TileShare& sh) {
+    auto bits = std::make_shared<std::vector<uint64_t>>((sh.ntiles + 63) / 64, 0ull);
+    const int grid = share_grid(sh);
+    for (int b = 0; b < grid; ++b) {
+      const int t = share_slot(sh, b);
+      if (t >= 0 && t < sh.ntiles) (*bits)[t >> 6] |= 1ull << (t & 63);
+    }
     HzRegion r;
     r.epoch = e;
-    r.part = p;
-    r.nparts = s;
+    r.slots = bits;
+    r.desc = sh.part < 0 ? std::string("every tile") :
+             "part " + std::to_string(sh.part) + "/" + std::to_string(sh.parts) +
+             (sh.rule == kShareSkew ? " (skewed share)" : "") + " (" + std::to_string(grid) + " tiles)";
     return r;
   }
-  bool whole() const { return nparts == 0; }
+  bool whole() const { return !slots; }
 };
 
 inline bool hz_overlap(const HzRegion& a, const HzRegion& b) {
   if (a.whole() || b.whole()) return true;
-  if (a.epoch != b.epoch || a.nparts != b.nparts) return true;
-  return a.part == b.part;
+  if (a.epoch != b.epoch || a.slots->size() != b.slots->size()) return true;
+  for (size_t i = 0; i < a.slots->size(); ++i)
+    if ((*a.slots)[i] & (*b.slots)[i]) return true;
+  return false;
 }
 
 // a is contained in b
 inline bool hz_within(const HzRegion& a, const HzRegion& b) {
   if (b.whole()) return true;
-  return !a.whole() && a.epoch == b.epoch && a.nparts == b.nparts && a.part == b.part;
+  if (a.whole() || a.epoch != b.epoch || a.slots->size() != b.slots->size()) return false;
+  for (size_t i = 0; i < a.slots->size(); ++i)
+    if ((*a.slots)[i] & ~(*b.slots)[i]) return false;
+  return true;
 }
 
 enum HzKind { kHzRead = 0, kHzWrite = 1, kHzAtomic = 2 };
@@ -120,7 +139,7 @@ struct HazardChecker {
   static const char* kind_name(int k) { return k == kHzRead ? "read" : k == kHzWrite ? "write" : "atomic add"; }
   std::string region_name(const HzRegion& r) const {
     if (r.whole()) return "all packets";
-    return "part " + std::to_string(r.part) + "/" + std::to_string(r.nparts) + " of binning " + std::to_string(r.epoch);
+    return r.desc + " of binning " + std::to_string(r.epoch);
   }
   std::string buf_name(const void* b) const {
     auto it = names.find(b);

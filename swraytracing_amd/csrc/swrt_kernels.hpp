@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "swrt_share.hpp"
+
 namespace swrt {
 
 constexpr int kNT = 6;            // taps per direction (Iord = 2, interpolate.m:12)
@@ -394,33 +396,6 @@ __device__ __forceinline__ void gather6_lean(const double* nodes0, const double*
   }
 }
 
-// Blend-then-interpolate from global memory (the out-of-window fallback of
-// the blend-in-LDS mode): each node value is (1-alpha)*F1 + alpha*F2 exactly
-// as stage_window_blend forms it, then one stencil sum.
-__device__ __forceinline__ void gather6_blend(const double* nodes0, const double* nodes1, int npad,
-                                              const Stencil& s, double alpha, double o[kRec]) {
-  const double oma = 1 - alpha;
-#pragma unroll
-  for (int f = 0; f < kRec; ++f) o[f] = -0.0;
-  const size_t off = ((size_t)s.ic * npad + s.jc) * kRec;
-#pragma unroll
-  for (int i = 0; i < kNT; ++i) {
-    const size_t ro = off + (size_t)i * npad * kRec;
-    const double2* r0 = reinterpret_cast<const double2*>(nodes0 + ro);
-    const double2* r1 = reinterpret_cast<const double2*>(nodes1 + ro);
-#pragma unroll
-    for (int j = 0; j < kNT; ++j) {
-      const double wij = s.wx[i] * s.wy[j];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const double2 u = r0[3 * j + c], v = r1[3 * j + c];
-        o[2 * c] = o[2 * c] + wij * (oma * u.x + alpha * v.x);
-        o[2 * c + 1] = o[2 * c + 1] + wij * (oma * u.y + alpha * v.y);
-      }
-    }
-  }
-}
-
 // interpolate_U.m:19-23 — (1 - alpha)*U1 + alpha*U2, per field.  Both
 // snapshots live on the same grid (checked on the host).
 template <bool TWO>
@@ -467,14 +442,6 @@ struct StepArgs {
   const int* perm;          // device order -> original packet index (history)
 };
 
-// XCD-aware block order: the dispatcher deals blocks round-robin over the 8
-// XCDs (b and b+8 share one); remap so each XCD walks one contiguous range of
-// the (spatially binned) packet array and its L2 holds one band of the field.
-// Bijective for any grid size (cdna_hip_programming.md §5 "XCD swizzle").
-__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nblk) {
-  const int64_t q = nblk / 8, r = nblk % 8, xcd = b % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
-}
 
 // ode_symplectic.m:13-37 fused: drift(dt/2) -> kick(dt) -> drift(dt/2), nsteps
 // times with the packet held in registers.

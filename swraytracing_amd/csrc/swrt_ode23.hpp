@@ -55,7 +55,6 @@ struct Ode23Args {
   const unsigned long long* gate;
   double gate_scale, gate_limit;
   const int* order;  // tile kernel: binned slots in in-tile cell order (NULL: slot order)
-  int split;         // tile kernel: half-tile workgroups at the end of each XCD band
 };
 
 __device__ __forceinline__ void ode_rhs(const Ode23Args& a, const double ys[4], double fo[4]) {
@@ -135,14 +134,14 @@ __global__ void __launch_bounds__(256) ode23_stage_kernel(Ode23Args a) {
 // kernel's own in-tile sort does).  Order only: results do not depend on it.
 template <int T, int NT>
 __global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, int64_t n, const int* starts,
-                                                             int split, int ntx, double inv_dx, int nx,
+                                                             int ntx, double inv_dx, int nx,
                                                              int* order) {
   constexpr int NB = T * T;
   constexpr int MAXB = 2 * NT;
   __shared__ int hist[NB];
   __shared__ int kr[MAXB];
   int pbeg, pend;
-  const int tile = wg_work_range(starts, nullptr, split, pbeg, pend);
+  const int tile = wg_work_range(starts, n, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int tid = threadIdx.x;
   for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
@@ -202,7 +201,7 @@ __global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, in
 // profiles/r04_ode23).  Order only: results do not depend on it.
 template <int T, int NT>
 __global__ void __launch_bounds__(NT) tile_cell_sort_kernel(const double* x, const double* k, const int* perm,
-                                                            int64_t n, const int* starts, int split, int ntx,
+                                                            int64_t n, const int* starts, int ntx,
                                                             double inv_dx, int nx, double* x_out, double* k_out,
                                                             int* perm_out) {
   constexpr int NB = T * T;
@@ -210,7 +209,7 @@ __global__ void __launch_bounds__(NT) tile_cell_sort_kernel(const double* x, con
   __shared__ int hist[NB];
   __shared__ int kr[MAXB];
   int pbeg, pend;
-  const int tile = wg_work_range(starts, nullptr, split, pbeg, pend);
+  const int tile = wg_work_range(starts, n, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int tid = threadIdx.x;
   for (int b0 = pbeg; b0 < pend; b0 += MAXB) {
@@ -319,7 +318,7 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
   if (a.dmax_clear && blockIdx.x == 0 && threadIdx.x == 0) *a.dmax_clear = 0ull;
   if (a.gate && !(a.gate_scale * __longlong_as_double((long long)*a.gate) < a.gate_limit)) return;
   int pbeg, pend;
-  const int tile = wg_work_range(starts, nullptr, a.split, pbeg, pend);
+  const int tile = wg_work_range(starts, a.n, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int nx = a.f0.nx;
   stage_window_regs<TWO, T, M, NT, WS, V5>(a.f0, a.f1, ox, oy, win);

@@ -42,12 +42,9 @@ struct TileArgs {
   const int* src;        // non-NULL (sort launches only): binned slot p holds input packet
                          // src[p] (indirect re-binning); NULL: slot p holds packet p
   double sort_lead;      // in-tile sort key: position + sort_lead * (group velocity)
-  int split;             // launch shape (wg_work_range): halves | quarters << 16 per XCD band
-  // Multi-stream form (swrt_set_packet_streams S = 2 or 4): this launch takes
-  // every S-th band position of each XCD band (those = spart mod S), the
-  // launches on the other streams the rest; the grid is then ntiles / S.
-  int spart;             // -1: one launch over every tile; 0 .. sparts-1: this launch's band positions
-  int sparts;            // S
+  // the band slots this launch takes (share_slot): all of them, or one
+  // part's share of a split launch
+  TileShare sh;
   // Multi-interval launch (ivmode, swrt_advance_intervals): nint consecutive
   // PDE intervals of s.nsteps steps each; interval i blends snapshots iv[i]
   // and iv[i+1] with alpha = alpha0 + st*dalpha (st = step within the
@@ -79,56 +76,29 @@ __device__ __forceinline__ double iv_dt(const TileArgs& ta, int i) {
 }
 
 // Workgroup -> (tile, packet range).  XCD-aware (xcd_block): XCD x walks one
-// contiguous band of tiles.  `split` = h | q << 16 (ntiles % 8 == 0): each
-// band ends with h tiles run as two half-tile workgroups and then q tiles run
-// as four quarter-tile workgroups (each stages the whole window), so the
-// dispatcher hands out ever smaller work items as CUs free up at the end of
-// the launch, which narrows the spread of CU finish times (the launch ends
-// with its slowest CU).  grid = ntiles + 8*(h + 3q).
-__device__ __forceinline__ int wg_work_range(const int* starts, const int* order, int split, int& pbeg,
-                                             int& pend, int spart = -1, int sparts = 1) {
-  int b = (int)blockIdx.x, nb = (int)gridDim.x;
-  if (spart >= 0) {  // 1/S of the tiles: band position S*j + spart of XCD band b % 8
-    b = (sparts * (b / 8) + spart) * 8 + b % 8;
-    nb *= sparts;
-  }
-  int tile, part = 0, nparts = 1;
-  if (split > 0) {
-    const int h = split & 0xffff, q = split >> 16;
-    const int x = b % 8, j = b / 8;
-    const int tpx = nb / 8 - h - 3 * q;  // tiles per XCD band
-    const int whole = tpx - h - q;
-    if (j < whole) {
-      tile = x * tpx + j;
-    } else if (j < whole + 2 * h) {
-      tile = x * tpx + whole + (j - whole) / 2;
-      part = (j - whole) & 1;
-      nparts = 2;
-    } else {
-      const int jj = j - whole - 2 * h;
-      tile = x * tpx + whole + h + jj / 4;
-      part = jj & 3;
-      nparts = 4;
-    }
-  } else {
-    tile = (int)xcd_block(b, nb);
-  }
-  if (order != nullptr) tile = order[tile];  // the tile at this band position
-  pbeg = starts[tile];
-  pend = starts[tile + 1];
-  if (nparts > 1) {
-    // parts of whole wavefronts (64 packets) but the last: no part adds a
-    // partial wave of its own
-    const int cnt = pend - pbeg;
-    const int per = ((cnt + nparts - 1) / nparts + 63) & ~63;
-    pend = pbeg + min(cnt, per * (part + 1));
-    pbeg = pbeg + min(cnt, per * part);
-  }
+// contiguous band of tiles; `order` (bin_scan_kernel) lists each band's tiles
+// longest first; a part launch takes its share's slots (share_slot).  The
+// range is clamped to [0, n]: a corrupted binning becomes an empty or short
+// range (and the scan's own check, bin_scan_kernel, reports it as an error),
+// never a loop over foreign memory.
+__device__ __forceinline__ int wg_work_range(const int* starts, const int* order, int64_t n, const TileShare& sh,
+                                             int& pbeg, int& pend) {
+  int tile = share_slot(sh, (int)blockIdx.x);
+  if (order != nullptr) tile = order[tile];  // the tile at this band slot
+  const int nn = (int)n;
+  pbeg = min(max(starts[tile], 0), nn);
+  pend = min(max(starts[tile + 1], pbeg), nn);
   return tile;
+}
+// one workgroup per tile (gridDim = the tiles), no tile order
+__device__ __forceinline__ int wg_work_range(const int* starts, int64_t n, int& pbeg, int& pend) {
+  TileShare sh;
+  sh.ntiles = (int)gridDim.x;
+  return wg_work_range(starts, nullptr, n, sh, pbeg, pend);
 }
 
 __device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend) {
-  return wg_work_range(ta.starts, ta.order, ta.split, pbeg, pend, ta.spart, ta.sparts);
+  return wg_work_range(ta.starts, ta.order, ta.s.n, ta.sh, pbeg, pend);
 }
 
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
@@ -302,69 +272,6 @@ __device__ __forceinline__ void gather5_lds(const double2* lds, int node0, const
   o1[5] = -o1[2];
 }
 
-// ---- paired lanes (small ensembles) ---------------------------------------
-// With few packets per tile a workgroup has one or two busy waves, one wave
-// per SIMD, and a lone wave issues far below the SIMD's rate.  The PAIR form
-// of the tile kernel advances each packet on two lanes of one wave, lane p
-// and lane p + 32: lane half h = 0 computes the x weights and snapshot 0's
-// five stencil sums, h = 1 the y weights and snapshot 1's — each sum in the
-// reference's order, so the results are those of the one-lane kernel bit for
-// bit — and v_permlane32_swap hands each half's values to the other.
-//
-// v_permlane32_swap_b32 exchanges lanes 32-63 of its first register with
-// lanes 0-31 of its second; given the same value v in both, the first comes
-// back as v of the lower half on every lane and the second as v of the
-// upper half: the h = 0 and h = 1 values of the lane's packet.
-__device__ __forceinline__ void halves_u32(unsigned v, unsigned& lo, unsigned& hi) {
-  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  lo = r[0];
-  hi = r[1];
-}
-__device__ __forceinline__ void halves_f64(double v, double& lo, double& hi) {
-  unsigned l0, l1, u0, u1;
-  halves_u32((unsigned)__double2loint(v), l0, l1);
-  halves_u32((unsigned)__double2hiint(v), u0, u1);
-  lo = __hiloint2double((int)u0, (int)l0);
-  hi = __hiloint2double((int)u1, (int)l1);
-}
-
-// One half's five sums of the V5 window (gather5_lds's snapshot h): chunks
-// 3h and 3h+1 hold {u,v} and {u_x,u_y}, chunk 2 holds {v_x of 0, v_x of 1}.
-// Same per-field order, pipelined one tap ahead as gather5_lds.
-template <int W, int WN, bool FMA = false>
-__device__ __forceinline__ void gather5_half(const double2* lds, int node0, int h, const double wx[kNT],
-                                             const double wy[kNT], double o[5]) {
-#pragma unroll
-  for (int f = 0; f < 5; ++f) o[f] = -0.0;
-  const double2* p = lds + node0 + 3 * h * WN;
-  const double* pc = reinterpret_cast<const double*>(lds + node0 + 2 * WN) + h;
-  double2 a0 = p[0], a1 = p[WN];
-  double c = pc[0];
-#pragma unroll
-  for (int t = 0; t < kNT * kNT; ++t) {
-    const int i = t / kNT, j = t % kNT;
-    double2 n0, n1;
-    double nc;
-    if (t + 1 < kNT * kNT) {
-      const int e = ((t + 1) / kNT) * W + (t + 1) % kNT;
-      n0 = p[e];
-      n1 = p[WN + e];
-      nc = pc[2 * e];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    const double wij = wx[i] * wy[j];
-    o[0] = madd<FMA>(o[0], wij, a0.x); o[1] = madd<FMA>(o[1], wij, a0.y);
-    o[2] = madd<FMA>(o[2], wij, a1.x); o[3] = madd<FMA>(o[3], wij, a1.y);
-    o[4] = madd<FMA>(o[4], wij, c);
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < kNT * kNT) {
-      a0 = n0;
-      a1 = n1;
-      c = nc;
-    }
-  }
-}
-
 // Stage tile (ox, oy)'s window into LDS, chunk-major (chunk c of node e at
 // win[c*WN + e]): node (wi, wj) <-> global node (ox-M-2+wi, oy-M-2+wj) mod nx.
 // Register staging: each lane copies whole 48-B records, 3 or 6 loads back
@@ -408,33 +315,6 @@ __device__ __forceinline__ void stage_window_regs(const FieldView& f0, const Fie
   }
 }
 
-// Blend-then-interpolate staging (swrt_set_blend_mode 1): the window holds
-// (1-alpha)*U1 + alpha*U2 per node and field, 3 chunks.  interpolate_U is
-// linear, so this is the same function as interpolating each snapshot and
-// blending (interpolate_U.m:19-23) with a different rounding order: half the
-// LDS reads and half the gather arithmetic, tolerance parity instead of bits.
-template <int T, int M, int NT, int WS = T + 5 + 2 * M>
-__device__ __forceinline__ void stage_window_blend(const FieldView& f0, const FieldView& f1, int ox, int oy,
-                                                   double alpha, double2* win) {
-  constexpr int W = T + 5 + 2 * M;
-  constexpr int WN = W * WS;
-  const int nx = f0.nx, npad = f0.npad;
-  const double oma = 1 - alpha;
-  for (int e = threadIdx.x; e < W * W; e += NT) {
-    const int wi = e / W, wj = e % W;
-    int gx = (ox - M - 2 + wi) % nx; gx += gx < 0 ? nx : 0;
-    int gy = (oy - M - 2 + wj) % nx; gy += gy < 0 ? nx : 0;
-    const size_t src = ((size_t)(gx + kPadLo) * npad + (gy + kPadLo)) * kRec;
-    const double2* s0 = reinterpret_cast<const double2*>(f0.nodes + src);
-    const double2* s1 = reinterpret_cast<const double2*>(f1.nodes + src);
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const double2 u = s0[c], v = s1[c];
-      win[c * WN + wi * WS + wj] = make_double2(oma * u.x + alpha * v.x, oma * u.y + alpha * v.y);
-    }
-  }
-}
-
 #ifdef SWRT_PHASE_TIMING
 // diagnostic build only: per-workgroup wall-clock stamps (100 MHz) of the
 // phases, read back by swrt_debug_phases; never compiled into the product.
@@ -455,27 +335,22 @@ __device__ unsigned long long swrt_phase_dbg[16384 * 8];
 
 // FMA (opt-in gather mode 1, V5 windows only): the stencil sums and the
 // snapshot blend as fused multiply-adds — tolerance parity, not bits.
-// PAIR (small ensembles): two lanes per packet (paired lanes, above); the
-// two-snapshot five-sum window only.
 // PF: the five-sum gather's prefetch depth (gather5_lds); MINW: the waves per
 // SIMD the register budget is sized for (4: 128 VGPRs; the sparse-tile
 // instantiation, 256 threads with PF 3, takes 2: 256 VGPRs).
-template <bool TWO, int T, int M, int NT, bool WBLEND = false, bool V5 = false, bool FMA = false, bool PAIR = false,
-          int PF = 1, int MINW = SWRT_TILE_MIN_WAVES>
+template <bool TWO, int T, int M, int NT, bool V5 = false, bool FMA = false, int PF = 1,
+          int MINW = SWRT_TILE_MIN_WAVES>
 __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
-  static_assert(!FMA || (V5 && !WBLEND), "the FMA gather exists for the five-sum window only");
-  static_assert(!PAIR || (TWO && V5 && !WBLEND), "paired lanes split the two snapshots of the five-sum window");
+  static_assert(!FMA || V5, "the FMA gather exists for the five-sum window only");
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
   // row stride = 12 (mod 16) nodes: any 4x4 block of window nodes falls on
   // 16 distinct ds_read_b128 bank quads (node n -> quad (n mod 16)), so lanes
   // of one 16-lane group reading a few neighbouring nodes never conflict
   constexpr int WS = W + ((12 - W % 16) + 16) % 16;
   constexpr int WNP = W * WS;       // nodes per chunk
-  constexpr bool GTWO = TWO && !WBLEND;  // two snapshots in the LDS window
-  constexpr int NCH = GTWO ? (V5 ? 5 : 6) : 3;  // 16-B chunks per node
+  constexpr int NCH = TWO ? (V5 ? 5 : 6) : 3;  // 16-B chunks per node
   constexpr int NB = T * T + 1;     // in-tile cell bins + "elsewhere"
-  // packets sorted per batch (the 32x32-cell tile's window leaves ~8 KB of LDS for the batch arrays)
-  constexpr int MAXB = T >= 32 ? 512 : 2 * NT;
+  constexpr int MAXB = 2 * NT;      // packets sorted per batch
   __shared__ double2 win[NCH * WNP];
   __shared__ int hist[NB];
   __shared__ int kr[MAXB];          // key << 16 | rank
@@ -530,11 +405,8 @@ __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
   const int64_t sbase = a.s0 + (int64_t)ivl * a.nsteps;
   if (!first) __syncthreads();  // every wave is done with the previous window
 
-  // 1. stage the window (WBLEND: one launch = one step, alpha fixed)
-  if constexpr (WBLEND)
-    stage_window_blend<T, M, NT, WS>(a.f0, a.f1, ox, oy, a.alpha0 + (double)a.s0 * a.dalpha, win);
-  else
-    stage_window_regs<TWO, T, M, NT, WS, V5>(fa, fb, ox, oy, win);
+  // 1. stage the window
+  stage_window_regs<TWO, T, M, NT, WS, V5>(fa, fb, ox, oy, win);
   if (!sortc) {
     __syncthreads();  // publish the window
     SWRT_STAMP(1);
@@ -621,112 +493,6 @@ __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
 
     // 3. advance the packets in sorted order (lane -> rank remapped for the
     //    ds_read_b128 lane groups; every rank of the batch is still taken once)
-    if constexpr (PAIR) {
-      const int h = (tid >> 5) & 1;  // this lane's half: x weights + snapshot 0, or y weights + snapshot 1
-      const double cper = h ? a.f0.py : a.f0.px, inv_cper = h ? a.f0.inv_py : a.f0.inv_px;
-      const int icper = h ? a.f0.ipy : a.f0.ipx;
-      // lane_rank & 31: the packet (0..31) of this lane within the wave's run of
-      // 32 cell-sorted packets, so each ds_read_b128 lane group takes 16
-      // consecutive packets (the upper half mirrors the lower)
-      for (int r0 = (tid >> 6) * 32; r0 < nb; r0 += NT / 2) {
-        const int r = r0 + (lane_rank & 31);
-        if (r >= nb) continue;
-        const int64_t pi = sortc ? order[r] : b0 + r;
-        const int64_t po = b0 + r;
-        double x0 = xin[pi], y0 = xin[a.n + pi];
-        double k0 = kin[pi], l0 = kin[a.n + pi];
-        const int orig = pin[pi];
-        double hcx, hcy;
-        drift_inc(k0, l0, a.f2, a.gH, half, a.fastdisp, hcx, hcy);
-        double sgd = (double)(ta.ivmode ? (int64_t)0 : sbase);
-        for (int st = 0; st < a.nsteps; ++st) {
-          const int64_t sg = sbase + st;
-          const double alpha = a.alpha0 + sgd * a.dalpha;
-          sgd = sgd + 1.0;
-          const double x1 = x0 + hcx;
-          const double y1 = y0 + hcy;
-          // this half's coordinate: its cell, offset and six 1-D weights
-          // (stencil_at's operations for x or y), then both halves' on every lane
-          double am;
-          const int cm = cell_frac(h ? y1 : x1, a.f0.dx, a.f0.inv_dx, cper, inv_cper, icper, nx, am);
-          double wm[kNT];
-          lagrange_w(am, a.bump, wm);
-          unsigned ic_, jc_;
-          halves_u32((unsigned)cm, ic_, jc_);
-          const int ic = (int)ic_, jc = (int)jc_;
-          double wx[kNT], wy[kNT];
-#pragma unroll
-          for (int q = 0; q < kNT; ++q) halves_f64(wm[q], wx[q], wy[q]);
-          const int dx_ = ring_diff(ic, ox, nx), dy_ = ring_diff(jc, oy, nx);
-          const bool inwin = dx_ >= -M && dx_ < T + M && dy_ >= -M && dy_ < T + M;
-          double S[kRec];
-          if (inwin) {
-#pragma unroll
-            for (int q = 0; q < kNT; ++q) {
-              asm volatile("" : "+v"(wx[q]));
-              asm volatile("" : "+v"(wy[q]));
-            }
-            gather5_half<WS, WNP, FMA>(win, (dx_ + M) * WS + (dy_ + M), h, wx, wy, S);
-          } else {
-            Stencil sc;
-            sc.ic = ic;
-            sc.jc = jc;
-#pragma unroll
-            for (int q = 0; q < kNT; ++q) { sc.wx[q] = wx[q]; sc.wy[q] = wy[q]; }
-            double dummy[kRec];
-            const double* own = h ? fb.nodes : fa.nodes;
-            gather6_lean<false, FMA>(own, own, npad, sc, S, dummy);
-          }
-          double I[kRec], J[kRec];
-#pragma unroll
-          for (int q = 0; q < 5; ++q) halves_f64(S[q], I[q], J[q]);
-          const double oma = 1 - alpha;
-#pragma unroll
-          for (int q = 0; q < 5; ++q) I[q] = madd<FMA>(oma * I[q], alpha, J[q]);
-          I[5] = -I[2];
-          const double x2 = x1 + dt * I[0];
-          const double y2 = y1 + dt * I[1];
-          const double k2 = k0 - dt * (I[2] * k0 + I[4] * l0);
-          const double l2 = l0 - dt * (I[3] * k0 + I[5] * l0);
-          drift_inc(k2, l2, a.f2, a.gH, half, a.fastdisp, hcx, hcy);
-          x0 = x2 + hcx;
-          y0 = y2 + hcy;
-          k0 = k2;
-          l0 = l2;
-          if (a.hist_x != nullptr && ((sg + 1) % a.save_every) == 0) {
-            const int64_t fr = a.frame0 + (sg + 1) / a.save_every - 1;
-            if (h == 0) {
-              double* hx = a.hist_x + fr * 2 * a.n;
-              hx[orig] = x0; hx[a.n + orig] = y0;
-            } else {
-              double* hk = a.hist_k + fr * 2 * a.n;
-              hk[orig] = k0; hk[a.n + orig] = l0;
-            }
-          }
-        }
-        if (h == 0) {
-          ta.x_out[po] = x0; ta.x_out[a.n + po] = y0;
-          ta.perm_out[po] = orig;
-        } else {
-          ta.k_out[po] = k0; ta.k_out[a.n + po] = l0;
-        }
-        if (nkeys != nullptr && h == 0) {  // fused histogram for the next re-binning (as below)
-          const int ic = fast_cell(x0, a.f0.inv_dx, nx);
-          const int jc = fast_cell(y0, a.f0.inv_dx, nx);
-          const int ntx_ = ta.ntx;
-          const int ntx2 = ic / T, nty2 = jc / T;
-          nkeys[po] = ntx2 * ntx_ + nty2;
-          const int ddx = ring_diff(ntx2, tx, ntx_), ddy = ring_diff(nty2, ty, ntx_);
-          if (ddx != 0 || ddy != 0) {
-            atomicAdd(&nbr[4], -1);
-            if (ddx >= -1 && ddx <= 1 && ddy >= -1 && ddy <= 1)
-              atomicAdd(&nbr[(ddx + 1) * 3 + (ddy + 1)], 1);
-            else
-              atomicAdd(&ta.next_counts[ntx2 * ntx_ + nty2], 1);
-          }
-        }
-      }
-    } else
     for (int r0 = tid & ~63; r0 < nb; r0 += NT) {
       const int r = r0 + lane_rank;
       if (r >= nb) continue;
@@ -758,29 +524,22 @@ __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
 #ifdef SWRT_PHASE_TIMING
         if (!inwin) atomicAdd(&nfall, 1);
 #endif
-        if constexpr (WBLEND) {
-          if (inwin)
-            gather6_lds<false, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
+        if (inwin) {
+          if constexpr (V5)
+            gather5_lds<TWO, WS, WNP, FMA, PF>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
           else
-            gather6_blend(a.f0.nodes, a.f1.nodes, npad, sc, alpha, I);
+            gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
         } else {
-          if (inwin) {
-            if constexpr (V5)
-              gather5_lds<TWO, WS, WNP, FMA, PF>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
-            else
-              gather6_lds<TWO, WS, WNP>(win, (dx_ + M) * WS + (dy_ + M), sc, I, J);
-          } else {
-            gather6_lean<TWO, FMA>(fa.nodes, fb.nodes, npad, sc, I, J);
-          }
-          if constexpr (TWO) {
-            const double oma = 1 - alpha;
-            // V5 fields have v_y == -u_x in both snapshots (and both gathers
-            // sum them in the same order), so the blended v_y is exactly the
-            // negated blended u_x: negation commutes with every rounding
+          gather6_lean<TWO, FMA>(fa.nodes, fb.nodes, npad, sc, I, J);
+        }
+        if constexpr (TWO) {
+          const double oma = 1 - alpha;
+          // V5 fields have v_y == -u_x in both snapshots (and both gathers
+          // sum them in the same order), so the blended v_y is exactly the
+          // negated blended u_x: negation commutes with every rounding
 #pragma unroll
-            for (int q = 0; q < (V5 ? 5 : kRec); ++q) I[q] = madd<FMA>(oma * I[q], alpha, J[q]);
-            if constexpr (V5) I[5] = -I[2];
-          }
+          for (int q = 0; q < (V5 ? 5 : kRec); ++q) I[q] = madd<FMA>(oma * I[q], alpha, J[q]);
+          if constexpr (V5) I[5] = -I[2];
         }
         const double x2 = x1 + dt * I[0];
         const double y2 = y1 + dt * I[1];

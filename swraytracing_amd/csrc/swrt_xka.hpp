@@ -15,6 +15,7 @@
 #include <stdint.h>
 
 #include "swrt_kernels.hpp"
+#include "swrt_tile.hpp"
 
 namespace swrt {
 
@@ -331,8 +332,8 @@ __global__ void __launch_bounds__(NT) xka_tile_kernel(XkaArgs a, const int* star
   constexpr int WS = W + ((12 - W % 16) + 16) % 16;
   constexpr int WN = W * WS;
   __shared__ double2 win[4 * WN];
-  const int tile = (int)xcd_block(blockIdx.x, gridDim.x);
-  const int pbeg = starts[tile], pend = starts[tile + 1];
+  int pbeg, pend;  // clamped to [0, n] (wg_work_range)
+  const int tile = wg_work_range(starts, a.n, pbeg, pend);
   if (pbeg == pend) return;  // uniform: no barrier is skipped by part of the block
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int nx = a.nx;

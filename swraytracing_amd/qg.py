@@ -40,6 +40,7 @@ class QGModel:
         self.nlayers = params.nlayers
         self.L = params.L
         self.dx = params.L / nx
+        self.spec_pending = False  # a speculative step is queued (step_speculative) and not yet resolved
         self.ctx.qg_init(params, nx, qk)
 
     @classmethod
@@ -58,19 +59,31 @@ class QGModel:
                      Cg=Cg, shear=shear, nu=nutune * dx ** (2 * alpha), hyper_order=float(alpha), r=r)
         return cls(qk, nx, p, **kw)
 
+    def settle(self):
+        """Drop a pending speculative step (the model stays at the committed
+        step).  The calls the library refuses while one is pending — step,
+        max_speed(_async), snapshot — settle first, so code that touches the
+        model after a TwoLayerLoop never meets SWRT_ERR_STATE."""
+        if self.spec_pending:
+            self.resolve(False)
+
     def step(self, dt, nsteps=1):
+        self.settle()
         self.ctx.qg_step(dt, nsteps)
 
     def step_speculative(self, dt):
         """Queue the next step with dt and its CFL read-back before the current
         U0 is known; the committed state stays until resolve()."""
         self.ctx.qg_step_speculative(dt)
+        self.spec_pending = True
 
     def resolve(self, accept):
         self.ctx.qg_resolve(accept)
+        self.spec_pending = False
 
     def max_speed(self):
         """U0 = sqrt(max(u.^2 + v.^2)) of grid_U(qk) (all layers, u + shear)."""
+        self.settle()
         return self.ctx.qg_max_speed()
 
     def cfl_rule(self, dt, U0, cfl_fraction):
@@ -89,6 +102,7 @@ class QGModel:
     def max_speed_async(self):
         """Enqueue U0 of the current qk; collect it with max_speed_result()
         after queueing other work (the driver queues the packets first)."""
+        self.settle()
         self.ctx.qg_max_speed_async()
 
     def max_speed_result(self):
@@ -113,6 +127,7 @@ class QGModel:
 
     def snapshot(self, slot, which=0, layer=0, ny_period=0):
         """grid_U of the current (0) / previous (1) qk into packet slot `slot`."""
+        self.settle()
         self.ctx.qg_snapshot(slot, which, layer, ny_period)
 
 
@@ -211,7 +226,11 @@ class TwoLayerLoop:
     never idles the GPU), and — once t > packet_delay — grid_U of (prev_qk,
     qk) into the packet slots and the packet interval [t, t+dt].  Used by
     :func:`qg2layersw_raytrace` (which adds the frame writes) and by bench.py's
-    end-to-end driver-step figure."""
+    end-to-end driver-step figure.
+
+    With ``speculate`` (default) every step returns with the next PDE step
+    queued speculatively (QGModel.spec_pending); the model's own calls drop
+    it before they run (QGModel.settle), and :meth:`settle` does so explicitly."""
 
     def __init__(self, model, ens, dt, U0, cfl_fraction=0.25, packet_delay=0.0, nsub=5, packet_intervals=1,
                  integrator="leapfrog", log=None, speculate=True):
@@ -222,7 +241,6 @@ class TwoLayerLoop:
         # the rule then accepts it, or drops it and steps with its new dt —
         # the same computation either way (bit-identical files)
         self.speculate = speculate
-        self._spec = False
         self.cfl_fraction, self.packet_delay = cfl_fraction, packet_delay
         self.nx = model.nx
         self.t = 0.0
@@ -239,10 +257,9 @@ class TwoLayerLoop:
         if changed and self.log is not None:
             self.log(f"CFL condition not met, max|u|={self.U0:f}, new dt={self.dt:f}\n")
         self.dts.append(self.dt)
-        if self._spec:
+        if self.model.spec_pending:
             # the step queued by the previous call with the previous dt
             self.model.resolve(not changed)
-            self._spec = False
             if changed:
                 self.model.step(self.dt)
                 self.model.max_speed_async()
@@ -262,7 +279,6 @@ class TwoLayerLoop:
             self.have_cur = False
         if self.speculate and self.model.params.nlayers == 2 and getattr(self.model.ctx, "qg_fused", True):
             self.model.step_speculative(self.dt)
-            self._spec = True
         self.U0 = self.model.max_speed_result()  # this step's (read-backs pop oldest first)
         return active
 
@@ -272,10 +288,9 @@ class TwoLayerLoop:
 
     def settle(self):
         """Drop a pending speculative step: the model stays at the committed
-        step (for PDE calls outside the loop after it)."""
-        if self._spec:
-            self.model.resolve(False)
-            self._spec = False
+        step.  Optional: QGModel's step / max_speed / snapshot settle on their
+        own, so PDE calls after the loop need no explicit settle."""
+        self.model.settle()
 
 
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,

@@ -53,8 +53,7 @@ def _run_calls(ctx, bench, w, calls, sub=5):
     return ctx.packets_get()
 
 
-@pytest.mark.parametrize("streams", [2, 4])
-def test_adversarial_overlap_bitexact_and_checker_silent(debug_ctx, oracle_lib, streams):
+def test_adversarial_overlap_bitexact_and_checker_silent(debug_ctx, oracle_lib):
     """A ~200 us sleep kernel before every extra-stream part launch: call k's
     extra parts run entirely under call k+1's packet-stream part — and under
     the sort launch that follows each re-binning, which gathers its input from
@@ -67,13 +66,13 @@ def test_adversarial_overlap_bitexact_and_checker_silent(debug_ctx, oracle_lib, 
     ctx.set_locality(20, 0)
     ctx.set_packet_streams(1)
     x1, k1 = _run_calls(ctx, bench, w, 12)
-    ctx.set_packet_streams(streams)
+    ctx.set_packet_streams(2)
     ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1)
     ctx.debug_set(L.DEBUG_SPIN_US, 200)
     xs, ks = _run_calls(ctx, bench, w, 12)
     checks = ctx.debug_get(L.DEBUG_HAZARD_CHECKS)
     assert checks > 1000, checks  # the checker saw the part launches
-    assert _bits_equal(x1, xs) and _bits_equal(k1, ks), streams
+    assert _bits_equal(x1, xs) and _bits_equal(k1, ks)
     p0, p1 = ctx.get_field_grid(0, 512), ctx.get_field_grid(1, 512)
     idx = np.sort(np.random.default_rng(11).choice(300_000, 1200, replace=False))
     xo, ko = w["x"][idx], w["k"][idx]
@@ -119,33 +118,26 @@ def test_checker_catches_the_pre_third_buffer_race(debug_ctx):
     assert _bits_equal(x1, xf) and _bits_equal(k1, kf)
 
 
-@pytest.mark.parametrize("switch", ["locality", "tail_split"])
-def test_single_launch_after_split_calls_joins_first(debug_ctx, switch):
+def test_single_launch_after_split_calls_joins_first(debug_ctx):
     """70,000 packets (above the one-stream threshold) advanced by split
     launches, then a call whose launch runs on the packet stream alone — the
-    per-packet kernel after swrt_set_locality(0, 0), or one whole tile launch
-    after swrt_set_tail_split(1, 0) — then split launches again: that launch
-    orders the extra stream's parts of the previous call before it (the
-    checker stays silent) and the bits equal one stream's."""
+    per-packet kernel after swrt_set_locality(0, 0) — then split launches
+    again: that launch orders the extra stream's parts of the previous call
+    before it (the checker stays silent) and the bits equal one stream's."""
     ctx, L = debug_ctx
     bench, w = _bench_workload(ctx, 70_000)
     out = {}
     for streams in (1, 2):
         ctx.set_packet_streams(streams)
         ctx.set_locality(20, 0)
-        ctx.set_tail_split(0, 0)
         ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1 if streams > 1 else 0)
         ctx.debug_set(L.DEBUG_SPIN_US, 100 if streams > 1 else 0)
         ctx.packets_set(w["x"], w["k"])
         for _ in range(3):
             bench.step(ctx, w, 5)
-        if switch == "locality":
-            ctx.set_locality(0, 0)
-        else:
-            ctx.set_tail_split(1, 0)
+        ctx.set_locality(0, 0)
         bench.step(ctx, w, 5)
         ctx.set_locality(20, 0)
-        ctx.set_tail_split(0, 0)
         for _ in range(3):
             bench.step(ctx, w, 5)
         out[streams] = ctx.packets_get()
@@ -156,13 +148,13 @@ def test_single_launch_after_split_calls_joins_first(debug_ctx, switch):
 def test_checker_silent_over_the_mixed_call_sequence(debug_ctx):
     """test_packet_streams_bit_identical's call sequence (history frames,
     re-binnings inside and between calls, slot rewrites, multi-interval
-    launches, reads, ode23) on 2 and 4 streams with the checker on."""
+    launches, reads, ode23) on 2 streams with the checker on."""
     import swraytracing_amd as sw
     ctx, L = debug_ctx
     bench, w = _bench_workload(ctx, 300_000)
     p0, p1 = ctx.get_field_grid(0).copy(), ctx.get_field_grid(1).copy()
     h = w["dt"] / 5
-    for streams in (2, 4):
+    for streams in (2,):
         ctx.set_packet_streams(streams)
         ctx.set_locality(20, 0)
         ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1)
@@ -184,3 +176,69 @@ def test_checker_silent_over_the_mixed_call_sequence(debug_ctx):
         ctx.packets_get()
         assert ctx.debug_get(L.DEBUG_HAZARD_CHECKS) > 0
         ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+
+
+def test_checker_refuses_a_skewed_cycle_end_share(debug_ctx):
+    """Round 4's hang (profiles/r04_stream_split): the launch that ends a
+    re-binning cycle split its tiles unevenly between the two packet streams
+    (SWRT_DEBUG_SHARE_SKEW: 2/3 : 1/3), so its packet-stream part took tiles
+    the other stream's part of the previous call could still be writing.  The
+    checker enumerates the tiles each part launch takes with the device's own
+    mapping (swrt_share.hpp), so it refuses that launch before anything is
+    queued; the skew is refused outright without the checker.  Reference
+    semantics guarded: ode_symplectic.m:18-21 — packets are independent, so
+    any tile schedule must give the same bits, which only a race can break."""
+    import swraytracing_amd as sw
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 300_000)
+    ctx.set_locality(20, 0)
+    ctx.set_packet_streams(2)
+    with pytest.raises(sw.SwrtError) as ei:
+        ctx.debug_set(L.DEBUG_SHARE_SKEW, 1)  # not without the checker
+    assert "SWRT_ERR_STATE" in str(ei.value)
+    ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1)
+    ctx.debug_set(L.DEBUG_SHARE_SKEW, 1)
+    ctx.packets_set(w["x"], w["k"])
+    for _ in range(3):  # the cycle's first three launches: the product share
+        bench.step(ctx, w, 5)
+    with pytest.raises(sw.SwrtError) as ei:
+        bench.step(ctx, w, 5)  # the cycle-ending launch, skewed
+    msg = str(ei.value)
+    assert "SWRT_ERR_STATE" in msg and "hazard" in msg and "skewed" in msg, msg
+    # nothing was queued: after a join the state is the one-stream state of 15 steps
+    ctx.debug_set(L.DEBUG_SHARE_SKEW, 0)
+    ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+    xa, ka = ctx.packets_get()
+    ctx.set_packet_streams(1)
+    x1, k1 = _run_calls(ctx, bench, w, 3)
+    assert _bits_equal(x1, xa) and _bits_equal(k1, ka)
+
+
+@pytest.mark.parametrize("delta", [1000, -7])
+def test_corrupted_tile_count_is_an_error_not_a_hang(debug_ctx, delta):
+    """One tile count corrupted before a re-binning's scan (on the packet
+    stream, with the second stream's parts in flight): the scan's own check
+    (counts >= 0 summing to the packets, bin_scan_kernel) leaves an empty
+    binning, so no launch walks a bad packet range, and the next host
+    synchronisation returns SWRT_ERR_STATE; the packet state stays refused
+    until swrt_packets_set, after which the run gives the one-stream bits."""
+    import swraytracing_amd as sw
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 300_000)
+    ctx.set_locality(20, 0)
+    ctx.set_packet_streams(1)
+    x1, k1 = _run_calls(ctx, bench, w, 6)
+    ctx.set_packet_streams(2)
+    ctx.packets_set(w["x"], w["k"])
+    for _ in range(2):
+        bench.step(ctx, w, 5)
+    ctx.debug_set(L.DEBUG_CORRUPT_COUNT, delta)
+    for _ in range(6):
+        bench.step(ctx, w, 5)  # queued asynchronously: the error surfaces at the next sync
+    with pytest.raises(sw.SwrtError) as ei:
+        ctx.synchronize()
+    assert "SWRT_ERR_STATE" in str(ei.value) and "binning" in str(ei.value)
+    with pytest.raises(sw.SwrtError):
+        ctx.packets_get()
+    x2, k2 = _run_calls(ctx, bench, w, 6)  # packets_set clears it
+    assert _bits_equal(x1, x2) and _bits_equal(k1, k2)

@@ -88,24 +88,22 @@ def test_intervals_match_sequential_calls(ctx, nint, rebin, kernel):
     assert a[2].shape[0] == nint  # one frame per interval
 
 
-@pytest.mark.parametrize("lanes,cells", [(1, 16), (2, 16), (1, 32)])
-def test_intervals_match_oracle_subset(ctx, oracle_lib, lanes, cells):
+@pytest.mark.parametrize("sparse", [1, 2])
+def test_intervals_match_oracle_subset(ctx, oracle_lib, sparse):
     """Four intervals in one launch vs the C oracle, interval by interval on
-    the device-prepared snapshots (a subset of the packets); one or two lanes
-    per packet (the window re-staged between intervals under paired lanes)."""
+    the device-prepared snapshots (a subset of the packets); the dense and the
+    sparse launch shape (the window re-staged between intervals in both)."""
     snaps = _snapshots(5)
     x, k = _packets(60_000, seed=9)
     dx = L / NX
     hs = [0.05 * dx / 0.7 * s for s in (1.0, 0.9, 1.1, 1.0)]
     ctx.set_locality(20, 0)
-    ctx.set_lanes_per_packet(lanes)
-    ctx.set_tile_cells(cells)
+    ctx.set_sparse_tiles(sparse)
     try:
         xs, ks, _, _ = _run_intervals(ctx, snaps, x, k, hs, 5, 0)
         planes = [ctx.get_field_grid(i, NX) for i in range(5)]
     finally:
-        ctx.set_tile_cells(0)
-        ctx.set_lanes_per_packet(0)
+        ctx.set_sparse_tiles(0)
         ctx.set_locality(4, 0)
     idx = np.sort(np.random.default_rng(3).choice(x.shape[0], 2000, replace=False))
     xo, ko = x[idx], k[idx]

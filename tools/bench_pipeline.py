@@ -41,7 +41,6 @@ def main():
     ap.add_argument("--ode23", action="store_true", help="also time the drivers' ode23 over one PDE interval")
     ap.add_argument("--ode23-controller", default=None, choices=["library", "python"],
                     help="ode23 step-size controller: in the C library (default) or the Python loop (A/B)")
-    ap.add_argument("--qg-graphs", action="store_true", help="hipGraph replay of the QG step (A/B; default off)")
     ap.add_argument("--one-stream", action="store_true", help="QG PDE on the packet stream (A/B)")
     ap.add_argument("--no-fused", action="store_true", help="separate transforms per QG call (A/B)")
     ap.add_argument("--intervals", type=int, default=1, help="PDE steps whose packet intervals go in one call")
@@ -50,7 +49,6 @@ def main():
     args = ap.parse_args()
     nx, L, f, Cg = args.nx, 20.0, 3.0, 1.0
     ctx = sw.Context(0)
-    ctx.qg_set_graphs(args.qg_graphs)
     ctx.qg_set_stream(not args.one_stream)
     ctx.qg_set_fused(not args.no_fused)
     rng = np.random.default_rng(5)
@@ -117,7 +115,7 @@ def main():
     out = {
         "metric": "driver step time, qg2layersw_raytrace loop on device (PDE + snapshots + packets)",
         "config": {"nx": nx, "layers": 2, "packets": args.packets, "nsub": args.nsub, "steps": r,
-                   "qg_graphs": args.qg_graphs, "qg_stream": not args.one_stream,
+                   "qg_stream": not args.one_stream,
                    "qg_fused": not args.no_fused,
                    "packet_intervals": args.intervals, "fixed_dt": args.fixed_dt},
         "pde_ms": pde, "cfl_ms": cfl, "snapshot_ms": snap, "packets_ms": pk, "step_ms": full,

@@ -45,9 +45,8 @@ def run(nx, N, steps, speculate=True):
             loop.dt, changed = model.cfl_rule(loop.dt, loop.U0, loop.cfl_fraction)
             loop.dts.append(loop.dt)
             t1 = time.perf_counter(); acc["cfl"] += t1 - t; t = t1
-            if loop._spec:
+            if model.spec_pending:
                 model.resolve(not changed)
-                loop._spec = False
                 if changed:
                     model.step(loop.dt)
                     model.max_speed_async()
@@ -66,7 +65,6 @@ def run(nx, N, steps, speculate=True):
             t1 = time.perf_counter(); acc["packets"] += t1 - t; t = t1
             if speculate:
                 model.step_speculative(loop.dt)
-                loop._spec = True
             t1 = time.perf_counter(); acc["speculate"] += t1 - t; t = t1
             loop.U0 = model.max_speed_result()
             t1 = time.perf_counter(); acc["U0 result"] += t1 - t

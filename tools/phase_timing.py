@@ -28,12 +28,9 @@ def main():
     ap.add_argument("--packets", type=int, default=1_000_000)
     ap.add_argument("--mode", default="blend")
     ap.add_argument("--samples", type=int, default=5)
-    ap.add_argument("--tail-split", type=int, default=-1)
-    ap.add_argument("--tail-quarters", type=int, default=0)
     ap.add_argument("--substeps", type=int, default=5)
     ap.add_argument("--rebin-every", type=int, default=20)
     ap.add_argument("--dump", default="", help="save every sample's raw stamps (npz) for offline analysis")
-    ap.add_argument("--lanes-per-packet", type=int, default=0)
     args = ap.parse_args()
     args.world, args.rank, args.seed = 1, 0, 146
     lib = _lib.load()
@@ -42,16 +39,13 @@ def main():
     ctx = sw.Context(0)
     ctx.set_locality(args.rebin_every, 0)
     ctx.set_kernel(2)
-    if args.tail_split >= 0:
-        ctx.set_tail_split(args.tail_split, args.tail_quarters)
-    ctx.set_lanes_per_packet(args.lanes_per_packet)
     bench._imports()
     w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
     ctx.packets_set(w["x"], w["k"])
     for _ in range(8):
         bench.step(ctx, w, args.substeps)
     ntiles = (args.nx // 16) ** 2
-    nrows = 4 * ntiles  # workgroups (half/quarter-tile workgroups with --tail-split)
+    nrows = 4 * ntiles  # workgroups
     buf = np.zeros(nrows * 8, dtype=np.uint64)
     ptr = buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong))
     res = []
