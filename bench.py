@@ -515,6 +515,12 @@ def relay(cmd):
     return proc.wait()
 
 
+def progress(msg):
+    """One line per bench phase on stderr (a run that prints nothing for
+    minutes looks hung to the GPU box's watchdog)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _imports():
     """torch and the library, imported only in a rank (never in the launcher)."""
     global torch, dist, sw, gather_packets, max_over_ranks, shard_range
@@ -643,6 +649,7 @@ def main(argv=None):
         if distributed:
             dist.barrier()
 
+    progress("metric")
     elapsed, kms, launches, (clock_ghz, clock_spread) = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
     if distributed:
         elapsed = max_over_ranks(elapsed, backend=args.dist_backend)
@@ -715,6 +722,7 @@ def main(argv=None):
     if not args.no_fma and args.kernel in (0, 2) and args.gather_mode == 0:
         # the opt-in FMA gather (tolerance parity, tests/test_gpu_parity.py::test_fma_gather_mode_tolerance):
         # the same workload and packets, timed the same way; the headline stays bit-exact
+        progress("fma_gather")
         ctx.packets_set(w["x"], w["k"])
         ctx.set_gather_mode(1)
         el2, kms2, l2, (clk2, _) = timed(ctx, w, args, dev, args.steps, args.warmup, barrier)
@@ -728,6 +736,7 @@ def main(argv=None):
                              "parity": "tolerance: stencil sums and blend by fused multiply-add, "
                                        "<= 1e-13 relative per step vs the bit-exact path"}
     if world == 1 and not args.no_forecast and args.scaling == "strong":
+        progress("strong_scaling_forecast")
         out["strong_scaling_forecast"] = strong_scaling_forecast(ctx, w, args, dev, n_total, value)
         if args.forecast_intervals > 1 and w["nslots"] == 2 and args.kernel in (0, 2):
             out["strong_scaling_forecast_intervals"] = intervals_forecast(ctx, w, args, dev, n_total, value,
@@ -735,6 +744,7 @@ def main(argv=None):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # the GPU box's CPU share for one GPU is 16 threads (OMP_NUM_THREADS there)
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        progress("cpu_baseline")
         out["cpu_baseline"] = cpu_baseline(ctx, w, args.cpu_seconds, threads)
         # all host cores (every CPU this process may run on) and 1 core
         try:
@@ -751,8 +761,10 @@ def main(argv=None):
     elif rank == 0:
         out["cpu_baseline"] = None
     if args.driver_steps > 0 and args.mode == "blend":
+        progress("driver_step")
         out["driver_step"] = driver_step(ctx, w, args, dev, distributed, n_total)
         if world == 1 and not args.no_forecast and args.scaling == "strong":
+            progress("driver_step_forecast")
             fc = driver_forecast(ctx, w, args, dev, n_total, out["driver_step"])
             pk = out.get("strong_scaling_forecast", {})
             for G in ("2", "4", "8"):
@@ -762,6 +774,7 @@ def main(argv=None):
             out["driver_step_forecast"] = fc
     if args.ode23_steps > 0 and args.mode == "blend" and world == 1:
         # (single rank: a sharded ode23 needs the error norm's allreduce, PacketEnsemble(shard=...))
+        progress("driver_step_ode23")
         out["driver_step_ode23"] = driver_step(ctx, w, args, dev, distributed, n_total, integrator="ode23",
                                                nsteps=args.ode23_steps)
     if rank == 0:

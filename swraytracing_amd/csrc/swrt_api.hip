@@ -68,8 +68,14 @@ constexpr int kTileThreads = SWRT_TILE_THREADS;
 #define SWRT_SPARSE_BELOW 192
 #endif
 constexpr int kSparseBelow = SWRT_SPARSE_BELOW;
-constexpr int kSparseThreads = 256;
-constexpr int kSparsePrefetch = 3;
+#ifndef SWRT_SPARSE_THREADS
+#define SWRT_SPARSE_THREADS 256
+#endif
+#ifndef SWRT_SPARSE_PREFETCH
+#define SWRT_SPARSE_PREFETCH 3
+#endif
+constexpr int kSparseThreads = SWRT_SPARSE_THREADS;
+constexpr int kSparsePrefetch = SWRT_SPARSE_PREFETCH;
 
 struct Slot {
   double* nodes = nullptr;  // padded interleaved records

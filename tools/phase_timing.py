@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--samples", type=int, default=5)
     ap.add_argument("--substeps", type=int, default=5)
     ap.add_argument("--rebin-every", type=int, default=20)
+    ap.add_argument("--streams", type=int, default=1,
+                    help="packet streams (1: the stamps are indexed by blockIdx, which two part launches share)")
     ap.add_argument("--dump", default="", help="save every sample's raw stamps (npz) for offline analysis")
     args = ap.parse_args()
     args.world, args.rank, args.seed = 1, 0, 146
@@ -39,6 +41,7 @@ def main():
     ctx = sw.Context(0)
     ctx.set_locality(args.rebin_every, 0)
     ctx.set_kernel(2)
+    ctx.set_packet_streams(args.streams)
     bench._imports()
     w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
     ctx.packets_set(w["x"], w["k"])
