@@ -456,12 +456,14 @@ int swrt_set_timing(swrt_ctx* ctx, int every);
 int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launches);
 /* Observed shader clock over a region of the packet stream: swrt_clock_stamp
  * (ctx, 0) before it and (ctx, 1) after it each enqueue (after every queued
- * packet launch) one-wave workgroups on every XCD that record the shader-cycle
- * counter (s_memtime) and the 100 MHz real-time counter (s_memrealtime);
- * swrt_clock_ghz synchronises and returns the median over same-XCD
- * (start, end) pairs of cycles / seconds, and (spread_out, may be NULL) the
- * pairs' (max - min) / median.  Normalises a throughput measured on one box to
- * the clock it actually ran at (the chip lowers its clock under load). */
+ * packet launch) 1024 one-wave workgroups that record the shader-cycle
+ * counter (s_memtime), the 100 MHz real-time counter (s_memrealtime) and the
+ * CU they ran on; swrt_clock_ghz synchronises and returns the median over
+ * the CUs stamped at both ends of cycles / seconds (a CU's own counter: the
+ * counters of different CUs are not aligned), and (spread_out, may be NULL)
+ * the per-CU clocks' (p90 - p10) / median.  Normalises a throughput measured
+ * on one box to the clock it actually ran at (the chip lowers its clock
+ * under load). */
 int swrt_clock_stamp(swrt_ctx* ctx, int which);
 int swrt_clock_ghz(swrt_ctx* ctx, double* ghz_out, double* spread_out);
 

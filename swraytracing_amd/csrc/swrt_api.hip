@@ -12,6 +12,7 @@
 #include <cstring>
 #include <algorithm>
 #include <climits>
+#include <map>
 #include <new>
 #include <string>
 #include <vector>
@@ -74,8 +75,12 @@ constexpr int kSparseBelow = SWRT_SPARSE_BELOW;
 #ifndef SWRT_SPARSE_PREFETCH
 #define SWRT_SPARSE_PREFETCH 3
 #endif
+#ifndef SWRT_SPARSE_MINW
+#define SWRT_SPARSE_MINW 2
+#endif
 constexpr int kSparseThreads = SWRT_SPARSE_THREADS;
 constexpr int kSparsePrefetch = SWRT_SPARSE_PREFETCH;
+constexpr int kSparseMinWaves = SWRT_SPARSE_MINW;  // waves per SIMD the sparse shape's registers are sized for
 
 struct Slot {
   double* nodes = nullptr;  // padded interleaved records
@@ -763,22 +768,26 @@ __global__ void debug_corrupt_count_kernel(int* counts, int tile, int delta) {
 }
 
 // Shader-clock probe (swrt_clock_stamp): kClockWaves one-wave workgroups
-// (dispatched round-robin over the 8 XCDs) each record the shader-cycle
-// counter (s_memtime), the 100 MHz real-time counter (s_memrealtime) and
-// their XCD.  Start and end stamps of one XCD bracket a timed region:
-// cycles / seconds = the clock the chip ran at over it (MI355X_MICROARCH.md,
-// "DVFS give-back" item 6).  Plain vector stores, a buffer of its own.
-constexpr int kClockWaves = 32;
+// (several per CU) each record the shader-cycle counter (s_memtime), the
+// 100 MHz real-time counter (s_memrealtime) and the CU they ran on (XCD, SE,
+// SH, CU ids).  A start and an end stamp of the SAME CU bracket a timed
+// region: cycles / seconds = the clock that CU ran at over it
+// (MI355X_MICROARCH.md, "DVFS give-back" item 6); s_memtime counters of
+// different CUs are not aligned, so only same-CU pairs are used.  Plain
+// vector stores, a buffer of its own.
+constexpr int kClockWaves = 1024;
 constexpr double kRealTimeHz = 100e6;
 __global__ void clock_stamp_kernel(unsigned long long* out) {
-  unsigned xcc;
+  unsigned xcc, hw;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
   const unsigned long long t = __builtin_amdgcn_s_memtime();
   const unsigned long long r = __builtin_amdgcn_s_memrealtime();
   if (threadIdx.x == 0) {
     out[3 * blockIdx.x + 0] = t;
     out[3 * blockIdx.x + 1] = r;
-    out[3 * blockIdx.x + 2] = xcc & 0xf;
+    // CU identity: XCD | SE | SH | CU (the wave/SIMD bits masked off)
+    out[3 * blockIdx.x + 2] = ((unsigned long long)(xcc & 0xf) << 16) | ((hw >> 8) & 0xffffu);
   }
 }
 
@@ -1062,9 +1071,9 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     if (iv ? iv->div_free : two_v5(c, 2, 0)) {
       if (tile_threads(c, true, ntiles) == kSparseThreads) {
         if (fma)
-          HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, true, true, kSparsePrefetch, 2>, kSparseThreads, t, zero));
+          HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, true, true, kSparsePrefetch, kSparseMinWaves>, kSparseThreads, t, zero));
         else
-          HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, true, false, kSparsePrefetch, 2>, kSparseThreads, t, zero));
+          HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kSparseThreads, true, false, kSparsePrefetch, kSparseMinWaves>, kSparseThreads, t, zero));
       } else if (fma) {
         HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTile, kMargin, kTileThreads, true, true>, kTileThreads, t, zero));
       } else {
@@ -2605,25 +2614,36 @@ int swrt_clock_ghz(swrt_ctx* c, double* ghz_out, double* spread_out) {
   if (!c->clk) return fail(c, SWRT_ERR_STATE, "no clock stamps (swrt_clock_stamp 0 and 1 first)");
   GUARD_BEGIN
   HIPCHK(c, hipSetDevice(c->device));
-  unsigned long long h[2 * kClockWaves * 3];
-  HIPCHK(c, hipMemcpyAsync(h, c->clk, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  std::vector<unsigned long long> h(2 * kClockWaves * 3);
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->clk, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
+                           c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   hz_synced(c);
-  // every (start, end) pair of waves on one XCD: shader cycles / real time
+  // per CU: its first start stamp and its last end stamp
+  std::map<unsigned long long, std::pair<int, int>> cu;  // id -> (start wave, end wave)
+  const unsigned long long* s = h.data();
+  const unsigned long long* e = h.data() + kClockWaves * 3;
+  for (int i = 0; i < kClockWaves; ++i) {
+    auto& p = cu.emplace(s[3 * i + 2], std::make_pair(-1, -1)).first->second;
+    if (p.first < 0 || s[3 * i + 1] < s[3 * p.first + 1]) p.first = i;
+  }
+  for (int j = 0; j < kClockWaves; ++j) {
+    auto it = cu.find(e[3 * j + 2]);
+    if (it != cu.end() && (it->second.second < 0 || e[3 * j + 1] > e[3 * it->second.second + 1])) it->second.second = j;
+  }
   std::vector<double> ghz;
-  const unsigned long long* s = h;
-  const unsigned long long* e = h + kClockWaves * 3;
-  for (int i = 0; i < kClockWaves; ++i)
-    for (int j = 0; j < kClockWaves; ++j) {
-      if (s[3 * i + 2] != e[3 * j + 2] || e[3 * j + 1] <= s[3 * i + 1] || e[3 * j] <= s[3 * i]) continue;
-      const double sec = (double)(e[3 * j + 1] - s[3 * i + 1]) / kRealTimeHz;
-      ghz.push_back((double)(e[3 * j] - s[3 * i]) / sec / 1e9);
-    }
-  if (ghz.empty()) return fail(c, SWRT_ERR_STATE, "no start/end stamp pair on one XCD");
+  for (const auto& kv : cu) {
+    const int i = kv.second.first, j = kv.second.second;
+    if (i < 0 || j < 0 || e[3 * j + 1] <= s[3 * i + 1] || e[3 * j] <= s[3 * i]) continue;
+    const double sec = (double)(e[3 * j + 1] - s[3 * i + 1]) / kRealTimeHz;
+    ghz.push_back((double)(e[3 * j] - s[3 * i]) / sec / 1e9);
+  }
+  if (ghz.empty()) return fail(c, SWRT_ERR_STATE, "no CU with both a start and an end stamp");
   std::sort(ghz.begin(), ghz.end());
   const double med = ghz[ghz.size() / 2];
   *ghz_out = med;
-  if (spread_out) *spread_out = (ghz.back() - ghz.front()) / med;
+  // spread of the per-CU clocks: (p90 - p10) / median over the CUs paired
+  if (spread_out) *spread_out = (ghz[(ghz.size() * 9) / 10] - ghz[ghz.size() / 10]) / med;
   return SWRT_OK;
   GUARD_END(c)
 }

@@ -540,45 +540,6 @@ __global__ void __launch_bounds__(1024) qg_post_rows_split_kernel(const double2*
   }
 }
 
-// The same with V of the eight planes per workgroup (V = 1, 2, 4; blockIdx =
-// (8/V) r + h: planes V h .. V h + V-1), blockDim = V n/4, dynamic LDS V n
-// double2.  Beside packet launches (two ~70 KB-window workgroups per CU) a
-// workgroup needing less LDS can run in what they leave free.  The element
-// functions compute every plane of their group and the sink keeps this
-// workgroup's: the same values as the split form.
-struct LdsRowPlanesSel {
-  double2* row;  // this workgroup's planes lo .. lo+V-1 at row + (pl - lo) n
-  int n;
-  int base;      // the element function's plane 0 is output plane `base`
-  int lo, V;
-  __device__ __forceinline__ void operator()(int pl, int64_t idx, double2 v) const {
-    const int q = pl + base - lo;
-    if ((unsigned)q < (unsigned)V) row[q * n + ((int)idx & (n - 1))] = v;
-  }
-};
-template <int V>
-__global__ void __launch_bounds__(1024) qg_post_rows_v_kernel(const double2* qk, QGDev g, int64_t nhalf, int logn,
-                                                              const double2* tw, double2* out,
-                                                              unsigned long long* dmax) {
-  extern __shared__ double2 rows[];
-  constexpr int H = 8 / V;
-  const int n = g.n;
-  const int64_t nn = (int64_t)n * n;
-  const int r = blockIdx.x / H, h = blockIdx.x % H, lo = V * h;
-  const int q = n >> 2, t = threadIdx.x;
-  if (blockIdx.x == 0 && t == 0) *dmax = 0ull;
-  for (int e = t; e < n; e += blockDim.x) {
-    const int64_t idx = (int64_t)e + (int64_t)n * r;
-    if (lo < 4) qg_jac_spectra_to<2>(idx, qk, g, LdsRowPlanesSel{rows, n, 0, lo, V});
-    if (lo <= 4 && 4 < lo + V) qg_vel_spectra_to<1>(idx, qk + nhalf, g, LdsRowPlanesSel{rows, n, 4, lo, V});
-    if (lo + V > 5) spectra_to(idx, qk, n, 1, g.K_d2, g.kscale, 0, LdsRowPlanesSel{rows, n, 5, lo, V}, n / 2, 1);
-  }
-  __syncthreads();
-  fft_stages_one_buffer(rows + (t / q) * n, t % q, n, logn, tw, 1);
-  for (int e = t; e < V * n; e += blockDim.x)
-    out[(int64_t)(lo + e / n) * nn + (int64_t)r * n + (e % n)] = rows[e];
-}
-
 // qg_jacobian_kernel + qg_max_speed2_kernel over the same grid points:
 // J1 + i J2, and max (u + shear)^2 + v^2 over the nl u+iv planes at `uv`.
 // Grid-stride (kQgMaxPer points per thread), the max reduced by wave
