@@ -63,14 +63,11 @@ def ring_spectrum(nx, kmin, kmax_ring, rng, phase_shift=0.0):
     return qk
 
 
-def build_workload(ctx, args, lo, hi, n_total, partition="index", world=1, rank=0):
+def build_workload(ctx, args, lo, hi, n_total):
     """The replicated field (every rank draws the same spectra from `seed`)
-    and this rank's packets of the n_total-packet ensemble (the same ensemble
-    at any world size: positions drawn for all n_total packets, ring angles
-    2*pi*i/n_total): the block [lo, hi) (partition "index"), or the packets in
-    y-strip `rank` of `world` (partition "spatial", dist.spatial_shard).
-    Returns the rank's arrays plus the whole ensemble (x_all, k_all) and the
-    rank's global indices (idx)."""
+    and this rank's packets [lo, hi) of the n_total-packet ensemble (the same
+    ensemble at any world size: positions drawn for all n_total packets,
+    ring angles 2*pi*i/n_total)."""
     rng = np.random.default_rng(args.seed)
     nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
     K_d2 = f / Cg
@@ -95,10 +92,8 @@ def build_workload(ctx, args, lo, hi, n_total, partition="index", world=1, rank=
     dt = 0.25 * (L / nx) / U0  # qg2layersw_raytrace.m:31,78
     w0 = 4.0
     wf = math.sqrt((w0 ** 2 - 1) * f ** 2 / Cg ** 2)
-    i = np.arange(1, n_total + 1, dtype=np.float64)
-    k_all = np.stack([wf * np.cos(2 * np.pi * i / n_total), wf * np.sin(2 * np.pi * i / n_total)], axis=1)
-    k = k_all[lo:hi]
-    x_all = None
+    i = np.arange(lo + 1, hi + 1, dtype=np.float64)
+    k = np.stack([wf * np.cos(2 * np.pi * i / n_total), wf * np.sin(2 * np.pi * i / n_total)], axis=1)
     if getattr(args, "positions", "uniform") == "stratified":
         # diagnostic: every 16x16-cell tile gets the same number of packets
         N = hi - lo
@@ -110,14 +105,8 @@ def build_workload(ctx, args, lo, hi, n_total, partition="index", world=1, rank=
         c = 0 if args.positions == "band" else 1
         x[:, c] = (x[:, c] + L / 2) / args.band_parts - L / 2
     else:
-        x_all = L * rng.random((n_total, 2)) - L / 2
-        x = x_all[lo:hi]
-    idx = np.arange(lo, hi)
-    if partition == "spatial" and x_all is not None:
-        idx = spatial_shard(x_all, L, nx, world, rank)
-        x, k = x_all[idx], k_all[idx]
+        x = (L * rng.random((n_total, 2)) - L / 2)[lo:hi]
     return dict(nx=nx, L=L, f=f, gH=Cg ** 2, dt=dt, nslots=nslots, x=x, k=k, qk1=qk1, qk2=qk2,
-                x_all=x_all, k_all=k_all, idx=idx,
                 K_d2=K_d2, ks=ks, shear=shear, intervals=getattr(args, "intervals", 1) if nslots == 2 else 1,
                 seed=args.seed)
 
@@ -230,7 +219,7 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     qk = np.stack([w["qk1"], -w["qk1"]], axis=2)  # the driver's (q1, -q1) layers
     model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
     ens = sw.PacketEnsemble(w["x"], w["k"], L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * math.pi / L, nlayers=2,
-                            bump=sw.BUMP_QG, ctx=ctx, tile=w.get("tile", args.tile))
+                            bump=sw.BUMP_QG, ctx=ctx)
     U0 = model.max_speed()
     loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
                            integrator=integrator, speculate=bool(args.speculate))
@@ -307,9 +296,8 @@ def driver_forecast(ctx, w, args, dev, n_total, full):
                    f"{args.substeps} leapfrog substeps); pde_alone_ms: the same loop without packets"}
     rate_full = full["packet_steps_per_s"]
     for G in (2, 4, 8):
-        xs, ks = shard_of(w, n_total, G, args.partition)
-        n = xs.shape[0]
-        ws = dict(w, x=xs, k=ks, tile=tile_for(args, args.partition, G))
+        n = -(-n_total // G)
+        ws = dict(w, x=w["x"][:n], k=w["k"][:n])
         d = driver_step(ctx, ws, args, dev, False, n, nsteps=args.forecast_driver_steps)
         r = {"packets_per_gpu": n, "ms_per_pde_step": d["ms_per_pde_step"],
              "value_1gpu": d["packet_steps_per_s"], "forecast_value": G * d["packet_steps_per_s"],
@@ -429,10 +417,6 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (ranks); without a torch.distributed environment N > 1 launches the ranks as a child "
                          "torch.distributed.run; under one it must equal WORLD_SIZE (default: WORLD_SIZE)")
-    ap.add_argument("--partition", choices=["spatial", "index"], default="spatial",
-                    help="which packets a rank advances: the packets in its y-strip of the domain (spatial, "
-                         "dist.spatial_shard: each GPU's packets as dense as the whole ensemble's) or a contiguous "
-                         "index block (index, dist.shard_range)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="strong: --packets in total, sharded over the ranks (the metric's fixed 1e6); "
                          "weak: --packets per GPU")
@@ -539,12 +523,12 @@ def progress(msg):
 
 def _imports():
     """torch and the library, imported only in a rank (never in the launcher)."""
-    global torch, dist, sw, gather_packets, max_over_ranks, shard_range, spatial_shard
+    global torch, dist, sw, gather_packets, max_over_ranks, shard_range
     import torch  # noqa: F401  (first: libswrt binds to the HIP runtime torch loads)
     import torch.distributed as dist  # noqa: F401
 
     import swraytracing_amd as sw  # noqa: F401
-    from swraytracing_amd.dist import gather_packets, max_over_ranks, shard_range, spatial_shard  # noqa: F401
+    from swraytracing_amd.dist import gather_packets, max_over_ranks, shard_range  # noqa: F401
 
 
 def steps_per_launch_of(args, ivs):
@@ -588,49 +572,24 @@ def timed(ctx, w, args, dev, steps, warmup, barrier=None):
     return t1 - t0, kms, launches, ctx.clock_ghz()
 
 
-def shard_of(w, n_total, G, partition, rank=0):
-    """(x, k) of rank `rank` of a G-GPU run of the bench ensemble."""
-    if partition == "spatial":
-        idx = spatial_shard(w["x_all"], w["L"], w["nx"], G, rank)
-        return w["x_all"][idx], w["k_all"][idx]
-    lo, hi = shard_range(n_total, G, rank)
-    return w["x_all"][lo:hi], w["k_all"][lo:hi]
-
-
-def tile_for(args, partition, G):
-    """Binning tile of a G-GPU shard: 8x8-cell tiles for spatial shards of
-    G >= 4 (their packets fill 1/G of the domain: 16x16 tiles would leave
-    1024/G occupied tiles, too few to fill the CUs), else automatic."""
-    if args.tile:
-        return args.tile
-    return 8 if partition == "spatial" and G >= 4 else 0
-
-
-def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu, sizes=(2, 4, 8), steps=None, partition=None):
+def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu, sizes=(2, 4, 8), steps=None):
     """One GPU timed on the packets rank 0 of a G-GPU strong-scaling run
-    holds for G = 2, 4, 8 — its block of ceil(n_total/G) (partition "index")
-    or its y-strip's packets (partition "spatial", dist.spatial_shard) of the
-    same ensemble: forecast value = G x that rate (the field is replicated and
-    the timed path has no collective), efficiency = rate(shard) / rate_1gpu
-    (the rate of all n_total packets on one GPU; G = 1 in `sizes` times that
-    too)."""
+    holds (the first ceil(n_total/G) of the same ensemble) for G = 2, 4, 8:
+    forecast value = G x that rate (the field is replicated and the timed path
+    has no collective), efficiency = rate(shard) / rate_1gpu (the rate of all
+    n_total packets on one GPU; G = 1 in `sizes` times that too)."""
     out = {}
-    partition = partition or args.partition
+    x, k = w["x"], w["k"]
     steps = steps or args.steps
     for G in sizes:
-        xs, ks = shard_of(w, n_total, G, partition) if G > 1 else (w["x_all"], w["k_all"])
-        n = xs.shape[0]
-        ctx.set_locality(args.rebin_every, tile_for(args, partition, G))
-        ctx.packets_set(xs, ks)
+        n = -(-n_total // G)
+        ctx.packets_set(x[:n], k[:n])
         el, kms, launches, (clk, _) = timed(ctx, w, args, dev, steps, args.warmup)
         rate = n * args.substeps * w["intervals"] * steps / el
-        out[str(G)] = {"packets_per_gpu": n, "value_1gpu": rate, "forecast_value": rate * n_total / n,
-                       "efficiency": (rate * n_total / n) / G / rate_1gpu if rate_1gpu else None,
-                       "ms_per_step": el / steps * 1e3, "partition": partition,
-                       "tile": tile_for(args, partition, G),
+        out[str(G)] = {"packets_per_gpu": n, "value_1gpu": rate, "forecast_value": G * rate,
+                       "efficiency": rate / rate_1gpu if rate_1gpu else None, "ms_per_step": el / steps * 1e3,
                        "avg_launch_ms": (kms / launches) if launches else None, "clock_ghz_observed": clk}
-    ctx.set_locality(args.rebin_every, args.tile)
-    ctx.packets_set(w["x"], w["k"])
+    ctx.packets_set(x, k)
     return out
 
 
@@ -675,9 +634,7 @@ def main(argv=None):
     n_total = args.packets if args.scaling == "strong" else args.packets * world
     lo, hi = shard_range(n_total, world, rank)
     ctx = sw.Context(device)
-    if args.scaling == "weak" or args.positions != "uniform":
-        args.partition = "index"  # (weak: every rank its own 1e6; the diagnostics place positions themselves)
-    ctx.set_locality(args.rebin_every, tile_for(args, args.partition, world))
+    ctx.set_locality(args.rebin_every, args.tile)
     ctx.set_kernel(args.kernel)
     ctx.set_sparse_tiles(args.sparse_tiles)
     ctx.debug_set(sw._lib.DEBUG_QG_JFUSE, args.qg_jfuse)
@@ -685,7 +642,7 @@ def main(argv=None):
     ctx.qg_set_stream(bool(args.qg_stream))
     ctx.set_packet_streams(args.packet_streams)
     ctx.set_gather_mode(args.gather_mode)
-    w = build_workload(ctx, args, lo, hi, n_total, args.partition, world, rank)
+    w = build_workload(ctx, args, lo, hi, n_total)
     ctx.packets_set(w["x"], w["k"])
 
     def barrier():
@@ -701,11 +658,11 @@ def main(argv=None):
     gathered = None
     if distributed and args.gather:
         # device-side gather of the trajectories (the frame writer's input): libswrt -> torch buffer -> all_gather
-        full = gather_packets(ctx, n_total, world, rank, indices=w["idx"])
+        full = gather_packets(ctx, n_total, world, rank)
         gathered = None if full is None else bool(np.isfinite(full[0]).all() and np.isfinite(full[1]).all()
                                                   and full[0].shape[0] == n_total)
 
-    N = w["x"].shape[0]
+    N = hi - lo
     ivs = w["intervals"]
     total_ps = n_total * args.substeps * ivs * args.steps
     value = total_ps / elapsed
@@ -755,8 +712,7 @@ def main(argv=None):
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "sparse_tiles": args.sparse_tiles,
                    "packet_streams": args.packet_streams, "gather_mode": args.gather_mode,
-                   "positions": args.positions, "partition": args.partition,
-                   "tile_used": tile_for(args, args.partition, world),
+                   "positions": args.positions,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,
         "finite": finite,

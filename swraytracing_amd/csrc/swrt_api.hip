@@ -51,14 +51,6 @@ constexpr int kXkaMargin = 3;           // xka_tile_kernel: drift margin (cells)
 constexpr int kTile = SWRT_TILE;                // LDS tile kernel: cells per tile side
 constexpr int kMargin = SWRT_MARGIN;            // LDS tile kernel: drift margin (cells)
 constexpr int kTileThreads = SWRT_TILE_THREADS;
-// 8x8-cell tiles (swrt_set_locality(ctx, r, 8)): for ensembles dense where
-// they are but confined to part of the domain (a spatially partitioned shard,
-// dist.py spatial_shard), 16x16 tiles leave too few occupied tiles to fill the
-// CUs.  A 19x19-node window (row stride 20) of two divergence-free snapshots
-// is 30 KB: four 256-thread workgroups per CU.  Two-snapshot five-sum
-// launches only; others keep 16x16 tiles.
-constexpr int kTileSmall = 8;
-constexpr int kTileSmallThreads = 256;
 // Sparse-tile launches: below SWRT_SPARSE_BELOW packets per 16x16 tile on
 // average (a strong-scaling shard: ~120 at 1.25e5 packets on 512^2) a
 // 512-thread workgroup has one or two busy waves, one per SIMD, each capped
@@ -937,12 +929,10 @@ bool sparse_tiles(const swrt_ctx* c, int64_t ntiles) {
 }
 
 // Threads per workgroup of the LDS-tiled leapfrog launch over `ntiles` tiles
-// of `tile` cells of snapshots that are (v5) two divergence-free slots: ONE
-// decision for the launch (tile_launch) and for the re-binning's
-// longest-first tile order, which ranks tiles by the rounds of this many
-// lanes their workgroup runs.
-int tile_threads(const swrt_ctx* c, bool v5_two, int64_t ntiles, int tile = kTile) {
-  if (tile == kTileSmall) return kTileSmallThreads;
+// of snapshots that are (v5) two divergence-free slots: ONE decision for the
+// launch (tile_launch) and for the re-binning's longest-first tile order,
+// which ranks tiles by the rounds of this many lanes their workgroup runs.
+int tile_threads(const swrt_ctx* c, bool v5_two, int64_t ntiles) {
   return v5_two && sparse_tiles(c, ntiles) ? kSparseThreads : kTileThreads;
 }
 
@@ -954,7 +944,7 @@ bool two_v5(const swrt_ctx* c, int nslots, int sa) {
 }
 
 int tile_cells(const swrt_ctx* c, int64_t nx) {
-  if (use_tile_kernel(c)) return c->tile == kTileSmall ? kTileSmall : kTile;
+  if (use_tile_kernel(c)) return kTile;
   if (c->tile > 0) return (int)std::min<int64_t>(c->tile, nx);
   // default: 8x8-cell tiles, coarser on big grids so bins stay <= 4096
   int t = 8;
@@ -1057,9 +1047,8 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
   t.perm_out = c->perm2;
   t.starts = c->bins + 2 * kMaxBins;
   t.order = tile_order_of(c);
-  const int T = c->bin_tile;
-  if (T != kTile && T != kTileSmall) return fail(c, SWRT_ERR_STATE, "the binning is not the LDS-tiled kernel's");
-  t.ntx = (int)((a.f0.nx + T - 1) / T);
+  if (c->bin_tile != kTile) return fail(c, SWRT_ERR_STATE, "the binning is not the LDS-tiled kernel's");
+  t.ntx = (int)((a.f0.nx + kTile - 1) / kTile);
   const int ntiles = t.ntx * t.ntx;
   t.next_keys = nullptr;
   t.next_counts = nullptr;
@@ -1078,14 +1067,7 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
     t.next_counts = c->bins;
   }
   const bool fma = c->gather_mode == 1;
-  if (T == kTileSmall) {  // leap_rebin_if_due bins by 8x8 tiles only for two divergence-free snapshots
-    if (a.nslots != 2 || !(iv ? iv->div_free : two_v5(c, 2, 0)))
-      return fail(c, SWRT_ERR_STATE, "8x8-cell tiles need two divergence-free snapshots");
-    if (fma)
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTileSmall, kMargin, kTileSmallThreads, true, true>, kTileSmallThreads, t, zero));
-    else
-      HIPCHK_RC(launch_tiles(c, tile_leapfrog_kernel<true, kTileSmall, kMargin, kTileSmallThreads, true>, kTileSmallThreads, t, zero));
-  } else if (a.nslots == 2) {
+  if (a.nslots == 2) {
     if (iv ? iv->div_free : two_v5(c, 2, 0)) {
       if (tile_threads(c, true, ntiles) == kSparseThreads) {
         if (fma)
@@ -1137,17 +1119,14 @@ int tile_launch(swrt_ctx* c, const StepArgs& a, bool count_next, const IvLaunch*
 }
 
 // the re-binning of a leapfrog call over slots sa .. sa+nslots-1, when due
-// (or when the launch shape it was ranked for changed)
 int leap_rebin_if_due(swrt_ctx* c, int nslots, int sa) {
   if (c->rebin_every <= 0) return SWRT_OK;
   const bool tiled = use_tile_kernel(c);
-  const bool v5 = two_v5(c, nslots, sa);
-  const int T = tiled && v5 && c->tile == kTileSmall ? kTileSmall : kTile;
-  const int64_t ntx = (c->slot[sa].nx + T - 1) / T;
-  const int lanes = tiled ? tile_threads(c, v5, ntx * ntx, T) : kTileThreads;
+  const int64_t ntiles = tiled ? ((c->slot[sa].nx + kTile - 1) / kTile) * ((c->slot[sa].nx + kTile - 1) / kTile) : 0;
+  const int lanes = tiled ? tile_threads(c, two_v5(c, nslots, sa), ntiles) : kTileThreads;
   if (!c->bin_valid || c->steps_since_bin >= c->rebin_every ||
-      (tiled && (c->bin_tile != T || c->bin_lanes != lanes)))
-    return rebin(c, tiled, tiled ? T : 0, lanes);
+      (tiled && (c->bin_tile != kTile || c->bin_lanes != lanes)))
+    return rebin(c, tiled, tiled ? kTile : 0, lanes);
   return SWRT_OK;
 }
 

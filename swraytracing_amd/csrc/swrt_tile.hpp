@@ -101,13 +101,6 @@ __device__ __forceinline__ int wg_work(const TileArgs& ta, int& pbeg, int& pend)
   return wg_work_range(ta.starts, ta.order, ta.s.n, ta.sh, pbeg, pend);
 }
 
-// LDS row stride (nodes) of a W-node window row: the smallest WS >= W with
-// WS = 4 or 12 (mod 16) — then WS*i + j (mod 16) is distinct over a 4x4 block
-__host__ __device__ constexpr int conflict_free_stride(int W) {
-  return (W + ((12 - W % 16) + 16) % 16) < (W + ((4 - W % 16) + 16) % 16) ? (W + ((12 - W % 16) + 16) % 16)
-                                                                          : (W + ((4 - W % 16) + 16) % 16);
-}
-
 // a - b on the periodic ring of n cells, mapped to [-n/2, n/2)
 __device__ __forceinline__ int ring_diff(int a, int b, int n) {
   int d = a - b;
@@ -350,11 +343,10 @@ template <bool TWO, int T, int M, int NT, bool V5 = false, bool FMA = false, int
 __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
   static_assert(!FMA || V5, "the FMA gather exists for the five-sum window only");
   constexpr int W = T + 5 + 2 * M;  // window side in nodes
-  // row stride = 4 or 12 (mod 16) nodes, the smallest >= W: any 4x4 block of
-  // window nodes falls on 16 distinct ds_read_b128 bank quads (node n -> quad
-  // (n mod 16)), so lanes of one 16-lane group reading a few neighbouring
-  // nodes never conflict (T = 16: 28; T = 8: 20)
-  constexpr int WS = conflict_free_stride(W);
+  // row stride = 12 (mod 16) nodes: any 4x4 block of window nodes falls on
+  // 16 distinct ds_read_b128 bank quads (node n -> quad (n mod 16)), so lanes
+  // of one 16-lane group reading a few neighbouring nodes never conflict
+  constexpr int WS = W + ((12 - W % 16) + 16) % 16;
   constexpr int WNP = W * WS;       // nodes per chunk
   constexpr int NCH = TWO ? (V5 ? 5 : 6) : 3;  // 16-B chunks per node
   constexpr int NB = T * T + 1;     // in-tile cell bins + "elsewhere"
@@ -372,9 +364,6 @@ __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
   const int tid = threadIdx.x;
   int pbeg, pend;
   const int tile = wg_work(ta, pbeg, pend);
-  // an empty tile (spatially partitioned ensembles leave most of them empty)
-  // stages nothing: it has no packets and adds nothing to the next counts
-  if (pbeg == pend) return;  // uniform across the workgroup
   const int tx = tile / ta.ntx, ty = tile % ta.ntx;
   const int nx = a.f0.nx, npad = a.f0.npad;
   const int ox = tx * T, oy = ty * T;  // tile origin (cells)

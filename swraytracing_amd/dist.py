@@ -23,24 +23,6 @@ def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     return lo, hi
 
 
-def spatial_shard(x, L: float, nx: int, world: int, rank: int) -> np.ndarray:
-    """Global indices (ascending) of the packets rank `rank` advances under
-    spatial partitioning: those whose position lies in y-strip `rank` of
-    `world` equal strips of the periodic domain, strip = floor(cy*world/nx)
-    with cell row cy = floor(mod(y, L)/dx) — so a GPU's packets are as dense
-    within its strip as the whole ensemble is in the domain, and its occupied
-    tiles lie in every x-row of the tile grid (every XCD band of the tile
-    order).  Packets are independent (ode_symplectic.m:18-21), so which rank
-    advances which packet changes no result; packets that later drift out of
-    their strip stay with their rank (correct, only less dense).  SURVEY §8e:
-    "spatial tiles for locality"."""
-    if world <= 0 or not 0 <= rank < world:
-        raise ValueError("bad world/rank")
-    y = np.asarray(x, dtype=np.float64)[:, 1]
-    cy = np.minimum(np.floor(np.mod(y, L) / (L / nx)).astype(np.int64), nx - 1)
-    return np.nonzero((cy * world) // nx == rank)[0]
-
-
 def _device_for(backend: str):
     import torch
     if backend == "nccl":
@@ -74,45 +56,34 @@ def gather_to_root(local: np.ndarray, n_total: int, world: int, rank: int, backe
     return np.concatenate(parts, axis=0).reshape((n_total,) + tail)
 
 
-def gather_packets(ctx, n_total: int, world: int, rank: int, group=None, indices=None):
+def gather_packets(ctx, n_total: int, world: int, rank: int, group=None):
     """Gather every rank's device-resident packets into the full (n_total, 2)
-    x and k on rank 0, in global packet order, without a host round trip on
-    the sending side: libswrt writes the shard's state in original order
-    straight into a torch device buffer (swrt_packets_get_device, on the
-    library's packet stream), and one all_gather of the (5, maxn) blocks — x,
-    y, k, l and each packet's global index — runs with that stream as torch's
-    current stream, so the collective (RCCL on "nccl"; gloo stages through the
-    host) is ordered after the write with no synchronisation.  `indices`: the
-    global indices this rank holds (spatial_shard); None = its shard_range
-    block.  Returns (x, k) numpy arrays on rank 0, None elsewhere."""
+    x and k on rank 0, in global packet order (shard_range layout), without a
+    host round trip on the sending side: libswrt writes the shard's state in
+    original order straight into a torch device buffer (swrt_packets_get_device,
+    on the library's packet stream), and one all_gather of the (4, ceil(n/world))
+    blocks runs with that stream as torch's current stream, so the collective
+    (RCCL on "nccl"; gloo stages through the host) is ordered after the write
+    with no synchronisation.  Returns (x, k) numpy arrays on rank 0, None
+    elsewhere."""
     import torch
     import torch.distributed as dist
     dev = torch.device("cuda", torch.cuda.current_device())
-    if indices is None:
-        lo, hi = shard_range(n_total, world, rank)
-        indices = np.arange(lo, hi)
-    indices = np.asarray(indices, dtype=np.int64)
-    if ctx.packets_count() != indices.shape[0]:
-        raise ValueError(f"rank {rank} holds {ctx.packets_count()} packets, its shard is {indices.shape[0]}")
-    cnt = torch.tensor([float(indices.shape[0])], dtype=torch.float64, device=dev)
-    dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=group)
-    maxn = max(1, int(cnt.item()))
+    maxn = max(1, -(-n_total // world))
+    lo, hi = shard_range(n_total, world, rank)
+    if ctx.packets_count() != hi - lo:
+        raise ValueError(f"rank {rank} holds {ctx.packets_count()} packets, its shard is {hi - lo}")
     stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
     with torch.cuda.stream(stream):
-        buf = torch.zeros((5, maxn), dtype=torch.float64, device=dev)  # rows x, y, k, l, global index
-        buf[4].fill_(-1.0)
-        buf[4, : indices.shape[0]] = torch.from_numpy(indices.astype(np.float64)).to(dev)
+        buf = torch.zeros((4, maxn), dtype=torch.float64, device=dev)  # rows x, y, k, l
         ctx.packets_get_device(buf.data_ptr(), buf.data_ptr() + 2 * maxn * 8, maxn)
         out = [torch.empty_like(buf) for _ in range(world)]
         dist.all_gather(out, buf, group=group)
         if rank != 0:
             torch.cuda.current_stream().synchronize()
             return None
-        allb = torch.cat(out, dim=1).cpu().numpy()
-    idx = allb[4]
-    keep = idx >= 0
-    full = np.empty((4, n_total))
-    full[:, idx[keep].astype(np.int64)] = allb[0:4, keep]
+        full = torch.cat([out[r][:, : shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0]]
+                          for r in range(world)], dim=1).cpu().numpy()
     return np.ascontiguousarray(full[0:2].T), np.ascontiguousarray(full[2:4].T)
 
 

@@ -175,15 +175,11 @@ class PacketEnsemble:
     """
 
     def __init__(self, x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, device=0,
-                 bump=BUMP_QG, ctx: Context | None = None, shard=None, partition="index", tile=None):
+                 bump=BUMP_QG, ctx: Context | None = None, shard=None):
         """``shard`` = (rank, world): x, k are the whole ensemble (the same on
-        every rank) and this rank advances its share — a
-        contiguous index block (partition "index") or the packets in its
-        y-strip of the domain (partition "spatial", dist.spatial_shard); frames
-        are gathered to rank 0 on the device in global packet order
-        (dist.gather_packets) and ode23's error norm is max-reduced over the
-        ranks.  ``tile``: the binning tile of the LDS-tiled launches (None:
-        8x8-cell tiles for spatial shards of >= 4 ranks, else automatic)."""
+        every rank) and this rank advances its contiguous shard (SURVEY §8e);
+        frames are gathered to rank 0 on the device (dist.gather_packets) and
+        ode23's error norm is max-reduced over the ranks."""
         self.ctx = ctx if ctx is not None else Context(device)
         self.L, self.f, self.Cg, self.nx = float(L), float(f), float(Cg), int(nx)
         self.gH = self.Cg ** 2
@@ -194,16 +190,10 @@ class PacketEnsemble:
         k = np.asarray(k, dtype=np.float64)
         self.n_total = x.shape[0]
         self.rank, self.world = shard if shard is not None else (0, 1)
-        self.indices = None  # global indices of this rank's packets (None: all, or its shard_range block)
         if self.world > 1:
-            from .dist import shard_range, spatial_shard
-            if partition == "spatial":
-                self.indices = spatial_shard(x, self.L, self.nx, self.world, self.rank)
-                x, k = x[self.indices], k[self.indices]
-            else:
-                lo, hi = shard_range(self.n_total, self.world, self.rank)
-                x, k = x[lo:hi], k[lo:hi]
-        self.tile = tile if tile is not None else (8 if partition == "spatial" and self.world >= 4 else 0)
+            from .dist import shard_range
+            lo, hi = shard_range(self.n_total, self.world, self.rank)
+            x, k = x[lo:hi], k[lo:hi]
         self.ctx.packets_set(x, k)
         self.n = x.shape[0]
         self._rebin = None
@@ -226,7 +216,7 @@ class PacketEnsemble:
         # substep per interval, every 20 at five (tuned on the bench workload)
         if self._rebin != 4 * nsub:
             self._rebin = 4 * nsub
-            self.ctx.set_locality(self._rebin, self.tile)
+            self.ctx.set_locality(self._rebin, 0)
         h = dt / nsub
         self.ctx.advance(h, nsub, self.f, self.gH, nslots=2, alpha0=0.5 / nsub, dalpha=1.0 / nsub,
                          bump=self.bump, save_every=save_every)
@@ -237,7 +227,7 @@ class PacketEnsemble:
         bits as one advance() per interval with the pair moved to slots 0, 1."""
         if self._rebin != 4 * nsub:
             self._rebin = 4 * nsub
-            self.ctx.set_locality(self._rebin, self.tile)
+            self.ctx.set_locality(self._rebin, 0)
         self.ctx.advance_intervals([dt / nsub for dt in dts], nsub, self.f, self.gH, alpha0=0.5 / nsub,
                                    dalpha=1.0 / nsub, bump=self.bump, save_every=save_every)
 
@@ -262,7 +252,7 @@ class PacketEnsemble:
         (every rank calls it); rank 0 writes the whole ensemble."""
         if self.world > 1:
             from .dist import gather_packets
-            full = gather_packets(self.ctx, self.n_total, self.world, self.rank, indices=self.indices)
+            full = gather_packets(self.ctx, self.n_total, self.world, self.rank)
             if full is None:
                 return
             x, k = full

@@ -295,8 +295,7 @@ class TwoLayerLoop:
 
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
                   out_dir="data", nsub=4, max_steps=None, seed=146, verbose=False, r_drag=0.1,
-                  packet_intervals=1, integrator="leapfrog", fresh=True, partition="index",
-                  ctx: Context | None = None):
+                  packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None):
     """qgsw_raytrace.m:1-180 with the PDE and the packets on the GPU.
 
     Writes ``out_dir``/packet_x.bin, packet_k.bin, packet_time.bin, pv.bin,
@@ -311,10 +310,8 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     "leapfrog" (``nsub`` fused symplectic substeps per PDE interval) or
     "ode23" (the reference's own ode23 over each interval, qgsw_raytrace.m:149).
     ``fresh``: remove earlier output files first (default) or append to
-    them as write_field.m:31 does.  ``partition``: under torch.distributed,
-    which packets a rank advances ("index" blocks or "spatial" y-strips,
-    PacketEnsemble); the files are the same either way.  Returns a dict of
-    run facts (dt, Nsteps, steps run, frames written, final t)."""
+    them as write_field.m:31 does.  Returns a dict of run facts (dt, Nsteps,
+    steps run, frames written, final t)."""
     ctx = ctx if ctx is not None else Context(0)
     rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
     if rank == 0:
@@ -342,7 +339,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     log(parameter_block(nx, Npackets, near_inertial_factor * f, dt, T, packet_delay, steps_per_save,
                         packet_steps_per_save, f, Cg, U_g, U0, Fr, K_d2))
     ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, bump=BUMP_QG, ctx=ctx,
-                         shard=(rank, world), partition=partition) \
+                         shard=(rank, world)) \
         if Npackets > 0 else None
     t = 0.0
     frames = 1
@@ -385,13 +382,12 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
 
 def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
                         out_dir="data", nsub=5, max_steps=None, seed=5, verbose=False,
-                        packet_intervals=1, integrator="leapfrog", fresh=True, partition="index",
-                        ctx: Context | None = None):
+                        packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None):
     """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
     (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and
     interpolate's 2*nx y-period).  Same packet outputs as :func:`qgsw_raytrace`;
     pv.bin holds the initial nx x nx x 2 frame only, as in the reference.
-    ``packet_intervals``, ``integrator``, ``fresh``, ``partition``: as in :func:`qgsw_raytrace`."""
+    ``packet_intervals``, ``integrator``, ``fresh``: as in :func:`qgsw_raytrace`."""
     ctx = ctx if ctx is not None else Context(0)
     rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
     if rank == 0:
@@ -423,7 +419,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     log(parameter_block(nx, Npackets, near_inertial_factor * f, dt, T, packet_delay_steps, steps_per_save,
                         packet_steps_per_save, f, Cg, U_g, U0, Fr, K_d2, two_layer=True))
     ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=shear, k_scale=2 * math.pi / L, nlayers=2,
-                         bump=BUMP_QG, ctx=ctx, shard=(rank, world), partition=partition) if Npackets > 0 else None
+                         bump=BUMP_QG, ctx=ctx, shard=(rank, world)) if Npackets > 0 else None
     t = 0.0
     frames = 1
     if ens is not None:

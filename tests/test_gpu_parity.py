@@ -1070,43 +1070,3 @@ def test_tile_path_non_finite_and_far_packets(fresh_ctx, oracle_lib, sparse):
                                            w["dt"] / 5, 5, w["f"], w["gH"])
     np.testing.assert_array_equal(xg[idx], xo)
     np.testing.assert_array_equal(kg[idx], ko)
-
-
-@pytest.mark.parametrize("G,tile", [(8, 8), (4, 8), (2, 0)])
-def test_spatial_shard_bitexact(fresh_ctx, oracle_lib, G, tile):
-    """Rank 0's share of a G-GPU spatially partitioned run of the bench
-    ensemble (dist.spatial_shard: the packets in y-strip 0 of G — as dense as
-    the whole 1e6 ensemble, confined to 1/G of the domain) on the bench's
-    512^2 fields, binned by 8x8-cell tiles (most 16x16... and 8x8 tiles are
-    empty: empty workgroups exit at once) or 16x16: a random subset
-    bit-identical to the C oracle, and every packet identical to the same
-    shard advanced with 16x16 tiles (interpolate.m:43-49, ode_symplectic.m:
-    23-28 — the tile schedule changes no bit)."""
-    import argparse
-    import bench
-    from swraytracing_amd.dist import spatial_shard
-    ctx = fresh_ctx
-    bench._imports()
-    args = argparse.Namespace(nx=512, packets=1_000_000, world=1, rank=0, seed=146, mode="blend")
-    w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
-    idx = spatial_shard(w["x_all"], w["L"], 512, G, 0)
-    assert abs(idx.shape[0] - 1_000_000 / G) < 5 * (1_000_000 / G) ** 0.5
-    xs, ks = w["x_all"][idx], w["k_all"][idx]
-    out = {}
-    for t in (tile, 16):
-        ctx.set_locality(20, t)
-        ctx.packets_set(xs, ks)
-        for _ in range(6):
-            bench.step(ctx, w, 5)
-        out[t] = ctx.packets_get()
-    ctx.set_locality(4, 0)
-    for a, b in zip(out[tile], out[16]):
-        assert np.array_equal(a.view(np.uint64), b.view(np.uint64))
-    p0, p1 = ctx.get_field_grid(0), ctx.get_field_grid(1)
-    sub = np.sort(np.random.default_rng(8).choice(idx.shape[0], 1500, replace=False))
-    xo, ko = xs[sub], ks[sub]
-    for _ in range(6):
-        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.2, 512, 1024, w["L"] / 512, orc.BUMP_QG, xo, ko,
-                                           w["dt"] / 5, 5, w["f"], w["gH"])
-    np.testing.assert_array_equal(out[tile][0][sub], xo)
-    np.testing.assert_array_equal(out[tile][1][sub], ko)
