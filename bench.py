@@ -256,6 +256,10 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
         out["packet_steps_per_s"] = n_total * args.substeps / (ms / 1e3)
     else:
         out["packet_intervals_per_s"] = n_total / (ms / 1e3)
+        # the controller's own counts over warm-up and timed intervals (attempts include rejected ones)
+        st = loop.group.ode23_stats
+        if st["intervals"]:
+            out["ode23_per_interval"] = {k: st[k] / st["intervals"] for k in ("steps", "failed", "attempts")}
     return out
 
 

@@ -338,6 +338,16 @@ int swrt_ode23_accept(swrt_ctx* ctx);
 int swrt_ode23_run(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                    double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
                    int64_t* stats3_out);
+/* swrt_ode23_run with a host hook: hook(hook_user) is called once, after
+ * stage 1 and the first attempt are queued and before the host first waits
+ * on the device — host work placed there (the drivers queue the next QG step,
+ * qg2layersw_raytrace.m:166-181, through swrt_qg_step_speculative) overlaps
+ * the interval's first launches instead of the gap between intervals.  The
+ * hook may call the library's QG entry points; it must not touch the packets
+ * or the field slots this call reads.  hook NULL: swrt_ode23_run. */
+int swrt_ode23_run_hooked(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
+                          double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
+                          int64_t* stats3_out, void (*hook)(void*), void* hook_user);
 
 /* ---------------------------------------------------------------------------
  * QG PDE stepper: the snapshots' producer, device-resident

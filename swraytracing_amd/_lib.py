@@ -33,6 +33,7 @@ _I = ctypes.c_int64
 _INT = ctypes.c_int
 _P = ctypes.POINTER(ctypes.c_double)
 _VP = ctypes.c_void_p
+_HOOK = ctypes.CFUNCTYPE(None, ctypes.c_void_p)  # void (*)(void*)
 
 class QGParams(ctypes.Structure):
     """swrt_qg_params (include/swrt.h)."""
@@ -87,6 +88,8 @@ SIGNATURES = {
     "swrt_ode23_accept": (_INT, [_VP]),
     "swrt_ode23_run": (_INT, [_VP, _D, _D, _D, _D, _D, _INT, _D, _D, _D, _P, _I, ctypes.POINTER(_I),
                               ctypes.POINTER(_I)]),
+    "swrt_ode23_run_hooked": (_INT, [_VP, _D, _D, _D, _D, _D, _INT, _D, _D, _D, _P, _I, ctypes.POINTER(_I),
+                                     ctypes.POINTER(_I), _HOOK, _VP]),
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_step_speculative": (_INT, [_VP, _D]),
@@ -194,6 +197,7 @@ class Context:
             raise SwrtError(f"swrt_create(device={device}) failed: {ERRORS.get(rc, rc)}")
         self._h = h
         self.device = device
+        self._ode23_cb = self._ode23_hook = self._ode23_raised = None  # ode23_run's hook callback
 
     def close(self):
         if getattr(self, "_h", None):
@@ -488,18 +492,38 @@ class Context:
     def ode23_accept(self):
         self._chk(self._L.swrt_ode23_accept(self._h), "swrt_ode23_accept")
 
-    def ode23_run(self, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_cap=100_000):
+    def ode23_run(self, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_cap=10_000, hook=None):
         """swrt_ode23_run: the whole ode23 call with the controller in the
         library.  Returns (accepted times, {steps, failed, attempts,
         accepted}); `accepted` counts every accepted time, and a warning is
         raised when more than ts_cap were accepted (the list then holds the
-        first ts_cap only)."""
+        first ts_cap only).  ``hook``: a callable run once after the first
+        launches are queued (swrt_ode23_run_hooked; QG calls only, never the
+        packets); an exception it raises is re-raised after the call."""
         ts = np.empty(ts_cap)
         nts = _I()
         st = (_I * 3)()
-        self._chk(self._L.swrt_ode23_run(self._h, float(t0), float(tfinal), float(tmax), float(f), float(Cg),
-                                         int(nslots), float(rtol), float(atol), float(bump), _p(ts), int(ts_cap),
-                                         ctypes.byref(nts), st), "swrt_ode23_run")
+        args = (self._h, float(t0), float(tfinal), float(tmax), float(f), float(Cg), int(nslots), float(rtol),
+                float(atol), float(bump), _p(ts), int(ts_cap), ctypes.byref(nts), st)
+        if hook is None:
+            self._chk(self._L.swrt_ode23_run(*args), "swrt_ode23_run")
+        else:
+            # one ctypes callback per context (made once), calling this call's hook
+            if self._ode23_cb is None:
+                def _call(_user):
+                    h, self._ode23_hook = self._ode23_hook, None
+                    try:
+                        h()
+                    except BaseException as e:  # ctypes would print and drop it
+                        self._ode23_raised = e
+                self._ode23_cb = _HOOK(_call)
+            self._ode23_hook, self._ode23_raised = hook, None
+            rc = self._L.swrt_ode23_run_hooked(*args, self._ode23_cb, None)
+            self._ode23_hook = None
+            raised, self._ode23_raised = self._ode23_raised, None
+            if raised is not None:
+                raise raised
+            self._chk(rc, "swrt_ode23_run_hooked")
         # ts_cap bounds the recorded times only (the interval always completes)
         if nts.value > ts_cap:
             import warnings

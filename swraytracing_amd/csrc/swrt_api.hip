@@ -275,6 +275,7 @@ struct swrt_ctx {
   int64_t o_order_cap = 0;
   bool o_order_valid = false;  // computed for the current binning
   bool o_sorted = false;       // the packets themselves are in the in-tile cell order of the current binning
+  int o_since_bin = 0;         // ode23 calls since the last one that re-binned
                                // (swrt_ode23_f1's tile_cell_sort_kernel): the stages take them in slot order
   double* o_ynx = nullptr;
   double* o_ynk = nullptr;
@@ -290,6 +291,18 @@ struct swrt_ctx {
   int o_dmax_cur = 0;
   unsigned long long* o_hmax = nullptr;
   hipEvent_t o_ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t o_evb[3] = {nullptr, nullptr, nullptr};  // ... of part 1 (split attempts, on sx[0])
+  // swrt_ode23_run's attempts store every workgroup's max here (host-mapped,
+  // [part][slot][workgroup], kMaxBins per slot): read after the launch's
+  // event, no copy queued between consecutive attempts
+  unsigned long long* o_hpart = nullptr;
+  unsigned long long* o_hpart_d = nullptr;
+  // swrt_ode23_run's first attempt: its coefficients from the device's own
+  // step-size computation (ode23_first_step_kernel), and the host-mapped copy
+  // {raw, absh, h, tnew, coefficients} the host checks its computation against
+  double* o_coef = nullptr;
+  double* o_shown = nullptr;
+  double* o_shown_d = nullptr;
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -707,6 +720,12 @@ void launch_k(swrt_ctx* c, F kernel, dim3 grid, dim3 block, Args... args) {
 // 3e4 packets 3.0 vs 3.4e9, 1e4 at 256^2 1.8 vs 2.8e9; 6.25e4 even; 1.25e5
 // +3 %, 2.5e5 +6 %, 5e5 +4 %, 1e6 +3.7 %).
 constexpr int64_t kMultiStreamFrom = 65536;
+
+// ode23 calls per spatial re-binning (ode23_f1_queue)
+#ifndef SWRT_ODE23_REBIN
+#define SWRT_ODE23_REBIN 2  // every 1 / 2 / 4 calls: 1.843-1.845 / 1.824-1.830 / 1.878-1.892 ms per driver interval (profiles/r05_ode23)
+#endif
+constexpr int kOde23RebinEvery = SWRT_ODE23_REBIN;
 
 // The LDS-tiled launch of TileArgs t: one launch over every tile, or (two
 // packet streams) two part launches, each a share of every XCD band's tiles
@@ -1366,7 +1385,12 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->qg.hmax) (void)hipHostFree(c->qg.hmax);
   if (c->o_hmax) (void)hipHostFree(c->o_hmax);
+  if (c->o_hpart) (void)hipHostFree(c->o_hpart);
+  if (c->o_shown) (void)hipHostFree(c->o_shown);
+  if (c->o_coef) (void)hipFree(c->o_coef);
   for (hipEvent_t e : c->o_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->o_evb)
     if (e) (void)hipEventDestroy(e);
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
   if (c->qg.ev_b) (void)hipEventDestroy(c->qg.ev_b);
@@ -3284,13 +3308,24 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
     HIPCHK(c, hipMalloc(&c->o_spF, sizeof(double) * 4 * c->cap));
     c->o_cap = c->cap;
   }
-  if (!c->o_dmax) {
-    HIPCHK(c, hipMalloc(&c->o_dmax, 3 * sizeof(unsigned long long)));
-    HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, 3 * sizeof(unsigned long long), c->stream));
+  if (!c->o_dmax) {  // 3 max slots per part (part 1: split attempts)
+    HIPCHK(c, hipMalloc(&c->o_dmax, 6 * sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(c->o_dmax, 0, 6 * sizeof(unsigned long long), c->stream));
     c->o_dmax_cur = 0;
   }
   if (!c->o_hmax) HIPCHK(c, hipHostMalloc(&c->o_hmax, 3 * sizeof(unsigned long long)));
+  if (!c->o_hpart) {
+    HIPCHK(c, hipHostMalloc((void**)&c->o_hpart, 6 * kMaxBins * sizeof(unsigned long long), hipHostMallocMapped));
+    HIPCHK(c, hipHostGetDevicePointer((void**)&c->o_hpart_d, c->o_hpart, 0));
+  }
+  if (!c->o_shown) {
+    HIPCHK(c, hipMalloc((void**)&c->o_coef, 8 * sizeof(double)));
+    HIPCHK(c, hipHostMalloc((void**)&c->o_shown, 12 * sizeof(double), hipHostMallocMapped));
+    HIPCHK(c, hipHostGetDevicePointer((void**)&c->o_shown_d, c->o_shown, 0));
+  }
   for (hipEvent_t& e : c->o_ev)
+    if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  for (hipEvent_t& e : c->o_evb)
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   a.f0 = view_of(c->slot[0]);
   a.f1 = nslots == 2 ? view_of(c->slot[1]) : a.f0;
@@ -3315,21 +3350,24 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   a.gate_scale = 0.0;
   a.gate_limit = 0.0;
   a.order = nullptr;
+  a.hpart = nullptr;
+  a.sh = TileShare{};
+  a.coef = nullptr;
   return SWRT_OK;
 }
 
-// ode23: f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2);
-// h4 = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew
+// an attempt's stage times and coefficients (swrt_ode23.hpp o23_coeffs)
 void attempt_coeffs(Ode23Args& a, double t, double h, double tnew) {
-  a.ts = t + h * 0.5;
-  a.c[0] = h * 0.5;
-  a.ts3 = t + h * 0.75;
-  a.c3 = h * 0.75;
-  const double h4 = tnew - t;
-  a.ts4 = tnew;
-  a.c4[0] = h4 * (2.0 / 9.0);
-  a.c4[1] = h4 * (1.0 / 3.0);
-  a.c4[2] = h4 * (4.0 / 9.0);
+  double cf[8];
+  o23_coeffs(t, h, tnew, cf);
+  a.ts = cf[0];
+  a.c[0] = cf[1];
+  a.ts3 = cf[2];
+  a.c3 = cf[3];
+  a.ts4 = cf[4];
+  a.c4[0] = cf[5];
+  a.c4[1] = cf[6];
+  a.c4[2] = cf[7];
 }
 
 // the max of the launch just queued (slot o_dmax_cur), then the next slot
@@ -3351,19 +3389,47 @@ namespace {
 // one ode23 stage over all packets: the LDS-tiled kernel when the packets are
 // binned by the tile kernel's 16x16-cell tiles, else one lane per packet
 template <int STAGE, bool TWO, bool V5>
-void ode23_tile_launch(swrt_ctx* c, const Ode23Args& a, unsigned grid, const int* starts, int ntx) {
+void ode23_tile_launch(swrt_ctx* c, const Ode23Args& a, unsigned grid, const int* starts, int ntx, hipStream_t st) {
+  if constexpr (STAGE == 0) {
+    if (a.coef) {  // coefficients from device memory (swrt_ode23_run's first attempt)
+      hipLaunchKernelGGL((tile_ode23_kernel<0, TWO, kTile, kMargin, kTileThreads, V5, true>), dim3(grid),
+                         dim3(kTileThreads), 0, st, a, starts, ntx);
+      return;
+    }
+  }
   hipLaunchKernelGGL((tile_ode23_kernel<STAGE, TWO, kTile, kMargin, kTileThreads, V5>), dim3(grid),
-                     dim3(kTileThreads), 0, c->stream, a, starts, ntx);
+                     dim3(kTileThreads), 0, st, a, starts, ntx);
 }
 
-template <int STAGE>
-int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
+// swrt_ode23_run may split each attempt into two part launches (the even and
+// the odd band positions of every XCD band, swrt_share.hpp), part 1 on the
+// extra packet stream: consecutive attempts then overlap one part's tail with
+// the other's next launch.  Parts touch disjoint packets of one binning, so
+// stream order alone orders each part's attempts; the packets must already be
+// in the tiles' cell order (no order kernel between the parts).
+bool ode23_split_ok(swrt_ctx* c) {
   const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  return use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx * ntx && c->o_sorted &&
+         (ntx * ntx) % 16 == 0 && c->n >= kMultiStreamFrom && c->packet_streams == 2 && c->stream == c->stream0 &&
+         c->sx[0] != nullptr;
+}
+
+// part -1: one launch over every tile on the packet stream; 0 / 1: that part
+// of a split attempt (part 1 on sx[0]).  *wg_out: the workgroups of the tile
+// launch (each stores its max to a.hpart), 0 for the per-packet kernels.
+template <int STAGE>
+int ode23_launch(swrt_ctx* c, const Ode23Args& a0, int part = -1, unsigned* wg_out = nullptr) {
+  if (wg_out) *wg_out = 0;
+  const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  if (part >= 0 && !ode23_split_ok(c)) return fail(c, SWRT_ERR_STATE, "ode23 split attempt without a split binning");
   if (use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx * ntx) {
     const int* starts = c->bins + 2 * kMaxBins;
     const unsigned ntiles = (unsigned)(ntx * ntx);
     Ode23Args a = a0;
-    const unsigned grid = ntiles;
+    a.sh = TileShare{(int)ntiles, part, part < 0 ? 1 : 2, kShareEven};
+    const unsigned grid = (unsigned)share_grid(a.sh);
+    const hipStream_t st = part == 1 ? c->sx[0] : c->stream;
+    if (wg_out) *wg_out = grid;
     // in-tile cell order of this binning, once (swrt_ode23.hpp): the packets'
     // own order after swrt_ode23_f1's sort, else an order array
     if (c->o_sorted) {
@@ -3386,11 +3452,11 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
     }
     const bool v5 = c->slot[0].div_free && (a.nslots == 1 || c->slot[1].div_free);
     if (a.nslots == 2) {
-      if (v5) ode23_tile_launch<STAGE, true, true>(c, a, grid, starts, ntx);
-      else ode23_tile_launch<STAGE, true, false>(c, a, grid, starts, ntx);
+      if (v5) ode23_tile_launch<STAGE, true, true>(c, a, grid, starts, ntx, st);
+      else ode23_tile_launch<STAGE, true, false>(c, a, grid, starts, ntx, st);
     } else {
-      if (v5) ode23_tile_launch<STAGE, false, true>(c, a, grid, starts, ntx);
-      else ode23_tile_launch<STAGE, false, false>(c, a, grid, starts, ntx);
+      if (v5) ode23_tile_launch<STAGE, false, true>(c, a, grid, starts, ntx, st);
+      else ode23_tile_launch<STAGE, false, false>(c, a, grid, starts, ntx, st);
     }
   } else if constexpr (STAGE == 0) {  // one lane per packet: the three stage launches
     const dim3 grid(nblocks(c->n, 256)), block(256);
@@ -3411,16 +3477,22 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0) {
 }  // namespace
 extern "C" {
 
-int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int nslots, double thr, double bump,
-                  double* rh_raw_out) {
-  if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
-  SlotUse slot_use(c);
+namespace {
+// swrt_ode23_f1 without the read: re-binning, in-tile sort and the stage-1
+// launch queued (its max in slot o_dmax_cur, not yet advanced)
+int ode23_f1_queue(swrt_ctx* c, double t, double tmax, double f, double Cg, int nslots, double thr, double bump) {
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
-  // one spatial re-binning per ode23 call (the packet order is free: the
-  // error norm is a max over all components)
-  if (c->rebin_every > 0 && c->slot[0].set) {
+  // a spatial re-binning per kOde23RebinEvery ode23 calls (the packet order
+  // is free: the error norm is a max over all components; a packet that has
+  // left its tile's window since takes the global gather, so a skipped
+  // re-binning changes speed only)
+  const int ntx0 = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  const bool binned = use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx0 * ntx0 &&
+                      c->bin_tile == kTile && c->o_sorted;
+  const bool due = !binned || ++c->o_since_bin >= kOde23RebinEvery;
+  if (c->rebin_every > 0 && c->slot[0].set && due) {
+    c->o_since_bin = 0;
     if ((rc = rebin(c, false, use_tile_kernel(c) ? kTile : 0))) return rc;  // the ode23 tile kernel's 16x16 tiles
     const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
     if (use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx * ntx) {
@@ -3440,7 +3512,17 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
   Ode23Args a;
   if ((rc = ode23_prepare(c, nslots, a, tmax, f, Cg, thr, bump))) return rc;
   a.ts = t;
-  if ((rc = ode23_launch<1>(c, a))) return rc;
+  return ode23_launch<1>(c, a);
+}
+}  // namespace
+
+int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int nslots, double thr, double bump,
+                  double* rh_raw_out) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  SlotUse slot_use(c);
+  int rc;
+  if ((rc = ode23_f1_queue(c, t, tmax, f, Cg, nslots, thr, bump))) return rc;
   return read_max(c, rh_raw_out);
   GUARD_END(c)
 }
@@ -3491,6 +3573,13 @@ double np_spacing(double t) {  // numpy.spacing
 int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                    double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
                    int64_t* stats3_out) {
+  return swrt_ode23_run_hooked(c, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_out, ts_cap, nts_out,
+                               stats3_out, nullptr, nullptr);
+}
+
+int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
+                          double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
+                          int64_t* stats3_out, void (*hook)(void*), void* hook_user) {
   if (!c) return SWRT_ERR_ARG;
   if (!ts_out || ts_cap < 1 || !nts_out) return fail(c, SWRT_ERR_ARG, "ts_out / ts_cap / nts_out");
   GUARD_BEGIN
@@ -3501,12 +3590,39 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
   const double thr = atol / rtol;
   const double htspan = std::fabs(tfinal - t0);
   const double hmax = 0.1 * htspan;
+  const double c0 = 0.8 * std::pow(rtol, pw);
   double t = t0;
   double raw = 0.0;
   int rc;
-  if ((rc = swrt_ode23_f1(c, t, tmax, f, Cg, nslots, thr, bump, &raw))) return rc;
+  // stage 1 (with this call's re-binning and in-tile sort), its max in slot sl_f1
+  if ((rc = ode23_f1_queue(c, t, tmax, f, Cg, nslots, thr, bump))) return rc;
+  const int sl_f1 = c->o_dmax_cur;
+  c->o_dmax_cur = (sl_f1 + 1) % 3;
   Ode23Args base;
   if ((rc = ode23_prepare(c, nslots, base, tmax, f, Cg, thr, bump))) return rc;
+  // The first attempt's step size on the device (ode23_first_step_kernel,
+  // the host's own operations), so the attempt is queued behind stage 1
+  // without a host round trip; the host then computes the same and checks
+  // it against the kernel's mapped copy (the tile path only: its attempt
+  // kernel reads device coefficients).
+  const int ntx_ = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  const bool dev_first = use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx_ * ntx_;
+  // Two part launches per attempt when the binning allows (ode23_split_ok):
+  // part p keeps max slots o_dmax[3p + sl] and its own events; the error max
+  // is the max over both parts' workgroups.  (Split implies dev_first.)
+  const bool split = ode23_split_ok(c);
+  const int P = split ? 2 : 1;
+  if (dev_first) {
+    // (part 1's slots start at zero, cleared here; each launch then clears its next one)
+    hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax, htspan,
+                       16 * np_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3,
+                       split ? 3 : 0);
+    HIPCHK(c, hipGetLastError());
+  } else {
+    HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl_f1, c->o_dmax + sl_f1, sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
+  }
+  HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
   // three state sets (x, k, F1/F4): an attempt reads set `from` and writes
   // ynew and F4 into set `to`; the accepted one becomes the current set
   struct Set {
@@ -3521,9 +3637,25 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
     c->keys_fresh = false;
     c->cells_sorted = false;
   };
-  auto queue = [&](int from, int to, double ta, double ha, double tnewa, const unsigned long long* gate,
-                   double gscale, double glimit, int* slot) -> int {
+  if (split) {
+    HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->fork_ev, 0));
+    if (c->hz.on) {
+      c->hz.record(c->fork_ev, 0);
+      c->hz.wait(1, c->fork_ev);
+    }
+    c->b_pending = 1;  // joined into the packet stream before anything else reads the packets (join_b)
+  }
+  unsigned wg[2][3] = {};  // workgroups of each part's launch in each slot (0: the max was copied)
+  struct Spec {  // a guessed attempt already queued (see below)
+    bool on, ran;
+    int slot, from, to;
+    double t, h, tnew;
+  } spec{false, false, 0, 0, 0, 0.0, 0.0, 0.0};
+  auto queue = [&](int from, int to, double ta, double ha, double tnewa, int gate_slot, double gscale,
+                   double glimit, int* slot, const double* coef = nullptr) -> int {
     Ode23Args a = base;
+    a.coef = coef;
     a.yx = S[from].x;
     a.yk = S[from].k;
     a.F[0] = S[from].F;
@@ -3532,51 +3664,112 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
     a.ynk = S[to].k;
     attempt_coeffs(a, ta, ha, tnewa);
     const int sl = c->o_dmax_cur;
-    a.dmax = c->o_dmax + sl;
-    a.dmax_clear = c->o_dmax + (sl + 1) % 3;
-    a.gate = gate;
     a.gate_scale = gscale;
     a.gate_limit = glimit;
-    int r;
-    if ((r = ode23_launch<0>(c, a))) return r;
-    HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl, c->o_dmax + sl, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                             c->stream));
-    HIPCHK(c, hipEventRecord(c->o_ev[sl], c->stream));
+    for (int p = 0; p < P; ++p) {
+      a.dmax = c->o_dmax + 3 * p + sl;
+      a.dmax_clear = c->o_dmax + 3 * p + (sl + 1) % 3;
+      // a part's guess is gated on its own part of the previous max: when the
+      // whole max passes, so does every part (err = absh * max is monotone)
+      a.gate = gate_slot >= 0 ? c->o_dmax + 3 * p + gate_slot : nullptr;
+      a.hpart = c->o_hpart_d + (size_t)(3 * p + sl) * kMaxBins;
+      int r;
+      if ((r = ode23_launch<0>(c, a, split ? p : -1, &wg[p][sl]))) return r;
+      const hipStream_t st = p == 0 ? c->stream : c->sx[0];
+      if (wg[p][sl] == 0)  // the per-packet stage kernels (never split): copy the max
+        HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl, c->o_dmax + sl, sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, st));
+      HIPCHK(c, hipEventRecord(p == 0 ? c->o_ev[sl] : c->o_evb[sl], st));
+    }
     c->o_dmax_cur = (sl + 1) % 3;
     *slot = sl;
     return SWRT_OK;
   };
+  // the raw error max of the attempt in slot sl: the bit-pattern max (= the
+  // value max of these non-negative doubles, as the device's atomicMax)
+  auto wait_max = [&](int sl, double* out) -> int {
+    unsigned long long m = 0;
+    for (int p = 0; p < P; ++p) {
+      HIPCHK(c, hipEventSynchronize(p == 0 ? c->o_ev[sl] : c->o_evb[sl]));
+      const unsigned g = wg[p][sl];
+      if (g == 0) {
+        m = std::max(m, c->o_hmax[sl]);
+      } else {
+        const unsigned long long* h = c->o_hpart + (size_t)(3 * p + sl) * kMaxBins;
+        for (unsigned i = 0; i < g; ++i) m = std::max(m, h[i]);
+      }
+    }
+    if (c->hz.on) {  // debug: the host-mapped maxima against the device's atomicMax slots
+      unsigned long long d = 0;
+      for (int p = 0; p < P; ++p) {
+        unsigned long long v = 0;
+        HIPCHK(c, hipMemcpy(&v, c->o_dmax + 3 * p + sl, sizeof(v), hipMemcpyDeviceToHost));
+        d = std::max(d, v);
+      }
+      if (d != m) return fail(c, SWRT_ERR_STATE, "ode23: host-mapped error max differs from the device's");
+    }
+    std::memcpy(out, &m, sizeof(double));
+    return SWRT_OK;
+  };
+  auto join = [&]() -> int {  // the extra stream's part launches ordered before the packet stream's next work
+    if (split) {
+      c->b_pending = 1;
+      HIPCHK_RC(join_b(c));
+    }
+    return SWRT_OK;
+  };
   // While the host waits for an attempt's error, the next attempt is already
-  // queued on the guess "accepted, next step MaxStep (or the clamp to
-  // tfinal)", gated on the device: it runs only if err = absh*raw <
-  // 0.5119*rtol, which with absh = MaxStep and a first try makes the
-  // controller's next absh certainly >= MaxStep (1.25*(err/rtol)^(1/3) < 1
-  // with margin for pow's last bit) — so then it is exactly the attempt the
-  // controller asks for next (checked again), and a wrong guess costs one
-  // empty launch instead of a whole attempt.
-  const double gate_limit = 0.5119 * rtol;
-  struct Spec {
-    bool on, ran;
-    int slot, from, to;
-    double t, h, tnew;
-  } spec{false, false, 0, 0, 0, 0.0, 0.0, 0.0};
-  const double rh = raw / (0.8 * std::pow(rtol, pw));
-  double absh = std::min(hmax, htspan);
-  if (absh * rh > 1) absh = 1.0 / rh;
-  absh = std::max(absh, 16 * np_spacing(t));
+  // queued on a guess of the controller's next step, gated on the device: it
+  // runs only if err = absh*raw < a limit under which the controller's
+  // answer for a first try is certain without its pow (margins far above
+  // pow's last bit): with temp = 1.25*(err/rtol)^(1/3) the controller takes
+  // absh/temp when temp > 0.2, else 5*absh, then clamps to MaxStep, so
+  //   absh == MaxStep:      MaxStep    when err < 0.5119*rtol         (temp < 1)
+  //   5*absh >= MaxStep:    MaxStep    when err < 0.999*rtol*(absh/(1.25*MaxStep))^3
+  //   else:                 5*absh     when err < 0.999*0.004096*rtol (temp < 0.2)
+  // (then the clamp to tfinal).  A right guess is exactly the attempt the
+  // controller asks for next (checked again), a wrong one costs one empty
+  // launch instead of a host round trip per attempt.
+  // the first attempt from the device's coefficients, queued now; then the
+  // caller's hook (host work that overlaps stage 1 and this attempt)
+  int first_slot = -1;
+  if (dev_first && (rc = queue(cur, (cur + 1) % 3, t, 0.0, 0.0, -1, 0.0, 0.0, &first_slot, c->o_coef))) return rc;
+  if (hook) {
+    // the hook may call the library (e.g. the next QG step on the QG stream);
+    // it must not touch the packets.  Its calls must not join the extra
+    // stream's attempt parts into the packet stream (they run on), so the
+    // split is hidden from them and re-marked after.
+    c->b_pending = 0;
+    hook(hook_user);
+    if (split) c->b_pending = 1;
+  }
+  HIPCHK(c, hipEventSynchronize(c->o_ev[sl_f1]));
+  if (dev_first)
+    std::memcpy(&raw, &c->o_shown[0], sizeof(double));
+  else
+    std::memcpy(&raw, c->o_hmax + sl_f1, sizeof(double));
+  HIPCHK_RC(dev_err_check(c));
+  double absh = o23_initial_absh(raw, c0, hmax, htspan, 16 * np_spacing(t));
+  if (dev_first) {
+    // the device's first attempt stands if it took exactly the controller's
+    // first step (always, by construction: the same operations) — else it is
+    // left to be overwritten by the attempt queued from the host's values
+    double ab = absh, h1, tn1, cf[8];
+    const bool d1 = o23_step_head(ab, hmax, 16 * np_spacing(t), tdir, t, tfinal, h1, tn1);
+    (void)d1;
+    o23_coeffs(t, h1, tn1, cf);
+    bool same = ab == c->o_shown[1] && h1 == c->o_shown[2] && tn1 == c->o_shown[3];
+    for (int i = 0; i < 8; ++i) same = same && cf[i] == c->o_shown[4 + i];
+    spec = {true, same, first_slot, cur, (cur + 1) % 3, t, h1, tn1};
+  }
   int64_t nts = 0;
   ts_out[nts++] = t;
   bool done = false;
   int64_t nfailed = 0, attempts = 0;
   while (!done) {
     const double hmin = 16 * np_spacing(t);
-    absh = std::min(hmax, std::max(hmin, absh));
-    double h = tdir * absh;
-    if (1.1 * absh >= std::fabs(tfinal - t)) {
-      h = tfinal - t;
-      absh = std::fabs(h);
-      done = true;
-    }
+    double h, tnew_head;
+    done = o23_step_head(absh, hmax, hmin, tdir, t, tfinal, h, tnew_head);
     bool nofailed = true;
     double tnew, err;
     int to;
@@ -3590,34 +3783,39 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
         to = spec.to;
       } else {
         to = (cur + 1) % 3;
-        if ((rc = queue(cur, to, t, h, tnew, nullptr, 0.0, 0.0, &slot))) return rc;
+        if ((rc = queue(cur, to, t, h, tnew, -1, 0.0, 0.0, &slot))) return rc;
       }
       spec.on = false;
-      if (!done && nofailed && absh == hmax) {
-        const double t2 = tnew;
-        const double hmin2 = 16 * np_spacing(t2);
-        double absh2 = std::min(hmax, std::max(hmin2, hmax));
-        double h2 = tdir * absh2;
-        bool done2 = false;
-        if (1.1 * absh2 >= std::fabs(tfinal - t2)) {
-          h2 = tfinal - t2;
-          absh2 = std::fabs(h2);
-          done2 = true;
+      double gate_limit = 0.0;
+      if (!done && nofailed) {
+        double guess;
+        if (absh == hmax) {
+          guess = hmax;
+          gate_limit = 0.5119 * rtol;
+        } else if (5.0 * absh >= hmax) {
+          guess = hmax;
+          const double r = absh / (1.25 * hmax);
+          gate_limit = 0.999 * rtol * (r * r * r);
+        } else {
+          guess = 5.0 * absh;
+          gate_limit = 0.999 * 0.004096 * rtol;
         }
-        const double tnew2 = done2 ? tfinal : t2 + h2 * 1.0;
+        const double t2 = tnew;
+        double absh2 = guess, h2, tnew2;
+        (void)o23_step_head(absh2, hmax, 16 * np_spacing(t2), tdir, t2, tfinal, h2, tnew2);
         const int sto = 3 - cur - to;
         int sl2;
-        if ((rc = queue(to, sto, t2, h2, tnew2, c->o_dmax + slot, absh, gate_limit, &sl2))) return rc;
+        if ((rc = queue(to, sto, t2, h2, tnew2, slot, absh, gate_limit, &sl2))) return rc;
         spec = {true, false, sl2, to, sto, t2, h2, tnew2};
       }
-      HIPCHK(c, hipEventSynchronize(c->o_ev[slot]));
-      std::memcpy(&raw, c->o_hmax + slot, sizeof(double));
+      if ((rc = wait_max(slot, &raw))) return rc;
       err = absh * raw;
       spec.ran = spec.on && err < gate_limit;  // the device's gate, the same operation
       h = tnew - t;
       if (err > rtol) {
         ++nfailed;
         if (absh <= hmin) {
+          HIPCHK_RC(join());
           HIPCHK(c, hipStreamSynchronize(c->stream));  // a queued guess may still be running
           commit();
           return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
@@ -3647,7 +3845,9 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
     }
   }
   // everything queued has finished: the last attempt (done) queues no guess,
-  // and every earlier guess precedes it on the stream
+  // and every earlier guess precedes it on its stream; the extra stream's
+  // part launches are joined into the packet stream
+  HIPCHK_RC(join());
   commit();
   *nts_out = nts;
   if (stats3_out) {

@@ -55,7 +55,89 @@ struct Ode23Args {
   const unsigned long long* gate;
   double gate_scale, gate_limit;
   const int* order;  // tile kernel: binned slots in in-tile cell order (NULL: slot order)
+  // tile kernel: every workgroup's max also stored at hpart[blockIdx.x]
+  // (host-mapped memory, read by swrt_ode23_run after the launch's event: no
+  // copy between consecutive attempts; NULL: none)
+  unsigned long long* hpart;
+  // tile kernel: the share of the tiles this launch takes (swrt_share.hpp;
+  // part -1: every tile, one workgroup each)
+  TileShare sh;
+  // STAGE 0: the attempt's coefficients {ts, c[0], ts3, c3, ts4, c4[0..2]}
+  // from device memory (ode23_first_step_kernel) instead of the fields
+  // above: the kernel's DC instantiation (NULL: the fields)
+  const double* coef;
 };
+
+// ---- MATLAB ode23's step-size arithmetic, shared by host and device ---------
+// (swrt_ode23_run's controller and ode23_first_step_kernel: the same source,
+// the same IEEE operations; std::min(a, b) = b < a ? b : a, std::max(a, b) =
+// a < b ? b : a, spelled out so both sides pick the same operand)
+__host__ __device__ inline double o23_min(double a, double b) { return b < a ? b : a; }
+__host__ __device__ inline double o23_max(double a, double b) { return a < b ? b : a; }
+// the initial step from stage 1's raw max (c0 = 0.8 * rtol^(1/3))
+__host__ __device__ inline double o23_initial_absh(double raw, double c0, double hmax, double htspan, double hmin0) {
+  const double rh = raw / c0;
+  double absh = o23_min(hmax, htspan);
+  if (absh * rh > 1) absh = 1.0 / rh;
+  return o23_max(absh, hmin0);
+}
+// the loop head: clamp absh, h, and the final-step rule; returns done
+__host__ __device__ inline bool o23_step_head(double& absh, double hmax, double hmin, double tdir, double t,
+                                              double tfinal, double& h, double& tnew) {
+  absh = o23_min(hmax, o23_max(hmin, absh));
+  h = tdir * absh;
+  bool done = false;
+  if (1.1 * absh >= fabs(tfinal - t)) {
+    h = tfinal - t;
+    absh = fabs(h);
+    done = true;
+  }
+  tnew = t + h * 1.0;
+  if (done) tnew = tfinal;
+  return done;
+}
+// an attempt's stage times and coefficients {ts, c0, ts3, c3, ts4, c4[0..2]}:
+// f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2);
+// h4 = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew
+__host__ __device__ inline void o23_coeffs(double t, double h, double tnew, double out[8]) {
+  out[0] = t + h * 0.5;
+  out[1] = h * 0.5;
+  out[2] = t + h * 0.75;
+  out[3] = h * 0.75;
+  const double h4 = tnew - t;
+  out[4] = tnew;
+  out[5] = h4 * (2.0 / 9.0);
+  out[6] = h4 * (1.0 / 3.0);
+  out[7] = h4 * (4.0 / 9.0);
+}
+
+// swrt_ode23_run's first attempt without a host round trip: from stage 1's
+// max (the f1 launch's atomicMax slot) the initial step and the loop head,
+// then the attempt's coefficients — to `coef` (read by the attempt launch
+// queued behind this one) and, with {raw bits, absh, h, tnew} ahead of
+// them, to host-mapped `shown`, against which the host checks its own
+// computation of the same.  `clear`/`nclear`: max slots zeroed on the way
+// (a split run's part-1 slots; no memset launch in front of the first
+// attempt).  One lane; plain vector stores.
+__global__ void ode23_first_step_kernel(const unsigned long long* dmax, double c0, double hmax, double htspan,
+                                        double hmin0, double tdir, double t0, double tfinal, double* coef,
+                                        double* shown, unsigned long long* clear, int nclear) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  for (int i = 0; i < nclear; ++i) clear[i] = 0ull;
+  const unsigned long long bits = *dmax;
+  const double raw = __longlong_as_double((long long)bits);
+  double absh = o23_initial_absh(raw, c0, hmax, htspan, hmin0);
+  double h, tnew;
+  (void)o23_step_head(absh, hmax, hmin0, tdir, t0, tfinal, h, tnew);
+  double cf[8];
+  o23_coeffs(t0, h, tnew, cf);
+  for (int i = 0; i < 8; ++i) coef[i] = cf[i];
+  shown[0] = raw;
+  shown[1] = absh;
+  shown[2] = h;
+  shown[3] = tnew;
+  for (int i = 0; i < 8; ++i) shown[4 + i] = cf[i];
+}
 
 __device__ __forceinline__ void ode_rhs(const Ode23Args& a, const double ys[4], double fo[4]) {
   const double alpha = a.tmax != 0.0 ? a.ts / a.tmax : 0.0;  // interpolate_U(..., t/tmax, ...)
@@ -132,6 +214,11 @@ __global__ void __launch_bounds__(256) ode23_stage_kernel(Ode23Args a) {
 // stages then take their packets in that order, so the lanes of one
 // ds_read_b128 group read neighbouring window nodes (as the leapfrog tile
 // kernel's own in-tile sort does).  Order only: results do not depend on it.
+// The rank of a packet within its cell comes from an LDS atomicAdd, so the
+// order of packets that share a cell may differ from run to run; each
+// packet's arithmetic reads only its own state and the field, and the error
+// norm is a max, so every output bit is the same for any such order (the
+// ode23 GPU tests compare bits across runs and against the oracle).
 template <int T, int NT>
 __global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, int64_t n, const int* starts,
                                                              int ntx, double inv_dx, int nx,
@@ -198,7 +285,10 @@ __global__ void __launch_bounds__(NT) tile_cell_order_kernel(const double* x, in
 // of writing an order array.  The stages then read y and F1 and write ynew
 // and F4 at contiguous slots (through order[] every 8-byte access was
 // scattered: 250 MB of writes per 1e6-packet attempt for 64 MB of outputs,
-// profiles/r04_ode23).  Order only: results do not depend on it.
+// profiles/r04_ode23).  Order only: results do not depend on it (the
+// in-cell order is run-dependent, as above; the packets' original indices
+// travel with them, so packets_get and the history frames are in the
+// original order regardless).
 template <int T, int NT>
 __global__ void __launch_bounds__(NT) tile_cell_sort_kernel(const double* x, const double* k, const int* perm,
                                                             int64_t n, const int* starts, int ntx,
@@ -307,7 +397,10 @@ __device__ __forceinline__ void tile_rhs(const Ode23Args& a, const double2* win,
   fo[3] = -(I[3] * k1 + I[5] * k2);
 }
 
-template <int STAGE, bool TWO, int T, int M, int NT, bool V5>
+// DC (STAGE 0): the attempt's coefficients from a.coef (a separate
+// instantiation: the first attempt of swrt_ode23_run only, so the others keep
+// their coefficients in the kernel arguments' scalar registers)
+template <int STAGE, bool TWO, int T, int M, int NT, bool V5, bool DC = false>
 __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const int* starts, int ntx) {
   constexpr int W = T + 5 + 2 * M;
   constexpr int WS = W + ((12 - W % 16) + 16) % 16;  // LDS row stride (nodes)
@@ -318,7 +411,9 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
   if (a.dmax_clear && blockIdx.x == 0 && threadIdx.x == 0) *a.dmax_clear = 0ull;
   if (a.gate && !(a.gate_scale * __longlong_as_double((long long)*a.gate) < a.gate_limit)) return;
   int pbeg, pend;
-  const int tile = wg_work_range(starts, a.n, pbeg, pend);
+  TileShare sh = a.sh;
+  if (sh.part < 0) sh.ntiles = (int)gridDim.x;
+  const int tile = wg_work_range(starts, nullptr, a.n, sh, pbeg, pend);
   const int ox = (tile / ntx) * T, oy = (tile % ntx) * T;
   const int nx = a.f0.nx;
   stage_window_regs<TWO, T, M, NT, WS, V5>(a.f0, a.f1, ox, oy, win);
@@ -350,6 +445,17 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
     }
     double fo[4];
     if constexpr (STAGE == 0) {
+      // the attempt's coefficients
+      double cf[8] = {a.ts, a.c[0], a.ts3, a.c3, a.ts4, a.c4[0], a.c4[1], a.c4[2]};
+      if constexpr (DC) {  // uniform values: kept in scalar registers (vector ones spilled)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned long long v = reinterpret_cast<const unsigned long long*>(a.coef)[i];
+          const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)v);
+          const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(v >> 32));
+          cf[i] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+        }
+      }
       // stages 2, 3, 4 of the attempt in one pass (a rolled loop: one copy of
       // the gather, so registers stay at the single-stage count).  The sums
       // that combine the stage derivatives are carried in registers, added
@@ -379,27 +485,27 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const double f1 = a.F[0][c * n + q];
-            ys[c] = yv[c] + f1 * a.c[0];
-            s4[c] = f1 * a.c4[0];
+            ys[c] = yv[c] + f1 * cf[1];
+            s4[c] = f1 * cf[5];
             fe[c] = f1 * E1;
           }
-          ts = a.ts;
+          ts = cf[0];
         } else if (sg == 1) {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + fo[c] * a.c3;
-          ts = a.ts3;
+          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + fo[c] * cf[3];
+          ts = cf[2];
         } else {
 #pragma unroll
-          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + (s4[c] + fo[c] * a.c4[2]);
+          for (int c = 0; c < 4; ++c) ys[c] = yv[c] + (s4[c] + fo[c] * cf[7]);
           a.ynx[q] = ys[0]; a.ynx[n + q] = ys[1];
           a.ynk[q] = ys[2]; a.ynk[n + q] = ys[3];
-          ts = a.ts4;
+          ts = cf[4];
         }
         tile_rhs<TWO, T, M, WS, WNP, V5>(a, win, ox, oy, nx, alpha_of(a, ts), ys, fo);
         if (sg == 0) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            s4[c] = s4[c] + fo[c] * a.c4[1];
+            s4[c] = s4[c] + fo[c] * cf[6];
             fe[c] = fe[c] + fo[c] * E2;
           }
         } else if (sg == 1) {
@@ -442,7 +548,9 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
     if (threadIdx.x == 0) {
       double b = red[0];
       for (int w = 1; w < NT / 64; ++w) b = fmax(b, red[w]);
-      atomicMax(a.dmax, (unsigned long long)__double_as_longlong(b));
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(b);
+      atomicMax(a.dmax, bits);
+      if (a.hpart) a.hpart[blockIdx.x] = bits;
     }
   }
 }

@@ -72,7 +72,7 @@ def ode_symplectic(x0, k0, dt, T, f, gH, scheme):
 
 
 def ode23_packets(ctx: Context, tspan, tmax, f, Cg, nslots=2, rtol=1e-3, atol=1e-6, bump=BUMP_QG,
-                  allreduce_max=None, stats=None, controller=None):
+                  allreduce_max=None, stats=None, controller=None, hook=None):
     """[~, y] = ode23(ray_ode, tspan, y0) for the device-resident packets
     (qgsw_raytrace.m:143-150, qg2layersw_raytrace.m:189-196): MATLAB ode23's
     Bogacki-Shampine controller (defaults RelTol 1e-3, AbsTol 1e-6, MaxStep
@@ -87,14 +87,20 @@ def ode23_packets(ctx: Context, tspan, tmax, f, Cg, nslots=2, rtol=1e-3, atol=1e
     ``controller``: "library" runs this same controller inside the C library
     (swrt_ode23_run: no interpreter between attempts), "python" the loop
     below; default "library" unless ``allreduce_max`` is given (the sharded
-    error norm needs the Python hook).  Same steps and bits either way."""
+    error norm needs the Python hook).  Same steps and bits either way.
+
+    ``hook``: a callable (QG calls only, never the packets) run once while
+    the interval's first launches run — the library controller calls it
+    after stage 1 and the first attempt are queued (swrt_ode23_run_hooked),
+    the Python loop after stage 1."""
     if controller is None:
         controller = "python" if allreduce_max is not None else "library"
     if controller == "library":
         if allreduce_max is not None:
             raise ValueError("the library controller has no allreduce hook (use controller='python')")
         try:
-            ts, st = ctx.ode23_run(float(tspan[0]), float(tspan[1]), tmax, f, Cg, nslots, rtol, atol, bump)
+            ts, st = ctx.ode23_run(float(tspan[0]), float(tspan[1]), tmax, f, Cg, nslots, rtol, atol, bump,
+                                   hook=hook)
         except SwrtError as e:
             if "below hmin" in str(e):
                 raise RuntimeError(str(e)) from e
@@ -112,6 +118,8 @@ def ode23_packets(ctx: Context, tspan, tmax, f, Cg, nslots=2, rtol=1e-3, atol=1e
     hmax = 0.1 * htspan
     t = t0
     rh = red(ctx.ode23_f1(t, tmax, f, Cg, nslots, thr, bump)) / (0.8 * rtol ** pw)
+    if hook is not None:
+        hook()
     absh = min(hmax, htspan)
     if absh * rh > 1:
         absh = 1.0 / rh
@@ -231,17 +239,18 @@ class PacketEnsemble:
         self.ctx.advance_intervals([dt / nsub for dt in dts], nsub, self.f, self.gH, alpha0=0.5 / nsub,
                                    dalpha=1.0 / nsub, bump=self.bump, save_every=save_every)
 
-    def advance_ode23(self, dt, rtol=1e-3, atol=1e-6, allreduce_max=None, stats=None, controller=None):
+    def advance_ode23(self, dt, rtol=1e-3, atol=1e-6, allreduce_max=None, stats=None, controller=None, hook=None):
         """The reference drivers' own integrator over [0, dt] with
         interpolate_U's alpha = t/dt (ode23(ray_ode, [0, dt], y0));
-        ``controller`` as in ode23_packets."""
+        ``controller`` and ``hook`` as in ode23_packets."""
         if allreduce_max is None and self.world > 1:
             import torch.distributed as dist
 
             from .dist import allreduce_max_fn
             allreduce_max = allreduce_max_fn(backend=dist.get_backend())
         return ode23_packets(self.ctx, (0.0, dt), dt, self.f, self.Cg, nslots=2, rtol=rtol, atol=atol,
-                             bump=self.bump, allreduce_max=allreduce_max, stats=stats, controller=controller)
+                             bump=self.bump, allreduce_max=allreduce_max, stats=stats, controller=controller,
+                             hook=hook)
 
     def state(self):
         return self.ctx.packets_get()

@@ -177,21 +177,33 @@ class _IntervalGroup:
         # ode23 (the reference's own packet integrator) takes one interval per call
         self.k = 1 if integrator == "ode23" else max(1, min(int(k), 4))
         self.dts = []
+        # ode23 controller totals over the calls (steps, failed, attempts)
+        self.ode23_stats = {"steps": 0, "failed": 0, "attempts": 0, "intervals": 0}
 
     def next_slot(self):
         return len(self.dts) + 1
 
-    def add(self, dt):
+    def add(self, dt, hook=None):
+        """hook (ode23 only): run while the interval's first launches run."""
         self.dts.append(dt)
         if len(self.dts) == self.k:
-            self.flush()
+            self.flush(hook)
+        elif hook is not None:
+            hook()
 
-    def flush(self):
+    def flush(self, hook=None):
         if self.dts:
             if self.integrator == "ode23":
-                self.ens.advance_ode23(self.dts[0])  # ode23(ray_ode, [0, dt], y0), alpha = t/dt
+                st = {}
+                # ode23(ray_ode, [0, dt], y0), alpha = t/dt
+                self.ens.advance_ode23(self.dts[0], stats=st, hook=hook)
+                for key in ("steps", "failed", "attempts"):
+                    self.ode23_stats[key] += int(st.get(key, 0))
+                self.ode23_stats["intervals"] += 1
             else:
                 self.ens.advance_intervals(self.dts, self.nsub)
+                if hook is not None:
+                    hook()
             self.ctx.swap_slots(0, len(self.dts))  # the last end snapshot starts the next group
             self.dts = []
 
@@ -268,16 +280,27 @@ class TwoLayerLoop:
             self.model.max_speed_async()
         self.t = self.t + self.dt
         active = self.ens is not None and self.t > self.packet_delay
+        spec = self.speculate and self.model.params.nlayers == 2 and getattr(self.model.ctx, "qg_fused", True)
         if active:
             ny = 2 * self.nx
             if not self.have_cur:
                 self.model.snapshot(0, which=1, layer=0, ny_period=ny)
             self.model.snapshot(self.group.next_slot(), which=0, layer=0, ny_period=ny)
             self.have_cur = True
-            self.group.add(self.dt)
+            if spec and self.group.integrator == "ode23":
+                # the ode23 interval holds the host until it ends (its step-size
+                # controller), so the next PDE step is queued from inside it,
+                # once its first launches are queued (swrt_ode23_run_hooked),
+                # and runs beside its attempts; the leapfrog interval only
+                # queues work and returns
+                dt = self.dt
+                self.group.add(dt, hook=lambda: self.model.step_speculative(dt))
+                spec = False
+            else:
+                self.group.add(self.dt)
         else:
             self.have_cur = False
-        if self.speculate and self.model.params.nlayers == 2 and getattr(self.model.ctx, "qg_fused", True):
+        if spec:
             self.model.step_speculative(self.dt)
         self.U0 = self.model.max_speed_result()  # this step's (read-backs pop oldest first)
         return active

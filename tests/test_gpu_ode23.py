@@ -131,3 +131,43 @@ def test_golden_ode23_fixture(ctx):
     xg, kg = ctx.packets_get()
     np.testing.assert_array_equal(ts, g["ts"])
     np.testing.assert_array_equal(np.concatenate([xg[:, 0], xg[:, 1], kg[:, 0], kg[:, 1]]), g["y"])
+
+
+@pytest.mark.parametrize("hz", [0, 1])
+def test_ode23_run_split_attempts_match_python_controller(ctx, qg_case, hz):
+    """70,000 packets on 16 tiles: swrt_ode23_run splits every attempt into
+    two part launches on the two packet streams, reads the error max from the
+    workgroups' host-mapped maxima (no copy between attempts) and queues a
+    gated guess of the next attempt through the ramp-up (5*absh) as well as at
+    MaxStep — the same steps and bits as the Python controller's one launch
+    and copied max per attempt.  With the hazard checker on (hz) the mapped
+    maxima are also checked against the device's atomicMax slots."""
+    from swraytracing_amd import _lib as L
+    c = qg_case
+    nx, Lx, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    flow1 = c["flow"]
+    flow2 = {n: np.asarray(v) * 1.3 for n, v in flow1.items()}
+    ctx.set_field_grid(0, _planes(flow1), nx, Lx)
+    ctx.set_field_grid(1, _planes(flow2), nx, Lx)
+    rng = np.random.default_rng(23)
+    n = 70_000
+    x = rng.uniform(-Lx / 2, Lx / 2, (n, 2))
+    k = c["k"][rng.integers(0, c["k"].shape[0], n)]
+    tmax = 40 * c["dt"]
+    ctx.set_locality(4, 0)
+    outs = []
+    try:
+        for controller in ("python", "library"):
+            ctx.debug_set(L.DEBUG_HAZARD_CHECK, hz if controller == "library" else 0)
+            ctx.packets_set(x, k)
+            st = {}
+            ts = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, stats=st, controller=controller)
+            outs.append((ts, st, *ctx.packets_get()))
+    finally:
+        ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+    (ts_p, st_p, xp, kp), (ts_l, st_l, xl, kl) = outs
+    assert st_l["steps"] > 5
+    np.testing.assert_array_equal(ts_l, ts_p)
+    assert (st_l["steps"], st_l["failed"], st_l["attempts"]) == (st_p["steps"], st_p["failed"], st_p["attempts"])
+    np.testing.assert_array_equal(xl, xp)
+    np.testing.assert_array_equal(kl, kp)

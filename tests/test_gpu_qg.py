@@ -566,7 +566,7 @@ def test_integrator_substitution_preserves_omega_statistics(ctx, tmp_path):
     assert abs(ea - eb) <= 4 * np.sqrt(wa.var() / N + wb.var() / N) + (edges[1] - edges[0])
 
 
-def _speculative_driver_run(ctx, speculate):
+def _speculative_driver_run(ctx, speculate, integrator="leapfrog"):
     nx, L, f, Cg, N = 128, 20.0, 3.0, 1.0, 70_000
     rng = np.random.default_rng(21)
     qk0 = _ring_qk(nx, L, rng)
@@ -575,7 +575,8 @@ def _speculative_driver_run(ctx, speculate):
     ens = sw.PacketEnsemble(x, k, L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * np.pi / L, nlayers=2,
                             bump=sw.BUMP_QG, ctx=ctx)
     U0 = model.max_speed()
-    loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=5, speculate=speculate)
+    loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=5, speculate=speculate,
+                           integrator=integrator)
     U0s = []
     for s in range(12):
         if s == 6:
@@ -589,17 +590,20 @@ def _speculative_driver_run(ctx, speculate):
     return model.qk, qk_pending, xs, ks, list(loop.dts), U0s, model.t, model.steps
 
 
-def test_qg2_speculative_steps_bit_identical(fresh_ctx):
+@pytest.mark.parametrize("integrator", ["leapfrog", "ode23"])
+def test_qg2_speculative_steps_bit_identical(fresh_ctx, integrator):
     """TwoLayerLoop(speculate=True) queues each next PDE step with the current
     dt before it reads this step's U0 (swrt_qg_step_speculative), then the CFL
     rule (qg2layersw_raytrace.m:156-165) accepts it or — when dt changes —
     drops it (swrt_qg_resolve) and steps again.  Against the plain loop: the
     same dt sequence (one change forced mid-run), U0 values, qk, PDE time and
     step count, and every packet's bits; swrt_qg_get reports the committed
-    step while a speculative one is queued."""
+    step while a speculative one is queued.  With the drivers' ode23 the next
+    step is queued from inside the interval (swrt_ode23_run_hooked's hook,
+    beside its attempts split over two streams)."""
     runs = {}
     for spec in (False, True):
-        runs[spec] = _speculative_driver_run(fresh_ctx, spec)
+        runs[spec] = _speculative_driver_run(fresh_ctx, spec, integrator)
     a, b = runs[False], runs[True]
     assert a[4] == b[4] and len(set(a[4])) >= 2  # dts, with a change
     assert a[5] == b[5]  # U0 per step

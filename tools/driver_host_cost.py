@@ -3,7 +3,11 @@ sequence, each call timed on the host, at a size where the GPU work is
 negligible (64^2, 1000 packets) and at the 8-GPU shard size (512^2 x 2,
 1.25e5 packets): when the host's time per step approaches the step time the
 driver is host-bound.
-usage: python tools/driver_host_cost.py [--steps 200]"""
+With --integrator ode23 the step runs the drivers' ode23 over the interval
+(the speculative PDE step queued before it, as TwoLayerLoop does): the
+"packets" call then holds the host for the whole interval, and the other
+calls are the host time between intervals.
+usage: python tools/driver_host_cost.py [--steps 200] [--integrator ode23]"""
 import argparse
 import math
 import os
@@ -18,7 +22,7 @@ import swraytracing_amd as sw  # noqa: E402
 import bench  # noqa: E402
 
 
-def run(nx, N, steps, speculate=True):
+def run(nx, N, steps, speculate=True, integrator="leapfrog"):
     L, f, Cg = 20.0, 3.0, 1.0
     rng = np.random.default_rng(7)
     qk1 = bench.ring_spectrum(nx, 1 if nx < 128 else 10, 3 if nx < 128 else 30, rng)
@@ -30,7 +34,8 @@ def run(nx, N, steps, speculate=True):
         ens = sw.PacketEnsemble(x, k, L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * math.pi / L, nlayers=2,
                                 bump=sw.BUMP_QG, ctx=ctx)
         U0 = model.max_speed()
-        loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=5, speculate=speculate)
+        loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=5, speculate=speculate,
+                               integrator=integrator)
         for _ in range(20):
             loop.step()
         loop.flush()
@@ -61,11 +66,15 @@ def run(nx, N, steps, speculate=True):
             model.snapshot(loop.group.next_slot(), which=0, layer=0, ny_period=ny)
             loop.have_cur = True
             t1 = time.perf_counter(); acc["snapshot"] += t1 - t; t = t1
+            early = speculate and integrator == "ode23"
+            if early:
+                model.step_speculative(loop.dt)
+                t1 = time.perf_counter(); acc["speculate"] += t1 - t; t = t1
             loop.group.add(loop.dt)
             t1 = time.perf_counter(); acc["packets"] += t1 - t; t = t1
-            if speculate:
+            if speculate and not early:
                 model.step_speculative(loop.dt)
-            t1 = time.perf_counter(); acc["speculate"] += t1 - t; t = t1
+                t1 = time.perf_counter(); acc["speculate"] += t1 - t; t = t1
             loop.U0 = model.max_speed_result()
             t1 = time.perf_counter(); acc["U0 result"] += t1 - t
         loop.flush()
@@ -73,7 +82,7 @@ def run(nx, N, steps, speculate=True):
         wall = (time.perf_counter() - t_start) / steps * 1e6
         loop.settle()
         parts = "  ".join(f"{n} {acc[n] / steps * 1e6:.1f}" for n in names)
-        print(f"nx={nx} N={N}: {wall:.1f} us per driver step; host per call (us): {parts}", flush=True)
+        print(f"{integrator} nx={nx} N={N}: {wall:.1f} us per driver step; host per call (us): {parts}", flush=True)
     finally:
         ctx.close()
 
@@ -81,9 +90,10 @@ def run(nx, N, steps, speculate=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--integrator", choices=["leapfrog", "ode23"], default="leapfrog")
     args = ap.parse_args()
     for nx, N in ((64, 1000), (512, 125_000), (512, 1_000_000)):
-        run(nx, N, args.steps)
+        run(nx, N, args.steps, integrator=args.integrator)
 
 
 if __name__ == "__main__":
