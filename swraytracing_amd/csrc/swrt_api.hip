@@ -3690,6 +3690,7 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
   auto wait_max = [&](int sl, double* out) -> int {
     unsigned long long m = 0;
     for (int p = 0; p < P; ++p) {
+      // (polling hipEventQuery instead: 1.802 / 1.831 vs 1.849 / 1.805 ms, noise; profiles/r05_ode23)
       HIPCHK(c, hipEventSynchronize(p == 0 ? c->o_ev[sl] : c->o_evb[sl]));
       const unsigned g = wg[p][sl];
       if (g == 0) {
