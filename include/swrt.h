@@ -439,6 +439,13 @@ int64_t swrt_qg_grid(const swrt_ctx* ctx, int* nlayers_out);
  * qg2layersw_raytrace.m:187-188: layer 1, u += shear_strength), no host copy.
  * ny_period as in swrt_set_field_grid (0 = nx). */
 int swrt_qg_snapshot(swrt_ctx* ctx, int slot, int which, int layer, int64_t ny_period);
+/* swrt_qg_snapshot(slot, which = 0, layer = 0, ny_period) of the pending
+ * speculative step's qk (swrt_qg_step_speculative; fused two-layer mode):
+ * the snapshot that the same call would write after swrt_qg_resolve(ctx, 1),
+ * bit for bit, queued before the CFL rule has decided — a driver queues it
+ * with the speculative step and discards it if the step is rejected.
+ * SWRT_ERR_STATE without a pending fused speculative step. */
+int swrt_qg_snapshot_speculative(swrt_ctx* ctx, int slot, int64_t ny_period);
 /* Exchange two packet field slots (the previous step's "current" snapshot
  * becomes the next step's "previous" one without recomputing it). */
 int swrt_swap_slots(swrt_ctx* ctx, int a, int b);

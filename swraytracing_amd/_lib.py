@@ -103,6 +103,7 @@ SIGNATURES = {
     "swrt_qg_get_q": (_INT, [_VP, _P]),
     "swrt_qg_grid": (_I, [_VP, ctypes.POINTER(_INT)]),
     "swrt_qg_snapshot": (_INT, [_VP, _INT, _INT, _INT, _I]),
+    "swrt_qg_snapshot_speculative": (_INT, [_VP, _INT, _I]),
     "swrt_swap_slots": (_INT, [_VP, _INT, _INT]),
     "swrt_field_div_free": (_INT, [_VP, _INT]),
     "swrt_check_arith": (_INT, [_VP, _I, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64)]),
@@ -598,6 +599,13 @@ class Context:
     def qg_snapshot(self, slot, which=0, layer=0, ny_period=0):
         self._chk(self._L.swrt_qg_snapshot(self._h, int(slot), int(which), int(layer), int(ny_period)),
                   "swrt_qg_snapshot")
+
+    def qg_snapshot_speculative(self, slot, ny_period=0):
+        """swrt_qg_snapshot_speculative: layer 0's grid_U of the pending
+        speculative step into `slot` (what qg_snapshot(slot) writes after
+        accepting it)."""
+        self._chk(self._L.swrt_qg_snapshot_speculative(self._h, int(slot), int(ny_period)),
+                  "swrt_qg_snapshot_speculative")
 
     def swap_slots(self, a=0, b=1):
         self._chk(self._L.swrt_swap_slots(self._h, int(a), int(b)), "swrt_swap_slots")

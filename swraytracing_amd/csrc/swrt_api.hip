@@ -3214,13 +3214,22 @@ int swrt_qg_get_q(swrt_ctx* c, double* q_out) {
   GUARD_END(c)
 }
 
-int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_period) {
-  if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+namespace {
+// swrt_qg_snapshot, or (spec) the same snapshot of the pending speculative
+// step's qk: its post-step transforms (swrt_qg_step_speculative) hold layer
+// 0's grid_U planes, which a snapshot after accepting the step would pack
+// unchanged — so the pack can run before the CFL rule has decided.
+int qg_snapshot_impl(swrt_ctx* c, int slot, int which, int layer, int64_t ny_period, bool spec) {
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
-  if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
+  if (spec) {
+    if (!q.spec) return fail(c, SWRT_ERR_STATE, "no speculative QG step pending");
+    if (!c->qg_fused || which != 0 || layer != 0 || q.g.n % 16 || !q.post_inv_valid || q.post_of != q.qk_spare)
+      return fail(c, SWRT_ERR_STATE, "a speculative snapshot needs the fused transforms of the pending step (layer 0)");
+  } else if (c->qg.spec) {
+    return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
+  }
   if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (current) or 1 (previous)");
   if (which == 1 && !q.has_prev) return fail(c, SWRT_ERR_STATE, "no previous qk before the first step");
   if (layer < 0 || layer >= q.g.nl) return fail(c, SWRT_ERR_ARG, "layer out of range");
@@ -3252,7 +3261,8 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   Slot& s = c->slot[slot];
   if (c->qg_fused && which == 0 && layer == 0 && nx % 16 == 0) {
     // layer 0's grid_U of the current qk is part of the post-step transforms
-    if ((rc = qg_post_inverse(c))) return rc;
+    // (of the speculative qk: already computed, checked above)
+    if (!spec && (rc = qg_post_inverse(c))) return rc;
     const double2* T = q.PT + (3 * q.g.nl - 1) * q.nn;
     hipLaunchKernelGGL(pack_pairs_kernel, dim3(nx / 16, nx / 16), dim3(256), 0, c->stream, T, (int)nx, (int)s.npad,
                        q.g.shear, s.nodes);
@@ -3273,6 +3283,20 @@ int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
     s.wpend = true;
   }
   return SWRT_OK;
+}
+}  // namespace
+
+int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_period) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  return qg_snapshot_impl(c, slot, which, layer, ny_period, false);
+  GUARD_END(c)
+}
+
+int swrt_qg_snapshot_speculative(swrt_ctx* c, int slot, int64_t ny_period) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN
+  return qg_snapshot_impl(c, slot, 0, 0, ny_period, true);
   GUARD_END(c)
 }
 

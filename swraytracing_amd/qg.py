@@ -130,6 +130,11 @@ class QGModel:
         self.settle()
         self.ctx.qg_snapshot(slot, which, layer, ny_period)
 
+    def snapshot_speculative(self, slot, ny_period=0):
+        """Layer 0's grid_U of the pending speculative step into `slot`: the
+        snapshot(slot) this step gives once accepted (bit for bit)."""
+        self.ctx.qg_snapshot_speculative(slot, ny_period)
+
 
 # ----------------------------------------------------------------------------
 # Drivers
@@ -232,6 +237,7 @@ def _fresh_outputs(out_dir, fresh):
 
 
 class TwoLayerLoop:
+    SPEC_SLOT = 2  # ode23 + speculate: where the next step's snapshot is packed ahead (slots 0/1: the interval's)
     """One iteration of qg2layersw_raytrace.m:152-197 on the device: the CFL
     rule (:156-165) on the current U0, the PDE step, U0 of the new qk read back
     asynchronously (collected after the packet work is queued, so the rule
@@ -261,6 +267,10 @@ class TwoLayerLoop:
         self.have_cur = False
         self.log = log
         self.group = _IntervalGroup(model.ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
+        # ode23 with speculation: the speculative step's snapshot is packed into
+        # slot SPEC_SLOT while the interval runs; an accepted step takes it by
+        # a slot swap instead of a snapshot launch between the intervals
+        self._spec_snap = False
 
     def step(self):
         """Returns True when the packets advanced through this PDE step."""
@@ -285,21 +295,32 @@ class TwoLayerLoop:
             ny = 2 * self.nx
             if not self.have_cur:
                 self.model.snapshot(0, which=1, layer=0, ny_period=ny)
-            self.model.snapshot(self.group.next_slot(), which=0, layer=0, ny_period=ny)
+            if self._spec_snap and not changed and self.have_cur:
+                # this (accepted) step's snapshot, packed during the last interval
+                self.model.ctx.swap_slots(self.group.next_slot(), self.SPEC_SLOT)
+            else:
+                self.model.snapshot(self.group.next_slot(), which=0, layer=0, ny_period=ny)
+            self._spec_snap = False
             self.have_cur = True
             if spec and self.group.integrator == "ode23":
                 # the ode23 interval holds the host until it ends (its step-size
-                # controller), so the next PDE step is queued from inside it,
-                # once its first launches are queued (swrt_ode23_run_hooked),
-                # and runs beside its attempts; the leapfrog interval only
-                # queues work and returns
+                # controller), so the next PDE step — and its snapshot — are
+                # queued from inside it, once its first launches are queued
+                # (swrt_ode23_run_hooked), and run beside its attempts; the
+                # leapfrog interval only queues work and returns
                 dt = self.dt
-                self.group.add(dt, hook=lambda: self.model.step_speculative(dt))
+
+                def hook():
+                    self.model.step_speculative(dt)
+                    self.model.snapshot_speculative(self.SPEC_SLOT, ny_period=ny)
+                    self._spec_snap = True
+                self.group.add(dt, hook=hook)
                 spec = False
             else:
                 self.group.add(self.dt)
         else:
             self.have_cur = False
+            self._spec_snap = False
         if spec:
             self.model.step_speculative(self.dt)
         self.U0 = self.model.max_speed_result()  # this step's (read-backs pop oldest first)

@@ -166,6 +166,27 @@ def test_qg_speculative_readback_popped_then_rejected(fresh_ctx):
     assert not m.spec_pending and m.steps == 2
 
 
+def test_qg_speculative_snapshot_is_the_accepted_snapshot(fresh_ctx):
+    """swrt_qg_snapshot_speculative packs layer 0's grid_U of the pending
+    speculative step (qg2layersw_raytrace.m:187-188) before the CFL rule has
+    decided: bit for bit the snapshot taken after accepting the step, and
+    refused (SWRT_ERR_STATE) without a pending step."""
+    nx, dt = 64, 0.01
+    ny = 2 * nx
+    m = sw.QGModel.two_layer(_two_layer_case(nx), nx, 3.0, 1.0, ctx=fresh_ctx)
+    m.step(dt)
+    m.max_speed()
+    with pytest.raises(sw.SwrtError, match="SWRT_ERR_STATE"):
+        m.snapshot_speculative(2, ny_period=ny)
+    m.step_speculative(dt)
+    m.snapshot_speculative(2, ny_period=ny)
+    m.resolve(True)
+    m.snapshot(3, which=0, layer=0, ny_period=ny)
+    a, b = fresh_ctx.get_field_grid(2, nx), fresh_ctx.get_field_grid(3, nx)
+    assert np.ascontiguousarray(a).tobytes() == np.ascontiguousarray(b).tobytes()
+    m.max_speed_result()  # the accepted step's read-back
+
+
 def test_qg_get_q_is_k2g(ctx):
     nx = 64
     qk0 = _two_layer_case(nx)
