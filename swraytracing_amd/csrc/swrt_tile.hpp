@@ -358,6 +358,7 @@ __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
   __shared__ int nbr[9];            // next-binning counts of the 3x3 neighbour tiles
 #ifdef SWRT_PHASE_TIMING
   __shared__ int nfall;             // diagnostic: packet-steps that took the global gather
+  __shared__ unsigned simds;        // diagnostic: SIMD id (2 bits) of every wave of the workgroup
 #endif
 
   const StepArgs& a = ta.s;
@@ -370,6 +371,7 @@ __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
   if (tid < 9) nbr[tid] = 0;
 #ifdef SWRT_PHASE_TIMING
   if (tid == 0) nfall = 0;
+  if (tid == 0) simds = 0;
 #endif
   SWRT_STAMP(0);
 #ifdef SWRT_PHASE_TIMING
@@ -380,6 +382,14 @@ __global__ void __launch_bounds__(NT, MINW) tile_leapfrog_kernel(TileArgs ta) {
     swrt_phase_dbg[blockIdx.x * 8 + 7] = ((unsigned long long)xcc << 32) | hw;
     swrt_phase_dbg[blockIdx.x * 8 + 6] = (unsigned long long)(pend - pbeg);
   }
+  __syncthreads();
+  if ((tid & 63) == 0) {
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    atomicOr(&simds, ((hw >> 4) & 3u) << (2 * (tid >> 6)));
+  }
+  __syncthreads();
+  if (tid == 0) swrt_phase_dbg[blockIdx.x * 8 + 6] |= (unsigned long long)simds << 32;
 #endif
 
   const int lane_rank = b128_lane_rank(tid & 63);

@@ -61,6 +61,8 @@ def main():
         d = buf.reshape(nrows, 8).astype(np.int64)
         d = d[d[:, 0] != 0]
         raw.append(d.copy())
+        # word 6: packets of the tile | the SIMD id of every wave (2 bits each) << 32
+        d[:, 6] &= 0xFFFFFFFF
         t0 = d[:, 0].min()
         P = (d[:, :5] - t0) * 10.0 / 1e3  # us
         stage = P[:, 1] - P[:, 0]
