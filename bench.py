@@ -476,7 +476,7 @@ def parse_args(argv=None):
                     help="timed driver steps per shard size in driver_step_forecast")
     ap.add_argument("--driver-warmup", type=int, default=16,
                     help="untimed driver steps before the timed ones (start-up, spare snapshot buffers)")
-    ap.add_argument("--ode23-steps", type=int, default=4,
+    ap.add_argument("--ode23-steps", type=int, default=8,
                     help="then this many driver steps with the reference's ode23 packet integrator (0: skip)")
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather all trajectories to rank 0 (one all_gather)")
