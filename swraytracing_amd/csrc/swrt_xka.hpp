@@ -125,9 +125,16 @@ __device__ __forceinline__ bool xka_velocity_t(const XkaArgs& a, const XkaStenci
                                                double l, double K2, double& Iu, double& Iv) {
   double su = 0.0, sv = 0.0;
   bool bad = false;
+  // the row weights shift through registers (a run-time index into s.wx
+  // would put the array in scratch)
+  double wxs[kNT];
+#pragma unroll
+  for (int q = 0; q < kNT; ++q) wxs[q] = s.wx[q];
 #pragma unroll 1
   for (int i = 0; i < kNT; ++i) {
-    const double wxi = s.wx[i];
+    const double wxi = wxs[0];
+#pragma unroll
+    for (int q = 0; q + 1 < kNT; ++q) wxs[q] = wxs[q + 1];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
       const double2 uv = tp.uv(i, j);
@@ -160,9 +167,14 @@ __device__ __forceinline__ bool xka_gradients_t(const XkaArgs& a, const XkaStenc
   bool bad = false;
 #pragma unroll
   for (int q = 0; q < 7; ++q) out[q] = 0.0;
+  double wxs[kNT];  // (as in xka_velocity_t)
+#pragma unroll
+  for (int q = 0; q < kNT; ++q) wxs[q] = s.wx[q];
 #pragma unroll 1
   for (int i = 0; i < kNT; ++i) {
-    const double wxi = s.wx[i];
+    const double wxi = wxs[0];
+#pragma unroll
+    for (int q = 0; q + 1 < kNT; ++q) wxs[q] = wxs[q + 1];
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
       const double2 uv = tp.uv(i, j);
