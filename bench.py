@@ -406,8 +406,10 @@ def add_observed_clock(r, ghz, spread):
     a throughput change attributable to code rather than to the box)."""
     r["clock_ghz_observed"] = ghz
     r["clock_probe_spread"] = spread
-    r["clock_note"] = ("median over same-XCD (start, end) probe pairs of s_memtime cycles / s_memrealtime seconds "
-                       "across the timed region; *_at_observed_clock = the fraction against the peak at that clock")
+    r["clock_note"] = ("median over CUs of s_memtime cycles / s_memrealtime seconds between the CU's first start "
+                       "and last end probe wave around the timed region (same-CU pairs: the cycle counters of "
+                       "different CUs are not aligned); *_at_observed_clock = the fraction against the peak at "
+                       "that clock; null when no CU ran both a start and an end probe (a GPU shared by ranks)")
     if ghz and ghz > 0:
         s = 2.4 / ghz
         if r.get("frac") is not None:
@@ -573,7 +575,13 @@ def timed(ctx, w, args, dev, steps, warmup, barrier=None):
         barrier()
     kms, launches = ctx.kernel_time(reset=True)
     ctx.set_timing(0)
-    return t1 - t0, kms, launches, ctx.clock_ghz()
+    try:
+        clk = ctx.clock_ghz()
+    except sw.SwrtError:
+        # no CU ran both a start and an end probe wave: another process's
+        # kernels held the CUs (ranks sharing one GPU); the clock is unobserved
+        clk = (None, None)
+    return t1 - t0, kms, launches, clk
 
 
 def strong_scaling_forecast(ctx, w, args, dev, n_total, rate_1gpu, sizes=(2, 4, 8), steps=None):
