@@ -225,8 +225,16 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
                            integrator=integrator, speculate=bool(args.speculate))
     # AB1/AB2 start-up and first-use allocations: the snapshot renaming (qg.py
     # TwoLayerLoop) allocates its spare slot buffers during the first steps, a
-    # hipMalloc each — outside the timed steps
+    # hipMalloc each — outside the timed steps.  Then warm-up steps until
+    # DRIVER_WARM_S of driver work have run: this phase follows seconds of
+    # host-only work (the CPU baseline) in the default run, and a GPU coming
+    # back from idle holds a different clock for its first milliseconds
+    # (0.297-0.304 vs 0.277-0.280 ms per step at 1e6 with and without the
+    # idle gap before a 16-step warm-up, profiles/r05_qg_copy)
     for _ in range(args.driver_warmup):
+        loop.step()
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < DRIVER_WARM_S:
         loop.step()
     loop.flush()
     ctx.synchronize()
@@ -234,13 +242,19 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     if distributed:
         dist.barrier()
     nd0 = len(loop.dts)
+    ctx.clock_stamp(0)
     t0 = time.perf_counter()
     for _ in range(nsteps):
         loop.step()
     loop.flush()
+    ctx.clock_stamp(1)
     ctx.synchronize()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
+    try:
+        clk = ctx.clock_ghz()[0]
+    except sw.SwrtError:  # no CU ran both probe waves (see timed)
+        clk = None
     if distributed:
         el = max_over_ranks(el, backend=args.dist_backend)
     ms = el / nsteps * 1e3
@@ -249,7 +263,7 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
                "(qg2layersw_raytrace.m:195: RelTol 1e-3, AbsTol 1e-6, MaxStep 0.1*dt)")
             + f" of {w['x'].shape[0]} packets/GPU (qg2layersw_raytrace.m:152-197)")
     timed_dts = loop.dts[nd0:]
-    out = {"ms_per_pde_step": ms, "steps": nsteps, "what": what,
+    out = {"ms_per_pde_step": ms, "steps": nsteps, "what": what, "clock_ghz_observed": clk,
            # the CFL rule (qg2layersw_raytrace.m:156-165) re-forms the exponential propagators when dt changes
            "dt_changes": int(sum(1 for a, b in zip(loop.dts[nd0 - 1:], timed_dts) if a != b))}
     if integrator == "leapfrog":
@@ -275,6 +289,9 @@ def pde_alone(ctx, w, args, dev, nsteps=None):
     loop = sw.TwoLayerLoop(model, None, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
                            speculate=bool(args.speculate))
     for _ in range(args.driver_warmup):
+        loop.step()
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < DRIVER_WARM_S:  # (as in driver_step)
         loop.step()
     ctx.synchronize()
     torch.cuda.synchronize(dev)
@@ -310,6 +327,7 @@ def driver_forecast(ctx, w, args, dev, n_total, full):
     return out
 
 
+DRIVER_WARM_S = 0.3  # seconds of untimed driver steps before each driver-step measurement
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s (78.6 TFLOP/s spec counts an FMA as 2)
 LDS_CYCLES_PEAK = 256 * 2.4e9               # LDS-array cycles/s over the chip (one array per CU, 2.4 GHz)
 # fp64 operations one packet-step of the reference arithmetic needs (each +, -, *, /, sqrt, floor one op;
