@@ -234,7 +234,7 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     for _ in range(args.driver_warmup):
         loop.step()
     tw = time.perf_counter()
-    while time.perf_counter() - tw < DRIVER_WARM_S:
+    while time.perf_counter() - tw < args.driver_warm_s:
         loop.step()
     loop.flush()
     ctx.synchronize()
@@ -291,7 +291,7 @@ def pde_alone(ctx, w, args, dev, nsteps=None):
     for _ in range(args.driver_warmup):
         loop.step()
     tw = time.perf_counter()
-    while time.perf_counter() - tw < DRIVER_WARM_S:  # (as in driver_step)
+    while time.perf_counter() - tw < args.driver_warm_s:  # (as in driver_step)
         loop.step()
     ctx.synchronize()
     torch.cuda.synchronize(dev)
@@ -494,6 +494,8 @@ def parse_args(argv=None):
                     help="driver steps: queue the next PDE step before reading U0 (TwoLayerLoop speculate)")
     ap.add_argument("--forecast-driver-steps", type=int, default=100,
                     help="timed driver steps per shard size in driver_step_forecast")
+    ap.add_argument("--driver-warm-s", type=float, default=DRIVER_WARM_S,
+                    help="then driver steps for this many seconds, untimed (a GPU back from idle; 0: none)")
     ap.add_argument("--driver-warmup", type=int, default=16,
                     help="untimed driver steps before the timed ones (start-up, spare snapshot buffers)")
     ap.add_argument("--ode23-steps", type=int, default=8,

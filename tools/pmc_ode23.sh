@@ -7,7 +7,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$1
-BARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-forecast --no-fma --driver-steps 0 --ode23-steps 2 --driver-warmup 2 --packet-streams 1"
+BARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-forecast --no-fma --driver-steps 0 --ode23-steps 2 --driver-warmup 2 --driver-warm-s 0 --packet-streams 1"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 GROUPS_=("FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVES"
