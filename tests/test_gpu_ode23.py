@@ -171,3 +171,33 @@ def test_ode23_run_split_attempts_match_python_controller(ctx, qg_case, hz):
     assert (st_l["steps"], st_l["failed"], st_l["attempts"]) == (st_p["steps"], st_p["failed"], st_p["attempts"])
     np.testing.assert_array_equal(xl, xp)
     np.testing.assert_array_equal(kl, kp)
+
+
+def test_ode23_run_hook_runs_once_and_its_exception_surfaces(ctx, qg_case):
+    """swrt_ode23_run_hooked calls the hook once, after the interval's first
+    launches are queued; an exception the hook raises reaches the caller after
+    the interval completes, with the packets advanced exactly as without a
+    hook (the hook may only queue other work)."""
+    c = qg_case
+    nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    ctx.set_field_grid(0, _planes(c["flow"]), nx, L)
+    ctx.set_field_grid(1, _planes({n: np.asarray(v) * 1.3 for n, v in c["flow"].items()}), nx, L)
+    x, k = c["x"][:128], c["k"][:128]
+    tmax = 20 * c["dt"]
+    ctx.packets_set(x, k)
+    ts0 = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg)
+    x0, k0 = ctx.packets_get()
+    calls = []
+    ctx.packets_set(x, k)
+    ts1 = sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, hook=lambda: calls.append(1))
+    assert calls == [1]
+    np.testing.assert_array_equal(ts1, ts0)
+
+    def bad():
+        raise ValueError("hook failed")
+    ctx.packets_set(x, k)
+    with pytest.raises(ValueError, match="hook failed"):
+        sw.ode23_packets(ctx, (0.0, tmax), tmax, f, Cg, hook=bad)
+    x2, k2 = ctx.packets_get()
+    np.testing.assert_array_equal(x2, x0)
+    np.testing.assert_array_equal(k2, k0)
