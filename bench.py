@@ -63,6 +63,22 @@ def ring_spectrum(nx, kmin, kmax_ring, rng, phase_shift=0.0):
     return qk
 
 
+def broadband_spectrum(nx, K_d2, ks, rng):
+    """SURVEY §8(d)'s broadband variant: psi-hat with random phases and
+    |psi-hat| ~ |k|^-3 for 1 <= |k| <= 0.75 kmax (k in grid units), handed to
+    grid_U as q-hat = -(K_d2 + K^2) psi-hat (its inversion, grid_U.m:2)."""
+    kmax = nx // 2 - 1
+    kx = np.arange(-kmax, kmax + 1)[:, None]
+    ky = np.arange(0, kmax + 1)[None, :]
+    r = np.sqrt(kx * kx + ky * ky)
+    ph = rng.uniform(0, 2 * np.pi, r.shape)
+    mask = (r >= 1) & (r <= 0.75 * kmax)
+    psi = np.zeros(r.shape, dtype=np.complex128)
+    psi[mask] = r[mask] ** -3.0 * np.exp(1j * ph[mask])
+    K2 = (kx * ks) ** 2 + (ky * ks) ** 2
+    return -(K_d2 + K2) * psi
+
+
 def build_workload(ctx, args, lo, hi, n_total):
     """The replicated field (every rank draws the same spectra from `seed`)
     and this rank's packets [lo, hi) of the n_total-packet ensemble (the same
@@ -72,7 +88,10 @@ def build_workload(ctx, args, lo, hi, n_total):
     nx, L, f, Cg, Ug = args.nx, 20.0, 3.0, 1.0, 0.2
     K_d2 = f / Cg
     ks = 2 * np.pi / L
-    qk1 = ring_spectrum(nx, 10, 30, rng)
+    if getattr(args, "field", "ring") == "broadband":
+        qk1 = broadband_spectrum(nx, K_d2, ks, rng)
+    else:
+        qk1 = ring_spectrum(nx, 10, 30, rng)
     rng2 = np.random.default_rng(args.seed + 1)
     qk2 = qk1 * np.exp(1j * rng2.normal(0, 0.05, qk1.shape))
     # normalise to max|U| = Ug (initial_q, qg2layersw_raytrace.m:279-280)
@@ -459,6 +478,9 @@ def parse_args(argv=None):
                     help="initial packet positions (stratified: equal packets per tile; band: all packets in the "
                          "first 1/--band-parts of the domain in x, a spatial-shard diagnostic)")
     ap.add_argument("--band-parts", type=int, default=8)
+    ap.add_argument("--field", choices=["ring", "broadband"], default="ring",
+                    help="flow: the drivers' ring spectrum 10 < |k| <= 30 (initial_q), or SURVEY 8(d)'s broadband "
+                         "|psi| ~ |k|^-3 up to 0.75 kmax (every scale, every tile)")
     ap.add_argument("--gather-mode", type=int, default=0, choices=[0, 1],
                     help="headline stencil arithmetic: 0 bit-exact (default), 1 FMA (tolerance; PMC diagnostics)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -744,7 +766,7 @@ def main(argv=None):
                    "mode": args.mode, "rebin_every": args.rebin_every, "tile": args.tile, "kernel": args.kernel,
                    "sparse_tiles": args.sparse_tiles,
                    "packet_streams": args.packet_streams, "gather_mode": args.gather_mode,
-                   "positions": args.positions,
+                   "positions": args.positions, "field": args.field,
                    "parallelism": f"packets sharded x{world} ({args.scaling}), field replicated"},
         "roofline": roof,
         "finite": finite,

@@ -465,6 +465,35 @@ def test_small_shard_bench_field_bitexact(ctx, oracle_lib, N):
     np.testing.assert_array_equal(kg[idx], ko)
 
 
+def test_broadband_bench_field_bitexact(ctx, oracle_lib):
+    """The bench workload on SURVEY §8(d)'s broadband field (bench.py --field
+    broadband: |psi| ~ |k|^-3 up to 0.75 kmax, every scale on the 512^2 x 2
+    grid): 1e6 packets, 6 calls of 5 steps, a random subset bit-identical to
+    the C oracle."""
+    import argparse
+    import bench
+    bench._imports()
+    args = argparse.Namespace(nx=512, packets=1_000_000, world=1, rank=0, seed=146, mode="blend",
+                              field="broadband")
+    w = bench.build_workload(ctx, args, 0, args.packets, args.packets)
+    ctx.set_locality(20, 0)
+    try:
+        ctx.packets_set(w["x"], w["k"])
+        for _ in range(6):
+            bench.step(ctx, w, 5)
+        xg, kg = ctx.packets_get()
+    finally:
+        ctx.set_locality(4, 0)
+    p0, p1 = ctx.get_field_grid(0), ctx.get_field_grid(1)
+    idx = np.sort(np.random.default_rng(5).choice(args.packets, 2000, replace=False))
+    xo, ko = w["x"][idx], w["k"][idx]
+    for _ in range(6):
+        xo, ko, _, _ = oracle_lib.leapfrog(p0, p1, 0.1, 0.2, 512, 1024, w["L"] / 512, orc.BUMP_QG, xo, ko,
+                                           w["dt"] / 5, 5, w["f"], w["gH"])
+    np.testing.assert_array_equal(xg[idx], xo)
+    np.testing.assert_array_equal(kg[idx], ko)
+
+
 @pytest.mark.parametrize("sparse", [1, 2])
 @pytest.mark.parametrize("dt_scale", [1.0, 40.0])
 def test_sparse_tiles_bitexact(ctx, oracle_lib, qg_case, sparse, dt_scale):
