@@ -348,6 +348,18 @@ int swrt_ode23_run(swrt_ctx* ctx, double t0, double tfinal, double tmax, double 
 int swrt_ode23_run_hooked(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                           double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
                           int64_t* stats3_out, void (*hook)(void*), void* hook_user);
+/* Chain the next swrt_ode23_run(_hooked) to the one running (or the next to
+ * run): when it ends, it queues the next call's stage 1 (re-binning when due,
+ * in-tile sort, f at t = 0) on the accepted packets with slot_a / slot_b as
+ * slots 0 / 1, so the device runs it while the host returns and prepares that
+ * call (the drivers arm it from the hook: their next interval reads this
+ * interval's end snapshot and the one the hook queued).  The next call takes
+ * it only if it would compute exactly that — its slots 0 / 1 hold the same
+ * nodes, not rewritten since, the same f, Cg, AbsTol/RelTol, bump and
+ * alpha(t0) = 0, and no call that may touch the packets ran in between — else
+ * it computes its own.  Same bits either way; one call's arming is consumed
+ * by that call. */
+int swrt_ode23_chain_next(swrt_ctx* ctx, int slot_a, int slot_b);
 
 /* ---------------------------------------------------------------------------
  * QG PDE stepper: the snapshots' producer, device-resident
@@ -525,7 +537,9 @@ int swrt_clock_ghz(swrt_ctx* ctx, double* ghz_out, double* spread_out);
  *   to the packets) then leaves an empty binning — no kernel runs over a bad
  *   range — and the next host synchronisation (swrt_synchronize,
  *   swrt_packets_get, ...) returns SWRT_ERR_STATE; the packet state is lost
- *   until swrt_packets_set. */
+ *   until swrt_packets_set.
+ * SWRT_DEBUG_ODE23_CHAINED (get only): ode23 calls that took the stage 1 the
+ *   previous call queued (swrt_ode23_chain_next). */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3
@@ -534,6 +548,7 @@ int swrt_clock_ghz(swrt_ctx* ctx, double* ghz_out, double* spread_out);
 #define SWRT_DEBUG_QG_UPDATE_COLS 7
 #define SWRT_DEBUG_SHARE_SKEW 8
 #define SWRT_DEBUG_CORRUPT_COUNT 9
+#define SWRT_DEBUG_ODE23_CHAINED 10
 int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
 int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
 

@@ -90,6 +90,7 @@ SIGNATURES = {
                               ctypes.POINTER(_I)]),
     "swrt_ode23_run_hooked": (_INT, [_VP, _D, _D, _D, _D, _D, _INT, _D, _D, _D, _P, _I, ctypes.POINTER(_I),
                                      ctypes.POINTER(_I), _HOOK, _VP]),
+    "swrt_ode23_chain_next": (_INT, [_VP, _INT, _INT]),
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_step_speculative": (_INT, [_VP, _D]),
@@ -126,6 +127,7 @@ DEBUG_QG_JFUSE = 5
 DEBUG_QG_UPDATE_COLS = 7
 DEBUG_SHARE_SKEW = 8
 DEBUG_CORRUPT_COUNT = 9
+DEBUG_ODE23_CHAINED = 10
 
 _lib = None
 
@@ -532,6 +534,12 @@ class Context:
                           RuntimeWarning, stacklevel=2)
         return ts[:min(nts.value, ts_cap)].copy(), {"steps": st[0], "failed": st[1], "attempts": st[2],
                                                     "accepted": nts.value}
+
+    def ode23_chain_next(self, slot_a, slot_b):
+        """swrt_ode23_chain_next: the running (or next) ode23_run queues the
+        next call's stage 1 with slots (slot_a, slot_b) as its slots 0 / 1
+        when it ends; the next call takes it only if it computes the same."""
+        self._chk(self._L.swrt_ode23_chain_next(self._h, int(slot_a), int(slot_b)), "swrt_ode23_chain_next")
 
     # ---- QG PDE stepper (swrt_qg_*) ---------------------------------------
     def qg_init(self, params: QGParams, nx, qk):

@@ -92,6 +92,7 @@ struct Slot {
   bool set = false;
   bool has_psi = false;
   bool div_free = false;    // every node's v_y is exactly -u_x (five-sum kernels apply)
+  uint64_t wgen = 0;        // write generation: a new value at every write of the nodes (ctx slot_wgen)
   // cross-stream order (they travel with the buffers through swaps and renames):
   hipEvent_t uev = nullptr;  // last context-stream use (packet kernels, field writes)
   hipEvent_t uref = nullptr; // the event that marks that use: uev, or the stop event attached to
@@ -303,6 +304,21 @@ struct swrt_ctx {
   double* o_coef = nullptr;
   double* o_shown = nullptr;
   double* o_shown_d = nullptr;
+  // the next swrt_ode23_run's stage 1, queued at the end of this one
+  // (swrt_ode23_chain_next): armed with the slots the next call reads as its
+  // slots 0 / 1; `queued` holds what it was computed from, and any API call
+  // that may touch the packets drops it (GUARD_BEGIN)
+  struct O23Chain {
+    bool want = false;
+    int sa = -1, sb = -1;
+    bool queued = false;
+    int dmax_slot = 0;
+    const double* nodes[2] = {nullptr, nullptr};
+    uint64_t wgen[2] = {0, 0};
+    double alpha = 0.0, f = 0.0, Cg = 0.0, thr = 0.0, bump = 0.0;
+    int64_t taken = 0;  // calls that took it (SWRT_DEBUG_ODE23_CHAINED)
+  } o_chain;
+  uint64_t slot_wgen = 0;  // Slot::wgen source
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
   int64_t launch_count = 0;
@@ -422,14 +438,21 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
     const int rc_ = (expr);   \
     if (rc_) return rc_;      \
   } while (0)
-#define GUARD_BEGIN_KEEP_SPLIT try {
-#define GUARD_BEGIN               \
+// GUARD_BEGIN drops a queued ode23 chain (the packets may change); the calls
+// that never touch the packets (QG, clock) use GUARD_BEGIN_KEEP_CHAIN.
+#define GUARD_BEGIN_KEEP_SPLIT \
+  try {                        \
+    c->o_chain.queued = false;
+#define GUARD_BEGIN_KEEP_CHAIN    \
   try {                           \
     {                             \
       const int jrc_ = join_b(c); \
       if (jrc_) return jrc_;      \
       hz_api(c);                  \
     }
+#define GUARD_BEGIN            \
+  GUARD_BEGIN_KEEP_CHAIN       \
+  c->o_chain.queued = false;
 #define GUARD_END(ctx)                                                \
   }                                                                   \
   catch (const std::bad_alloc&) {                                     \
@@ -1444,6 +1467,7 @@ int swrt_set_field_grid(swrt_ctx* c, int slot, const double* fields6, int64_t nx
   s.ny_period = ny_period;
   s.has_psi = false;
   s.set = true;
+  s.wgen = ++c->slot_wgen;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -1486,6 +1510,7 @@ int swrt_set_field_psi(swrt_ctx* c, int slot, const double* psi_grid, int64_t nx
   s.L = L;
   s.ny_period = nx;
   s.set = true;
+  s.wgen = ++c->slot_wgen;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -1523,6 +1548,7 @@ int swrt_set_field_qk(swrt_ctx* c, int slot, const double* qk_interleaved, int64
   s.L = L;
   s.ny_period = ny_period;
   s.set = true;
+  s.wgen = ++c->slot_wgen;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -1567,6 +1593,7 @@ int swrt_set_field_q(swrt_ctx* c, int slot, const double* q_grid, int64_t nx, do
   s.L = L;
   s.ny_period = ny_period;
   s.set = true;
+  s.wgen = ++c->slot_wgen;
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -2506,6 +2533,7 @@ int swrt_synchronize(swrt_ctx* c) {
 
 int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
   if (!c) return SWRT_ERR_ARG;
+  c->o_chain.queued = false;
   switch (key) {
     case SWRT_DEBUG_HAZARD_CHECK:
       if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "hazard check must be 0 or 1");
@@ -2565,6 +2593,7 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_SHARE_SKEW: *value_out = c->debug_share_skew ? 1 : 0; return SWRT_OK;
     case SWRT_DEBUG_CORRUPT_COUNT: *value_out = c->debug_corrupt_count; return SWRT_OK;
     case SWRT_DEBUG_QG_UPDATE_COLS: *value_out = c->qg_update_cols; return SWRT_OK;
+    case SWRT_DEBUG_ODE23_CHAINED: *value_out = c->o_chain.taken; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
 }
@@ -2623,7 +2652,7 @@ int swrt_kernel_time(swrt_ctx* c, int reset, double* total_ms, int64_t* launches
 
 int swrt_clock_stamp(swrt_ctx* c, int which) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN  // join_b: the stamp follows every packet launch queued on any packet stream
+  GUARD_BEGIN_KEEP_CHAIN  // join_b: the stamp follows every packet launch queued on any packet stream
   if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (start) or 1 (end)");
   HIPCHK(c, hipSetDevice(c->device));
   if (!c->clk) HIPCHK(c, hipMalloc(&c->clk, sizeof(unsigned long long) * 2 * kClockWaves * 3));
@@ -2636,7 +2665,7 @@ int swrt_clock_stamp(swrt_ctx* c, int which) {
 int swrt_clock_ghz(swrt_ctx* c, double* ghz_out, double* spread_out) {
   if (!c || !ghz_out) return SWRT_ERR_ARG;
   if (!c->clk) return fail(c, SWRT_ERR_STATE, "no clock stamps (swrt_clock_stamp 0 and 1 first)");
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   HIPCHK(c, hipSetDevice(c->device));
   std::vector<unsigned long long> h(2 * kClockWaves * 3);
   HIPCHK(c, hipMemcpyAsync(h.data(), c->clk, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
@@ -2677,7 +2706,7 @@ int swrt_clock_ghz(swrt_ctx* c, double* ghz_out, double* spread_out) {
 // ---------------------------------------------------------------------------
 int swrt_qg_init(swrt_ctx* c, const swrt_qg_params* p, int64_t nx, const double* qk_in) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   if (!p || !qk_in) return fail(c, SWRT_ERR_ARG, "NULL argument");
   if (p->nlayers != 1 && p->nlayers != 2) return fail(c, SWRT_ERR_ARG, "nlayers must be 1 or 2");
@@ -2948,7 +2977,7 @@ int qg_post(swrt_ctx* c) {
 
 int swrt_qg_step(swrt_ctx* c, double dt, int64_t nsteps) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
@@ -2996,7 +3025,7 @@ int qg_speed_launch(swrt_ctx* c);
 
 int swrt_qg_step_speculative(swrt_ctx* c, double dt) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
@@ -3039,7 +3068,7 @@ int swrt_qg_step_speculative(swrt_ctx* c, double dt) {
 
 int swrt_qg_resolve(swrt_ctx* c, int accept) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.spec) return fail(c, SWRT_ERR_STATE, "no speculative QG step pending");
@@ -3129,7 +3158,7 @@ int qg_speed_wait(swrt_ctx* c, double* U0_out) {
 
 int swrt_qg_max_speed(swrt_ctx* c, double* U0_out) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
@@ -3146,7 +3175,7 @@ int swrt_qg_max_speed(swrt_ctx* c, double* U0_out) {
 
 int swrt_qg_max_speed_async(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   if (!c->qg.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
   if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
@@ -3157,7 +3186,7 @@ int swrt_qg_max_speed_async(swrt_ctx* c) {
 
 int swrt_qg_max_speed_result(swrt_ctx* c, double* U0_out) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   if (c->qg.sp_count == 0) return fail(c, SWRT_ERR_STATE, "no swrt_qg_max_speed_async pending");
   if (!U0_out) return fail(c, SWRT_ERR_ARG, "NULL output");
@@ -3167,7 +3196,7 @@ int swrt_qg_max_speed_result(swrt_ctx* c, double* U0_out) {
 
 int swrt_qg_get(swrt_ctx* c, double* qk_out, double* t_out, int64_t* steps_out) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
@@ -3189,7 +3218,7 @@ int swrt_qg_get(swrt_ctx* c, double* qk_out, double* t_out, int64_t* steps_out) 
 
 int swrt_qg_get_q(swrt_ctx* c, double* q_out) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
@@ -3278,6 +3307,7 @@ int qg_snapshot_impl(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   s.L = q.g.dx * (double)nx;
   s.ny_period = ny_period;
   s.set = true;
+  s.wgen = ++c->slot_wgen;
   if (c->qg_sep) {
     HIPCHK(c, hipEventRecord(s.wev, c->stream));
     s.wpend = true;
@@ -3288,14 +3318,14 @@ int qg_snapshot_impl(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
 
 int swrt_qg_snapshot(swrt_ctx* c, int slot, int which, int layer, int64_t ny_period) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   return qg_snapshot_impl(c, slot, which, layer, ny_period, false);
   GUARD_END(c)
 }
 
 int swrt_qg_snapshot_speculative(swrt_ctx* c, int slot, int64_t ny_period) {
   if (!c) return SWRT_ERR_ARG;
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   return qg_snapshot_impl(c, slot, 0, 0, ny_period, true);
   GUARD_END(c)
 }
@@ -3571,6 +3601,7 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
 
 int swrt_ode23_accept(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
+  c->o_chain.queued = false;
   if (!c->o_ynx) return fail(c, SWRT_ERR_STATE, "no ode23 step attempted");
   std::swap(c->dx, c->o_ynx);
   std::swap(c->dk, c->o_ynk);
@@ -3594,6 +3625,75 @@ double np_spacing(double t) {  // numpy.spacing
 }
 }  // namespace
 
+namespace {
+double o23_alpha(double t, double tmax) { return tmax != 0.0 ? t / tmax : 0.0; }  // the kernels' alpha_of
+
+bool same_bits(double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; }
+
+// The chain (swrt_ode23_chain_next): at the end of an ode23 call, the next
+// call's stage 1 — re-binning when due, in-tile sort, f at t = 0 — queued on
+// the accepted packets with the armed slots as slots 0 / 1, so the device runs
+// it while the host returns and prepares that call.  The next call takes it
+// only if it would compute exactly that (ode23_chain_take).  (Chaining the
+// first step size and a whole first attempt as well measured no faster,
+// profiles/r05_chain.)
+int ode23_chain_queue(swrt_ctx* c, double tmax, double f, double Cg, int nslots, double thr, double bump) {
+  swrt_ctx::O23Chain& ch = c->o_chain;
+  const bool want = ch.want;
+  ch.want = false;
+  ch.queued = false;
+  if (!want || nslots != 2 || ch.sa < 0 || ch.sb < 0 || ch.sa == ch.sb) return SWRT_OK;
+  if (!c->slot[ch.sa].set || !c->slot[ch.sb].set || c->slot[ch.sa].nx != c->slot[ch.sb].nx) return SWRT_OK;
+  slot_writes_wait(c);  // e.g. the hook's snapshot into slot sb on the QG stream
+  Slot saved[SWRT_MAX_SLOTS];
+  for (int i = 0; i < SWRT_MAX_SLOTS; ++i) saved[i] = c->slot[i];
+  c->slot[0] = saved[ch.sa];
+  c->slot[1] = saved[ch.sb];
+  const int rc = ode23_f1_queue(c, 0.0, tmax, f, Cg, 2, thr, bump);
+  for (int i = 0; i < SWRT_MAX_SLOTS; ++i) c->slot[i] = saved[i];
+  if (rc) return rc;
+  ch.dmax_slot = c->o_dmax_cur;
+  c->o_dmax_cur = (ch.dmax_slot + 1) % 3;
+  for (int i = 0; i < 2; ++i) {
+    const Slot& s = c->slot[i == 0 ? ch.sa : ch.sb];
+    ch.nodes[i] = s.nodes;
+    ch.wgen[i] = s.wgen;
+  }
+  ch.alpha = o23_alpha(0.0, tmax);
+  ch.f = f;
+  ch.Cg = Cg;
+  ch.thr = thr;
+  ch.bump = bump;
+  ch.queued = true;
+  return SWRT_OK;
+}
+
+// The queued chain is this call's stage 1: nothing touched the packets since
+// (GUARD_BEGIN drops the chain), slots 0 / 1 hold the same, unrewritten nodes,
+// and stage 1's inputs are the same bits.
+bool ode23_chain_take(swrt_ctx* c, double t0, double tmax, double f, double Cg, int nslots, double thr,
+                      double bump) {
+  swrt_ctx::O23Chain& ch = c->o_chain;
+  const bool q = ch.queued;
+  ch.queued = false;
+  if (!q || nslots != 2) return false;
+  for (int i = 0; i < 2; ++i)
+    if (!c->slot[i].set || c->slot[i].nodes != ch.nodes[i] || c->slot[i].wgen != ch.wgen[i]) return false;
+  return same_bits(o23_alpha(t0, tmax), ch.alpha) && same_bits(f, ch.f) && same_bits(Cg, ch.Cg) &&
+         same_bits(thr, ch.thr) && same_bits(bump, ch.bump);
+}
+}  // namespace
+
+int swrt_ode23_chain_next(swrt_ctx* c, int slot_a, int slot_b) {
+  if (!c) return SWRT_ERR_ARG;
+  if (slot_a < 0 || slot_a >= SWRT_MAX_SLOTS || slot_b < 0 || slot_b >= SWRT_MAX_SLOTS || slot_a == slot_b)
+    return fail(c, SWRT_ERR_ARG, "chain slots out of range or equal");
+  c->o_chain.want = true;
+  c->o_chain.sa = slot_a;
+  c->o_chain.sb = slot_b;
+  return SWRT_OK;
+}
+
 int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                    double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
                    int64_t* stats3_out) {
@@ -3606,7 +3706,7 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
                           int64_t* stats3_out, void (*hook)(void*), void* hook_user) {
   if (!c) return SWRT_ERR_ARG;
   if (!ts_out || ts_cap < 1 || !nts_out) return fail(c, SWRT_ERR_ARG, "ts_out / ts_cap / nts_out");
-  GUARD_BEGIN
+  GUARD_BEGIN_KEEP_CHAIN
   SlotUse slot_use(c);
   const double tdir = std::copysign(1.0, tfinal - t0);
   const double pw = 1.0 / 3.0;
@@ -3618,10 +3718,17 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
   double t = t0;
   double raw = 0.0;
   int rc;
-  // stage 1 (with this call's re-binning and in-tile sort), its max in slot sl_f1
-  if ((rc = ode23_f1_queue(c, t, tmax, f, Cg, nslots, thr, bump))) return rc;
-  const int sl_f1 = c->o_dmax_cur;
-  c->o_dmax_cur = (sl_f1 + 1) % 3;
+  // stage 1 (with this call's re-binning and in-tile sort), its max in slot
+  // sl_f1: queued by the previous call when it was chained to this one
+  int sl_f1;
+  if (ode23_chain_take(c, t0, tmax, f, Cg, nslots, thr, bump)) {
+    sl_f1 = c->o_chain.dmax_slot;
+    ++c->o_chain.taken;
+  } else {
+    if ((rc = ode23_f1_queue(c, t, tmax, f, Cg, nslots, thr, bump))) return rc;
+    sl_f1 = c->o_dmax_cur;
+    c->o_dmax_cur = (sl_f1 + 1) % 3;
+  }
   Ode23Args base;
   if ((rc = ode23_prepare(c, nslots, base, tmax, f, Cg, thr, bump))) return rc;
   // The first attempt's step size on the device (ode23_first_step_kernel,
@@ -3874,6 +3981,7 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
   // part launches are joined into the packet stream
   HIPCHK_RC(join());
   commit();
+  if ((rc = ode23_chain_queue(c, tmax, f, Cg, nslots, thr, bump))) return rc;
   *nts_out = nts;
   if (stats3_out) {
     stats3_out[0] = nts - 1;

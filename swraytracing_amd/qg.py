@@ -271,6 +271,9 @@ class TwoLayerLoop:
         # slot SPEC_SLOT while the interval runs; an accepted step takes it by
         # a slot swap instead of a snapshot launch between the intervals
         self._spec_snap = False
+        # ode23 + speculate: chain each interval's stage 1 to the previous call
+        # (swrt_ode23_chain_next; SWRT_ODE23_CHAIN=0 turns it off for A/B runs)
+        self.chain = os.environ.get("SWRT_ODE23_CHAIN", "1") != "0"
 
     def step(self):
         """Returns True when the packets advanced through this PDE step."""
@@ -314,6 +317,11 @@ class TwoLayerLoop:
                     self.model.step_speculative(dt)
                     self.model.snapshot_speculative(self.SPEC_SLOT, ny_period=ny)
                     self._spec_snap = True
+                    if self.chain:
+                        # the next interval reads this one's end snapshot (slot
+                        # 1) and the one just queued: its stage 1 is queued as
+                        # this interval ends (taken only if still exact)
+                        self.model.ctx.ode23_chain_next(1, self.SPEC_SLOT)
                 self.group.add(dt, hook=hook)
                 spec = False
             else:

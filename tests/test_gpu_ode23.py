@@ -201,3 +201,72 @@ def test_ode23_run_hook_runs_once_and_its_exception_surfaces(ctx, qg_case):
     x2, k2 = ctx.packets_get()
     np.testing.assert_array_equal(x2, x0)
     np.testing.assert_array_equal(k2, k0)
+
+
+def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
+    """swrt_ode23_chain_next: an ode23 call queues the next call's stage 1
+    (f at t = 0 on its accepted packets, the armed slots as slots 0 / 1) as
+    it ends; the next call takes it only when it computes exactly that.  Two
+    chained intervals (the drivers' slot rotation between them) against the
+    same two unchained: the same times and packet bits whether the chain is
+    taken (plain, with the hazard checker modelling its launches, and for an
+    interval of another length: alpha(0) = 0 all the same) or dropped — by a
+    rewrite of a slot it read (even with the same data), by a call that may
+    touch the packets, or by another RelTol."""
+    from swraytracing_amd import _lib as L
+    c = qg_case
+    nx, Lx, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    flows = [c["flow"]] + [{n: np.asarray(v) * s for n, v in c["flow"].items()} for s in (1.3, -0.7)]
+    rng = np.random.default_rng(29)
+    n = 70_000  # two part launches per attempt (the split) on 16 tiles
+    x = rng.uniform(-Lx / 2, Lx / 2, (n, 2))
+    k = c["k"][rng.integers(0, c["k"].shape[0], n)]
+    tmax = 30 * c["dt"]
+    bump = orc.BUMP_QG
+
+    def run(arm, between=None, rtol2=1e-3, tfinal2=tmax, hz=0):
+        for s in range(3):
+            ctx.set_field_grid(s, _planes(flows[s]), nx, Lx)
+        ctx.debug_set(L.DEBUG_HAZARD_CHECK, hz)
+        try:
+            ctx.packets_set(x, k)
+            n0 = ctx.debug_get(L.DEBUG_ODE23_CHAINED)
+            hook = (lambda: ctx.ode23_chain_next(1, 2)) if arm else None
+            ts1, _ = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump, hook=hook)
+            ctx.swap_slots(0, 1)
+            ctx.swap_slots(1, 2)  # the armed slots 1 / 2 are now slots 0 / 1
+            if between is not None:
+                between()
+            ts2, st2 = ctx.ode23_run(0.0, tfinal2, tmax, f, Cg, 2, rtol2, 1e-6, bump)
+            taken = ctx.debug_get(L.DEBUG_ODE23_CHAINED) - n0
+            return ts1, ts2, *ctx.packets_get(), taken, st2
+        finally:
+            ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+
+    ctx.set_locality(4, 0)
+
+    def same(a, b):
+        for u, v in zip(a[:4], b[:4]):
+            np.testing.assert_array_equal(u, v)
+        assert a[5] == b[5]  # steps, failed, attempts of the second interval
+
+    ref = run(False)
+    assert ref[4] == 0 and len(ref[0]) > 5 and len(ref[1]) > 5
+    for hz in (0, 1):
+        chained = run(True, hz=hz)
+        assert chained[4] == 1
+        same(chained, ref)
+    rewrite = run(True, between=lambda: ctx.set_field_grid(1, _planes(flows[2]), nx, Lx))
+    assert rewrite[4] == 0
+    same(rewrite, ref)
+    touched = run(True, between=lambda: ctx.packets_get())
+    assert touched[4] == 0
+    same(touched, ref)
+    # another RelTol: another stage-1 input (AbsTol/RelTol), dropped
+    other = run(True, rtol2=1e-4)
+    assert other[4] == 0
+    same(other, run(False, rtol2=1e-4))
+    # another interval length (same tmax, t0 = 0): the same stage 1, taken
+    half = run(True, tfinal2=0.5 * tmax)
+    assert half[4] == 1
+    same(half, run(False, tfinal2=0.5 * tmax))

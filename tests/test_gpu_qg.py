@@ -605,10 +605,12 @@ def _speculative_driver_run(ctx, speculate, integrator="leapfrog"):
         assert loop.step()
         U0s.append(loop.U0)
     loop.flush()
+    import swraytracing_amd._lib as L_
+    chained = ctx.debug_get(L_.DEBUG_ODE23_CHAINED)
     qk_pending = model.qk  # the committed step while a speculative one is queued
     loop.settle()
     xs, ks = ens.state()
-    return model.qk, qk_pending, xs, ks, list(loop.dts), U0s, model.t, model.steps
+    return model.qk, qk_pending, xs, ks, list(loop.dts), U0s, model.t, model.steps, chained
 
 
 @pytest.mark.parametrize("integrator", ["leapfrog", "ode23"])
@@ -631,6 +633,11 @@ def test_qg2_speculative_steps_bit_identical(fresh_ctx, integrator):
     for u, v in zip(a[:4], b[:4]):
         assert np.ascontiguousarray(u).tobytes() == np.ascontiguousarray(v).tobytes()
     assert a[6] == b[6] and a[7] == b[7] == 12
+    if integrator == "ode23":
+        # the speculative loop chains each interval's stage 1 to the previous
+        # call (swrt_ode23_chain_next); the forced dt change drops one chain
+        # (a fresh snapshot rewrites slot 1) and the plain loop never arms it
+        assert a[8] == 0 and 8 <= b[8] <= 10, (a[8], b[8])
 
 
 @pytest.mark.parametrize("nx", [64, 512])
