@@ -261,6 +261,7 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     if distributed:
         dist.barrier()
     nd0 = len(loop.dts)
+    chained0 = ctx.debug_get(sw._lib.DEBUG_ODE23_CHAINED)
     ctx.clock_stamp(0)
     t0 = time.perf_counter()
     for _ in range(nsteps):
@@ -293,6 +294,8 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
         st = loop.group.ode23_stats
         if st["intervals"]:
             out["ode23_per_interval"] = {k: st[k] / st["intervals"] for k in ("steps", "failed", "attempts")}
+        # timed intervals whose stage 1 the previous one queued (swrt_ode23_chain_next)
+        out["ode23_chained_intervals"] = ctx.debug_get(sw._lib.DEBUG_ODE23_CHAINED) - chained0
     return out
 
 
