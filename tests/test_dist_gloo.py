@@ -1,4 +1,4 @@
-"""Multi-process path on CPU: world_size-2 gloo (no GPU needed).
+"""Multi-process path on CPU: world_size-2 and -4 gloo (no GPU needed).
 
 Covers the sharding / gather / max-reduce logic that bench.py and the
 distributed driver use; the per-shard physics is the (bit-exact) oracle so
@@ -63,12 +63,13 @@ def _worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [101, 64])
-def test_gloo_world2_shard_gather_matches_single_process(n):
+@pytest.mark.parametrize("world,n", [(2, 101), (2, 64), (4, 101)])
+def test_gloo_shard_gather_matches_single_process(world, n):
+    """world ranks (gloo), ragged shards when world does not divide n."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -76,7 +77,7 @@ def test_gloo_world2_shard_gather_matches_single_process(n):
         assert p.exitcode == 0
     ok, tmax = q.get(timeout=10)
     assert ok
-    assert tmax == 1.5
+    assert tmax == world - 0.5  # max over ranks of rank + 0.5
 
 
 class _ShardCtx:
@@ -144,14 +145,15 @@ def _ode23_worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_sharded_ode23_takes_the_global_steps():
-    """ode23's error norm is global: with the packets split over 2 ranks and
-    the per-attempt error max-reduced over them, both ranks take exactly the
-    single-process step sequence and the gathered state is bit-identical."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_sharded_ode23_takes_the_global_steps(world):
+    """ode23's error norm is global: with the packets split over `world` ranks
+    and the per-attempt error max-reduced over them, every rank takes exactly
+    the single-process step sequence and the gathered state is bit-identical."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ode23_worker, args=(r, 2, port, 90, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ode23_worker, args=(r, world, port, 90, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
