@@ -224,7 +224,7 @@ def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
     tmax = 30 * c["dt"]
     bump = orc.BUMP_QG
 
-    def run(arm, between=None, rtol2=1e-3, tfinal2=tmax, hz=0):
+    def run(arm, between=None, rtol2=1e-3, tfinal2=tmax, hz=0, rtol1=1e-3):
         for s in range(3):
             ctx.set_field_grid(s, _planes(flows[s]), nx, Lx)
         ctx.debug_set(L.DEBUG_HAZARD_CHECK, hz)
@@ -232,7 +232,7 @@ def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
             ctx.packets_set(x, k)
             n0 = ctx.debug_get(L.DEBUG_ODE23_CHAINED)
             hook = (lambda: ctx.ode23_chain_next(1, 2)) if arm else None
-            ts1, _ = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump, hook=hook)
+            ts1, _ = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, rtol1, 1e-6, bump, hook=hook)
             ctx.swap_slots(0, 1)
             ctx.swap_slots(1, 2)  # the armed slots 1 / 2 are now slots 0 / 1
             if between is not None:
@@ -266,6 +266,10 @@ def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
     other = run(True, rtol2=1e-4)
     assert other[4] == 0
     same(other, run(False, rtol2=1e-4))
+    # tight tolerances: rejected attempts in both intervals, chain taken
+    tight = run(True, rtol1=1e-7, rtol2=1e-7)
+    assert tight[4] == 1 and tight[5]["failed"] > 0
+    same(tight, run(False, rtol1=1e-7, rtol2=1e-7))
     # another interval length (same tmax, t0 = 0): the same stage 1, taken
     half = run(True, tfinal2=0.5 * tmax)
     assert half[4] == 1
