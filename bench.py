@@ -349,6 +349,119 @@ def driver_forecast(ctx, w, args, dev, n_total, full):
     return out
 
 
+def _time_loop(ctx, loop, args, dev, nsteps):
+    """ms per step of a driver loop on this GPU: start-up steps, then steps
+    for DRIVER_WARM_S seconds (see driver_step), then `nsteps` timed."""
+    for _ in range(args.driver_warmup):
+        loop.step()
+    tw = time.perf_counter()
+    while time.perf_counter() - tw < args.driver_warm_s:
+        loop.step()
+    loop.flush()
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(nsteps):
+        loop.step()
+    loop.flush()
+    ctx.synchronize()
+    torch.cuda.synchronize(dev)
+    return (time.perf_counter() - t0) / nsteps * 1e3
+
+
+def _owner_links():
+    """OwnerLink stand-ins for one GPU: the owner's export without the
+    broadcast, a receiver whose 'broadcast' is already in its buffers."""
+    from swraytracing_amd.dist import OwnerLink
+
+    class ExportOnly(OwnerLink):
+        def publish(self, ctx, dt):
+            b = self.bufs[self.cur ^ 1]
+            self._export(ctx, b)
+            b[-1].fill_(float(dt))
+            self.cur ^= 1
+
+    class Preloaded(OwnerLink):
+        def __init__(self, nx, dt):
+            super().__init__(nx, "nccl")
+            self.fixed_dt = dt
+
+        def receive(self):
+            self.cur ^= 1
+            return self.fixed_dt
+
+    return ExportOnly, Preloaded
+
+
+OWNER_WEIGHTS = (0.0, 0.25, 0.5, 1.0)
+
+
+def owner_forecast(ctx, w, args, dev, n_total, full_ms):
+    """The PDE-owner form of the sharded 2-layer driver (qg.py: rank 0 steps
+    the PDE, publishes each step's top-layer qk and dt; every other rank only
+    builds its snapshot from it and advances its packets), forecast from its
+    two legs measured on this one GPU, each timed as the loop the rank runs:
+      owner leg:    TwoLayerLoop with n0 packets + the export of qk (PDE, CFL
+                    read-back, snapshot, packets; the broadcast itself omitted)
+      receiver leg: ReceiverLoop with nr packets (swrt_snapshot_qk from a
+                    device buffer on the QG stream + the packet interval)
+    with n0 = N w/(w + G - 1) and nr = N/(w + G - 1) (dist.owner_bounds) for
+    owner weights w in OWNER_WEIGHTS; per G the step is max(owner, receiver)
+    at the best w, efficiency = the one-GPU driver step (all N) / (G x step)."""
+    ExportOnly, Preloaded = _owner_links()
+    nx, L, f, Cg = w["nx"], w["L"], w["f"], math.sqrt(w["gH"])
+    qk = np.stack([w["qk1"], -w["qk1"]], axis=2)
+    nsteps = args.forecast_driver_steps
+    legs = {}
+
+    def ensemble(n):
+        return sw.PacketEnsemble(w["x"][:n], w["k"][:n], L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * math.pi / L,
+                                 nlayers=2, bump=sw.BUMP_QG, ctx=ctx)
+
+    def owner_ms(n0):
+        if ("o", n0) not in legs:
+            model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
+            U0 = model.max_speed()
+            ens = ensemble(n0) if n0 > 0 else None
+            loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
+                                   speculate=bool(args.speculate), link=ExportOnly(nx, "nccl"))
+            legs[("o", n0)] = _time_loop(ctx, loop, args, dev, nsteps)
+            loop.settle()
+        return legs[("o", n0)]
+
+    def receiver_ms(nr):
+        if ("r", nr) not in legs:
+            model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)  # (a receiving rank holds one too)
+            dt = 0.25 * (L / nx) / model.max_speed()
+            link = Preloaded(nx, dt)
+            link.seed(ctx)
+            link.bufs[1].copy_(link.bufs[0])
+            loop = sw.ReceiverLoop(link, ensemble(nr), dt, 0.0, nsub=args.substeps)
+            legs[("r", nr)] = _time_loop(ctx, loop, args, dev, nsteps)
+        return legs[("r", nr)]
+
+    out = {"what": "PDE-owner form (qg.py OwnerLink/ReceiverLoop): rank 0 = TwoLayerLoop with n0 packets + qk export; "
+                   "ranks 1..G-1 = ReceiverLoop with nr packets (snapshot from the broadcast qk + packets); both "
+                   "legs timed on this GPU; step = max(owner, receiver) at the best owner weight",
+           "assumption": "the per-step RCCL broadcast of the top-layer qk (2.1 MB at 512^2) + dt from rank 0 is not "
+                         "measured (one GPU here): it is queued behind the owner's export and ahead of the "
+                         "receivers' snapshot, and is assumed to complete while their previous packet interval runs",
+           "one_gpu_ms": full_ms, "weights": list(OWNER_WEIGHTS)}
+    for G in (2, 4, 8):
+        from swraytracing_amd.dist import owner_bounds
+        tried = []
+        for wt in OWNER_WEIGHTS:
+            b = owner_bounds(n_total, G, wt)
+            n0, nr = b[0][1] - b[0][0], b[1][1] - b[1][0]
+            o, r = owner_ms(n0), receiver_ms(nr)
+            tried.append({"owner_weight": wt, "packets_owner": n0, "packets_per_receiver": nr, "owner_ms": o,
+                          "receiver_ms": r, "step_ms": max(o, r)})
+        best = min(tried, key=lambda d: d["step_ms"])
+        out[str(G)] = dict(best, forecast_value=n_total * args.substeps / (best["step_ms"] / 1e3),
+                           efficiency=full_ms / (G * best["step_ms"]), legs=tried)
+    return out
+
+
 DRIVER_WARM_S = 0.3  # seconds of untimed driver steps before each driver-step measurement
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s (78.6 TFLOP/s spec counts an FMA as 2)
 LDS_CYCLES_PEAK = 256 * 2.4e9               # LDS-array cycles/s over the chip (one array per CU, 2.4 GHz)
@@ -828,6 +941,8 @@ def main(argv=None):
                 if G in pk:  # packets alone at this shard (the metric's form) vs the PDE alone
                     fc[G]["packets_alone_ms"] = pk[G]["ms_per_step"]
                     fc[G]["bound"] = "pde" if fc["pde_alone_ms"] > pk[G]["ms_per_step"] else "packets"
+            progress("driver_step_forecast owner")
+            fc["owner"] = owner_forecast(ctx, w, args, dev, n_total, out["driver_step"]["ms_per_pde_step"])
             out["driver_step_forecast"] = fc
     if args.ode23_steps > 0 and args.mode == "blend" and world == 1:
         # (single rank: a sharded ode23 needs the error norm's allreduce, PacketEnsemble(shard=...))

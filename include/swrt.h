@@ -360,6 +360,23 @@ int swrt_ode23_run_hooked(swrt_ctx* ctx, double t0, double tfinal, double tmax, 
  * it computes its own.  Same bits either way; one call's arming is consumed
  * by that call. */
 int swrt_ode23_chain_next(swrt_ctx* ctx, int slot_a, int slot_b);
+/* swrt_ode23_run's controller (MATLAB ode23's step-size logic, the library's
+ * own code: swrt_ode23_ctl.cpp) replayed against a scripted error sequence
+ * instead of the device stages — host only, no context, no GPU.  raw[0] is
+ * stage 1's max (max |F1| ./ max(|y|, thr)), raw[1..nraw) the attempts' raw
+ * error maxima in the order the controller consumes them; dev_first: a first
+ * attempt is queued from the device's own step size, as on the tile path.
+ * log_out: per consumed attempt {t, h, tnew, raw} (4 doubles; *nlog_out
+ * counts all of them); ts_out / ts_cap / nts_out as in swrt_ode23_run;
+ * stats9_out: {steps, failed, attempts, first attempts taken, guesses queued,
+ * guesses taken by rule (MaxStep at MaxStep, MaxStep from 5*absh, 5*absh),
+ * consumed guesses whose device gate would have skipped them (always 0)}.
+ * Returns SWRT_ERR_STATE below hmin (as swrt_ode23_run), SWRT_ERR_ARG if the
+ * script runs out.  Replaces nothing in the reference: it pins the library's
+ * controller to swraytracing_amd/integrate.py's (qgsw_raytrace.m:149). */
+int swrt_ode23_replay(double t0, double tfinal, double rtol, double atol, int dev_first, const double* raw,
+                      int64_t nraw, double* log_out, int64_t log_cap, int64_t* nlog_out, double* ts_out,
+                      int64_t ts_cap, int64_t* nts_out, int64_t* stats9_out);
 
 /* ---------------------------------------------------------------------------
  * QG PDE stepper: the snapshots' producer, device-resident
@@ -458,6 +475,29 @@ int swrt_qg_snapshot(swrt_ctx* ctx, int slot, int which, int layer, int64_t ny_p
  * with the speculative step and discards it if the step is rejected.
  * SWRT_ERR_STATE without a pending fused speculative step. */
 int swrt_qg_snapshot_speculative(swrt_ctx* ctx, int slot, int64_t ny_period);
+/* Owner-driver hand-off (qg2layersw_raytrace.m:186-188: the packets read the
+ * top layer only).  In a sharded run one rank steps the PDE and the others
+ * build their snapshots from the top layer's spectral PV it sends them.
+ * swrt_qg_export: layer `layer` of the current (which = 0) or previous (1) qk,
+ * (2kmax+1)*(kmax+1) interleaved complex in the device order (ky fastest:
+ * element (kx, ky) at (kx + kmax)*(kmax + 1) + ky), to dst.  dst_on_device = 1:
+ * a device buffer; the copy runs on the QG stream behind the step that made
+ * qk, after `stream`'s work queued so far (its last read of dst) and before
+ * `stream`'s later work (stream: a hipStream_t of the caller, e.g. the one a
+ * broadcast is queued on; NULL = the context's packet stream).  0: host
+ * memory, returns once copied.  SWRT_ERR_STATE while a speculative step is
+ * pending (swrt_qg_resolve first). */
+int swrt_qg_export(swrt_ctx* ctx, int which, int layer, double* dst, int dst_on_device, void* stream);
+/* grid_U (grid_U.m:1-18: psi = -q/(K_d2 + K^2), u += shear) of a half plane in
+ * swrt_qg_export's order into packet slot `slot`: bit for bit the
+ * swrt_qg_snapshot(slot, which, layer, ny_period) of the context that exported
+ * it, given that context's K_d2, shear and k_scale (2*pi/L for two layers, 1
+ * for one).  src_on_device = 1: read after `stream`'s work queued so far (the
+ * broadcast that filled it) and before `stream`'s later work (its next fill);
+ * 0: host memory.  Runs on the QG stream with swrt_qg_snapshot's renaming: it
+ * never waits for a packet launch that still reads the slot. */
+int swrt_snapshot_qk(swrt_ctx* ctx, int slot, const double* qk, int src_on_device, void* stream, int64_t nx,
+                     double L, double K_d2, double shear, double k_scale, int64_t ny_period);
 /* Exchange two packet field slots (the previous step's "current" snapshot
  * becomes the next step's "previous" one without recomputing it). */
 int swrt_swap_slots(swrt_ctx* ctx, int a, int b);
@@ -495,6 +535,12 @@ int swrt_kernel_time(swrt_ctx* ctx, int reset, double* total_ms, int64_t* launch
  * under load). */
 int swrt_clock_stamp(swrt_ctx* ctx, int which);
 int swrt_clock_ghz(swrt_ctx* ctx, double* ghz_out, double* spread_out);
+/* swrt_clock_ghz's arithmetic on given stamps (host only, no context): stamps
+ * = `waves` start waves then `waves` end waves, each {shader cycles, realtime
+ * ticks, CU id}; realtime_hz the realtime counter's rate (100e6 on gfx950).
+ * SWRT_ERR_STATE when no CU holds both a start and an end wave. */
+int swrt_clock_ghz_stamps(const uint64_t* stamps, int64_t waves, double realtime_hz, double* ghz_out,
+                          double* spread_out);
 
 /* Debug knobs (test infrastructure; no reference counterpart).
  * SWRT_DEBUG_HAZARD_CHECK 0/1: a host-side happens-before checker of the
@@ -539,7 +585,13 @@ int swrt_clock_ghz(swrt_ctx* ctx, double* ghz_out, double* spread_out);
  *   swrt_packets_get, ...) returns SWRT_ERR_STATE; the packet state is lost
  *   until swrt_packets_set.
  * SWRT_DEBUG_ODE23_CHAINED (get only): ode23 calls that took the stage 1 the
- *   previous call queued (swrt_ode23_chain_next). */
+ *   previous call queued (swrt_ode23_chain_next).
+ * SWRT_DEBUG_ODE23_FIRST_TAKEN, SWRT_DEBUG_ODE23_GUESSES_TAKEN (get only):
+ *   swrt_ode23_run calls whose first attempt was the one the device queued
+ *   from its own step size, and attempts taken from a gated guess (queued
+ *   before the previous attempt's error was known), summed over the calls.
+ * SWRT_DEBUG_ODE23_SPLIT_RUNS (get only): swrt_ode23_run calls whose attempts
+ *   ran as two part launches on the two packet streams. */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3
@@ -549,6 +601,9 @@ int swrt_clock_ghz(swrt_ctx* ctx, double* ghz_out, double* spread_out);
 #define SWRT_DEBUG_SHARE_SKEW 8
 #define SWRT_DEBUG_CORRUPT_COUNT 9
 #define SWRT_DEBUG_ODE23_CHAINED 10
+#define SWRT_DEBUG_ODE23_FIRST_TAKEN 11
+#define SWRT_DEBUG_ODE23_GUESSES_TAKEN 12
+#define SWRT_DEBUG_ODE23_SPLIT_RUNS 13
 int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
 int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
 

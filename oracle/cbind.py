@@ -110,3 +110,21 @@ def leapfrog(planes0, planes1, alpha0, dalpha, nx, nyF, dx, bump, x, k, dt, nste
                           x.ctypes.data_as(_P), k.ctypes.data_as(_P), n, dt, nsteps, f, gH,
                           save_every if nfr else 0, _ptr(hx), _ptr(hk))
     return x, k, hx, hk
+
+
+def raytracing_rhs(planes0, planes1, f, Cg, tmax, nx, nyF, dx, bump):
+    """odefun of qgsw_raytrace.m:258-268 (the restatement swrt_oracle.
+    raytracing_rhs) with interpolate_U by oracle_eval (OpenMP): the same
+    operations in the same order, so the same bits — tests check that on a
+    subset before relying on it for large ensembles."""
+    def odefun(t, y):
+        n = y.size // 4
+        e = eval6(planes0, planes1, t / tmax, nx, nyF, dx, bump, y[0:n], y[n:2 * n])
+        k1, k2 = y[2 * n:3 * n], y[3 * n:4 * n]
+        s = np.sqrt(f**2 + Cg**2 * (k1 * k1 + k2 * k2))
+        dx1 = e[0] + (Cg * k1) / s
+        dx2 = e[1] + (Cg * k2) / s
+        dk1 = -(e[2] * k1 + e[4] * k2)
+        dk2 = -(e[3] * k1 + e[5] * k2)
+        return np.concatenate([dx1, dx2, dk1, dk2])
+    return odefun

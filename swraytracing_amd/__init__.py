@@ -9,7 +9,7 @@ from ._lib import Context, SwrtError, load
 from .integrate import (PacketEnsemble, ode23_packets, ode_symplectic, raytrace_sw, raytrace_xka, rsw_background,
                         step_packet_xka)
 from .io import read_field, write_field
-from .qg import QGModel, TwoLayerLoop, qg2layersw_raytrace, qgsw_raytrace
+from .qg import QGModel, ReceiverLoop, TwoLayerLoop, qg2layersw_raytrace, qgsw_raytrace
 from .stored import read_frame, trace_stored
 from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, FourierScheme, RaytracingScheme, SnapshotPairScheme,
                      SpectralScheme, g2k, grid_U, interpolate, interpolate_U, k2g)
@@ -17,7 +17,7 @@ from .scheme import (BUMP_QG, BUMP_SW, DifferenceScheme, FourierScheme, Raytraci
 __all__ = [
     "Context", "SwrtError", "load", "PacketEnsemble", "ode23_packets", "ode_symplectic", "raytrace_sw", "raytrace_xka",
     "rsw_background", "step_packet_xka",
-    "read_field", "write_field", "QGModel", "TwoLayerLoop", "qgsw_raytrace", "qg2layersw_raytrace",
+    "read_field", "write_field", "QGModel", "ReceiverLoop", "TwoLayerLoop", "qgsw_raytrace", "qg2layersw_raytrace",
     "BUMP_QG", "BUMP_SW", "DifferenceScheme", "FourierScheme", "RaytracingScheme", "SnapshotPairScheme",
     "SpectralScheme", "g2k", "grid_U", "interpolate", "interpolate_U", "k2g", "read_frame", "trace_stored",
 ]

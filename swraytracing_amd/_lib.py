@@ -91,6 +91,8 @@ SIGNATURES = {
     "swrt_ode23_run_hooked": (_INT, [_VP, _D, _D, _D, _D, _D, _INT, _D, _D, _D, _P, _I, ctypes.POINTER(_I),
                                      ctypes.POINTER(_I), _HOOK, _VP]),
     "swrt_ode23_chain_next": (_INT, [_VP, _INT, _INT]),
+    "swrt_ode23_replay": (_INT, [_D, _D, _D, _D, _INT, _P, _I, _P, _I, ctypes.POINTER(_I), _P, _I,
+                                 ctypes.POINTER(_I), ctypes.POINTER(_I)]),
     "swrt_qg_init": (_INT, [_VP, ctypes.POINTER(QGParams), _I, _P]),
     "swrt_qg_step": (_INT, [_VP, _D, _I]),
     "swrt_qg_step_speculative": (_INT, [_VP, _D]),
@@ -105,6 +107,8 @@ SIGNATURES = {
     "swrt_qg_grid": (_I, [_VP, ctypes.POINTER(_INT)]),
     "swrt_qg_snapshot": (_INT, [_VP, _INT, _INT, _INT, _I]),
     "swrt_qg_snapshot_speculative": (_INT, [_VP, _INT, _I]),
+    "swrt_qg_export": (_INT, [_VP, _INT, _INT, _VP, _INT, _VP]),
+    "swrt_snapshot_qk": (_INT, [_VP, _INT, _VP, _INT, _VP, _I, _D, _D, _D, _D, _I]),
     "swrt_swap_slots": (_INT, [_VP, _INT, _INT]),
     "swrt_field_div_free": (_INT, [_VP, _INT]),
     "swrt_check_arith": (_INT, [_VP, _I, ctypes.c_uint64, ctypes.POINTER(ctypes.c_int64)]),
@@ -114,6 +118,8 @@ SIGNATURES = {
     "swrt_kernel_time": (_INT, [_VP, _INT, ctypes.POINTER(_D), ctypes.POINTER(_I)]),
     "swrt_clock_stamp": (_INT, [_VP, _INT]),
     "swrt_clock_ghz": (_INT, [_VP, ctypes.POINTER(_D), ctypes.POINTER(_D)]),
+    "swrt_clock_ghz_stamps": (_INT, [ctypes.POINTER(ctypes.c_uint64), _I, _D, ctypes.POINTER(_D),
+                                     ctypes.POINTER(_D)]),
     "swrt_debug_set": (_INT, [_VP, _INT, _I]),
     "swrt_debug_get": (_INT, [_VP, _INT, ctypes.POINTER(_I)]),
 }
@@ -128,6 +134,9 @@ DEBUG_QG_UPDATE_COLS = 7
 DEBUG_SHARE_SKEW = 8
 DEBUG_CORRUPT_COUNT = 9
 DEBUG_ODE23_CHAINED = 10
+DEBUG_ODE23_FIRST_TAKEN = 11
+DEBUG_ODE23_GUESSES_TAKEN = 12
+DEBUG_ODE23_SPLIT_RUNS = 13
 
 _lib = None
 
@@ -541,6 +550,41 @@ class Context:
         when it ends; the next call takes it only if it computes the same."""
         self._chk(self._L.swrt_ode23_chain_next(self._h, int(slot_a), int(slot_b)), "swrt_ode23_chain_next")
 
+    # ---- owner-driver hand-off (swrt_qg_export / swrt_snapshot_qk) -----------
+    def qg_export(self, dst, which=0, layer=0, stream=None):
+        """Layer `layer` of the current (0) / previous (1) qk in the device's
+        half-plane order (ky fastest) into `dst`: a float64 numpy array of
+        2*(2kmax+1)*(kmax+1) values (host copy, returns when done), or an
+        int device address (queued; ordered after and before the work of the
+        hipStream_t `stream`, default the packet stream)."""
+        if isinstance(dst, np.ndarray):
+            if dst.dtype != np.float64 or not dst.flags["C_CONTIGUOUS"] or dst.size != 2 * self._qg_nhalf():
+                raise ValueError("dst must be a contiguous float64 array of 2*(2kmax+1)*(kmax+1) values")
+            self._chk(self._L.swrt_qg_export(self._h, int(which), int(layer), dst.ctypes.data_as(_VP), 0, None),
+                      "swrt_qg_export")
+        else:
+            self._chk(self._L.swrt_qg_export(self._h, int(which), int(layer), _VP(int(dst)), 1,
+                                             None if stream is None else _VP(int(stream))), "swrt_qg_export")
+
+    def _qg_nhalf(self):
+        kmax = self._qg_nx // 2 - 1
+        return (2 * kmax + 1) * (kmax + 1)
+
+    def snapshot_qk(self, slot, qk, nx, L, K_d2, shear=0.0, k_scale=1.0, ny_period=0, stream=None):
+        """grid_U of a half plane in qg_export's order into `slot`
+        (swrt_snapshot_qk): `qk` a float64 numpy array (host) or an int device
+        address (read after / before `stream`'s work)."""
+        kmax = int(nx) // 2 - 1
+        nh = (2 * kmax + 1) * (kmax + 1)
+        if isinstance(qk, np.ndarray):
+            if qk.dtype != np.float64 or not qk.flags["C_CONTIGUOUS"] or qk.size != 2 * nh:
+                raise ValueError("qk must be a contiguous float64 array of 2*(2kmax+1)*(kmax+1) values")
+            src, on_dev, st = qk.ctypes.data_as(_VP), 0, None
+        else:
+            src, on_dev, st = _VP(int(qk)), 1, None if stream is None else _VP(int(stream))
+        self._chk(self._L.swrt_snapshot_qk(self._h, int(slot), src, on_dev, st, int(nx), float(L), float(K_d2),
+                                           float(shear), float(k_scale), int(ny_period)), "swrt_snapshot_qk")
+
     # ---- QG PDE stepper (swrt_qg_*) ---------------------------------------
     def qg_init(self, params: QGParams, nx, qk):
         """qk: (2kmax+1, kmax+1) complex, or (2kmax+1, kmax+1, nlayers)."""
@@ -663,6 +707,45 @@ class Context:
         v = _I()
         self._chk(self._L.swrt_debug_get(self._h, int(key), ctypes.byref(v)), "swrt_debug_get")
         return v.value
+
+
+def ode23_replay(t0, tfinal, raw, rtol=1e-3, atol=1e-6, dev_first=True, ts_cap=100_000):
+    """swrt_ode23_replay: the library's ode23 controller (swrt_ode23_ctl.cpp)
+    over a scripted raw-error sequence, on the host (no GPU, no context).
+    raw[0] = stage 1's max, then one per attempt the controller consumes.
+    Returns (status, attempts (n, 4) [t, h, tnew, raw], accepted times, stats
+    dict); status is SWRT_OK, "below hmin" or "script exhausted"."""
+    L = load()
+    raw = np.ascontiguousarray(raw, dtype=np.float64)
+    cap = max(1, raw.size)
+    log = np.empty(4 * cap)
+    ts = np.empty(ts_cap)
+    nlog, nts = _I(), _I()
+    st = (_I * 9)()
+    rc = L.swrt_ode23_replay(float(t0), float(tfinal), float(rtol), float(atol), int(bool(dev_first)), _p(raw),
+                             raw.size, _p(log), cap, ctypes.byref(nlog), _p(ts), ts_cap, ctypes.byref(nts), st)
+    status = {SWRT_OK: SWRT_OK, 3: "below hmin", 1: "script exhausted"}.get(rc, rc)
+    keys = ("steps", "failed", "attempts", "first_taken", "guesses", "taken_maxstep", "taken_ramp_maxstep",
+            "taken_ramp_5x", "gate_violations")
+    return (status, log[:4 * min(nlog.value, cap)].reshape(-1, 4).copy(), ts[:min(nts.value, ts_cap)].copy(),
+            {k: int(v) for k, v in zip(keys, st)})
+
+
+def clock_ghz_stamps(stamps, realtime_hz=100e6):
+    """swrt_clock_ghz_stamps: (GHz, spread) from probe stamps shaped (2, waves,
+    3) = start/end x wave x {cycles, realtime ticks, CU id}; raises SwrtError
+    when no CU holds both a start and an end wave (host only)."""
+    L = load()
+    a = np.ascontiguousarray(stamps, dtype=np.uint64)
+    if a.ndim != 3 or a.shape[0] != 2 or a.shape[2] != 3:
+        raise ValueError("stamps must be (2, waves, 3)")
+    g, s = _D(), _D()
+    rc = L.swrt_clock_ghz_stamps(a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), a.shape[1], float(realtime_hz),
+                                 ctypes.byref(g), ctypes.byref(s))
+    if rc != SWRT_OK:
+        raise SwrtError(f"swrt_clock_ghz_stamps: {ERRORS.get(rc, rc)}: no CU with both a start and an end stamp"
+                        if rc == 3 else f"swrt_clock_ghz_stamps: {ERRORS.get(rc, rc)}")
+    return g.value, s.value
 
 
 def exported_symbols():

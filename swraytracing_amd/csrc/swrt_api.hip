@@ -347,6 +347,18 @@ struct swrt_ctx {
   int* dev_err = nullptr;
   int* dev_err_d = nullptr;
   bool packets_lost = false;  // a failed binning left the packet state undefined (until swrt_packets_set)
+  bool in_hook = false;       // an ode23 hook is running (swrt_ode23_run_hooked): packet calls are refused
+  // swrt_snapshot_qk (snapshots from a half plane another context exported):
+  // transform scratch, the staged host half plane, the cross-stream events
+  double2* xq_Z = nullptr;
+  double2* xq_T = nullptr;
+  double2* xq_fk = nullptr;
+  int64_t xq_nx = 0;
+  bool xq_init = false;   // slot writes may come from the QG stream (slot_events)
+  hipEvent_t xev[2] = {nullptr, nullptr};
+  O23Stats o23_last;          // the last swrt_ode23_run's controller counts
+  int64_t o23_first_taken = 0, o23_guesses_taken = 0;  // ... summed over runs (SWRT_DEBUG_ODE23_*)
+  int64_t o23_split_runs = 0;  // runs whose attempts ran as two part launches (SWRT_DEBUG_ODE23_SPLIT_RUNS)
   // shader-clock probe (swrt_clock_stamp): 2 stamps x kClockWaves waves x
   // {s_memtime, s_memrealtime, XCC id}
   unsigned long long* clk = nullptr;
@@ -378,17 +390,20 @@ struct OnQGStream {
 // the packet launches (swrt_qg_init on a separate stream); without one a
 // packet launch carries no event at all (each costs ~5 us of idle GPU at the
 // launch boundary, tools/gap_probe.py).
-bool slot_events(const swrt_ctx* c) { return c->qg_sep && c->qg.init; }
+bool slot_events(const swrt_ctx* c) { return c->qg_sep && (c->qg.init || c->xq_init); }
 
 // The packet stream waits for the QG stream's pending snapshot writes before
 // the first kernel that reads a slot.  Deferred (swrt_advance / _intervals):
 // the wait is placed by slot_writes_wait() just before the first packet
 // launch, so a re-binning at the start of the call (packet buffers only)
 // runs while the PDE chain is still producing the snapshot.
-void slot_writes_wait(swrt_ctx* c) {
+constexpr unsigned kAllSlots = (1u << SWRT_MAX_SLOTS) - 1;
+constexpr unsigned kSlots01 = 3u;  // the ode23 calls read slots 0 and 1 only
+
+void slot_writes_wait(swrt_ctx* c, unsigned mask = kAllSlots) {
   if (!c->qg_sep) return;
-  for (Slot& s : c->slot)
-    if (s.wpend) {
+  for (int i = 0; i < SWRT_MAX_SLOTS; ++i)
+    if (Slot& s = c->slot[i]; (mask >> i & 1u) && s.wpend) {
       (void)hipStreamWaitEvent(c->stream, s.wev, 0);
       s.wpend = false;
     }
@@ -396,9 +411,12 @@ void slot_writes_wait(swrt_ctx* c) {
 
 struct SlotUse {
   swrt_ctx* c;
-  explicit SlotUse(swrt_ctx* c_, bool defer_writes = false) : c(c_) {
+  // wait_mask: the slots whose pending QG-stream writes this call's reads wait
+  // for (the ode23 calls read slots 0 and 1 only: a hook's snapshot into slot
+  // 2 keeps running beside their attempts)
+  explicit SlotUse(swrt_ctx* c_, bool defer_writes = false, unsigned wait_mask = kAllSlots) : c(c_) {
     c->tail_ev = nullptr;
-    if (!defer_writes) slot_writes_wait(c);
+    if (!defer_writes) slot_writes_wait(c, wait_mask);
   }
   ~SlotUse() {
     if (!slot_events(c)) return;
@@ -440,7 +458,12 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
   } while (0)
 // GUARD_BEGIN drops a queued ode23 chain (the packets may change); the calls
 // that never touch the packets (QG, clock) use GUARD_BEGIN_KEEP_CHAIN.
+// A call that may touch the packets is refused inside an ode23 hook
+// (swrt_ode23_run_hooked): it would race the interval's attempts in flight.
+#define HOOK_REFUSE \
+  if (c->in_hook) return fail(c, SWRT_ERR_STATE, "this call may touch the packets: not allowed inside an ode23 hook");
 #define GUARD_BEGIN_KEEP_SPLIT \
+  HOOK_REFUSE                  \
   try {                        \
     c->o_chain.queued = false;
 #define GUARD_BEGIN_KEEP_CHAIN    \
@@ -451,6 +474,7 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
       hz_api(c);                  \
     }
 #define GUARD_BEGIN            \
+  HOOK_REFUSE                  \
   GUARD_BEGIN_KEEP_CHAIN       \
   c->o_chain.queued = false;
 #define GUARD_END(ctx)                                                \
@@ -522,6 +546,14 @@ int dev_err_check(swrt_ctx* c) {
               "packet binning corrupted: the tile counts do not sum to the packets (device check in "
               "bin_scan_kernel); no packet kernel ran over the bad ranges, but the packet state is lost — "
               "swrt_packets_set again");
+}
+
+// The packet state stays refused after a corrupted binning until
+// swrt_packets_set (every entry point that reads the packets checks).
+int lost_check(swrt_ctx* c) {
+  if (c->packets_lost)
+    return fail(c, SWRT_ERR_STATE, "the packet state was lost to a corrupted binning (swrt_packets_set again)");
+  return SWRT_OK;
 }
 
 // Wait for the extra packet streams (host side).
@@ -1418,6 +1450,10 @@ void swrt_destroy(swrt_ctx* c) {
   if (c->qg.ev) (void)hipEventDestroy(c->qg.ev);
   if (c->qg.ev_b) (void)hipEventDestroy(c->qg.ev_b);
   if (c->o_order) (void)hipFree(c->o_order);
+  for (void* p : {(void*)c->xq_Z, (void*)c->xq_T, (void*)c->xq_fk})
+    if (p) (void)hipFree(p);
+  for (hipEvent_t e : c->xev)
+    if (e) (void)hipEventDestroy(e);
   for (void* p : {(void*)c->o_spx, (void*)c->o_spk, (void*)c->o_spF})
     if (p) (void)hipFree(p);
   for (void* p : {(void*)c->oF[0], (void*)c->oF[1], (void*)c->oF[2], (void*)c->oF[3], (void*)c->o_ynx,
@@ -1856,6 +1892,7 @@ int swrt_packets_get(swrt_ctx* c, double* x, double* k) {
 int swrt_packets_get_device(swrt_ctx* c, double* x_dev, double* k_dev, int64_t ld) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
+  HIPCHK_RC(lost_check(c));  // (perm would be stale: never unpermute a lost state)
   if (c->n == 0) return SWRT_OK;
   if (!x_dev || !k_dev) return fail(c, SWRT_ERR_ARG, "NULL buffer");
   if (ld < c->n) return fail(c, SWRT_ERR_ARG, "leading dimension below the packet count");
@@ -2594,6 +2631,9 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_CORRUPT_COUNT: *value_out = c->debug_corrupt_count; return SWRT_OK;
     case SWRT_DEBUG_QG_UPDATE_COLS: *value_out = c->qg_update_cols; return SWRT_OK;
     case SWRT_DEBUG_ODE23_CHAINED: *value_out = c->o_chain.taken; return SWRT_OK;
+    case SWRT_DEBUG_ODE23_FIRST_TAKEN: *value_out = c->o23_first_taken; return SWRT_OK;
+    case SWRT_DEBUG_ODE23_GUESSES_TAKEN: *value_out = c->o23_guesses_taken; return SWRT_OK;
+    case SWRT_DEBUG_ODE23_SPLIT_RUNS: *value_out = c->o23_split_runs; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
 }
@@ -2667,36 +2707,14 @@ int swrt_clock_ghz(swrt_ctx* c, double* ghz_out, double* spread_out) {
   if (!c->clk) return fail(c, SWRT_ERR_STATE, "no clock stamps (swrt_clock_stamp 0 and 1 first)");
   GUARD_BEGIN_KEEP_CHAIN
   HIPCHK(c, hipSetDevice(c->device));
-  std::vector<unsigned long long> h(2 * kClockWaves * 3);
-  HIPCHK(c, hipMemcpyAsync(h.data(), c->clk, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost,
-                           c->stream));
+  std::vector<uint64_t> h(2 * kClockWaves * 3);
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->clk, sizeof(uint64_t) * h.size(), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   hz_synced(c);
-  // per CU: its first start stamp and its last end stamp
-  std::map<unsigned long long, std::pair<int, int>> cu;  // id -> (start wave, end wave)
-  const unsigned long long* s = h.data();
-  const unsigned long long* e = h.data() + kClockWaves * 3;
-  for (int i = 0; i < kClockWaves; ++i) {
-    auto& p = cu.emplace(s[3 * i + 2], std::make_pair(-1, -1)).first->second;
-    if (p.first < 0 || s[3 * i + 1] < s[3 * p.first + 1]) p.first = i;
-  }
-  for (int j = 0; j < kClockWaves; ++j) {
-    auto it = cu.find(e[3 * j + 2]);
-    if (it != cu.end() && (it->second.second < 0 || e[3 * j + 1] > e[3 * it->second.second + 1])) it->second.second = j;
-  }
-  std::vector<double> ghz;
-  for (const auto& kv : cu) {
-    const int i = kv.second.first, j = kv.second.second;
-    if (i < 0 || j < 0 || e[3 * j + 1] <= s[3 * i + 1] || e[3 * j] <= s[3 * i]) continue;
-    const double sec = (double)(e[3 * j + 1] - s[3 * i + 1]) / kRealTimeHz;
-    ghz.push_back((double)(e[3 * j] - s[3 * i]) / sec / 1e9);
-  }
-  if (ghz.empty()) return fail(c, SWRT_ERR_STATE, "no CU with both a start and an end stamp");
-  std::sort(ghz.begin(), ghz.end());
-  const double med = ghz[ghz.size() / 2];
-  *ghz_out = med;
-  // spread of the per-CU clocks: (p90 - p10) / median over the CUs paired
-  if (spread_out) *spread_out = (ghz[(ghz.size() * 9) / 10] - ghz[ghz.size() / 10]) / med;
+  // the pairing and median (swrt_clock.cpp, host-only, tested on synthetic stamps)
+  const int rc = swrt_clock_ghz_stamps(h.data(), kClockWaves, kRealTimeHz, ghz_out, spread_out);
+  if (rc == SWRT_ERR_STATE) return fail(c, rc, "no CU with both a start and an end stamp");
+  if (rc) return fail(c, rc, "swrt_clock_ghz_stamps");
   return SWRT_OK;
   GUARD_END(c)
 }
@@ -3244,6 +3262,41 @@ int swrt_qg_get_q(swrt_ctx* c, double* q_out) {
 }
 
 namespace {
+// A snapshot written on the QG stream (c->stream = the QG stream, OnQGStream):
+// a slot buffer still read by a queued packet launch is renamed (an idle
+// spare takes its place), else the write waits for the slot's last reader.
+int qg_slot_acquire(swrt_ctx* c, int slot) {
+  if (!c->qg_sep) return SWRT_OK;
+  if (c->slot[slot].upend && event_pending(c->slot[slot].uref)) {
+    int pick = -1;
+    for (size_t i = 0; i < c->spares.size() && pick < 0; ++i)
+      if (!c->spares[i].upend || !event_pending(c->spares[i].uref)) pick = (int)i;
+    if (pick < 0 && c->spares.size() < kMaxSpares) {
+      Slot sp;
+      HIPCHK(c, hipEventCreateWithFlags(&sp.uev, hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&sp.wev, hipEventDisableTiming));
+      c->spares.push_back(sp);
+      pick = (int)c->spares.size() - 1;
+    }
+    if (pick >= 0) std::swap(c->slot[slot], c->spares[pick]);  // else wait for the slot's own reader
+  }
+  if (c->slot[slot].upend) HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot[slot].uref, 0));
+  return SWRT_OK;
+}
+
+// ... and done: a new write generation; the packet stream's next reader waits
+// for the write's event (slot_writes_wait)
+int qg_slot_written(swrt_ctx* c, int slot) {
+  Slot& s = c->slot[slot];
+  s.set = true;
+  s.wgen = ++c->slot_wgen;
+  if (c->qg_sep) {
+    HIPCHK(c, hipEventRecord(s.wev, c->stream));
+    s.wpend = true;
+  }
+  return SWRT_OK;
+}
+
 // swrt_qg_snapshot, or (spec) the same snapshot of the pending speculative
 // step's qk: its post-step transforms (swrt_qg_step_speculative) hold layer
 // 0's grid_U planes, which a snapshot after accepting the step would pack
@@ -3268,23 +3321,7 @@ int qg_snapshot_impl(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   if (ny_period == 0) ny_period = nx;
   if (ny_period % nx) return fail(c, SWRT_ERR_ARG, "ny_period must be a multiple of nx");
   HIPCHK(c, hipSetDevice(c->device));
-  if (c->qg_sep) {
-    // rename a buffer still read by a queued packet launch, else wait for its last use
-    if (c->slot[slot].upend && event_pending(c->slot[slot].uref)) {
-      int pick = -1;
-      for (size_t i = 0; i < c->spares.size() && pick < 0; ++i)
-        if (!c->spares[i].upend || !event_pending(c->spares[i].uref)) pick = (int)i;
-      if (pick < 0 && c->spares.size() < kMaxSpares) {
-        Slot sp;
-        HIPCHK(c, hipEventCreateWithFlags(&sp.uev, hipEventDisableTiming));
-        HIPCHK(c, hipEventCreateWithFlags(&sp.wev, hipEventDisableTiming));
-        c->spares.push_back(sp);
-        pick = (int)c->spares.size() - 1;
-      }
-      if (pick >= 0) std::swap(c->slot[slot], c->spares[pick]);  // else wait for the slot's own reader
-    }
-    if (c->slot[slot].upend) HIPCHK(c, hipStreamWaitEvent(c->stream, c->slot[slot].uref, 0));
-  }
+  if ((rc = qg_slot_acquire(c, slot))) return rc;
   if ((rc = ensure_slot(c, slot, nx))) return rc;
   if ((rc = ensure_twiddles(c, (int)nx))) return rc;
   Slot& s = c->slot[slot];
@@ -3306,13 +3343,7 @@ int qg_snapshot_impl(swrt_ctx* c, int slot, int which, int layer, int64_t ny_per
   }
   s.L = q.g.dx * (double)nx;
   s.ny_period = ny_period;
-  s.set = true;
-  s.wgen = ++c->slot_wgen;
-  if (c->qg_sep) {
-    HIPCHK(c, hipEventRecord(s.wev, c->stream));
-    s.wpend = true;
-  }
-  return SWRT_OK;
+  return qg_slot_written(c, slot);
 }
 }  // namespace
 
@@ -3327,6 +3358,111 @@ int swrt_qg_snapshot_speculative(swrt_ctx* c, int slot, int64_t ny_period) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN_KEEP_CHAIN
   return qg_snapshot_impl(c, slot, 0, 0, ny_period, true);
+  GUARD_END(c)
+}
+
+// ---------------------------------------------------------------------------
+// Owner-driver hand-off: one rank steps the PDE, the others build their
+// snapshots from the top layer's spectral PV it sends (qg2layersw_raytrace.m
+// :186-188 reads layer 1 only)
+// ---------------------------------------------------------------------------
+namespace {
+// order `from`'s work so far before `to`'s later work (no-op on one stream)
+int stream_order(swrt_ctx* c, hipStream_t from, hipStream_t to, int ev) {
+  if (from == to) return SWRT_OK;
+  if (!c->xev[ev]) HIPCHK(c, hipEventCreateWithFlags(&c->xev[ev], hipEventDisableTiming));
+  HIPCHK(c, hipEventRecord(c->xev[ev], from));
+  HIPCHK(c, hipStreamWaitEvent(to, c->xev[ev], 0));
+  return SWRT_OK;
+}
+}  // namespace
+
+int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_on_device, void* stream) {
+  if (!c) return SWRT_ERR_ARG;
+  GUARD_BEGIN_KEEP_CHAIN
+  OnQGStream on_qg(c);
+  QGState& q = c->qg;
+  if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
+  if (q.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
+  if (!dst) return fail(c, SWRT_ERR_ARG, "dst is NULL");
+  if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (current) or 1 (previous)");
+  if (which == 1 && !q.has_prev) return fail(c, SWRT_ERR_STATE, "no previous qk before the first step");
+  if (layer < 0 || layer >= q.g.nl) return fail(c, SWRT_ERR_ARG, "layer out of range");
+  HIPCHK(c, hipSetDevice(c->device));
+  const double2* src = (which == 0 ? q.qk : q.qk_prev) + layer * q.nhalf;
+  const size_t bytes = sizeof(double2) * q.nhalf;
+  if (dst_on_device) {
+    const hipStream_t ext = stream ? (hipStream_t)stream : on_qg.saved;
+    HIPCHK_RC(stream_order(c, ext, c->stream, 0));  // the caller's last read of dst
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK_RC(stream_order(c, c->stream, ext, 1));  // the caller's next use of dst
+  } else {
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
+  return SWRT_OK;
+  GUARD_END(c)
+}
+
+int swrt_snapshot_qk(swrt_ctx* c, int slot, const double* qk, int src_on_device, void* stream, int64_t nx,
+                     double L, double K_d2, double shear, double k_scale, int64_t ny_period) {
+  int rc = check_slot_args(c, slot, nx);
+  if (rc) return rc;
+  GUARD_BEGIN_KEEP_CHAIN
+  if (!qk) return fail(c, SWRT_ERR_ARG, "qk is NULL");
+  if (!is_pow2(nx)) return fail(c, SWRT_ERR_ARG, "nx must be a power of two for the GPU FFT");
+  if (!(L > 0)) return fail(c, SWRT_ERR_ARG, "L must be > 0");
+  if (ny_period == 0) ny_period = nx;
+  if (ny_period % nx) return fail(c, SWRT_ERR_ARG, "ny_period must be a multiple of nx");
+  if (c->qg.init && c->qg.g.n != nx) return fail(c, SWRT_ERR_ARG, "nx differs from the QG state's");
+  HIPCHK(c, hipSetDevice(c->device));
+  const hipStream_t pk = c->stream;  // the packet stream
+  if (!c->xq_init && !c->qg.init && c->qg_sep) {
+    // from here on packet launches mark their slot use; everything queued on
+    // the packet stream so far is marked by one record per slot (as swrt_qg_init)
+    for (Slot& sl : c->slot)
+      if (sl.nodes && hipEventRecord(sl.uev, pk) == hipSuccess) {
+        sl.uref = sl.uev;
+        sl.upend = true;
+      }
+  }
+  c->xq_init = true;
+  OnQGStream on_qg(c);
+  const int n = (int)nx, kmax = n / 2 - 1;
+  const int64_t nn = nx * nx, nhalf = (int64_t)(2 * kmax + 1) * (kmax + 1);
+  if (c->xq_nx != nx) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // a queued snapshot may still use them
+    for (double2** p : {&c->xq_Z, &c->xq_T, &c->xq_fk}) {
+      if (*p) (void)hipFree(*p);
+      *p = nullptr;
+    }
+    c->xq_nx = 0;
+    HIPCHK(c, hipMalloc(&c->xq_Z, sizeof(double2) * 3 * nn));
+    HIPCHK(c, hipMalloc(&c->xq_T, sizeof(double2) * 3 * nn));
+    HIPCHK(c, hipMalloc(&c->xq_fk, sizeof(double2) * nhalf));
+    c->xq_nx = nx;
+  }
+  if ((rc = ensure_twiddles(c, n))) return rc;
+  if ((rc = qg_slot_acquire(c, slot))) return rc;
+  if ((rc = ensure_slot(c, slot, nx))) return rc;
+  const hipStream_t ext = stream ? (hipStream_t)stream : pk;
+  const double2* fk = (const double2*)qk;
+  if (src_on_device) {
+    HIPCHK_RC(stream_order(c, ext, c->stream, 0));  // the caller's fill of qk (e.g. a broadcast)
+  } else {
+    HIPCHK(c, hipMemcpyAsync(c->xq_fk, qk, sizeof(double2) * nhalf, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // the caller's host buffer is free on return
+    fk = c->xq_fk;
+  }
+  // grid_U of the half plane in the QG state's order (ky fastest): the
+  // unfused path of swrt_qg_snapshot, bit for bit
+  if ((rc = fields_from_halfplane(c, slot, fk, n, 1, K_d2, k_scale, shear, 0, c->xq_Z, c->xq_T, n / 2, 1)))
+    return rc;
+  if (src_on_device) HIPCHK_RC(stream_order(c, c->stream, ext, 1));  // qk read: the caller may refill it
+  Slot& s = c->slot[slot];
+  s.L = L;
+  s.ny_period = ny_period;
+  return qg_slot_written(c, slot);
   GUARD_END(c)
 }
 
@@ -3574,7 +3710,8 @@ int swrt_ode23_f1(swrt_ctx* c, double t, double tmax, double f, double Cg, int n
                   double* rh_raw_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
-  SlotUse slot_use(c);
+  HIPCHK_RC(lost_check(c));
+  SlotUse slot_use(c, false, kSlots01);
   int rc;
   if ((rc = ode23_f1_queue(c, t, tmax, f, Cg, nslots, thr, bump))) return rc;
   return read_max(c, rh_raw_out);
@@ -3585,7 +3722,8 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
                        int nslots, double thr, double bump, double* err_raw_out) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN
-  SlotUse slot_use(c);
+  HIPCHK_RC(lost_check(c));
+  SlotUse slot_use(c, false, kSlots01);
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   Ode23Args a;
@@ -3601,6 +3739,8 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
 
 int swrt_ode23_accept(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
+  if (c->in_hook) return fail(c, SWRT_ERR_STATE, "this call may touch the packets: not allowed inside an ode23 hook");
+  HIPCHK_RC(lost_check(c));
   c->o_chain.queued = false;
   if (!c->o_ynx) return fail(c, SWRT_ERR_STATE, "no ode23 step attempted");
   std::swap(c->dx, c->o_ynx);
@@ -3610,20 +3750,6 @@ int swrt_ode23_accept(swrt_ctx* c) {
   c->cells_sorted = false;
   return SWRT_OK;
 }
-
-// MATLAB ode23's step-size controller (the restatement of
-// swraytracing_amd/integrate.py ode23_packets, operation for operation:
-// std::pow is the C pow() Python's float ** calls, min/max keep Python's
-// tie order) around the device stages, without a host interpreter between
-// attempts.  Single-rank: the sharded form needs the error norm's allreduce
-// and stays in Python.
-namespace {
-double np_spacing(double t) {  // numpy.spacing
-  const double a = std::fabs(t);
-  const double d = std::nextafter(a, INFINITY) - a;
-  return std::signbit(t) ? -d : d;
-}
-}  // namespace
 
 namespace {
 double o23_alpha(double t, double tmax) { return tmax != 0.0 ? t / tmax : 0.0; }  // the kernels' alpha_of
@@ -3642,7 +3768,7 @@ int ode23_chain_queue(swrt_ctx* c, double tmax, double f, double Cg, int nslots,
   const bool want = ch.want;
   ch.want = false;
   ch.queued = false;
-  if (!want || nslots != 2 || ch.sa < 0 || ch.sb < 0 || ch.sa == ch.sb) return SWRT_OK;
+  if (!want || nslots != 2 || ch.sa < 0 || ch.sb < 0 || ch.sa == ch.sb || c->packets_lost) return SWRT_OK;
   if (!c->slot[ch.sa].set || !c->slot[ch.sb].set || c->slot[ch.sa].nx != c->slot[ch.sb].nx) return SWRT_OK;
   slot_writes_wait(c);  // e.g. the hook's snapshot into slot sb on the QG stream
   Slot saved[SWRT_MAX_SLOTS];
@@ -3701,90 +3827,24 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
                                stats3_out, nullptr, nullptr);
 }
 
-int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
-                          double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
-                          int64_t* stats3_out, void (*hook)(void*), void* hook_user) {
-  if (!c) return SWRT_ERR_ARG;
-  if (!ts_out || ts_cap < 1 || !nts_out) return fail(c, SWRT_ERR_ARG, "ts_out / ts_cap / nts_out");
-  GUARD_BEGIN_KEEP_CHAIN
-  SlotUse slot_use(c);
-  const double tdir = std::copysign(1.0, tfinal - t0);
-  const double pw = 1.0 / 3.0;
-  rtol = std::max(rtol, 100 * 2.220446049250313e-16);
-  const double thr = atol / rtol;
-  const double htspan = std::fabs(tfinal - t0);
-  const double hmax = 0.1 * htspan;
-  const double c0 = 0.8 * std::pow(rtol, pw);
-  double t = t0;
-  double raw = 0.0;
-  int rc;
-  // stage 1 (with this call's re-binning and in-tile sort), its max in slot
-  // sl_f1: queued by the previous call when it was chained to this one
-  int sl_f1;
-  if (ode23_chain_take(c, t0, tmax, f, Cg, nslots, thr, bump)) {
-    sl_f1 = c->o_chain.dmax_slot;
-    ++c->o_chain.taken;
-  } else {
-    if ((rc = ode23_f1_queue(c, t, tmax, f, Cg, nslots, thr, bump))) return rc;
-    sl_f1 = c->o_dmax_cur;
-    c->o_dmax_cur = (sl_f1 + 1) % 3;
-  }
-  Ode23Args base;
-  if ((rc = ode23_prepare(c, nslots, base, tmax, f, Cg, thr, bump))) return rc;
-  // The first attempt's step size on the device (ode23_first_step_kernel,
-  // the host's own operations), so the attempt is queued behind stage 1
-  // without a host round trip; the host then computes the same and checks
-  // it against the kernel's mapped copy (the tile path only: its attempt
-  // kernel reads device coefficients).
-  const int ntx_ = (int)((c->slot[0].nx + kTile - 1) / kTile);
-  const bool dev_first = use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx_ * ntx_;
-  // Two part launches per attempt when the binning allows (ode23_split_ok):
-  // part p keeps max slots o_dmax[3p + sl] and its own events; the error max
-  // is the max over both parts' workgroups.  (Split implies dev_first.)
-  const bool split = ode23_split_ok(c);
-  const int P = split ? 2 : 1;
-  if (dev_first) {
-    // (part 1's slots start at zero, cleared here; each launch then clears its next one)
-    hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax, htspan,
-                       16 * np_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3,
-                       split ? 3 : 0);
-    HIPCHK(c, hipGetLastError());
-  } else {
-    HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl_f1, c->o_dmax + sl_f1, sizeof(unsigned long long),
-                             hipMemcpyDeviceToHost, c->stream));
-  }
-  HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
-  // three state sets (x, k, F1/F4): an attempt reads set `from` and writes
-  // ynew and F4 into set `to`; the accepted one becomes the current set
-  struct Set {
-    double *x, *k, *F;
-  } S[3] = {{c->dx, c->dk, c->oF[0]}, {c->o_ynx, c->o_ynk, c->oF[3]}, {c->o_spx, c->o_spk, c->o_spF}};
-  int cur = 0;
-  auto commit = [&]() {  // the current set becomes the packets (and F1), the others the spares
-    const int o1 = (cur + 1) % 3, o2 = (cur + 2) % 3;
-    c->dx = S[cur].x; c->dk = S[cur].k; c->oF[0] = S[cur].F;
-    c->o_ynx = S[o1].x; c->o_ynk = S[o1].k; c->oF[3] = S[o1].F;
-    c->o_spx = S[o2].x; c->o_spk = S[o2].k; c->o_spF = S[o2].F;
-    c->keys_fresh = false;
-    c->cells_sorted = false;
-  };
-  if (split) {
-    HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->fork_ev, 0));
-    if (c->hz.on) {
-      c->hz.record(c->fork_ev, 0);
-      c->hz.wait(1, c->fork_ev);
-    }
-    c->b_pending = 1;  // joined into the packet stream before anything else reads the packets (join_b)
-  }
-  unsigned wg[2][3] = {};  // workgroups of each part's launch in each slot (0: the max was copied)
-  struct Spec {  // a guessed attempt already queued (see below)
-    bool on, ran;
-    int slot, from, to;
-    double t, h, tnew;
-  } spec{false, false, 0, 0, 0, 0.0, 0.0, 0.0};
-  auto queue = [&](int from, int to, double ta, double ha, double tnewa, int gate_slot, double gscale,
-                   double glimit, int* slot, const double* coef = nullptr) -> int {
+namespace {
+// swrt_ode23_run's stages for the controller (ode23_control, swrt_ode23_ctl.cpp):
+// each attempt one tile launch — two part launches when the binning allows
+// (ode23_split_ok), part 1 on the extra packet stream, part p keeping max
+// slots o_dmax[3p + sl] and its own events — its maxima read from host-mapped
+// memory after the launch's event; three state sets (x, k, F1/F4): an attempt
+// reads set `from` and writes ynew and F4 into set `to`.
+class DeviceExec final : public O23Exec {
+ public:
+  DeviceExec(swrt_ctx* c_, const Ode23Args& base_, bool split_, bool dev_first_, int sl_f1_, void (*hook_)(void*),
+             void* hook_user_)
+      : c(c_), base(base_), split(split_), P(split_ ? 2 : 1), dev_first(dev_first_), sl_f1(sl_f1_), hook(hook_),
+        hook_user(hook_user_),
+        S{{c_->dx, c_->dk, c_->oF[0]}, {c_->o_ynx, c_->o_ynk, c_->oF[3]}, {c_->o_spx, c_->o_spk, c_->o_spF}} {}
+
+  // queue an attempt (coef: its coefficients from device memory, the first attempt)
+  int launch(int from, int to, double ta, double ha, double tnewa, int gate_slot, double gscale, double glimit,
+             int* slot, const double* coef) {
     Ode23Args a = base;
     a.coef = coef;
     a.yx = S[from].x;
@@ -3804,21 +3864,54 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
       // whole max passes, so does every part (err = absh * max is monotone)
       a.gate = gate_slot >= 0 ? c->o_dmax + 3 * p + gate_slot : nullptr;
       a.hpart = c->o_hpart_d + (size_t)(3 * p + sl) * kMaxBins;
-      int r;
-      if ((r = ode23_launch<0>(c, a, split ? p : -1, &wg[p][sl]))) return r;
+      HIPCHK_RC((ode23_launch<0>(c, a, split ? p : -1, &wg[p][sl])));
       const hipStream_t st = p == 0 ? c->stream : c->sx[0];
       if (wg[p][sl] == 0)  // the per-packet stage kernels (never split): copy the max
-        HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl, c->o_dmax + sl, sizeof(unsigned long long),
-                                 hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl, c->o_dmax + sl, sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                                 st));
       HIPCHK(c, hipEventRecord(p == 0 ? c->o_ev[sl] : c->o_evb[sl], st));
     }
     c->o_dmax_cur = (sl + 1) % 3;
     *slot = sl;
     return SWRT_OK;
-  };
+  }
+  // the device's first attempt, from its own step size (before the hook)
+  int queue_first() { return launch(0, 1, 0.0, 0.0, 0.0, -1, 0.0, 0.0, &first_slot, c->o_coef); }
+
+  int stage1(double* raw) override {
+    if (hook) {
+      // the hook may call the library (e.g. the next QG step on the QG stream);
+      // it must not touch the packets (c->in_hook refuses those calls).  Its
+      // calls must not join the extra stream's attempt parts into the packet
+      // stream (they run on), so the split is hidden from them and re-marked after.
+      c->b_pending = 0;
+      c->in_hook = true;
+      hook(hook_user);
+      c->in_hook = false;
+      if (split) c->b_pending = 1;
+    }
+    HIPCHK(c, hipEventSynchronize(c->o_ev[sl_f1]));
+    if (dev_first)
+      std::memcpy(raw, &c->o_shown[0], sizeof(double));
+    else
+      std::memcpy(raw, c->o_hmax + sl_f1, sizeof(double));
+    return dev_err_check(c);
+  }
+  bool first_attempt(double absh, double h, double tnew, const double cf[8], int* slot) override {
+    if (!dev_first) return false;
+    // the host's computation against the kernel's mapped copy
+    bool same = absh == c->o_shown[1] && h == c->o_shown[2] && tnew == c->o_shown[3];
+    for (int i = 0; i < 8; ++i) same = same && cf[i] == c->o_shown[4 + i];
+    *slot = first_slot;
+    return same;  // else left to be overwritten by the attempt queued from the host's values
+  }
+  int queue(int from, int to, double t, double h, double tnew, int gate_slot, double gate_scale, double gate_limit,
+            int* slot) override {
+    return launch(from, to, t, h, tnew, gate_slot, gate_scale, gate_limit, slot, nullptr);
+  }
   // the raw error max of the attempt in slot sl: the bit-pattern max (= the
   // value max of these non-negative doubles, as the device's atomicMax)
-  auto wait_max = [&](int sl, double* out) -> int {
+  int wait_max(int sl, double* out) override {
     unsigned long long m = 0;
     for (int p = 0; p < P; ++p) {
       // (polling hipEventQuery instead: 1.802 / 1.831 vs 1.849 / 1.805 ms, noise; profiles/r05_ode23)
@@ -3827,8 +3920,8 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
       if (g == 0) {
         m = std::max(m, c->o_hmax[sl]);
       } else {
-        const unsigned long long* h = c->o_hpart + (size_t)(3 * p + sl) * kMaxBins;
-        for (unsigned i = 0; i < g; ++i) m = std::max(m, h[i]);
+        const unsigned long long* hp = c->o_hpart + (size_t)(3 * p + sl) * kMaxBins;
+        for (unsigned i = 0; i < g; ++i) m = std::max(m, hp[i]);
       }
     }
     if (c->hz.on) {  // debug: the host-mapped maxima against the device's atomicMax slots
@@ -3842,152 +3935,125 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
     }
     std::memcpy(out, &m, sizeof(double));
     return SWRT_OK;
-  };
-  auto join = [&]() -> int {  // the extra stream's part launches ordered before the packet stream's next work
+  }
+  // The extra stream's part launches ordered before the packet stream's next
+  // work; set `cur` becomes the packets (and F1), the others the spares.
+  int finish(int cur, bool failed) override {
     if (split) {
       c->b_pending = 1;
       HIPCHK_RC(join_b(c));
     }
+    if (failed) HIPCHK(c, hipStreamSynchronize(c->stream));  // a queued guess may still be running
+    const int o1 = (cur + 1) % 3, o2 = (cur + 2) % 3;
+    c->dx = S[cur].x;
+    c->dk = S[cur].k;
+    c->oF[0] = S[cur].F;
+    c->o_ynx = S[o1].x;
+    c->o_ynk = S[o1].k;
+    c->oF[3] = S[o1].F;
+    c->o_spx = S[o2].x;
+    c->o_spk = S[o2].k;
+    c->o_spF = S[o2].F;
+    c->keys_fresh = false;
+    c->cells_sorted = false;
     return SWRT_OK;
-  };
-  // While the host waits for an attempt's error, the next attempt is already
-  // queued on a guess of the controller's next step, gated on the device: it
-  // runs only if err = absh*raw < a limit under which the controller's
-  // answer for a first try is certain without its pow (margins far above
-  // pow's last bit): with temp = 1.25*(err/rtol)^(1/3) the controller takes
-  // absh/temp when temp > 0.2, else 5*absh, then clamps to MaxStep, so
-  //   absh == MaxStep:      MaxStep    when err < 0.5119*rtol         (temp < 1)
-  //   5*absh >= MaxStep:    MaxStep    when err < 0.999*rtol*(absh/(1.25*MaxStep))^3
-  //   else:                 5*absh     when err < 0.999*0.004096*rtol (temp < 0.2)
-  // (then the clamp to tfinal).  A right guess is exactly the attempt the
-  // controller asks for next (checked again), a wrong one costs one empty
-  // launch instead of a host round trip per attempt.
-  // the first attempt from the device's coefficients, queued now; then the
-  // caller's hook (host work that overlaps stage 1 and this attempt)
+  }
+
+ private:
+  swrt_ctx* c;
+  Ode23Args base;
+  bool split;
+  int P;
+  bool dev_first;
+  int sl_f1;
   int first_slot = -1;
-  if (dev_first && (rc = queue(cur, (cur + 1) % 3, t, 0.0, 0.0, -1, 0.0, 0.0, &first_slot, c->o_coef))) return rc;
-  if (hook) {
-    // the hook may call the library (e.g. the next QG step on the QG stream);
-    // it must not touch the packets.  Its calls must not join the extra
-    // stream's attempt parts into the packet stream (they run on), so the
-    // split is hidden from them and re-marked after.
-    c->b_pending = 0;
-    hook(hook_user);
-    if (split) c->b_pending = 1;
+  void (*hook)(void*);
+  void* hook_user;
+  struct Set {
+    double *x, *k, *F;
+  } S[3];
+  unsigned wg[2][3] = {};  // workgroups of each part's launch in each slot (0: the max was copied)
+};
+}  // namespace
+
+int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
+                          double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
+                          int64_t* stats3_out, void (*hook)(void*), void* hook_user) {
+  if (!c) return SWRT_ERR_ARG;
+  if (!ts_out || ts_cap < 1 || !nts_out) return fail(c, SWRT_ERR_ARG, "ts_out / ts_cap / nts_out");
+  if (c->in_hook) return fail(c, SWRT_ERR_STATE, "an ode23 hook may not start another ode23 call");
+  GUARD_BEGIN_KEEP_CHAIN
+  HIPCHK_RC(lost_check(c));
+  SlotUse slot_use(c, false, kSlots01);
+  const double tdir = std::copysign(1.0, tfinal - t0);
+  const double rtol_c = std::max(rtol, 100 * 2.220446049250313e-16);
+  const double thr = atol / rtol_c;
+  const double htspan = std::fabs(tfinal - t0);
+  const double hmax = 0.1 * htspan;
+  const double c0 = 0.8 * std::pow(rtol_c, 1.0 / 3.0);
+  int rc;
+  // stage 1 (with this call's re-binning and in-tile sort), its max in slot
+  // sl_f1: queued by the previous call when it was chained to this one
+  int sl_f1;
+  if (ode23_chain_take(c, t0, tmax, f, Cg, nslots, thr, bump)) {
+    sl_f1 = c->o_chain.dmax_slot;
+    ++c->o_chain.taken;
+  } else {
+    if ((rc = ode23_f1_queue(c, t0, tmax, f, Cg, nslots, thr, bump))) return rc;
+    sl_f1 = c->o_dmax_cur;
+    c->o_dmax_cur = (sl_f1 + 1) % 3;
   }
-  HIPCHK(c, hipEventSynchronize(c->o_ev[sl_f1]));
-  if (dev_first)
-    std::memcpy(&raw, &c->o_shown[0], sizeof(double));
-  else
-    std::memcpy(&raw, c->o_hmax + sl_f1, sizeof(double));
-  HIPCHK_RC(dev_err_check(c));
-  double absh = o23_initial_absh(raw, c0, hmax, htspan, 16 * np_spacing(t));
+  Ode23Args base;
+  if ((rc = ode23_prepare(c, nslots, base, tmax, f, Cg, thr, bump))) return rc;
+  // The first attempt's step size on the device (ode23_first_step_kernel,
+  // the host's own operations), so the attempt is queued behind stage 1
+  // without a host round trip; the controller then computes the same and
+  // checks it against the kernel's mapped copy (the tile path only: its
+  // attempt kernel reads device coefficients).
+  const int ntx_ = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  const bool dev_first = use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx_ * ntx_;
+  // Two part launches per attempt when the binning allows (split implies dev_first).
+  const bool split = ode23_split_ok(c);
   if (dev_first) {
-    // the device's first attempt stands if it took exactly the controller's
-    // first step (always, by construction: the same operations) — else it is
-    // left to be overwritten by the attempt queued from the host's values
-    double ab = absh, h1, tn1, cf[8];
-    const bool d1 = o23_step_head(ab, hmax, 16 * np_spacing(t), tdir, t, tfinal, h1, tn1);
-    (void)d1;
-    o23_coeffs(t, h1, tn1, cf);
-    bool same = ab == c->o_shown[1] && h1 == c->o_shown[2] && tn1 == c->o_shown[3];
-    for (int i = 0; i < 8; ++i) same = same && cf[i] == c->o_shown[4 + i];
-    spec = {true, same, first_slot, cur, (cur + 1) % 3, t, h1, tn1};
+    // (part 1's slots start at zero, cleared here; each launch then clears its next one)
+    hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax, htspan,
+                       16 * o23_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3,
+                       split ? 3 : 0);
+    HIPCHK(c, hipGetLastError());
+  } else {
+    HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl_f1, c->o_dmax + sl_f1, sizeof(unsigned long long),
+                             hipMemcpyDeviceToHost, c->stream));
   }
+  HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
+  if (split) {
+    HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->fork_ev, 0));
+    if (c->hz.on) {
+      c->hz.record(c->fork_ev, 0);
+      c->hz.wait(1, c->fork_ev);
+    }
+    c->b_pending = 1;  // joined into the packet stream before anything else reads the packets (join_b)
+  }
+  DeviceExec ex(c, base, split, dev_first, sl_f1, hook, hook_user);
+  // the first attempt from the device's coefficients, queued now; the
+  // caller's hook then runs (host work that overlaps stage 1 and this attempt)
+  if (dev_first && (rc = ex.queue_first())) return rc;
+  O23Stats st;
   int64_t nts = 0;
-  ts_out[nts++] = t;
-  bool done = false;
-  int64_t nfailed = 0, attempts = 0;
-  while (!done) {
-    const double hmin = 16 * np_spacing(t);
-    double h, tnew_head;
-    done = o23_step_head(absh, hmax, hmin, tdir, t, tfinal, h, tnew_head);
-    bool nofailed = true;
-    double tnew, err;
-    int to;
-    while (true) {
-      tnew = t + h * 1.0;
-      if (done) tnew = tfinal;
-      ++attempts;
-      int slot;
-      if (spec.on && spec.ran && spec.from == cur && spec.t == t && spec.h == h && spec.tnew == tnew) {
-        slot = spec.slot;
-        to = spec.to;
-      } else {
-        to = (cur + 1) % 3;
-        if ((rc = queue(cur, to, t, h, tnew, -1, 0.0, 0.0, &slot))) return rc;
-      }
-      spec.on = false;
-      double gate_limit = 0.0;
-      if (!done && nofailed) {
-        double guess;
-        if (absh == hmax) {
-          guess = hmax;
-          gate_limit = 0.5119 * rtol;
-        } else if (5.0 * absh >= hmax) {
-          guess = hmax;
-          const double r = absh / (1.25 * hmax);
-          gate_limit = 0.999 * rtol * (r * r * r);
-        } else {
-          guess = 5.0 * absh;
-          gate_limit = 0.999 * 0.004096 * rtol;
-        }
-        const double t2 = tnew;
-        double absh2 = guess, h2, tnew2;
-        (void)o23_step_head(absh2, hmax, 16 * np_spacing(t2), tdir, t2, tfinal, h2, tnew2);
-        const int sto = 3 - cur - to;
-        int sl2;
-        if ((rc = queue(to, sto, t2, h2, tnew2, slot, absh, gate_limit, &sl2))) return rc;
-        spec = {true, false, sl2, to, sto, t2, h2, tnew2};
-      }
-      if ((rc = wait_max(slot, &raw))) return rc;
-      err = absh * raw;
-      spec.ran = spec.on && err < gate_limit;  // the device's gate, the same operation
-      h = tnew - t;
-      if (err > rtol) {
-        ++nfailed;
-        if (absh <= hmin) {
-          HIPCHK_RC(join());
-          HIPCHK(c, hipStreamSynchronize(c->stream));  // a queued guess may still be running
-          commit();
-          return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
-        }
-        if (nofailed) {
-          nofailed = false;
-          absh = std::max(hmin, absh * std::max(0.5, 0.8 * std::pow(rtol / err, pw)));
-        } else {
-          absh = std::max(hmin, 0.5 * absh);
-        }
-        h = tdir * absh;
-        done = false;
-      } else {
-        break;
-      }
-    }
-    cur = to;  // accept: y = ynew, F1 = F4
-    t = tnew;
-    // ts_cap bounds the times recorded, never the integration: the interval
-    // always completes and nts_out counts every accepted time
-    if (nts < ts_cap) ts_out[nts] = t;
-    ++nts;
-    if (done) break;
-    if (nofailed) {
-      const double temp = 1.25 * std::pow(err / rtol, pw);
-      absh = temp > 0.2 ? absh / temp : 5.0 * absh;
-    }
-  }
-  // everything queued has finished: the last attempt (done) queues no guess,
-  // and every earlier guess precedes it on its stream; the extra stream's
-  // part launches are joined into the packet stream
-  HIPCHK_RC(join());
-  commit();
+  rc = ode23_control(ex, t0, tfinal, rtol, atol, ts_out, ts_cap, &nts, &st);
+  if (rc == kO23BelowHmin) return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
+  if (rc) return rc;
   if ((rc = ode23_chain_queue(c, tmax, f, Cg, nslots, thr, bump))) return rc;
   *nts_out = nts;
   if (stats3_out) {
-    stats3_out[0] = nts - 1;
-    stats3_out[1] = nfailed;
-    stats3_out[2] = attempts;
+    stats3_out[0] = st.steps;
+    stats3_out[1] = st.failed;
+    stats3_out[2] = st.attempts;
   }
+  c->o23_last = st;
+  c->o23_first_taken += st.first_taken;
+  c->o23_guesses_taken += st.guesses_taken[0] + st.guesses_taken[1] + st.guesses_taken[2];
+  c->o23_split_runs += split ? 1 : 0;
   return SWRT_OK;
   GUARD_END(c)
 }

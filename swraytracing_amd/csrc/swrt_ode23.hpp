@@ -21,6 +21,7 @@
 #include <stdint.h>
 
 #include "swrt_kernels.hpp"
+#include "swrt_ode23_ctl.hpp"
 #include "swrt_tile.hpp"
 
 namespace swrt {
@@ -68,48 +69,8 @@ struct Ode23Args {
   const double* coef;
 };
 
-// ---- MATLAB ode23's step-size arithmetic, shared by host and device ---------
-// (swrt_ode23_run's controller and ode23_first_step_kernel: the same source,
-// the same IEEE operations; std::min(a, b) = b < a ? b : a, std::max(a, b) =
-// a < b ? b : a, spelled out so both sides pick the same operand)
-__host__ __device__ inline double o23_min(double a, double b) { return b < a ? b : a; }
-__host__ __device__ inline double o23_max(double a, double b) { return a < b ? b : a; }
-// the initial step from stage 1's raw max (c0 = 0.8 * rtol^(1/3))
-__host__ __device__ inline double o23_initial_absh(double raw, double c0, double hmax, double htspan, double hmin0) {
-  const double rh = raw / c0;
-  double absh = o23_min(hmax, htspan);
-  if (absh * rh > 1) absh = 1.0 / rh;
-  return o23_max(absh, hmin0);
-}
-// the loop head: clamp absh, h, and the final-step rule; returns done
-__host__ __device__ inline bool o23_step_head(double& absh, double hmax, double hmin, double tdir, double t,
-                                              double tfinal, double& h, double& tnew) {
-  absh = o23_min(hmax, o23_max(hmin, absh));
-  h = tdir * absh;
-  bool done = false;
-  if (1.1 * absh >= fabs(tfinal - t)) {
-    h = tfinal - t;
-    absh = fabs(h);
-    done = true;
-  }
-  tnew = t + h * 1.0;
-  if (done) tnew = tfinal;
-  return done;
-}
-// an attempt's stage times and coefficients {ts, c0, ts3, c3, ts4, c4[0..2]}:
-// f(:,2) at t + h*A(1), y + f*hB(:,1); f(:,3) at t + h*A(2), y + f*hB(:,2);
-// h4 = tnew - t; ynew = y + f*hB(:,3); f(:,4) at tnew
-__host__ __device__ inline void o23_coeffs(double t, double h, double tnew, double out[8]) {
-  out[0] = t + h * 0.5;
-  out[1] = h * 0.5;
-  out[2] = t + h * 0.75;
-  out[3] = h * 0.75;
-  const double h4 = tnew - t;
-  out[4] = tnew;
-  out[5] = h4 * (2.0 / 9.0);
-  out[6] = h4 * (1.0 / 3.0);
-  out[7] = h4 * (4.0 / 9.0);
-}
+// MATLAB ode23's step-size arithmetic (o23_initial_absh, o23_step_head,
+// o23_coeffs) is shared with the host controller: swrt_ode23_ctl.hpp.
 
 // swrt_ode23_run's first attempt without a host round trip: from stage 1's
 // max (the f1 launch's atomicMax slot) the initial step and the loop head,

@@ -23,6 +23,36 @@ def shard_range(n_total: int, world: int, rank: int) -> tuple[int, int]:
     return lo, hi
 
 
+def shard_bounds(n_total: int, weights) -> list[tuple[int, int]]:
+    """Contiguous blocks [lo, hi) of n_total packets in proportion to
+    `weights` (one per rank, >= 0): rank r's block ends at
+    round(n_total * sum(weights[:r+1]) / sum(weights)).  The same float
+    operations on every rank, so every rank computes the same partition."""
+    w = [float(v) for v in weights]
+    if not w or any(v < 0 for v in w) or sum(w) <= 0:
+        raise ValueError("weights must be >= 0 with a positive sum")
+    tot = sum(w)
+    ends, acc = [], 0.0
+    for v in w:
+        acc += v
+        ends.append(int(round(n_total * acc / tot)))
+    ends[-1] = n_total
+    out, lo = [], 0
+    for e in ends:
+        hi = max(lo, min(e, n_total))
+        out.append((lo, hi))
+        lo = hi
+    return out
+
+
+def owner_bounds(n_total: int, world: int, owner_weight: float) -> list[tuple[int, int]]:
+    """The PDE-owner partition: rank 0 steps the PDE and takes `owner_weight`
+    packets for every 1 a receiving rank takes (OwnerLink)."""
+    if world == 1:
+        return [(0, n_total)]
+    return shard_bounds(n_total, [owner_weight] + [1.0] * (world - 1))
+
+
 def _device_for(backend: str):
     import torch
     if backend == "nccl":
@@ -56,7 +86,7 @@ def gather_to_root(local: np.ndarray, n_total: int, world: int, rank: int, backe
     return np.concatenate(parts, axis=0).reshape((n_total,) + tail)
 
 
-def gather_packets(ctx, n_total: int, world: int, rank: int, group=None):
+def gather_packets(ctx, n_total: int, world: int, rank: int, group=None, bounds=None):
     """Gather every rank's device-resident packets into the full (n_total, 2)
     x and k on rank 0, in global packet order (shard_range layout), without a
     host round trip on the sending side: libswrt writes the shard's state in
@@ -65,25 +95,27 @@ def gather_packets(ctx, n_total: int, world: int, rank: int, group=None):
     blocks runs with that stream as torch's current stream, so the collective
     (RCCL on "nccl"; gloo stages through the host) is ordered after the write
     with no synchronisation.  Returns (x, k) numpy arrays on rank 0, None
-    elsewhere."""
+    elsewhere.  ``bounds``: each rank's [lo, hi) (shard_bounds; default the
+    even shard_range blocks)."""
     import torch
     import torch.distributed as dist
     dev = torch.device("cuda", torch.cuda.current_device())
-    maxn = max(1, -(-n_total // world))
-    lo, hi = shard_range(n_total, world, rank)
+    bounds = bounds or [shard_range(n_total, world, r) for r in range(world)]
+    maxn = max(1, max(hi - lo for lo, hi in bounds))
+    lo, hi = bounds[rank]
     if ctx.packets_count() != hi - lo:
         raise ValueError(f"rank {rank} holds {ctx.packets_count()} packets, its shard is {hi - lo}")
     stream = torch.cuda.ExternalStream(ctx.stream(), device=dev)
     with torch.cuda.stream(stream):
         buf = torch.zeros((4, maxn), dtype=torch.float64, device=dev)  # rows x, y, k, l
-        ctx.packets_get_device(buf.data_ptr(), buf.data_ptr() + 2 * maxn * 8, maxn)
+        if hi > lo:
+            ctx.packets_get_device(buf.data_ptr(), buf.data_ptr() + 2 * maxn * 8, maxn)
         out = [torch.empty_like(buf) for _ in range(world)]
         dist.all_gather(out, buf, group=group)
         if rank != 0:
             torch.cuda.current_stream().synchronize()
             return None
-        full = torch.cat([out[r][:, : shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0]]
-                          for r in range(world)], dim=1).cpu().numpy()
+        full = torch.cat([out[r][:, : bounds[r][1] - bounds[r][0]] for r in range(world)], dim=1).cpu().numpy()
     return np.ascontiguousarray(full[0:2].T), np.ascontiguousarray(full[2:4].T)
 
 
@@ -101,3 +133,69 @@ def allreduce_max_fn(backend: str = "nccl", group=None):
     norm when packets are sharded (one 8-byte all_reduce per attempted step,
     RCCL on "nccl")."""
     return lambda v: max_over_ranks(v, backend=backend, group=group)
+
+
+class OwnerLink:
+    """The PDE-owner driver's per-step hand-off (qg2layersw_raytrace.m:152-197
+    sharded with the PDE on ONE rank): the packets read only the top layer of
+    qk (:186-188), so the owner rank broadcasts that layer's spectral PV
+    (the (2kmax+1)(kmax+1) half plane, 2.1 MB at 512^2) and the step's dt after
+    every PDE step, and every other rank builds its snapshots from it
+    (swrt_snapshot_qk: bit for bit the owner's swrt_qg_snapshot) instead of
+    stepping the replicated 2-layer PDE.  One broadcast per step of a
+    device buffer on "nccl" (RCCL over xGMI; the export and the snapshot are
+    ordered on torch's current stream, the host reads only the dt word), of
+    a host buffer on "gloo".  Two buffers in turn: the current step's and
+    the previous step's qk (the first active step's grid_U(prev_qk))."""
+
+    def __init__(self, nx, backend, owner=0, group=None):
+        import torch
+        kmax = nx // 2 - 1
+        self.nx = int(nx)
+        self.nh = (2 * kmax + 1) * (kmax + 1)
+        self.owner, self.group = owner, group
+        self.device = backend == "nccl"
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.device else torch.device("cpu")
+        # [qk half plane (2*nh doubles) | dt]
+        self.bufs = [torch.zeros(2 * self.nh + 1, dtype=torch.float64, device=dev) for _ in range(2)]
+        self.cur = 0  # the buffer holding the latest qk
+
+    def _stream(self):
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+
+    def _export(self, ctx, b, which=0):
+        if self.device:
+            ctx.qg_export(b.data_ptr(), which=which, layer=0, stream=self._stream())
+        else:
+            ctx.qg_export(b[: 2 * self.nh].numpy(), which=which, layer=0)
+
+    def seed(self, ctx):
+        """Every rank: the model's initial qk as the 'previous' buffer (all
+        ranks hold the same initial state)."""
+        self._export(ctx, self.bufs[self.cur])
+
+    def publish(self, ctx, dt):
+        """Owner: the committed current qk's top layer and dt to every rank."""
+        import torch.distributed as dist
+        b = self.bufs[self.cur ^ 1]
+        self._export(ctx, b)
+        b[-1].fill_(float(dt))
+        dist.broadcast(b, src=self.owner, group=self.group)
+        self.cur ^= 1
+
+    def receive(self):
+        """Receiver: the owner's next (qk, dt); returns dt (a host float)."""
+        import torch.distributed as dist
+        b = self.bufs[self.cur ^ 1]
+        dist.broadcast(b, src=self.owner, group=self.group)
+        self.cur ^= 1
+        return float(b[-1].item())
+
+    def snapshot(self, ctx, slot, which, L, K_d2, shear, k_scale, ny_period):
+        """grid_U of the latest (which 0) or the previous (1) qk into `slot`."""
+        b = self.bufs[self.cur if which == 0 else self.cur ^ 1]
+        if self.device:
+            ctx.snapshot_qk(slot, b.data_ptr(), self.nx, L, K_d2, shear, k_scale, ny_period, stream=self._stream())
+        else:
+            ctx.snapshot_qk(slot, b[: 2 * self.nh].numpy(), self.nx, L, K_d2, shear, k_scale, ny_period)

@@ -170,6 +170,19 @@ def ode23_packets(ctx: Context, tspan, tmax, f, Cg, nslots=2, rtol=1e-3, atol=1e
     return np.array(ts)
 
 
+class _EmptyShard:
+    """The ode23 stages of a rank that holds no packets: every max is 0."""
+
+    def ode23_f1(self, *a):
+        return 0.0
+
+    def ode23_attempt(self, *a):
+        return 0.0
+
+    def ode23_accept(self):
+        pass
+
+
 class PacketEnsemble:
     """Device-resident packets advanced through a sequence of background
     snapshots — the packet branch of qgsw_raytrace.m:140-163 /
@@ -183,11 +196,14 @@ class PacketEnsemble:
     """
 
     def __init__(self, x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, device=0,
-                 bump=BUMP_QG, ctx: Context | None = None, shard=None):
+                 bump=BUMP_QG, ctx: Context | None = None, shard=None, bounds=None):
         """``shard`` = (rank, world): x, k are the whole ensemble (the same on
         every rank) and this rank advances its contiguous shard (SURVEY §8e);
         frames are gathered to rank 0 on the device (dist.gather_packets) and
-        ode23's error norm is max-reduced over the ranks."""
+        ode23's error norm is max-reduced over the ranks.  ``bounds``: every
+        rank's [lo, hi) (dist.shard_bounds / owner_bounds; default the even
+        split).  A rank's shard may be empty (the PDE owner's, with weight 0):
+        it then only takes part in the collectives."""
         self.ctx = ctx if ctx is not None else Context(device)
         self.L, self.f, self.Cg, self.nx = float(L), float(f), float(Cg), int(nx)
         self.gH = self.Cg ** 2
@@ -198,9 +214,14 @@ class PacketEnsemble:
         k = np.asarray(k, dtype=np.float64)
         self.n_total = x.shape[0]
         self.rank, self.world = shard if shard is not None else (0, 1)
+        self.bounds = None
         if self.world > 1:
             from .dist import shard_range
-            lo, hi = shard_range(self.n_total, self.world, self.rank)
+            self.bounds = list(bounds) if bounds is not None else \
+                [shard_range(self.n_total, self.world, r) for r in range(self.world)]
+            if len(self.bounds) != self.world or self.bounds[-1][1] != self.n_total:
+                raise ValueError("bounds must give one [lo, hi) per rank covering the ensemble")
+            lo, hi = self.bounds[self.rank]
             x, k = x[lo:hi], k[lo:hi]
         self.ctx.packets_set(x, k)
         self.n = x.shape[0]
@@ -220,6 +241,8 @@ class PacketEnsemble:
             self.ctx.set_field_grid(slot, flow_planes(fl), self.nx, self.L, self.ny_period)
 
     def advance(self, dt, nsub=1, save_every=0):
+        if self.n == 0:
+            return
         # re-bin after ~4 PDE intervals of packet motion: every 4 steps at one
         # substep per interval, every 20 at five (tuned on the bench workload)
         if self._rebin != 4 * nsub:
@@ -233,6 +256,8 @@ class PacketEnsemble:
         """len(dts) consecutive PDE intervals in one call, interval i between
         the snapshots in slots i and i+1 (swrt_advance_intervals): the same
         bits as one advance() per interval with the pair moved to slots 0, 1."""
+        if self.n == 0:
+            return
         if self._rebin != 4 * nsub:
             self._rebin = 4 * nsub
             self.ctx.set_locality(self._rebin, 0)
@@ -248,7 +273,9 @@ class PacketEnsemble:
 
             from .dist import allreduce_max_fn
             allreduce_max = allreduce_max_fn(backend=dist.get_backend())
-        return ode23_packets(self.ctx, (0.0, dt), dt, self.f, self.Cg, nslots=2, rtol=rtol, atol=atol,
+        # an empty shard contributes 0 to every error max (the max-norm's identity)
+        ctx = self.ctx if self.n > 0 else _EmptyShard()
+        return ode23_packets(ctx, (0.0, dt), dt, self.f, self.Cg, nslots=2, rtol=rtol, atol=atol,
                              bump=self.bump, allreduce_max=allreduce_max, stats=stats, controller=controller,
                              hook=hook)
 
@@ -261,7 +288,7 @@ class PacketEnsemble:
         (every rank calls it); rank 0 writes the whole ensemble."""
         if self.world > 1:
             from .dist import gather_packets
-            full = gather_packets(self.ctx, self.n_total, self.world, self.rank)
+            full = gather_packets(self.ctx, self.n_total, self.world, self.rank, bounds=self.bounds)
             if full is None:
                 return
             x, k = full

@@ -236,8 +236,23 @@ def _fresh_outputs(out_dir, fresh):
             os.remove(p)
 
 
+def _owner_setup(world, pde, owner_weight, nx, Npackets):
+    """(link, bounds) of a sharded run in the PDE-owner form, or (None, None)
+    for the replicated form (every rank steps the PDE)."""
+    if world <= 1 or pde == "replicated":
+        return None, None
+    if pde != "owner":
+        raise ValueError("pde must be 'owner' or 'replicated'")
+    import torch.distributed as dist
+
+    from .dist import OwnerLink, owner_bounds
+    return OwnerLink(nx, dist.get_backend()), owner_bounds(Npackets, world, owner_weight)
+
+
+OWNER_WEIGHT = 0.5  # packets of the PDE owner per packet of a receiving rank (bench.py driver_step_forecast "owner")
+
+
 class TwoLayerLoop:
-    SPEC_SLOT = 2  # ode23 + speculate: where the next step's snapshot is packed ahead (slots 0/1: the interval's)
     """One iteration of qg2layersw_raytrace.m:152-197 on the device: the CFL
     rule (:156-165) on the current U0, the PDE step, U0 of the new qk read back
     asynchronously (collected after the packet work is queued, so the rule
@@ -248,11 +263,18 @@ class TwoLayerLoop:
 
     With ``speculate`` (default) every step returns with the next PDE step
     queued speculatively (QGModel.spec_pending); the model's own calls drop
-    it before they run (QGModel.settle), and :meth:`settle` does so explicitly."""
+    it before they run (QGModel.settle), and :meth:`settle` does so explicitly.
+
+    ``link`` (dist.OwnerLink): this rank is the PDE owner of a sharded run —
+    after each PDE step it publishes the new qk's top layer and dt to the
+    other ranks (:class:`ReceiverLoop`), which build their snapshots from it."""
+
+    SPEC_SLOT = 2  # ode23 + speculate: where the next step's snapshot is packed ahead (slots 0/1: the interval's)
 
     def __init__(self, model, ens, dt, U0, cfl_fraction=0.25, packet_delay=0.0, nsub=5, packet_intervals=1,
-                 integrator="leapfrog", log=None, speculate=True):
+                 integrator="leapfrog", log=None, speculate=True, link=None):
         self.model, self.ens, self.dt, self.U0 = model, ens, dt, U0
+        self.link = link
         # speculate: each step also queues the NEXT PDE step with this step's
         # dt (swrt_qg_step_speculative) before waiting for this step's U0, so
         # the QG stream never idles through the host's read-back and CFL rule;
@@ -291,10 +313,21 @@ class TwoLayerLoop:
         else:
             self.model.step(self.dt)
             self.model.max_speed_async()
+        if self.link is not None:
+            self.link.publish(self.model.ctx, self.dt)  # the committed qk of this step, before the next is queued
         self.t = self.t + self.dt
         active = self.ens is not None and self.t > self.packet_delay
         spec = self.speculate and self.model.params.nlayers == 2 and getattr(self.model.ctx, "qg_fused", True)
-        if active:
+        if active and self.ens.n == 0:
+            # an owner without packets: no snapshots; the interval still runs
+            # (ode23: its error-norm collectives) with the speculative step inside
+            if spec and self.group.integrator == "ode23":
+                dt = self.dt
+                self.group.add(dt, hook=lambda: self.model.step_speculative(dt))
+                spec = False
+            else:
+                self.group.add(self.dt)
+        elif active:
             ny = 2 * self.nx
             if not self.have_cur:
                 self.model.snapshot(0, which=1, layer=0, ny_period=ny)
@@ -317,7 +350,7 @@ class TwoLayerLoop:
                     self.model.step_speculative(dt)
                     self.model.snapshot_speculative(self.SPEC_SLOT, ny_period=ny)
                     self._spec_snap = True
-                    if self.chain:
+                    if self.chain and self.ens.world == 1:  # (a sharded interval runs the Python controller)
                         # the next interval reads this one's end snapshot (slot
                         # 1) and the one just queued: its stage 1 is queued as
                         # this interval ends (taken only if still exact)
@@ -345,9 +378,57 @@ class TwoLayerLoop:
         self.model.settle()
 
 
+class ReceiverLoop:
+    """A receiving rank's iteration of qg2layersw_raytrace.m:152-197 in the
+    PDE-owner form of a sharded run: no PDE here — the owner's dt and the
+    new qk's top layer arrive through ``link`` (dist.OwnerLink) each step,
+    grid_U of it (and, on the first active step, of the previous qk) goes
+    into the packet slots (swrt_snapshot_qk: the owner's snapshot bits), and
+    this rank's packets take the interval [t, t+dt] exactly as the owner's
+    TwoLayerLoop does (same t, dt sequence, active steps and frame points)."""
+
+    def __init__(self, link, ens, dt, packet_delay=0.0, nsub=5, packet_intervals=1, integrator="leapfrog"):
+        self.link, self.ens, self.dt = link, ens, dt
+        self.packet_delay = packet_delay
+        self.t = 0.0
+        self.steps = 0
+        self.dts = []
+        self.have_cur = False
+        self.group = _IntervalGroup(ens.ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
+
+    def _snapshot(self, slot, which):
+        e = self.ens
+        self.link.snapshot(e.ctx, slot, which, e.L, e.K_d2, e.shear, e.k_scale, e.ny_period)
+
+    def step(self):
+        self.steps += 1
+        self.dt = self.link.receive()
+        self.dts.append(self.dt)
+        self.t = self.t + self.dt
+        active = self.ens is not None and self.t > self.packet_delay
+        if active:
+            if self.ens.n > 0:
+                if not self.have_cur:
+                    self._snapshot(0, 1)  # grid_U(prev_qk)
+                self._snapshot(self.group.next_slot(), 0)  # grid_U(qk)
+                self.have_cur = True
+            self.group.add(self.dt)
+        else:
+            self.have_cur = False
+        return active
+
+    def flush(self):
+        if self.group is not None:
+            self.group.flush()
+
+    def settle(self):
+        pass
+
+
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
                   out_dir="data", nsub=4, max_steps=None, seed=146, verbose=False, r_drag=0.1,
-                  packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None):
+                  packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None,
+                  pde="owner", owner_weight=OWNER_WEIGHT):
     """qgsw_raytrace.m:1-180 with the PDE and the packets on the GPU.
 
     Writes ``out_dir``/packet_x.bin, packet_k.bin, packet_time.bin, pv.bin,
@@ -362,10 +443,11 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     "leapfrog" (``nsub`` fused symplectic substeps per PDE interval) or
     "ode23" (the reference's own ode23 over each interval, qgsw_raytrace.m:149).
     ``fresh``: remove earlier output files first (default) or append to
-    them as write_field.m:31 does.  Returns a dict of run facts (dt, Nsteps,
-    steps run, frames written, final t)."""
+    them as write_field.m:31 does.  ``pde``, ``owner_weight``: the sharded
+    forms, as in :func:`qg2layersw_raytrace`.  Returns a dict of run facts
+    (dt, Nsteps, steps run, frames written, final t)."""
     ctx = ctx if ctx is not None else Context(0)
-    rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
+    rank, world = _dist_info()  # sharded run: packets split over the ranks
     if rank == 0:
         _fresh_outputs(out_dir, fresh)
     log = RunLog(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
@@ -382,6 +464,10 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     qk = ctx.g2k(q)
     x, k = _packets(Npackets, L, near_inertial_factor, f, Cg, rng)
     model = QGModel.one_layer(qk, nx, f, Cg, r_drag=r_drag, ctx=ctx)
+    link, bounds = _owner_setup(world, pde, owner_weight, nx, Npackets)
+    if link is not None:
+        link.seed(ctx)
+    owner = link is None or rank == 0  # this rank steps the PDE
     U0 = model.max_speed()
     Fr = U0 / Cg
     T = T_days / Fr ** 2
@@ -391,8 +477,14 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     log(parameter_block(nx, Npackets, near_inertial_factor * f, dt, T, packet_delay, steps_per_save,
                         packet_steps_per_save, f, Cg, U_g, U0, Fr, K_d2))
     ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=0.0, k_scale=1.0, nlayers=1, bump=BUMP_QG, ctx=ctx,
-                         shard=(rank, world)) \
+                         shard=(rank, world), bounds=bounds) \
         if Npackets > 0 else None
+
+    def snapshot(slot, which):
+        if owner:
+            model.snapshot(slot, which=which)
+        else:
+            link.snapshot(ctx, slot, which, L, K_d2, 0.0, 1.0, 0)
     t = 0.0
     frames = 1
     if ens is not None:
@@ -405,12 +497,18 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     group = _IntervalGroup(ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
     log.start()
     for step in range(1, nrun + 1):
-        model.step(dt)
+        if owner:
+            model.step(dt)
+            if link is not None:
+                link.publish(ctx, dt)
+        else:
+            link.receive()  # (the 1-layer driver's dt is fixed)
         t = t + dt
         if ens is not None and t > packet_delay:
-            if not have_cur:
-                model.snapshot(0, which=1)    # grid_U(prev_qk); later groups start from the last grid_U(qk)
-            model.snapshot(group.next_slot(), which=0)  # grid_U(qk)
+            if ens.n > 0:
+                if not have_cur:
+                    snapshot(0, 1)  # grid_U(prev_qk); later groups start from the last grid_U(qk)
+                snapshot(group.next_slot(), 0)  # grid_U(qk)
             have_cur = True
             group.add(dt)
             if (step - packet_step_start + 1) % packet_steps_per_save == 0:
@@ -434,14 +532,22 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
 
 def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
                         out_dir="data", nsub=5, max_steps=None, seed=5, verbose=False,
-                        packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None):
+                        packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None,
+                        pde="owner", owner_weight=OWNER_WEIGHT):
     """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
     (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and
     interpolate's 2*nx y-period).  Same packet outputs as :func:`qgsw_raytrace`;
     pv.bin holds the initial nx x nx x 2 frame only, as in the reference.
-    ``packet_intervals``, ``integrator``, ``fresh``: as in :func:`qgsw_raytrace`."""
+    ``packet_intervals``, ``integrator``, ``fresh``: as in :func:`qgsw_raytrace`.
+
+    Sharded (torch.distributed, world > 1): ``pde="owner"`` (default) — rank 0
+    steps the PDE and sends each step's top-layer qk and dt to the other
+    ranks, which only build snapshots and advance packets; rank 0 holds
+    ``owner_weight`` packets per packet of another rank (dist.owner_bounds).
+    ``pde="replicated"``: every rank steps the same PDE, packets split evenly.
+    Both write the single-process files byte for byte."""
     ctx = ctx if ctx is not None else Context(0)
-    rank, world = _dist_info()  # sharded run: packets split over the ranks, field replicated
+    rank, world = _dist_info()  # sharded run: packets split over the ranks
     if rank == 0:
         _fresh_outputs(out_dir, fresh)
     log = RunLog(os.path.join(out_dir, "run.log") if rank == 0 else None, verbose and rank == 0)
@@ -461,7 +567,10 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     qk2 = ctx.g2k(-q1)
     qk = np.stack([qk1, qk2], axis=2)
     x, k = _packets(Npackets, L, near_inertial_factor, f, Cg, rng)
-    model = QGModel.two_layer(qk, nx, f, Cg, L=L, shear=shear, ctx=ctx)
+    model = QGModel.two_layer(qk, nx, f, Cg, L=L, shear=shear, ctx=ctx)  # (every rank: the same U0, T, dt)
+    link, bounds = _owner_setup(world, pde, owner_weight, nx, Npackets)
+    if link is not None:
+        link.seed(ctx)
     U0 = model.max_speed()
     Fr = U0 / Cg
     T = T_Fr / Fr ** 2
@@ -471,7 +580,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     log(parameter_block(nx, Npackets, near_inertial_factor * f, dt, T, packet_delay_steps, steps_per_save,
                         packet_steps_per_save, f, Cg, U_g, U0, Fr, K_d2, two_layer=True))
     ens = PacketEnsemble(x, k, L, f, Cg, nx, K_d2, shear=shear, k_scale=2 * math.pi / L, nlayers=2,
-                         bump=BUMP_QG, ctx=ctx, shard=(rank, world)) if Npackets > 0 else None
+                         bump=BUMP_QG, ctx=ctx, shard=(rank, world), bounds=bounds) if Npackets > 0 else None
     t = 0.0
     frames = 1
     if ens is not None:
@@ -479,8 +588,11 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     if rank == 0:
         write_field(model.q(), os.path.join(out_dir, "pv"))
         write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
-    loop = TwoLayerLoop(model, ens, dt, U0, CFL_fraction, packet_delay_steps, nsub, packet_intervals, integrator,
-                        log)
+    if link is not None and rank != 0:
+        loop = ReceiverLoop(link, ens, dt, packet_delay_steps, nsub, packet_intervals, integrator)
+    else:
+        loop = TwoLayerLoop(model, ens, dt, U0, CFL_fraction, packet_delay_steps, nsub, packet_intervals, integrator,
+                            log, link=link)
     # (the reference only plots q every steps_per_save steps in this loop; its
     # pv.bin writes are commented out, qg2layersw_raytrace.m:211-239)
     log.start()
@@ -495,6 +607,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     ctx.synchronize()
     log.finish()
     log.close()
-    dt, dts, step, t, U0 = loop.dt, loop.dts, loop.steps, loop.t, loop.U0
+    dt, dts, step, t = loop.dt, loop.dts, loop.steps, loop.t
+    U0 = getattr(loop, "U0", U0)  # (a receiving rank never sees the owner's U0)
     return dict(dt=dt, dts=dts, Nsteps=Nsteps, steps=step, packet_frames=frames, t=t, U0=U0,
                 packet_step_start=packet_step_start)

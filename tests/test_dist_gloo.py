@@ -161,3 +161,105 @@ def test_gloo_sharded_ode23_takes_the_global_steps(world):
         assert p.exitcode == 0
     same_ts, same_y, steps = q.get(timeout=10)
     assert same_ts and same_y and steps >= 10
+
+
+def test_owner_bounds_partition_and_weight():
+    from swraytracing_amd.dist import owner_bounds, shard_bounds
+    for n in (0, 1, 5001, 1_000_000):
+        for world in (1, 2, 4, 8):
+            for w0 in (0.0, 0.35, 0.5, 1.0, 2.0):
+                b = owner_bounds(n, world, w0)
+                assert len(b) == world and b[0][0] == 0 and b[-1][1] == n
+                assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+                assert all(lo <= hi for lo, hi in b)
+                if world > 1 and n >= 1000:
+                    n0 = b[0][1] - b[0][0]
+                    assert abs(n0 - n * w0 / (w0 + world - 1)) <= 1
+    assert shard_bounds(10, [1, 1]) == [(0, 5), (5, 10)]
+    with pytest.raises(ValueError):
+        shard_bounds(10, [0, 0])
+
+
+class _FakeQG:
+    """The owner's model context: qg_export hands out this step's qk."""
+
+    def __init__(self, nh):
+        self.nh = nh
+        self.qk = None
+
+    def qg_export(self, dst, which=0, layer=0, stream=None):
+        assert which == 0 and layer == 0
+        dst[:] = self.qk
+
+
+class _FakeSnap:
+    """A receiving rank's context: snapshot_qk records what it was given."""
+
+    def __init__(self):
+        self.got = []
+
+    def snapshot_qk(self, slot, qk, nx, L, K_d2, shear, k_scale, ny_period, stream=None):
+        self.got.append((slot, qk.copy(), (nx, L, K_d2, shear, k_scale, ny_period)))
+
+
+def _owner_link_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    from swraytracing_amd.dist import OwnerLink
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nx = 16
+        link = OwnerLink(nx, "gloo")
+        rng = np.random.default_rng(11)  # the same stream on every rank: rank 0 sends, the others check
+        seq = [rng.standard_normal(2 * link.nh) for _ in range(6)]
+        dts = [0.01 * (1 + i) for i in range(5)]
+        if rank == 0:
+            m = _FakeQG(link.nh)
+            m.qk = seq[0]
+            link.seed(m)
+            for i, dt in enumerate(dts):
+                m.qk = seq[i + 1]
+                link.publish(m, dt)
+            ok = True
+        else:
+            c = _FakeSnap()
+            m = _FakeQG(link.nh)
+            m.qk = seq[0]
+            link.seed(m)  # every rank holds the initial state
+            got_dt = []
+            for i in range(len(dts)):
+                got_dt.append(link.receive())
+                if i == 0:
+                    link.snapshot(c, 0, 1, 20.0, 3.0, 0.5, 0.3, 2 * nx)  # grid_U(prev_qk) on the first active step
+                link.snapshot(c, 1, 0, 20.0, 3.0, 0.5, 0.3, 2 * nx)
+            want = [(0, seq[0])] + [(1, seq[i + 1]) for i in range(len(dts))]
+            ok = (got_dt == dts and len(c.got) == len(want)
+                  and all(s == ws and np.array_equal(a, wa) for (s, a, _), (ws, wa) in zip(c.got, want))
+                  and all(p == (nx, 20.0, 3.0, 0.5, 0.3, 2 * nx) for _, _, p in c.got))
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        if rank == 0:
+            q.put(all(flags))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_owner_link_hands_every_step_to_every_rank(world):
+    """The PDE-owner hand-off (dist.OwnerLink, gloo): each PDE step's top-layer
+    qk and dt, published by rank 0 after the step, reach every other rank in
+    order, with the previous step's qk kept for the first active step's
+    grid_U(prev_qk) — the inputs of ReceiverLoop's snapshots (the GPU tests
+    check the resulting driver files byte for byte)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_owner_link_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10)

@@ -100,33 +100,76 @@ import swraytracing_amd as sw
 torch.cuda.set_device(0)
 dist.init_process_group("gloo")
 ctx = sw.Context(0)
-sw.qg2layersw_raytrace(64, 5001, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=sys.argv[1], nsub=2, max_steps=30, seed=5,
-                       integrator=sys.argv[2], ctx=ctx)
+drv, integrator, pde, w0 = sys.argv[2], sys.argv[3], sys.argv[4], float(sys.argv[5])
+if drv == "qg2":
+    sw.qg2layersw_raytrace(64, 5001, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=sys.argv[1], nsub=2, max_steps=30,
+                           seed=5, integrator=integrator, ctx=ctx, pde=pde, owner_weight=w0)
+else:
+    sw.qgsw_raytrace(64, 4001, 4.0, 20.0, 0.0, 0.2, 3.0, 1.0, out_dir=sys.argv[1], nsub=2, max_steps=24,
+                     integrator=integrator, r_drag=0.0, ctx=ctx, pde=pde, owner_weight=w0)
 ctx.close()
 dist.destroy_process_group()
 """
 
+_REF = {}
 
-@pytest.mark.parametrize("integrator", ["leapfrog", "ode23"])
-def test_two_rank_driver_files_equal_single_process(ctx, tmp_path, integrator):
-    """qg2layersw_raytrace sharded over two ranks (packets split, field
-    replicated, frames gathered on the device and written by rank 0; ode23's
-    error norm max-reduced over the ranks so both take the same steps)
-    writes the same packet_x/k/time.bin and pv.bin as one process."""
+
+def _single(ctx, tmp_path, drv, integrator):
+    """The single-process run's files (cached per driver and integrator)."""
     import swraytracing_amd as sw
-    ref = tmp_path / "single"
-    sw.qg2layersw_raytrace(64, 5001, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(ref), nsub=2, max_steps=30, seed=5,
-                           integrator=integrator, ctx=ctx)
+    key = (drv, integrator)
+    if key not in _REF:
+        ref = tmp_path / "single"
+        if drv == "qg2":
+            sw.qg2layersw_raytrace(64, 5001, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(ref), nsub=2, max_steps=30,
+                                   seed=5, integrator=integrator, ctx=ctx)
+        else:
+            sw.qgsw_raytrace(64, 4001, 4.0, 20.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(ref), nsub=2, max_steps=24,
+                             integrator=integrator, r_drag=0.0, ctx=ctx)
+        _REF[key] = {n: (ref / n).read_bytes() for n in ("packet_x.bin", "packet_k.bin", "packet_time.bin", "pv.bin")}
+    return _REF[key]
+
+
+def _rank_report(stderr, tail=40):
+    """The last lines of each rank's own output ([rankN]: prefixes) and of the
+    launcher, so a failing rank's traceback is never cut off by another's."""
+    by = {}
+    for ln in stderr.splitlines():
+        key = ln.split("]:", 1)[0] + "]" if ln.startswith("[rank") else "launcher"
+        by.setdefault(key, []).append(ln)
+    return "\n".join(f"--- {k} ---\n" + "\n".join(v[-tail:]) for k, v in sorted(by.items()))
+
+
+@pytest.mark.parametrize("drv,world,pde,w0,integrator", [
+    ("qg2", 2, "replicated", 1.0, "leapfrog"),
+    ("qg2", 2, "replicated", 1.0, "ode23"),
+    ("qg2", 2, "owner", 0.5, "leapfrog"),
+    ("qg2", 2, "owner", 0.5, "ode23"),
+    ("qg2", 4, "owner", 0.5, "leapfrog"),
+    ("qg2", 4, "owner", 0.5, "ode23"),
+    ("qg2", 2, "owner", 0.0, "ode23"),  # the owner holds no packets: it only joins the collectives
+    ("qg1", 2, "owner", 0.5, "leapfrog"),
+])
+def test_sharded_driver_files_equal_single_process(ctx, tmp_path, drv, world, pde, w0, integrator):
+    """The drivers sharded over `world` ranks sharing GPU 0 (gloo), frames
+    gathered on the device and written by rank 0, ode23's error norm
+    max-reduced over the ranks: with the replicated PDE (every rank steps it,
+    packets split evenly) and in the PDE-owner form (rank 0 steps the PDE and
+    broadcasts each step's top-layer qk and dt, qg2layersw_raytrace.m:186-188;
+    the others build their snapshots from it, swrt_snapshot_qk), the run
+    writes the same packet_x/k/time.bin and pv.bin as one process, byte for
+    byte."""
+    ref = _single(ctx, tmp_path, drv, integrator)
     (tmp_path / "driver.py").write_text(DRIVER)
     out = tmp_path / "sharded"
     env = dict(os.environ, SWRT_ROOT=ROOT)
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(tmp_path / "driver.py"), str(out),
-           integrator]
+           drv, integrator, pde, str(w0)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-3000:]
-    for name in ("packet_x.bin", "packet_k.bin", "packet_time.bin", "pv.bin"):
-        a, b = (ref / name).read_bytes(), (out / name).read_bytes()
+    assert r.returncode == 0, _rank_report(r.stderr)
+    for name, a in ref.items():
+        b = (out / name).read_bytes()
         assert len(a) > 0 and a == b, name
 
 
@@ -142,8 +185,8 @@ def test_bench_gpus_2_strong_scaling_line(tmp_path):
                         "--steps", "3", "--warmup", "1", "--driver-steps", "0", "--ode23-steps", "0",
                         "--no-cpu-baseline", "--gather"], cwd=str(tmp_path), env=env, capture_output=True, text=True,
                        timeout=240)
-    # a failing rank's traceback sits mid-stream, before the launcher's report
-    assert r.returncode == 0, "\n".join(ln for ln in r.stderr.splitlines() if "[rank" in ln)[-4000:] or r.stderr[-3000:]
+    # every rank's own last lines (a failing rank's traceback sits mid-stream, before the launcher's report)
+    assert r.returncode == 0, _rank_report(r.stderr)
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])

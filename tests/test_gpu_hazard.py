@@ -249,3 +249,48 @@ def test_corrupted_tile_count_is_an_error_not_a_hang(debug_ctx, delta):
         ctx.packets_get()
     x2, k2 = _run_calls(ctx, bench, w, 6)  # packets_set clears it
     assert _bits_equal(x1, x2) and _bits_equal(k1, k2)
+
+
+def test_corrupted_binning_in_ode23_refuses_the_packets_until_reset(debug_ctx):
+    """The same device check inside the drivers' ode23 (its calls re-bin every
+    2nd interval): the call that meets it returns SWRT_ERR_STATE, and every
+    entry point that reads the packets — the ode23 calls, swrt_packets_get(_device),
+    swrt_advance — refuses the lost state until swrt_packets_set, instead of
+    integrating it (or unpermuting it through a stale permutation) and
+    returning SWRT_OK.  qgsw_raytrace.m:149 semantics are unaffected: after
+    packets_set the interval gives the bits of a fresh context."""
+    import torch
+
+    import swraytracing_amd as sw
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 300_000)
+    f, Cg, dt = w["f"], 1.0, w["dt"]
+    run = lambda: ctx.ode23_run(0.0, dt, dt, f, Cg, 2, 1e-3, 1e-6, sw.BUMP_QG)  # noqa: E731
+    ctx.packets_set(w["x"], w["k"])
+    ts_ref, st_ref = run()
+    x_ref, k_ref = ctx.packets_get()
+    ctx.packets_set(w["x"], w["k"])
+    ctx.debug_set(L.DEBUG_CORRUPT_COUNT, 1000)
+    with pytest.raises(sw.SwrtError, match="binning"):
+        for _ in range(3):  # the next re-binning meets the corrupted count
+            run()
+    buf = torch.zeros((4, 300_000), dtype=torch.float64, device="cuda")
+    refused = {
+        "ode23_run": run,
+        "ode23_f1": lambda: ctx.ode23_f1(0.0, dt, f, Cg, 2, 1e-3, sw.BUMP_QG),
+        "ode23_attempt": lambda: ctx.ode23_attempt(0.0, dt / 10, dt / 10, dt, f, Cg, 2, 1e-3, sw.BUMP_QG),
+        "ode23_accept": ctx.ode23_accept,
+        "packets_get": ctx.packets_get,
+        "packets_get_device": lambda: ctx.packets_get_device(buf.data_ptr(), buf.data_ptr() + 2 * 300_000 * 8,
+                                                             300_000),
+        "advance": lambda: bench.step(ctx, w, 5),
+    }
+    for name, call in refused.items():
+        with pytest.raises(sw.SwrtError, match="lost"):
+            call()
+    torch.cuda.synchronize()
+    ctx.packets_set(w["x"], w["k"])
+    ts, st = run()
+    x, k = ctx.packets_get()
+    assert _bits_equal(ts, ts_ref) and st == st_ref
+    assert _bits_equal(x, x_ref) and _bits_equal(k, k_ref)

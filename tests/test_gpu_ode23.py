@@ -274,3 +274,146 @@ def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
     half = run(True, tfinal2=0.5 * tmax)
     assert half[4] == 1
     same(half, run(False, tfinal2=0.5 * tmax))
+
+
+def test_ode23_driver_path_at_scale_matches_oracle(fresh_ctx, qg_case, oracle_lib):
+    """The library ode23 path exactly as the drivers run it (qgsw_raytrace.m:
+    143-150, qg2layersw_raytrace.m:195-196), against the oracle's ode23 rather
+    than against the Python controller: 70,000 packets on 16 tiles so every
+    attempt is split into two part launches (ode23_split_ok), maxima read from
+    host-mapped memory, the first attempt queued from the device's own step
+    size, gated guesses, and two intervals chained (the second one's stage 1
+    queued by the first as it ends, the drivers' slot rotation between them).
+    The events are asserted to have happened; times, step counts and the
+    final packet bits equal orc.ode23 over the same two intervals (its odefun
+    through the C oracle's interpolation, checked bit-identical to the numpy
+    restatement first)."""
+    from oracle import cbind
+    from swraytracing_amd import _lib as L
+    ctx = fresh_ctx
+    c = qg_case
+    nx, Lx, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    flows = [c["flow"]] + [{n: np.asarray(v) * s for n, v in c["flow"].items()} for s in (1.3, -0.7)]
+    planes = [_planes(fl) for fl in flows]
+    rng = np.random.default_rng(31)
+    n = 70_000
+    x = rng.uniform(-Lx / 2, Lx / 2, (n, 2))
+    k = c["k"][rng.integers(0, c["k"].shape[0], n)]
+    tmax = 40 * c["dt"]  # MaxStep 4 dt: the controller rejects some steps at the default tolerances
+    bump = orc.BUMP_QG
+    keys = (L.DEBUG_ODE23_CHAINED, L.DEBUG_ODE23_FIRST_TAKEN, L.DEBUG_ODE23_GUESSES_TAKEN, L.DEBUG_ODE23_SPLIT_RUNS)
+    ctx.set_locality(4, 0)
+    for s in range(3):
+        ctx.set_field_grid(s, planes[s], nx, Lx)
+    ctx.packets_set(x, k)
+    before = [ctx.debug_get(key) for key in keys]
+    ts1, st1 = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump, hook=lambda: ctx.ode23_chain_next(1, 2))
+    ctx.swap_slots(0, 1)
+    ctx.swap_slots(1, 2)  # the armed slots 1 / 2 are now slots 0 / 1
+    ts2, st2 = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump)
+    xg, kg = ctx.packets_get()
+    chained, first, guesses, split = [ctx.debug_get(key) - b for key, b in zip(keys, before)]
+    assert split == 2 and first == 2 and chained == 1, (split, first, chained)
+    assert guesses >= 1 and st1["failed"] + st2["failed"] >= 1, (guesses, st1, st2)
+    dx = Lx / nx
+    rhs = [cbind.raytracing_rhs(planes[i], planes[i + 1], f, Cg, tmax, nx, nx, dx, bump) for i in (0, 1)]
+    sub = _y0(x[:3000], k[:3000])
+    for i, t in ((0, 0.0), (1, 0.37 * tmax)):
+        np.testing.assert_array_equal(rhs[i](t, sub), orc.raytracing_rhs(flows[i], flows[i + 1], f, Cg, tmax, dx)(t, sub))
+    so1, so2 = {}, {}
+    to1, y1 = orc.ode23(rhs[0], [0.0, tmax], _y0(x, k), stats=so1)
+    to2, y2 = orc.ode23(rhs[1], [0.0, tmax], y1, stats=so2)
+    np.testing.assert_array_equal(ts1, to1)
+    np.testing.assert_array_equal(ts2, to2)
+    assert (st1["steps"], st1["failed"]) == (so1["steps"], so1["failed"])
+    assert (st2["steps"], st2["failed"]) == (so2["steps"], so2["failed"])
+    np.testing.assert_array_equal(np.concatenate([xg[:, 0], xg[:, 1], kg[:, 0], kg[:, 1]]), y2)
+
+
+def test_ode23_hook_may_not_touch_the_packets(fresh_ctx, qg_case):
+    """A hook that calls an entry point that may touch the packets (packets_set,
+    advance, packets_get, another ode23 call) is refused with SWRT_ERR_STATE
+    (it would race the interval's attempts in flight); the interval itself
+    completes with the bits of a hook-free run.  QG-stream calls and
+    swrt_ode23_chain_next stay allowed (the drivers' hook)."""
+    ctx = fresh_ctx
+    c = qg_case
+    nx, L, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    ctx.set_field_grid(0, _planes(c["flow"]), nx, L)
+    ctx.set_field_grid(1, _planes({n: np.asarray(v) * 1.3 for n, v in c["flow"].items()}), nx, L)
+    rng = np.random.default_rng(5)
+    n = 70_000
+    x = rng.uniform(-L / 2, L / 2, (n, 2))
+    k = c["k"][rng.integers(0, c["k"].shape[0], n)]
+    tmax = 20 * c["dt"]
+    ctx.set_locality(4, 0)
+    ctx.packets_set(x, k)
+    ts0, _ = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG)
+    x0, k0 = ctx.packets_get()
+    bad = {
+        "packets_set": lambda: ctx.packets_set(x, k),
+        "advance": lambda: ctx.advance(1e-3, 1, f, 1.0, nslots=2, bump=orc.BUMP_QG),
+        "packets_get": ctx.packets_get,
+        "ode23_run": lambda: ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG),
+    }
+    for name, call in bad.items():
+        ctx.packets_set(x, k)
+        with pytest.raises(sw.SwrtError, match="SWRT_ERR_STATE"):
+            ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG, hook=call)
+        x1, k1 = ctx.packets_get()
+        np.testing.assert_array_equal(x1, x0, err_msg=name)
+        np.testing.assert_array_equal(k1, k0, err_msg=name)
+    ctx.packets_set(x, k)
+    ts2, _ = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG, hook=lambda: ctx.ode23_chain_next(0, 1))
+    np.testing.assert_array_equal(ts2, ts0)
+
+
+def test_ode23_chain_dropped_by_a_qg_snapshot_rewrite(fresh_ctx, qg_case):
+    """swrt_qg_snapshot keeps a queued chain (it never touches the packets), so
+    the chain's own check — the slots hold the same nodes, not rewritten
+    since (write generation) — is what drops it when a snapshot rewrites a
+    slot it read, even with identical data (the drivers' CFL-rejection path).
+    The bits then equal the unchained run's."""
+    from swraytracing_amd import _lib as L
+    ctx = fresh_ctx
+    c = qg_case
+    nx, Lx, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    model = sw.QGModel.one_layer(c["qk"], nx, f, Cg, ctx=ctx)
+    model.step(c["dt"])
+    model.snapshot(2)  # slot 2 = grid_U of the QG state's qk
+    snap = ctx.get_field_grid(2, nx)
+    flows = [_planes(c["flow"]), _planes({n: np.asarray(v) * 1.3 for n, v in c["flow"].items()}), snap]
+    rng = np.random.default_rng(37)
+    n = 70_000
+    x = rng.uniform(-Lx / 2, Lx / 2, (n, 2))
+    k = c["k"][rng.integers(0, c["k"].shape[0], n)]
+    tmax = 30 * c["dt"]
+    ctx.set_locality(4, 0)
+
+    def run(arm, rewrite):
+        for s in range(3):
+            if s == 2:
+                model.snapshot(2)
+            else:
+                ctx.set_field_grid(s, flows[s], nx, Lx)
+        ctx.packets_set(x, k)
+        n0 = ctx.debug_get(L.DEBUG_ODE23_CHAINED)
+        hook = (lambda: ctx.ode23_chain_next(1, 2)) if arm else None
+        ts1, _ = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG, hook=hook)
+        ctx.swap_slots(0, 1)
+        ctx.swap_slots(1, 2)
+        if rewrite:
+            model.snapshot(1)  # the same grid_U into the slot the chain read as its slot 1
+        ts2, st2 = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, orc.BUMP_QG)
+        return ts1, ts2, *ctx.packets_get(), ctx.debug_get(L.DEBUG_ODE23_CHAINED) - n0, st2
+
+    ref = run(False, False)
+    np.testing.assert_array_equal(ctx.get_field_grid(1, nx), snap)
+    kept = run(True, False)
+    assert kept[4] == 1
+    dropped = run(True, True)
+    assert dropped[4] == 0
+    for a in (kept, dropped):
+        for u, v in zip(a[:4], ref[:4]):
+            np.testing.assert_array_equal(u, v)
+        assert a[5] == ref[5]
