@@ -370,27 +370,20 @@ def _time_loop(ctx, loop, args, dev, nsteps):
 
 
 def _owner_links():
-    """OwnerLink stand-ins for one GPU: the owner's export without the
-    broadcast, a receiver whose 'broadcast' is already in its buffers."""
+    """The OwnerLink of both legs on one GPU: every step's export (owner) or
+    dt read and snapshot (receiver) on the link's own stream with its event
+    ordering — only the broadcast itself is left out (its buffer already
+    holds what it would carry)."""
     from swraytracing_amd.dist import OwnerLink
 
-    class ExportOnly(OwnerLink):
-        def publish(self, ctx, dt):
-            b = self.bufs[self.cur ^ 1]
-            self._export(ctx, b)
-            b[-1].fill_(float(dt))
-            self.cur ^= 1
-
-    class Preloaded(OwnerLink):
-        def __init__(self, nx, dt):
+    class OneGPU(OwnerLink):  # the link's stream, export, snapshot and dt read, without the broadcast
+        def __init__(self, nx):
             super().__init__(nx, "nccl")
-            self.fixed_dt = dt
 
-        def receive(self):
-            self.cur ^= 1
-            return self.fixed_dt
+        def _bcast(self, b):
+            pass
 
-    return ExportOnly, Preloaded
+    return OneGPU
 
 
 OWNER_WEIGHTS = (0.0, 0.25, 0.5, 1.0)
@@ -408,7 +401,7 @@ def owner_forecast(ctx, w, args, dev, n_total, full_ms):
     with n0 = N w/(w + G - 1) and nr = N/(w + G - 1) (dist.owner_bounds) for
     owner weights w in OWNER_WEIGHTS; per G the step is max(owner, receiver)
     at the best w, efficiency = the one-GPU driver step (all N) / (G x step)."""
-    ExportOnly, Preloaded = _owner_links()
+    OneGPU = _owner_links()
     nx, L, f, Cg = w["nx"], w["L"], w["f"], math.sqrt(w["gH"])
     qk = np.stack([w["qk1"], -w["qk1"]], axis=2)
     nsteps = args.forecast_driver_steps
@@ -424,7 +417,7 @@ def owner_forecast(ctx, w, args, dev, n_total, full_ms):
             U0 = model.max_speed()
             ens = ensemble(n0) if n0 > 0 else None
             loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
-                                   speculate=bool(args.speculate), link=ExportOnly(nx, "nccl"))
+                                   speculate=bool(args.speculate), link=OneGPU(nx))
             legs[("o", n0)] = _time_loop(ctx, loop, args, dev, nsteps)
             loop.settle()
         return legs[("o", n0)]
@@ -433,9 +426,9 @@ def owner_forecast(ctx, w, args, dev, n_total, full_ms):
         if ("r", nr) not in legs:
             model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)  # (a receiving rank holds one too)
             dt = 0.25 * (L / nx) / model.max_speed()
-            link = Preloaded(nx, dt)
-            link.seed(ctx)
-            link.bufs[1].copy_(link.bufs[0])
+            link = OneGPU(nx)
+            for b in link.bufs:  # every step 'receives' this qk and dt
+                link._export(ctx, b, dt)
             loop = sw.ReceiverLoop(link, ensemble(nr), dt, 0.0, nsub=args.substeps)
             legs[("r", nr)] = _time_loop(ctx, loop, args, dev, nsteps)
         return legs[("r", nr)]

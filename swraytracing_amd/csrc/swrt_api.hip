@@ -3377,7 +3377,7 @@ int stream_order(swrt_ctx* c, hipStream_t from, hipStream_t to, int ev) {
 }
 }  // namespace
 
-int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_on_device, void* stream) {
+int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_on_device, void* stream, double tail) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
@@ -3394,11 +3394,14 @@ int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_on_de
   if (dst_on_device) {
     const hipStream_t ext = stream ? (hipStream_t)stream : on_qg.saved;
     HIPCHK_RC(stream_order(c, ext, c->stream, 0));  // the caller's last read of dst
-    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    hipLaunchKernelGGL(export_half_kernel, dim3(nblocks(q.nhalf + 1, 256)), dim3(256), 0, c->stream, src, dst,
+                       q.nhalf, tail);
+    HIPCHK(c, hipGetLastError());
     HIPCHK_RC(stream_order(c, c->stream, ext, 1));  // the caller's next use of dst
   } else {
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    dst[2 * q.nhalf] = tail;
   }
   return SWRT_OK;
   GUARD_END(c)

@@ -560,6 +560,19 @@ __global__ void halfplane_relayout_kernel(const double2* in, double2* out, int n
   }
 }
 
+// swrt_qg_export: a half plane copied out and `tail` stored right after it
+// (the owner driver's one broadcast buffer: qk's top layer, then dt)
+__global__ void export_half_kernel(const double2* src, double* dst, int64_t nh, double tail) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nh) {
+    const double2 v = src[i];
+    dst[2 * i] = v.x;
+    dst[2 * i + 1] = v.y;
+  } else if (i == nh) {
+    dst[2 * nh] = tail;
+  }
+}
+
 __global__ void real_part_kernel(const double2* Z, double* out, int64_t cnt) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < cnt) out[i] = Z[i].x;

@@ -138,15 +138,22 @@ def allreduce_max_fn(backend: str = "nccl", group=None):
 class OwnerLink:
     """The PDE-owner driver's per-step hand-off (qg2layersw_raytrace.m:152-197
     sharded with the PDE on ONE rank): the packets read only the top layer of
-    qk (:186-188), so the owner rank broadcasts that layer's spectral PV
-    (the (2kmax+1)(kmax+1) half plane, 2.1 MB at 512^2) and the step's dt after
+    qk (:186-188), so the owner rank broadcasts that layer's spectral PV (the
+    (2kmax+1)(kmax+1) half plane, 2.1 MB at 512^2) with the step's dt after
     every PDE step, and every other rank builds its snapshots from it
     (swrt_snapshot_qk: bit for bit the owner's swrt_qg_snapshot) instead of
-    stepping the replicated 2-layer PDE.  One broadcast per step of a
-    device buffer on "nccl" (RCCL over xGMI; the export and the snapshot are
-    ordered on torch's current stream, the host reads only the dt word), of
-    a host buffer on "gloo".  Two buffers in turn: the current step's and
-    the previous step's qk (the first active step's grid_U(prev_qk))."""
+    stepping the replicated 2-layer PDE.
+
+    "nccl" (RCCL over xGMI): one broadcast of a device buffer per step on a
+    stream of its own (a non-blocking torch stream, so it runs beside the
+    owner's next PDE step and the receivers' packet launches); swrt_qg_export
+    fills the buffer (qk, then dt) on the QG stream and swrt_snapshot_qk reads
+    it there, each ordered against this stream by events; the host reads only
+    the dt word.  "gloo": the same through host buffers.  Two buffers in turn:
+    the current step's and the previous step's qk (the first active step's
+    grid_U(prev_qk)); a buffer is refilled only after the snapshot that read
+    it, which also bounds how far a receiving rank's host runs ahead of its
+    GPU (to ~2 steps: queued snapshots then always find an idle slot buffer)."""
 
     def __init__(self, nx, backend, owner=0, group=None):
         import torch
@@ -156,19 +163,27 @@ class OwnerLink:
         self.owner, self.group = owner, group
         self.device = backend == "nccl"
         dev = torch.device("cuda", torch.cuda.current_device()) if self.device else torch.device("cpu")
+        self.stream = torch.cuda.Stream(device=dev) if self.device else None
         # [qk half plane (2*nh doubles) | dt]
         self.bufs = [torch.zeros(2 * self.nh + 1, dtype=torch.float64, device=dev) for _ in range(2)]
         self.cur = 0  # the buffer holding the latest qk
 
-    def _stream(self):
-        import torch
-        return torch.cuda.current_stream().cuda_stream
+    def _on_stream(self):
+        import contextlib
 
-    def _export(self, ctx, b, which=0):
+        import torch
+        return torch.cuda.stream(self.stream) if self.device else contextlib.nullcontext()
+
+    def _export(self, ctx, b, dt=0.0):
         if self.device:
-            ctx.qg_export(b.data_ptr(), which=which, layer=0, stream=self._stream())
+            ctx.qg_export(b.data_ptr(), which=0, layer=0, stream=self.stream.cuda_stream, tail=dt)
         else:
-            ctx.qg_export(b[: 2 * self.nh].numpy(), which=which, layer=0)
+            ctx.qg_export(b.numpy(), which=0, layer=0, tail=dt)
+
+    def _bcast(self, b):
+        import torch.distributed as dist
+        with self._on_stream():
+            dist.broadcast(b, src=self.owner, group=self.group)
 
     def seed(self, ctx):
         """Every rank: the model's initial qk as the 'previous' buffer (all
@@ -177,25 +192,24 @@ class OwnerLink:
 
     def publish(self, ctx, dt):
         """Owner: the committed current qk's top layer and dt to every rank."""
-        import torch.distributed as dist
         b = self.bufs[self.cur ^ 1]
-        self._export(ctx, b)
-        b[-1].fill_(float(dt))
-        dist.broadcast(b, src=self.owner, group=self.group)
+        self._export(ctx, b, dt)
+        self._bcast(b)
         self.cur ^= 1
 
     def receive(self):
         """Receiver: the owner's next (qk, dt); returns dt (a host float)."""
-        import torch.distributed as dist
         b = self.bufs[self.cur ^ 1]
-        dist.broadcast(b, src=self.owner, group=self.group)
+        self._bcast(b)
         self.cur ^= 1
-        return float(b[-1].item())
+        with self._on_stream():
+            return float(b[-1].item())
 
     def snapshot(self, ctx, slot, which, L, K_d2, shear, k_scale, ny_period):
         """grid_U of the latest (which 0) or the previous (1) qk into `slot`."""
         b = self.bufs[self.cur if which == 0 else self.cur ^ 1]
         if self.device:
-            ctx.snapshot_qk(slot, b.data_ptr(), self.nx, L, K_d2, shear, k_scale, ny_period, stream=self._stream())
+            ctx.snapshot_qk(slot, b.data_ptr(), self.nx, L, K_d2, shear, k_scale, ny_period,
+                            stream=self.stream.cuda_stream)
         else:
             ctx.snapshot_qk(slot, b[: 2 * self.nh].numpy(), self.nx, L, K_d2, shear, k_scale, ny_period)

@@ -187,9 +187,10 @@ class _FakeQG:
         self.nh = nh
         self.qk = None
 
-    def qg_export(self, dst, which=0, layer=0, stream=None):
-        assert which == 0 and layer == 0
-        dst[:] = self.qk
+    def qg_export(self, dst, which=0, layer=0, stream=None, tail=0.0):
+        assert which == 0 and layer == 0 and dst.size == self.nh * 2 + 1
+        dst[:-1] = self.qk
+        dst[-1] = tail
 
 
 class _FakeSnap:
