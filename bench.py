@@ -415,7 +415,7 @@ def owner_forecast(ctx, w, args, dev, n_total, full_ms):
         if ("o", n0) not in legs:
             model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
             U0 = model.max_speed()
-            ens = ensemble(n0) if n0 > 0 else None
+            ens = ensemble(n0)  # (n0 = 0: an empty ensemble — the context then holds no packets, as the owner's)
             loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
                                    speculate=bool(args.speculate), link=OneGPU(nx))
             legs[("o", n0)] = _time_loop(ctx, loop, args, dev, nsteps)

@@ -487,8 +487,9 @@ int swrt_qg_snapshot_speculative(swrt_ctx* ctx, int slot, int64_t ny_period);
  * qk, after `stream`'s work queued so far (its last read of dst) and before
  * `stream`'s later work (stream: a hipStream_t of the caller, e.g. the one a
  * broadcast is queued on; NULL = the context's packet stream).  0: host
- * memory, returns once copied.  SWRT_ERR_STATE while a speculative step is
- * pending (swrt_qg_resolve first). */
+ * memory, returns once copied.  The committed state is exported: a pending
+ * speculative step (swrt_qg_step_speculative) is neither waited for nor
+ * included. */
 int swrt_qg_export(swrt_ctx* ctx, int which, int layer, double* dst, int dst_on_device, void* stream, double tail);
 /* grid_U (grid_U.m:1-18: psi = -q/(K_d2 + K^2), u += shear) of a half plane in
  * swrt_qg_export's order into packet slot `slot`: bit for bit the

@@ -3383,7 +3383,8 @@ int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_on_de
   OnQGStream on_qg(c);
   QGState& q = c->qg;
   if (!q.init) return fail(c, SWRT_ERR_STATE, "swrt_qg_init not called");
-  if (q.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
+  // (a pending speculative step writes the spare buffers only: the committed
+  // qk and prev_qk stay as they are until swrt_qg_resolve)
   if (!dst) return fail(c, SWRT_ERR_ARG, "dst is NULL");
   if (which != 0 && which != 1) return fail(c, SWRT_ERR_ARG, "which must be 0 (current) or 1 (previous)");
   if (which == 1 && !q.has_prev) return fail(c, SWRT_ERR_STATE, "no previous qk before the first step");

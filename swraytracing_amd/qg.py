@@ -313,11 +313,15 @@ class TwoLayerLoop:
         else:
             self.model.step(self.dt)
             self.model.max_speed_async()
-        if self.link is not None:
-            self.link.publish(self.model.ctx, self.dt)  # the committed qk of this step, before the next is queued
         self.t = self.t + self.dt
         active = self.ens is not None and self.t > self.packet_delay
         spec = self.speculate and self.model.params.nlayers == 2 and getattr(self.model.ctx, "qg_fused", True)
+        # ode23 intervals of a sharded run hold collectives (the error norm's
+        # allreduce per attempt): the owner publishes before its interval, as
+        # the receivers need this step's qk before theirs
+        publish_first = self.link is not None and self.group is not None and self.group.integrator == "ode23"
+        if publish_first:
+            self.link.publish(self.model.ctx, self.dt)
         if active and self.ens.n == 0:
             # an owner without packets: no snapshots; the interval still runs
             # (ode23: its error-norm collectives) with the speculative step inside
@@ -364,6 +368,11 @@ class TwoLayerLoop:
             self._spec_snap = False
         if spec:
             self.model.step_speculative(self.dt)
+        if self.link is not None and not publish_first:
+            # this step's committed qk to the other ranks: queued after the
+            # next (speculative) step, so its host calls are off the PDE's
+            # critical path (U0 read-back -> CFL rule -> next step)
+            self.link.publish(self.model.ctx, self.dt)
         self.U0 = self.model.max_speed_result()  # this step's (read-backs pop oldest first)
         return active
 
@@ -387,7 +396,8 @@ class ReceiverLoop:
     this rank's packets take the interval [t, t+dt] exactly as the owner's
     TwoLayerLoop does (same t, dt sequence, active steps and frame points)."""
 
-    def __init__(self, link, ens, dt, packet_delay=0.0, nsub=5, packet_intervals=1, integrator="leapfrog"):
+    def __init__(self, link, ens, dt, packet_delay=0.0, nsub=5, packet_intervals=1, integrator="leapfrog",
+                 ahead=2):
         self.link, self.ens, self.dt = link, ens, dt
         self.packet_delay = packet_delay
         self.t = 0.0
@@ -395,6 +405,18 @@ class ReceiverLoop:
         self.dts = []
         self.have_cur = False
         self.group = _IntervalGroup(ens.ctx, ens, packet_intervals, nsub, integrator) if ens is not None else None
+        # The host queues step n only once the packet work of step n - ahead
+        # has finished.  Unpaced, a receiver whose packets are slower than the
+        # owner's PDE queues snapshots until every spare slot buffer still
+        # looks in use; the next snapshot then waits for the packet launch
+        # before it and packets and snapshots run one after the other
+        # (swrt_qg_snapshot's renaming decides at queue time).
+        self.ahead = int(ahead)
+        self._done = []
+        self._pk = None
+        if self.ahead > 0 and ens is not None and ens.n > 0 and getattr(link, "device", False):
+            import torch
+            self._pk = torch.cuda.ExternalStream(ens.ctx.stream())
 
     def _snapshot(self, slot, which):
         e = self.ens
@@ -408,11 +430,18 @@ class ReceiverLoop:
         active = self.ens is not None and self.t > self.packet_delay
         if active:
             if self.ens.n > 0:
+                if len(self._done) >= self.ahead:
+                    self._done.pop(0).synchronize()
                 if not self.have_cur:
                     self._snapshot(0, 1)  # grid_U(prev_qk)
                 self._snapshot(self.group.next_slot(), 0)  # grid_U(qk)
                 self.have_cur = True
             self.group.add(self.dt)
+            if self._pk is not None:
+                import torch
+                ev = torch.cuda.Event()
+                ev.record(self._pk)
+                self._done.append(ev)
         else:
             self.have_cur = False
         return active
