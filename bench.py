@@ -376,12 +376,19 @@ def _owner_links():
     holds what it would carry)."""
     from swraytracing_amd.dist import OwnerLink
 
-    class OneGPU(OwnerLink):  # the link's stream, export, snapshot and dt read, without the broadcast
-        def __init__(self, nx):
+    class OneGPU(OwnerLink):  # the link's stream, export and snapshot, without the broadcasts
+        def __init__(self, nx, dt=0.0):
             super().__init__(nx, "nccl")
+            self.fixed_dt = dt
 
         def _bcast(self, b):
             pass
+
+        def _send_dt(self, dt):
+            pass
+
+        def _recv_dt(self, b):
+            return self.fixed_dt
 
     return OneGPU
 
@@ -424,13 +431,17 @@ def owner_forecast(ctx, w, args, dev, n_total, full_ms):
 
     def receiver_ms(nr):
         if ("r", nr) not in legs:
+            ctx.qg_set_stream(False)  # a receiving rank's snapshots run in series with its packets (qg.py)
+            ctx.set_packet_streams(1)
             model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)  # (a receiving rank holds one too)
             dt = 0.25 * (L / nx) / model.max_speed()
-            link = OneGPU(nx)
+            link = OneGPU(nx, dt)
             for b in link.bufs:  # every step 'receives' this qk and dt
                 link._export(ctx, b, dt)
             loop = sw.ReceiverLoop(link, ensemble(nr), dt, 0.0, nsub=args.substeps)
             legs[("r", nr)] = _time_loop(ctx, loop, args, dev, nsteps)
+            ctx.qg_set_stream(bool(args.qg_stream))
+            ctx.set_packet_streams(args.packet_streams)
         return legs[("r", nr)]
 
     out = {"what": "PDE-owner form (qg.py OwnerLink/ReceiverLoop): rank 0 = TwoLayerLoop with n0 packets + qk export; "

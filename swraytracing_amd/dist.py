@@ -138,35 +138,47 @@ def allreduce_max_fn(backend: str = "nccl", group=None):
 class OwnerLink:
     """The PDE-owner driver's per-step hand-off (qg2layersw_raytrace.m:152-197
     sharded with the PDE on ONE rank): the packets read only the top layer of
-    qk (:186-188), so the owner rank broadcasts that layer's spectral PV (the
-    (2kmax+1)(kmax+1) half plane, 2.1 MB at 512^2) with the step's dt after
+    qk (:186-188), so the owner rank sends that layer's spectral PV (the
+    (2kmax+1)(kmax+1) half plane, 2.1 MB at 512^2) and the step's dt after
     every PDE step, and every other rank builds its snapshots from it
     (swrt_snapshot_qk: bit for bit the owner's swrt_qg_snapshot) instead of
     stepping the replicated 2-layer PDE.
 
-    "nccl" (RCCL over xGMI): one broadcast of a device buffer per step on a
-    stream of its own (a non-blocking torch stream, so it runs beside the
-    owner's next PDE step and the receivers' packet launches); swrt_qg_export
-    fills the buffer (qk, then dt) on the QG stream and swrt_snapshot_qk reads
-    it there, each ordered against this stream by events; the host reads only
-    the dt word.  "gloo": the same through host buffers.  Two buffers in turn:
-    the current step's and the previous step's qk (the first active step's
-    grid_U(prev_qk)); a buffer is refilled only after the snapshot that read
-    it, which also bounds how far a receiving rank's host runs ahead of its
-    GPU (to ~2 steps: queued snapshots then always find an idle slot buffer)."""
+    "nccl" (RCCL over xGMI): the half plane goes by one broadcast of a device
+    buffer per step on a stream of its own (a non-blocking torch stream), so
+    it runs beside the owner's next PDE step and the receivers' packet
+    launches; swrt_qg_export fills the buffer on the QG stream and
+    swrt_snapshot_qk reads it, each ordered against that stream by events —
+    no host synchronisation on the device data.  dt, which a receiving host
+    needs to queue its packets, goes by a host-side broadcast on a gloo group
+    (reading it back from the device would wait behind the packet launches
+    that hold the GPU).  "gloo": both through one host buffer.  Two buffers in
+    turn: the current step's and the previous step's qk (the first active
+    step's grid_U(prev_qk)); swrt_snapshot_qk orders the next fill of a
+    buffer after its read."""
 
-    def __init__(self, nx, backend, owner=0, group=None):
+    def __init__(self, nx, backend, owner=0, group=None, device=None):
+        """``device``: device buffers (default: with "nccl"); True with
+        "gloo" runs the device form over gloo's CUDA-tensor broadcast (the
+        tests' way to exercise it with ranks sharing one GPU)."""
         import torch
         kmax = nx // 2 - 1
         self.nx = int(nx)
         self.nh = (2 * kmax + 1) * (kmax + 1)
         self.owner, self.group = owner, group
-        self.device = backend == "nccl"
+        self.device = (backend == "nccl") if device is None else bool(device)
         dev = torch.device("cuda", torch.cuda.current_device()) if self.device else torch.device("cpu")
         self.stream = torch.cuda.Stream(device=dev) if self.device else None
         # [qk half plane (2*nh doubles) | dt]
         self.bufs = [torch.zeros(2 * self.nh + 1, dtype=torch.float64, device=dev) for _ in range(2)]
         self.cur = 0  # the buffer holding the latest qk
+        self.dt_group = None
+        self._dt = [torch.zeros(1, dtype=torch.float64) for _ in range(2)]
+        self._dt_work = None
+        if self.device:
+            import torch.distributed as dist
+            if dist.is_available() and dist.is_initialized():
+                self.dt_group = dist.new_group(backend="gloo")  # (a collective: every rank builds the link)
 
     def _on_stream(self):
         import contextlib
@@ -185,6 +197,24 @@ class OwnerLink:
         with self._on_stream():
             dist.broadcast(b, src=self.owner, group=self.group)
 
+    def _send_dt(self, dt):
+        if not self.device:
+            return  # (the host buffer carried it)
+        import torch.distributed as dist
+        if self._dt_work is not None:
+            self._dt_work.wait()
+        t = self._dt[self.cur]
+        t[0] = float(dt)
+        self._dt_work = dist.broadcast(t, src=self.owner, group=self.dt_group, async_op=True)
+
+    def _recv_dt(self, b):
+        if not self.device:
+            return float(b[-1])
+        import torch.distributed as dist
+        t = self._dt[self.cur]
+        dist.broadcast(t, src=self.owner, group=self.dt_group)
+        return float(t[0])
+
     def seed(self, ctx):
         """Every rank: the model's initial qk as the 'previous' buffer (all
         ranks hold the same initial state)."""
@@ -196,14 +226,21 @@ class OwnerLink:
         self._export(ctx, b, dt)
         self._bcast(b)
         self.cur ^= 1
+        self._send_dt(dt)
 
     def receive(self):
-        """Receiver: the owner's next (qk, dt); returns dt (a host float)."""
+        """Receiver: the owner's next (qk, dt); returns dt (a host float).
+        The qk half plane may still be in flight (device): the snapshot that
+        reads it waits for it on the device."""
         b = self.bufs[self.cur ^ 1]
         self._bcast(b)
         self.cur ^= 1
-        with self._on_stream():
-            return float(b[-1].item())
+        return self._recv_dt(b)
+
+    def close(self):
+        if self._dt_work is not None:
+            self._dt_work.wait()
+            self._dt_work = None
 
     def snapshot(self, ctx, slot, which, L, K_d2, shear, k_scale, ny_period):
         """grid_U of the latest (which 0) or the previous (1) qk into `slot`."""

@@ -424,14 +424,14 @@ class ReceiverLoop:
 
     def step(self):
         self.steps += 1
+        if len(self._done) >= self.ahead:
+            self._done.pop(0).synchronize()
         self.dt = self.link.receive()
         self.dts.append(self.dt)
         self.t = self.t + self.dt
         active = self.ens is not None and self.t > self.packet_delay
         if active:
             if self.ens.n > 0:
-                if len(self._done) >= self.ahead:
-                    self._done.pop(0).synchronize()
                 if not self.have_cur:
                     self._snapshot(0, 1)  # grid_U(prev_qk)
                 self._snapshot(self.group.next_slot(), 0)  # grid_U(qk)
@@ -497,6 +497,9 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     if link is not None:
         link.seed(ctx)
     owner = link is None or rank == 0  # this rank steps the PDE
+    if not owner:
+        ctx.qg_set_stream(False)  # (snapshots in series with the packets, as in qg2layersw_raytrace)
+        ctx.set_packet_streams(1)
     U0 = model.max_speed()
     Fr = U0 / Cg
     T = T_days / Fr ** 2
@@ -552,6 +555,8 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
         log.progress(step, Nsteps)
     if group is not None:
         group.flush()
+    if link is not None:
+        link.close()
     ctx.synchronize()
     log.finish()
     log.close()
@@ -618,6 +623,11 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
         write_field(model.q(), os.path.join(out_dir, "pv"))
         write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
     if link is not None and rank != 0:
+        # a receiving rank runs its snapshots on the packet stream: beside its
+        # packet launches the transforms run several times slower (they find
+        # no free slots), so in series they cost less (bench.py owner legs)
+        ctx.qg_set_stream(False)
+        ctx.set_packet_streams(1)  # (the snapshot follows the whole previous launch, not beside its second part)
         loop = ReceiverLoop(link, ens, dt, packet_delay_steps, nsub, packet_intervals, integrator)
     else:
         loop = TwoLayerLoop(model, ens, dt, U0, CFL_fraction, packet_delay_steps, nsub, packet_intervals, integrator,
@@ -633,6 +643,8 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
         log.progress(loop.steps, Nsteps)
     loop.flush()
     loop.settle()
+    if link is not None:
+        link.close()
     ctx.synchronize()
     log.finish()
     log.close()
