@@ -236,9 +236,10 @@ def _fresh_outputs(out_dir, fresh):
             os.remove(p)
 
 
-def _owner_setup(world, pde, owner_weight, nx, Npackets):
+def _owner_setup(world, pde, owner_weight, nx, Npackets, link_buffers="auto"):
     """(link, bounds) of a sharded run in the PDE-owner form, or (None, None)
-    for the replicated form (every rank steps the PDE)."""
+    for the replicated form (every rank steps the PDE).  link_buffers: "auto"
+    (device buffers with nccl, host buffers with gloo), "device" or "host"."""
     if world <= 1 or pde == "replicated":
         return None, None
     if pde != "owner":
@@ -246,7 +247,8 @@ def _owner_setup(world, pde, owner_weight, nx, Npackets):
     import torch.distributed as dist
 
     from .dist import OwnerLink, owner_bounds
-    return OwnerLink(nx, dist.get_backend()), owner_bounds(Npackets, world, owner_weight)
+    device = {"auto": None, "device": True, "host": False}[link_buffers]
+    return OwnerLink(nx, dist.get_backend(), device=device), owner_bounds(Npackets, world, owner_weight)
 
 
 OWNER_WEIGHT = 0.5  # packets of the PDE owner per packet of a receiving rank (bench.py driver_step_forecast "owner")
@@ -457,7 +459,7 @@ class ReceiverLoop:
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
                   out_dir="data", nsub=4, max_steps=None, seed=146, verbose=False, r_drag=0.1,
                   packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None,
-                  pde="owner", owner_weight=OWNER_WEIGHT):
+                  pde="owner", owner_weight=OWNER_WEIGHT, link_buffers="auto"):
     """qgsw_raytrace.m:1-180 with the PDE and the packets on the GPU.
 
     Writes ``out_dir``/packet_x.bin, packet_k.bin, packet_time.bin, pv.bin,
@@ -493,7 +495,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     qk = ctx.g2k(q)
     x, k = _packets(Npackets, L, near_inertial_factor, f, Cg, rng)
     model = QGModel.one_layer(qk, nx, f, Cg, r_drag=r_drag, ctx=ctx)
-    link, bounds = _owner_setup(world, pde, owner_weight, nx, Npackets)
+    link, bounds = _owner_setup(world, pde, owner_weight, nx, Npackets, link_buffers)
     if link is not None:
         link.seed(ctx)
     owner = link is None or rank == 0  # this rank steps the PDE
@@ -567,7 +569,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
 def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
                         out_dir="data", nsub=5, max_steps=None, seed=5, verbose=False,
                         packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None,
-                        pde="owner", owner_weight=OWNER_WEIGHT):
+                        pde="owner", owner_weight=OWNER_WEIGHT, link_buffers="auto"):
     """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
     (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and
     interpolate's 2*nx y-period).  Same packet outputs as :func:`qgsw_raytrace`;
@@ -579,7 +581,9 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     ranks, which only build snapshots and advance packets; rank 0 holds
     ``owner_weight`` packets per packet of another rank (dist.owner_bounds).
     ``pde="replicated"``: every rank steps the same PDE, packets split evenly.
-    Both write the single-process files byte for byte."""
+    Both write the single-process files byte for byte.  ``link_buffers``: the
+    owner link's buffers ("auto": on the device with nccl, on the host with
+    gloo; "device" / "host" to force one)."""
     ctx = ctx if ctx is not None else Context(0)
     rank, world = _dist_info()  # sharded run: packets split over the ranks
     if rank == 0:
@@ -602,7 +606,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     qk = np.stack([qk1, qk2], axis=2)
     x, k = _packets(Npackets, L, near_inertial_factor, f, Cg, rng)
     model = QGModel.two_layer(qk, nx, f, Cg, L=L, shear=shear, ctx=ctx)  # (every rank: the same U0, T, dt)
-    link, bounds = _owner_setup(world, pde, owner_weight, nx, Npackets)
+    link, bounds = _owner_setup(world, pde, owner_weight, nx, Npackets, link_buffers)
     if link is not None:
         link.seed(ctx)
     U0 = model.max_speed()

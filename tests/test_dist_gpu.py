@@ -100,13 +100,13 @@ import swraytracing_amd as sw
 torch.cuda.set_device(0)
 dist.init_process_group("gloo")
 ctx = sw.Context(0)
-drv, integrator, pde, w0 = sys.argv[2], sys.argv[3], sys.argv[4], float(sys.argv[5])
+drv, integrator, pde, w0, lb = sys.argv[2], sys.argv[3], sys.argv[4], float(sys.argv[5]), sys.argv[6]
 if drv == "qg2":
     sw.qg2layersw_raytrace(64, 5001, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=sys.argv[1], nsub=2, max_steps=30,
-                           seed=5, integrator=integrator, ctx=ctx, pde=pde, owner_weight=w0)
+                           seed=5, integrator=integrator, ctx=ctx, pde=pde, owner_weight=w0, link_buffers=lb)
 else:
     sw.qgsw_raytrace(64, 4001, 4.0, 20.0, 0.0, 0.2, 3.0, 1.0, out_dir=sys.argv[1], nsub=2, max_steps=24,
-                     integrator=integrator, r_drag=0.0, ctx=ctx, pde=pde, owner_weight=w0)
+                     integrator=integrator, r_drag=0.0, ctx=ctx, pde=pde, owner_weight=w0, link_buffers=lb)
 ctx.close()
 dist.destroy_process_group()
 """
@@ -140,17 +140,24 @@ def _rank_report(stderr, tail=40):
     return "\n".join(f"--- {k} ---\n" + "\n".join(v[-tail:]) for k, v in sorted(by.items()))
 
 
-@pytest.mark.parametrize("drv,world,pde,w0,integrator", [
-    ("qg2", 2, "replicated", 1.0, "leapfrog"),
-    ("qg2", 2, "replicated", 1.0, "ode23"),
-    ("qg2", 2, "owner", 0.5, "leapfrog"),
-    ("qg2", 2, "owner", 0.5, "ode23"),
-    ("qg2", 4, "owner", 0.5, "leapfrog"),
-    ("qg2", 4, "owner", 0.5, "ode23"),
-    ("qg2", 2, "owner", 0.0, "ode23"),  # the owner holds no packets: it only joins the collectives
-    ("qg1", 2, "owner", 0.5, "leapfrog"),
+@pytest.mark.parametrize("drv,world,pde,w0,integrator,lb", [
+    ("qg2", 2, "replicated", 1.0, "leapfrog", "auto"),
+    ("qg2", 2, "replicated", 1.0, "ode23", "auto"),
+    ("qg2", 2, "owner", 0.5, "leapfrog", "host"),
+    ("qg2", 2, "owner", 0.5, "ode23", "host"),
+    ("qg2", 4, "owner", 0.5, "leapfrog", "host"),
+    ("qg2", 4, "owner", 0.5, "ode23", "host"),
+    ("qg2", 2, "owner", 0.0, "ode23", "host"),  # the owner holds no packets: it only joins the collectives
+    ("qg1", 2, "owner", 0.5, "leapfrog", "host"),
+    # the nccl form of the link (device buffers, export / snapshot ordered by
+    # events on the link's stream, dt on a gloo side group) over gloo's
+    # CUDA-tensor broadcast: RCCL itself needs one GPU per rank
+    ("qg2", 2, "owner", 0.5, "leapfrog", "device"),
+    ("qg2", 4, "owner", 0.25, "leapfrog", "device"),
+    ("qg2", 2, "owner", 0.5, "ode23", "device"),
+    ("qg1", 2, "owner", 0.5, "leapfrog", "device"),
 ])
-def test_sharded_driver_files_equal_single_process(ctx, tmp_path, drv, world, pde, w0, integrator):
+def test_sharded_driver_files_equal_single_process(ctx, tmp_path, drv, world, pde, w0, integrator, lb):
     """The drivers sharded over `world` ranks sharing GPU 0 (gloo), frames
     gathered on the device and written by rank 0, ode23's error norm
     max-reduced over the ranks: with the replicated PDE (every rank steps it,
@@ -165,7 +172,7 @@ def test_sharded_driver_files_equal_single_process(ctx, tmp_path, drv, world, pd
     env = dict(os.environ, SWRT_ROOT=ROOT)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(tmp_path / "driver.py"), str(out),
-           drv, integrator, pde, str(w0)]
+           drv, integrator, pde, str(w0), lb]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, _rank_report(r.stderr)
     for name, a in ref.items():
