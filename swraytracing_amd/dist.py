@@ -228,25 +228,36 @@ class OwnerLink:
         self.cur ^= 1
         self._send_dt(dt)
 
-    def receive(self):
+    def receive(self, wait=False):
         """Receiver: the owner's next (qk, dt); returns dt (a host float).
-        The qk half plane may still be in flight (device): the snapshot that
-        reads it waits for it on the device."""
+        The qk half plane may still be in flight (device) — the snapshot that
+        reads it waits for it on the device — unless ``wait``: then the host
+        waits for it here (see snapshot's ``fenced``)."""
         b = self.bufs[self.cur ^ 1]
         self._bcast(b)
         self.cur ^= 1
-        return self._recv_dt(b)
+        dt = self._recv_dt(b)
+        if wait and self.device:
+            self.stream.synchronize()
+        return dt
 
     def close(self):
         if self._dt_work is not None:
             self._dt_work.wait()
             self._dt_work = None
 
-    def snapshot(self, ctx, slot, which, L, K_d2, shear, k_scale, ny_period):
-        """grid_U of the latest (which 0) or the previous (1) qk into `slot`."""
+    def snapshot(self, ctx, slot, which, L, K_d2, shear, k_scale, ny_period, fenced=False):
+        """grid_U of the latest (which 0) or the previous (1) qk into `slot`.
+        ``fenced``: the caller guarantees the order itself — the buffer's
+        broadcast has completed (receive(wait=True)) and its next fill comes
+        only after this snapshot has run (ReceiverLoop's pacing) — so no event
+        ties the library's stream to the link's.  (A cross-stream wait on the
+        link stream measured ~0.2 ms per step on ROCm beside packet launches:
+        every hop of a barrier between queues waits on the command processor,
+        tools/owner_legs.py.)"""
         b = self.bufs[self.cur if which == 0 else self.cur ^ 1]
         if self.device:
             ctx.snapshot_qk(slot, b.data_ptr(), self.nx, L, K_d2, shear, k_scale, ny_period,
-                            stream=self.stream.cuda_stream)
+                            stream=None if fenced else self.stream.cuda_stream)
         else:
             ctx.snapshot_qk(slot, b[: 2 * self.nh].numpy(), self.nx, L, K_d2, shear, k_scale, ny_period)

@@ -419,16 +419,26 @@ class ReceiverLoop:
         if self.ahead > 0 and ens is not None and ens.n > 0 and getattr(link, "device", False):
             import torch
             self._pk = torch.cuda.ExternalStream(ens.ctx.stream())
+        # device link with pacing: the host waits for each broadcast and the
+        # pacing orders the buffers' refills, so the snapshots need no
+        # cross-stream events (OwnerLink.snapshot fenced; at most 2 steps ahead:
+        # a buffer is refilled two receives after the snapshot that read it)
+        self._fenced = self._pk is not None and self.ahead <= 2
+        self._prev_read = False
 
     def _snapshot(self, slot, which):
         e = self.ens
-        self.link.snapshot(e.ctx, slot, which, e.L, e.K_d2, e.shear, e.k_scale, e.ny_period)
+        self.link.snapshot(e.ctx, slot, which, e.L, e.K_d2, e.shear, e.k_scale, e.ny_period, fenced=self._fenced)
 
     def step(self):
         self.steps += 1
-        if len(self._done) >= self.ahead:
+        if self._done and len(self._done) >= self.ahead:
             self._done.pop(0).synchronize()
-        self.dt = self.link.receive()
+        if self._prev_read:
+            # last step's grid_U(prev_qk) read the buffer this receive refills
+            self._done[-1].synchronize()
+            self._prev_read = False
+        self.dt = self.link.receive(wait=self._fenced)
         self.dts.append(self.dt)
         self.t = self.t + self.dt
         active = self.ens is not None and self.t > self.packet_delay
@@ -436,6 +446,7 @@ class ReceiverLoop:
             if self.ens.n > 0:
                 if not self.have_cur:
                     self._snapshot(0, 1)  # grid_U(prev_qk)
+                    self._prev_read = self._fenced
                 self._snapshot(self.group.next_slot(), 0)  # grid_U(qk)
                 self.have_cur = True
             self.group.add(self.dt)

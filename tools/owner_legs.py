@@ -92,8 +92,17 @@ def main():
         def adv():
             ens.advance_intervals([dt], 5)
 
+        def snap_ev():
+            ctx.snapshot_qk(1, link.bufs[0].data_ptr(), nx, L, f / Cg, 0.5, 2 * math.pi / L, 2 * nx,
+                            stream=link.stream.cuda_stream)
+
+        def swap():
+            ctx.swap_slots(0, 1)
+
         res = {}
-        for name, fns in (("snapshot", [snap]), ("packets", [adv]), ("both", [snap, adv])):
+        for name, fns in (("snapshot", [snap]), ("packets", [adv]), ("both", [snap, adv]),
+                          ("snapshot_ev", [snap_ev]), ("both_ev", [snap_ev, adv]), ("both_swap", [snap, adv, swap]),
+                          ("both_ev_swap", [snap_ev, adv, swap])):
             for rep in range(2):
                 ctx.synchronize()
                 t0 = time.perf_counter()
