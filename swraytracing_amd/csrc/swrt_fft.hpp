@@ -461,6 +461,30 @@ __global__ void spectra_kernel(const double2* fk, int n, int mode, double K_d2, 
   spectra_at(idx, fk, n, mode, K_d2, kscale, with_psi, Z, sx, sy);
 }
 
+// spectra_kernel fused with the first (row) pass of the inverse 2-D FFT:
+// workgroup r builds row r of the nb grid_U planes in LDS with spectra_to
+// and runs their inverse row FFTs side by side (n/4 lanes each,
+// fft_stages_one_buffer), writing what the spectra launch followed by the
+// in-place row pass writes — the same element function and per-vector FFT,
+// so the same bits (qg_post_rows_kernel's construction, for a grid_U alone:
+// swrt_set_field_qk / swrt_snapshot_qk / the unfused swrt_qg_snapshot).
+// blockDim nb*n/4 <= 1024, dynamic LDS nb*n double2.
+__global__ void __launch_bounds__(1024) spectra_rows_kernel(const double2* fk, int n, int mode, double K_d2,
+                                                            double kscale, int with_psi, int sx, int sy, int logn,
+                                                            const double2* tw, double2* out) {
+  extern __shared__ double2 rows[];
+  const int nb = with_psi ? 4 : 3;
+  const int64_t nn = (int64_t)n * n;
+  const int r = blockIdx.x;
+  for (int e = threadIdx.x; e < n; e += blockDim.x)
+    spectra_to((int64_t)e + (int64_t)n * r, fk, n, mode, K_d2, kscale, with_psi, LdsRowPlanes{rows, n}, sx, sy);
+  __syncthreads();
+  const int q = n >> 2;
+  fft_stages_one_buffer(rows + (threadIdx.x / q) * n, threadIdx.x % q, n, logn, tw, 1);
+  for (int e = threadIdx.x; e < nb * n; e += blockDim.x)
+    out[(int64_t)(e / n) * nn + (int64_t)r * n + (e % n)] = rows[e];
+}
+
 // After the inverse 2-D transform Z is in layout [r + n*c] (x contiguous):
 // unpack to six column-major planes (+ psi plane).
 __global__ void unpair_kernel(const double2* Z, int n, int with_psi, double* planes, double* psi) {
