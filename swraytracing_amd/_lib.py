@@ -210,6 +210,7 @@ class Context:
         self._h = h
         self.device = device
         self._ode23_cb = self._ode23_hook = self._ode23_raised = None  # ode23_run's hook callback
+        self.timing_every = 1  # swrt_set_timing's setting (the library default)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -683,6 +684,7 @@ class Context:
 
     def set_timing(self, every=1):
         self._chk(self._L.swrt_set_timing(self._h, int(every)), "swrt_set_timing")
+        self.timing_every = int(every)
 
     def kernel_time(self, reset=True):
         ms = _D()

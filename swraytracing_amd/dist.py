@@ -157,10 +157,13 @@ class OwnerLink:
     step's grid_U(prev_qk)); swrt_snapshot_qk orders the next fill of a
     buffer after its read."""
 
-    def __init__(self, nx, backend, owner=0, group=None, device=None):
+    def __init__(self, nx, backend, owner=0, group=None, device=None, nbuf=3):
         """``device``: device buffers (default: with "nccl"); True with
         "gloo" runs the device form over gloo's CUDA-tensor broadcast (the
-        tests' way to exercise it with ranks sharing one GPU)."""
+        tests' way to exercise it with ranks sharing one GPU).  ``nbuf``:
+        buffers in turn (>= 2: the latest qk and the previous one; a receiver
+        that paces its host `ahead` steps needs ahead + 1 for fenced
+        snapshots)."""
         import torch
         kmax = nx // 2 - 1
         self.nx = int(nx)
@@ -170,7 +173,8 @@ class OwnerLink:
         dev = torch.device("cuda", torch.cuda.current_device()) if self.device else torch.device("cpu")
         self.stream = torch.cuda.Stream(device=dev) if self.device else None
         # [qk half plane (2*nh doubles) | dt]
-        self.bufs = [torch.zeros(2 * self.nh + 1, dtype=torch.float64, device=dev) for _ in range(2)]
+        self.nbuf = max(2, int(nbuf))
+        self.bufs = [torch.zeros(2 * self.nh + 1, dtype=torch.float64, device=dev) for _ in range(self.nbuf)]
         self.cur = 0  # the buffer holding the latest qk
         self.dt_group = None
         self._dt = [torch.zeros(1, dtype=torch.float64) for _ in range(2)]
@@ -203,7 +207,7 @@ class OwnerLink:
         import torch.distributed as dist
         if self._dt_work is not None:
             self._dt_work.wait()
-        t = self._dt[self.cur]
+        t = self._dt[self.cur & 1]
         t[0] = float(dt)
         self._dt_work = dist.broadcast(t, src=self.owner, group=self.dt_group, async_op=True)
 
@@ -211,9 +215,12 @@ class OwnerLink:
         if not self.device:
             return float(b[-1])
         import torch.distributed as dist
-        t = self._dt[self.cur]
+        t = self._dt[self.cur & 1]
         dist.broadcast(t, src=self.owner, group=self.dt_group)
         return float(t[0])
+
+    def _next(self):
+        return (self.cur + 1) % self.nbuf
 
     def seed(self, ctx):
         """Every rank: the model's initial qk as the 'previous' buffer (all
@@ -222,10 +229,10 @@ class OwnerLink:
 
     def publish(self, ctx, dt):
         """Owner: the committed current qk's top layer and dt to every rank."""
-        b = self.bufs[self.cur ^ 1]
+        b = self.bufs[self._next()]
         self._export(ctx, b, dt)
         self._bcast(b)
-        self.cur ^= 1
+        self.cur = self._next()
         self._send_dt(dt)
 
     def receive(self, wait=False):
@@ -233,9 +240,9 @@ class OwnerLink:
         The qk half plane may still be in flight (device) — the snapshot that
         reads it waits for it on the device — unless ``wait``: then the host
         waits for it here (see snapshot's ``fenced``)."""
-        b = self.bufs[self.cur ^ 1]
+        b = self.bufs[self._next()]
         self._bcast(b)
-        self.cur ^= 1
+        self.cur = self._next()
         dt = self._recv_dt(b)
         if wait and self.device:
             self.stream.synchronize()
@@ -255,7 +262,7 @@ class OwnerLink:
         link stream measured ~0.2 ms per step on ROCm beside packet launches:
         every hop of a barrier between queues waits on the command processor,
         tools/owner_legs.py.)"""
-        b = self.bufs[self.cur if which == 0 else self.cur ^ 1]
+        b = self.bufs[self.cur if which == 0 else (self.cur - 1) % self.nbuf]
         if self.device:
             ctx.snapshot_qk(slot, b.data_ptr(), self.nx, L, K_d2, shear, k_scale, ny_period,
                             stream=None if fenced else self.stream.cuda_stream)

@@ -399,7 +399,7 @@ class ReceiverLoop:
     TwoLayerLoop does (same t, dt sequence, active steps and frame points)."""
 
     def __init__(self, link, ens, dt, packet_delay=0.0, nsub=5, packet_intervals=1, integrator="leapfrog",
-                 ahead=2):
+                 ahead=None):
         self.link, self.ens, self.dt = link, ens, dt
         self.packet_delay = packet_delay
         self.t = 0.0
@@ -413,18 +413,20 @@ class ReceiverLoop:
         # looks in use; the next snapshot then waits for the packet launch
         # before it and packets and snapshots run one after the other
         # (swrt_qg_snapshot's renaming decides at queue time).
-        self.ahead = int(ahead)
+        self.ahead = (getattr(link, "nbuf", 2) - 1) if ahead is None else int(ahead)
         self._done = []
         self._pk = None
         if self.ahead > 0 and ens is not None and ens.n > 0 and getattr(link, "device", False):
             import torch
             self._pk = torch.cuda.ExternalStream(ens.ctx.stream())
+            self._events = [torch.cuda.Event() for _ in range(self.ahead + 1)]
+            self._ev_i = 0
         # device link with pacing: the host waits for each broadcast and the
         # pacing orders the buffers' refills, so the snapshots need no
-        # cross-stream events (OwnerLink.snapshot fenced; at most 2 steps ahead:
-        # a buffer is refilled two receives after the snapshot that read it)
-        self._fenced = self._pk is not None and self.ahead <= 2
-        self._prev_read = False
+        # cross-stream events (OwnerLink.snapshot fenced; at most nbuf - 1
+        # steps ahead: a buffer is refilled nbuf receives after the snapshot
+        # that read it)
+        self._fenced = self._pk is not None and self.ahead <= getattr(link, "nbuf", 2) - 1
 
     def _snapshot(self, slot, which):
         e = self.ens
@@ -434,10 +436,6 @@ class ReceiverLoop:
         self.steps += 1
         if self._done and len(self._done) >= self.ahead:
             self._done.pop(0).synchronize()
-        if self._prev_read:
-            # last step's grid_U(prev_qk) read the buffer this receive refills
-            self._done[-1].synchronize()
-            self._prev_read = False
         self.dt = self.link.receive(wait=self._fenced)
         self.dts.append(self.dt)
         self.t = self.t + self.dt
@@ -446,13 +444,12 @@ class ReceiverLoop:
             if self.ens.n > 0:
                 if not self.have_cur:
                     self._snapshot(0, 1)  # grid_U(prev_qk)
-                    self._prev_read = self._fenced
                 self._snapshot(self.group.next_slot(), 0)  # grid_U(qk)
                 self.have_cur = True
             self.group.add(self.dt)
             if self._pk is not None:
-                import torch
-                ev = torch.cuda.Event()
+                ev = self._events[self._ev_i]
+                self._ev_i = (self._ev_i + 1) % len(self._events)
                 ev.record(self._pk)
                 self._done.append(ev)
         else:
@@ -489,6 +486,8 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     forms, as in :func:`qg2layersw_raytrace`.  Returns a dict of run facts
     (dt, Nsteps, steps run, frames written, final t)."""
     ctx = ctx if ctx is not None else Context(0)
+    timing = getattr(ctx, "timing_every", 1)
+    ctx.set_timing(0)  # (no HIP-event pair around every packet launch; restored at the end)
     rank, world = _dist_info()  # sharded run: packets split over the ranks
     if rank == 0:
         _fresh_outputs(out_dir, fresh)
@@ -571,6 +570,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     if link is not None:
         link.close()
     ctx.synchronize()
+    ctx.set_timing(timing)
     log.finish()
     log.close()
     return dict(dt=dt, Nsteps=Nsteps, steps=nrun, packet_frames=frames, t=t, U0=U0,
@@ -596,6 +596,8 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     owner link's buffers ("auto": on the device with nccl, on the host with
     gloo; "device" / "host" to force one)."""
     ctx = ctx if ctx is not None else Context(0)
+    timing = getattr(ctx, "timing_every", 1)
+    ctx.set_timing(0)  # (no HIP-event pair around every packet launch; restored at the end)
     rank, world = _dist_info()  # sharded run: packets split over the ranks
     if rank == 0:
         _fresh_outputs(out_dir, fresh)
@@ -661,6 +663,7 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     if link is not None:
         link.close()
     ctx.synchronize()
+    ctx.set_timing(timing)
     log.finish()
     log.close()
     dt, dts, step, t = loop.dt, loop.dts, loop.steps, loop.t

@@ -33,7 +33,8 @@ def main():
     ap.add_argument("--receiver", type=int, nargs="*", default=[142857])
     ap.add_argument("--owner", type=int, nargs="*", default=[0, 76923, 142857])
     ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--ahead", type=int, default=2)
+    ap.add_argument("--ahead", type=int, default=None)
+    ap.add_argument("--nbuf", type=int, default=3)
     ap.add_argument("--recv-qg-stream", type=int, default=0, help="receiver legs: snapshots on the QG stream (1)")
     ap.add_argument("--recv-streams", type=int, default=1, help="receiver legs: packet streams (1 or 2)")
     ap.add_argument("--micro", type=int, nargs="*", default=[],
@@ -49,6 +50,7 @@ def main():
     dev = torch.device("cuda", 0)
     ctx = sw.Context(0)
     w = bench.build_workload(ctx, args, 0, 1_000_000, 1_000_000)
+    ctx.set_timing(0)  # (as the drivers)
     OneGPU = bench._owner_links()
     nx, L, f, Cg = w["nx"], w["L"], w["f"], math.sqrt(w["gH"])
     qk = np.stack([w["qk1"], -w["qk1"]], axis=2)
@@ -117,12 +119,13 @@ def main():
         ctx.set_packet_streams(a.recv_streams)
         model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
         dt = 0.25 * (L / nx) / model.max_speed()
-        link = OneGPU(nx, dt)
+        link = OneGPU(nx, dt, nbuf=a.nbuf)
         for b in link.bufs:
             link._export(ctx, b, dt)
         ens = ensemble(nr)
         loop = sw.ReceiverLoop(link, ens, dt, 0.0, nsub=5, ahead=a.ahead)
         acc = {}
+        loop.step = Timed(acc, "step_total", loop.step)
         link.receive = Timed(acc, "receive", link.receive)
         link.snapshot = Timed(acc, "snapshot", link.snapshot)
         ens.advance_intervals = Timed(acc, "advance", ens.advance_intervals)
