@@ -724,6 +724,24 @@ int fields_from_halfplane(swrt_ctx* c, int slot, const double2* dfk, int n, int 
   int rc;
   const int64_t nn = (int64_t)n * n;
   const int nb = with_psi ? 4 : 3;
+  Slot& s0 = c->slot[slot];
+  if (!with_psi && n % 16 == 0 && 3 * 2 * n / 4 <= 1024 && (n / 2) % 8 == 0) {
+    // the spectra built by the row pass (spectra_rows_kernel), the column
+    // pass fused with the pack into the node records (fft_cols_pack_kernel):
+    // two launches, the values of the four below
+    int logn = 0;
+    while ((1 << logn) < n) ++logn;
+    hipLaunchKernelGGL(spectra_rows_kernel, dim3((unsigned)n), dim3(3 * n / 4), sizeof(double2) * 3 * n, c->stream,
+                       dfk, n, mode, K_d2, kscale, 0, sx, sy, logn, (const double2*)c->tw, Z);
+    HIPCHK(c, hipGetLastError());
+    hipLaunchKernelGGL(fft_cols_pack_kernel<2>, dim3((unsigned)(n / 2)), dim3(3 * 2 * n / 4),
+                       sizeof(double2) * 3 * 2 * (n + 1), c->stream, (const double2*)Z, n, logn,
+                       (const double2*)c->tw, (int)s0.npad, shear, s0.nodes);
+    HIPCHK(c, hipGetLastError());
+    s0.has_psi = false;
+    s0.div_free = true;  // v_y = -u_x, as pack_pairs_kernel
+    return SWRT_OK;
+  }
   if (nb * n / 4 <= 1024 && ((int64_t)n * nb) % 8 == 0) {
     // the spectra built row by row in LDS by the first inverse pass
     // (spectra_rows_kernel: the same values as the separate launches below,

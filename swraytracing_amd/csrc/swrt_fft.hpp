@@ -562,6 +562,61 @@ __global__ void __launch_bounds__(256) pack_pairs_kernel(const double2* T, int n
   }
 }
 
+// The column pass of grid_U's inverse 2-D FFT fused with pack_pairs_kernel:
+// workgroup g takes CY adjacent columns y of all three planes of the row pass
+// output (Z, layout [plane][r][y]), runs their 3*CY inverse column FFTs side
+// by side (n/4 lanes each, fft_stages_one_buffer: the column pass's own
+// per-vector arithmetic) and writes the node records {u + shear, v, u_x, u_y,
+// v_x, -u_x} of those columns, with their periodic ghost images, straight
+// from LDS — the values fft_vec_kernel<true> + pack_pairs_kernel write, bit
+// for bit, without the 12.6 MB round trip of the transformed planes (512^2).
+// Loads: lanes c, c+1, ... of one plane read a row's CY adjacent columns
+// (contiguous); consecutive groups run on one XCD (its L2 shares the rows'
+// 128-B lines).  Stores: the CY records of one x are contiguous (y fastest).
+// blockDim 3*CY*n/4 <= 1024, dynamic LDS 3*CY*(n+1) double2, n/CY % 8 == 0.
+template <int CY>
+__global__ void __launch_bounds__(1024) fft_cols_pack_kernel(const double2* Z, int n, int logn, const double2* tw,
+                                                             int npad, double shear, double* nodes) {
+  extern __shared__ double2 sbuf[];
+  const int quarter = n >> 2, t = threadIdx.x, ld = n + 1;
+  const int64_t nn = (int64_t)n * n;
+  const int ng = n / CY;
+  const int g = (int)(blockIdx.x & 7) * (ng >> 3) + (int)(blockIdx.x >> 3);
+  const int y0 = g * CY;
+  {
+    // lane -> (plane, column c, rows j0 + k*quarter)
+    const int per = CY * quarter, pl = t / per, u = t - pl * per;
+    const int c = u % CY, j0 = u / CY;
+    const double2* src = Z + pl * nn + y0 + c;
+    double2 r[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = src[(int64_t)(j0 + k * quarter) * n];
+    double2* dst = sbuf + (pl * CY + c) * ld;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[j0 + k * quarter] = r[k];
+  }
+  __syncthreads();
+  fft_stages_one_buffer(sbuf + (t / quarter) * ld, t % quarter, n, logn, tw, 1);
+  const int hi = npad - n - 2;
+  for (int e = t; e < n * CY; e += blockDim.x) {
+    const int x = e / CY, cy = e - (e / CY) * CY, y = y0 + cy;
+    const double2 a = sbuf[(0 * CY + cy) * ld + x], b = sbuf[(1 * CY + cy) * ld + x],
+                  cc = sbuf[(2 * CY + cy) * ld + x];
+    const double rec[6] = {a.x + shear, a.y, b.x, b.y, cc.x, -b.x};
+    const int px[3] = {x + 2, x >= n - 2 ? x + 2 - n : -1, x < hi ? x + 2 + n : -1};
+    const int py[3] = {y + 2, y >= n - 2 ? y + 2 - n : -1, y < hi ? y + 2 + n : -1};
+    for (int i = 0; i < 3; ++i) {
+      if (px[i] < 0) continue;
+      for (int j = 0; j < 3; ++j) {
+        if (py[j] < 0) continue;
+        double* d = nodes + ((int64_t)px[i] * npad + py[j]) * 6;
+#pragma unroll
+        for (int f = 0; f < 6; ++f) d[f] = rec[f];
+      }
+    }
+  }
+}
+
 // psi plane of the packed transform T3 (layout [x + n*y]).
 __global__ void psi_plane_kernel(const double2* T3, double* psi, int64_t cnt) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
