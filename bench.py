@@ -377,7 +377,7 @@ def _owner_links():
     from swraytracing_amd.dist import OwnerLink
 
     class OneGPU(OwnerLink):  # the link's stream, export and snapshot, without the broadcasts
-        def __init__(self, nx, dt=0.0, nbuf=3):
+        def __init__(self, nx, dt=0.0, nbuf=5):
             super().__init__(nx, "nccl", nbuf=nbuf)
             self.fixed_dt = dt
 

@@ -157,13 +157,12 @@ class OwnerLink:
     step's grid_U(prev_qk)); swrt_snapshot_qk orders the next fill of a
     buffer after its read."""
 
-    def __init__(self, nx, backend, owner=0, group=None, device=None, nbuf=3):
+    def __init__(self, nx, backend, owner=0, group=None, device=None, nbuf=5):
         """``device``: device buffers (default: with "nccl"); True with
         "gloo" runs the device form over gloo's CUDA-tensor broadcast (the
         tests' way to exercise it with ranks sharing one GPU).  ``nbuf``:
-        buffers in turn (>= 2: the latest qk and the previous one; a receiver
-        that paces its host `ahead` steps needs ahead + 1 for fenced
-        snapshots)."""
+        buffers in turn (>= 2: the latest qk and the previous one; a receiver's
+        fenced snapshots need ReceiverLoop.ahead + mark_every of them)."""
         import torch
         kmax = nx // 2 - 1
         self.nx = int(nx)

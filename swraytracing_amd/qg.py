@@ -413,20 +413,27 @@ class ReceiverLoop:
         # looks in use; the next snapshot then waits for the packet launch
         # before it and packets and snapshots run one after the other
         # (swrt_qg_snapshot's renaming decides at queue time).
-        self.ahead = (getattr(link, "nbuf", 2) - 1) if ahead is None else int(ahead)
-        self._done = []
+        # the mark is an event recorded after every 2nd step's packet work (an
+        # event between two kernels costs ~6 us of idle GPU, tools/owner_legs.py
+        # traces), so the host is `ahead` to `ahead` + 1 steps ahead
+        self.mark_every = 2
+        nbuf = getattr(link, "nbuf", 2)
+        self.ahead = (nbuf - self.mark_every - 1) if ahead is None else int(ahead)
+        self._done = []  # (step, event)
         self._pk = None
         if self.ahead > 0 and ens is not None and ens.n > 0 and getattr(link, "device", False):
             import torch
             self._pk = torch.cuda.ExternalStream(ens.ctx.stream())
-            self._events = [torch.cuda.Event() for _ in range(self.ahead + 1)]
+            self._events = [torch.cuda.Event() for _ in range(self.ahead + 2)]
             self._ev_i = 0
         # device link with pacing: the host waits for each broadcast and the
         # pacing orders the buffers' refills, so the snapshots need no
-        # cross-stream events (OwnerLink.snapshot fenced; at most nbuf - 1
-        # steps ahead: a buffer is refilled nbuf receives after the snapshot
-        # that read it)
-        self._fenced = self._pk is not None and self.ahead <= getattr(link, "nbuf", 2) - 1
+        # cross-stream events (OwnerLink.snapshot fenced): the buffer of step m
+        # is read by step m's snapshot and, on a first active step, by step
+        # m + 1's grid_U(prev_qk); it is refilled by receive m + nbuf, by which
+        # the host has waited for the packet work of step m + nbuf - ahead -
+        # mark_every or later — after both reads when that is >= m + 1
+        self._fenced = self._pk is not None and self.ahead + self.mark_every + 1 <= nbuf
 
     def _snapshot(self, slot, which):
         e = self.ens
@@ -434,8 +441,8 @@ class ReceiverLoop:
 
     def step(self):
         self.steps += 1
-        if self._done and len(self._done) >= self.ahead:
-            self._done.pop(0).synchronize()
+        while self._done and self._done[0][0] <= self.steps - 1 - self.ahead:
+            self._done.pop(0)[1].synchronize()
         self.dt = self.link.receive(wait=self._fenced)
         self.dts.append(self.dt)
         self.t = self.t + self.dt
@@ -447,11 +454,11 @@ class ReceiverLoop:
                 self._snapshot(self.group.next_slot(), 0)  # grid_U(qk)
                 self.have_cur = True
             self.group.add(self.dt)
-            if self._pk is not None:
+            if self._pk is not None and self.steps % self.mark_every == 0:
                 ev = self._events[self._ev_i]
                 self._ev_i = (self._ev_i + 1) % len(self._events)
                 ev.record(self._pk)
-                self._done.append(ev)
+                self._done.append((self.steps, ev))
         else:
             self.have_cur = False
         return active

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--owner", type=int, nargs="*", default=[0, 76923, 142857])
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--ahead", type=int, default=None)
-    ap.add_argument("--nbuf", type=int, default=3)
+    ap.add_argument("--nbuf", type=int, default=5)
     ap.add_argument("--recv-qg-stream", type=int, default=0, help="receiver legs: snapshots on the QG stream (1)")
     ap.add_argument("--recv-streams", type=int, default=1, help="receiver legs: packet streams (1 or 2)")
     ap.add_argument("--micro", type=int, nargs="*", default=[],
