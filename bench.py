@@ -393,7 +393,7 @@ def _owner_links():
     return OneGPU
 
 
-OWNER_WEIGHTS = (0.0, 0.25, 0.5, 1.0)
+OWNER_WEIGHTS = (0.0, 0.05, 0.1, 0.25, 0.5, 1.0)
 
 
 def owner_forecast(ctx, w, args, dev, n_total, full_ms):

@@ -609,9 +609,11 @@ __global__ void __launch_bounds__(1024) fft_cols_pack_kernel(const double2* Z, i
       if (px[i] < 0) continue;
       for (int j = 0; j < 3; ++j) {
         if (py[j] < 0) continue;
-        double* d = nodes + ((int64_t)px[i] * npad + py[j]) * 6;
-#pragma unroll
-        for (int f = 0; f < 6; ++f) d[f] = rec[f];
+        // a record is 48 B at a multiple of 48 B: three 16-B stores
+        double2* d = reinterpret_cast<double2*>(nodes + ((int64_t)px[i] * npad + py[j]) * 6);
+        d[0] = make_double2(rec[0], rec[1]);
+        d[1] = make_double2(rec[2], rec[3]);
+        d[2] = make_double2(rec[4], rec[5]);
       }
     }
   }
