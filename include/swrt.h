@@ -482,15 +482,17 @@ int swrt_qg_snapshot_speculative(swrt_ctx* ctx, int slot, int64_t ny_period);
  * (2kmax+1)*(kmax+1) interleaved complex in the device order (ky fastest:
  * element (kx, ky) at (kx + kmax)*(kmax + 1) + ky), to dst, followed by
  * `tail` (e.g. the step's dt, so one broadcast carries both: dst holds
- * 2*(2kmax+1)*(kmax+1) + 1 doubles).  dst_on_device = 1:
- * a device buffer; the copy runs on the QG stream behind the step that made
- * qk, after `stream`'s work queued so far (its last read of dst) and before
- * `stream`'s later work (stream: a hipStream_t of the caller, e.g. the one a
- * broadcast is queued on; NULL = the context's packet stream).  0: host
- * memory, returns once copied.  The committed state is exported: a pending
+ * 2*(2kmax+1)*(kmax+1) + 1 doubles).  dst_mode = 1: a device buffer; the
+ * copy runs on the QG stream behind the step that made qk, after `stream`'s
+ * work queued so far (its last read of dst) and before `stream`'s later work
+ * (stream: a hipStream_t of the caller, e.g. the one a broadcast is queued
+ * on; NULL = the context's packet stream).  2: the same without the first
+ * ordering — the caller guarantees dst is no longer read (a wait of the QG
+ * stream on another stream's event measured ~0.1 ms per step on ROCm while
+ * packet launches hold the GPU).  0: host memory, returns once copied.  The committed state is exported: a pending
  * speculative step (swrt_qg_step_speculative) is neither waited for nor
  * included. */
-int swrt_qg_export(swrt_ctx* ctx, int which, int layer, double* dst, int dst_on_device, void* stream, double tail);
+int swrt_qg_export(swrt_ctx* ctx, int which, int layer, double* dst, int dst_mode, void* stream, double tail);
 /* grid_U (grid_U.m:1-18: psi = -q/(K_d2 + K^2), u += shear) of a half plane in
  * swrt_qg_export's order into packet slot `slot`: bit for bit the
  * swrt_qg_snapshot(slot, which, layer, ny_period) of the context that exported

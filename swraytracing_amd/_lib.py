@@ -552,20 +552,21 @@ class Context:
         self._chk(self._L.swrt_ode23_chain_next(self._h, int(slot_a), int(slot_b)), "swrt_ode23_chain_next")
 
     # ---- owner-driver hand-off (swrt_qg_export / swrt_snapshot_qk) -----------
-    def qg_export(self, dst, which=0, layer=0, stream=None, tail=0.0):
+    def qg_export(self, dst, which=0, layer=0, stream=None, tail=0.0, fenced=False):
         """Layer `layer` of the current (0) / previous (1) qk in the device's
         half-plane order (ky fastest), then `tail`, into `dst`: a float64
         numpy array of 2*(2kmax+1)*(kmax+1) + 1 values (host copy, returns
         when done), or an int device address (queued; ordered after and
         before the work of the hipStream_t `stream`, default the packet
-        stream)."""
+        stream — ``fenced``: only before it, the caller guarantees dst is
+        free; swrt_qg_export dst_mode 2)."""
         if isinstance(dst, np.ndarray):
             if dst.dtype != np.float64 or not dst.flags["C_CONTIGUOUS"] or dst.size != 2 * self._qg_nhalf() + 1:
                 raise ValueError("dst must be a contiguous float64 array of 2*(2kmax+1)*(kmax+1) + 1 values")
             self._chk(self._L.swrt_qg_export(self._h, int(which), int(layer), dst.ctypes.data_as(_VP), 0, None,
                                              float(tail)), "swrt_qg_export")
         else:
-            self._chk(self._L.swrt_qg_export(self._h, int(which), int(layer), _VP(int(dst)), 1,
+            self._chk(self._L.swrt_qg_export(self._h, int(which), int(layer), _VP(int(dst)), 2 if fenced else 1,
                                              None if stream is None else _VP(int(stream)), float(tail)),
                       "swrt_qg_export")
 

@@ -3408,7 +3408,7 @@ int stream_order(swrt_ctx* c, hipStream_t from, hipStream_t to, int ev) {
 }
 }  // namespace
 
-int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_on_device, void* stream, double tail) {
+int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_mode, void* stream, double tail) {
   if (!c) return SWRT_ERR_ARG;
   GUARD_BEGIN_KEEP_CHAIN
   OnQGStream on_qg(c);
@@ -3423,9 +3423,10 @@ int swrt_qg_export(swrt_ctx* c, int which, int layer, double* dst, int dst_on_de
   HIPCHK(c, hipSetDevice(c->device));
   const double2* src = (which == 0 ? q.qk : q.qk_prev) + layer * q.nhalf;
   const size_t bytes = sizeof(double2) * q.nhalf;
-  if (dst_on_device) {
+  if (dst_mode != 0 && dst_mode != 1 && dst_mode != 2) return fail(c, SWRT_ERR_ARG, "dst_mode must be 0, 1 or 2");
+  if (dst_mode) {
     const hipStream_t ext = stream ? (hipStream_t)stream : on_qg.saved;
-    HIPCHK_RC(stream_order(c, ext, c->stream, 0));  // the caller's last read of dst
+    if (dst_mode == 1) HIPCHK_RC(stream_order(c, ext, c->stream, 0));  // the caller's last read of dst
     hipLaunchKernelGGL(export_half_kernel, dim3(nblocks(q.nhalf + 1, 256)), dim3(256), 0, c->stream, src, dst,
                        q.nhalf, tail);
     HIPCHK(c, hipGetLastError());

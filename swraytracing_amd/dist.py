@@ -177,6 +177,7 @@ class OwnerLink:
         self.cur = 0  # the buffer holding the latest qk
         self.dt_group = None
         self._dt = [torch.zeros(1, dtype=torch.float64) for _ in range(2)]
+        self._sent = [None] * self.nbuf if self.device else None
         self._dt_work = None
         if self.device:
             import torch.distributed as dist
@@ -191,7 +192,13 @@ class OwnerLink:
 
     def _export(self, ctx, b, dt=0.0):
         if self.device:
-            ctx.qg_export(b.data_ptr(), which=0, layer=0, stream=self.stream.cuda_stream, tail=dt)
+            # host-fenced: the broadcast that last read this buffer (nbuf
+            # publishes ago) is waited for here, so the QG stream never waits
+            # on the link stream (see swrt_qg_export dst_mode 2)
+            i = self.bufs.index(b) if self._sent is not None else 0
+            if self._sent is not None and self._sent[i] is not None:
+                self._sent[i].synchronize()
+            ctx.qg_export(b.data_ptr(), which=0, layer=0, stream=self.stream.cuda_stream, tail=dt, fenced=True)
         else:
             ctx.qg_export(b.numpy(), which=0, layer=0, tail=dt)
 
@@ -228,10 +235,16 @@ class OwnerLink:
 
     def publish(self, ctx, dt):
         """Owner: the committed current qk's top layer and dt to every rank."""
-        b = self.bufs[self._next()]
+        i = self._next()
+        b = self.bufs[i]
         self._export(ctx, b, dt)
         self._bcast(b)
-        self.cur = self._next()
+        if self._sent is not None:  # (the broadcast's completion, for the buffer's next export)
+            import torch
+            if self._sent[i] is None:
+                self._sent[i] = torch.cuda.Event()
+            self._sent[i].record(self.stream)
+        self.cur = i
         self._send_dt(dt)
 
     def receive(self, wait=False):
