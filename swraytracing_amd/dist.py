@@ -195,7 +195,7 @@ class OwnerLink:
             # host-fenced: the broadcast that last read this buffer (nbuf
             # publishes ago) is waited for here, so the QG stream never waits
             # on the link stream (see swrt_qg_export dst_mode 2)
-            i = self.bufs.index(b) if self._sent is not None else 0
+            i = next(k for k, x in enumerate(self.bufs) if x is b)
             if self._sent is not None and self._sent[i] is not None:
                 self._sent[i].synchronize()
             ctx.qg_export(b.data_ptr(), which=0, layer=0, stream=self.stream.cuda_stream, tail=dt, fenced=True)
