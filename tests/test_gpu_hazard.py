@@ -110,9 +110,11 @@ def test_checker_catches_the_pre_third_buffer_race(debug_ctx):
     ctx.synchronize()
     # unchecked, under the spin schedule: the race corrupts the packets (a
     # race: the spin before each extra-stream part makes it all but certain;
-    # a longer spin is tried once if the first schedule happened to miss it)
+    # longer spins are tried if a schedule happened to miss it — one did, once
+    # in round 6's first session, gpurun_out r6a; every other run corrupts at
+    # the first spin)
     corrupted = False
-    for spin in (200, 2000):
+    for spin in (200, 2000, 5000, 10000):
         ctx.debug_set(L.DEBUG_SPIN_US, spin)
         xr, kr = _run_calls(ctx, bench, w, 6)
         if not (_bits_equal(x1, xr) and _bits_equal(k1, kr)):
