@@ -235,13 +235,34 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     the driver-level rates are observed by the same run."""
     nx, L, f, Cg = w["nx"], w["L"], w["f"], math.sqrt(w["gH"])
     nsteps = args.driver_steps if nsteps is None else nsteps
+    w_in = w
     qk = np.stack([w["qk1"], -w["qk1"]], axis=2)  # the driver's (q1, -q1) layers
+    owner_form = distributed and args.driver_pde == "owner" and integrator == "leapfrog"
+    if owner_form:
+        # the PDE-owner form across the ranks (qg.py OwnerLink / ReceiverLoop):
+        # the ensemble re-split by dist.owner_bounds (every rank draws all
+        # n_total packets from the same seed: build_workload), rank 0 steps the
+        # PDE and broadcasts each step's top-layer qk and dt
+        from swraytracing_amd.dist import OwnerLink, owner_bounds
+        full = build_workload(ctx, args, 0, n_total, n_total)
+        lo, hi = owner_bounds(n_total, args.world, args.owner_weight)[args.rank]
+        w = dict(w, x=full["x"][lo:hi], k=full["k"][lo:hi])
+        link = OwnerLink(nx, args.dist_backend)
     model = sw.QGModel.two_layer(qk, nx, f, Cg, L=L, ctx=ctx)
     ens = sw.PacketEnsemble(w["x"], w["k"], L, f, Cg, nx, f / Cg, shear=0.5, k_scale=2 * math.pi / L, nlayers=2,
                             bump=sw.BUMP_QG, ctx=ctx)
     U0 = model.max_speed()
-    loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
-                           integrator=integrator, speculate=bool(args.speculate))
+    if owner_form and args.rank != 0:
+        ctx.qg_set_stream(False)
+        ctx.set_packet_streams(1)
+        link.seed(ctx)
+        loop = sw.ReceiverLoop(link, ens, 0.25 * (L / nx) / U0, 0.0, nsub=args.substeps)
+    else:
+        if owner_form:
+            link.seed(ctx)
+        loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
+                               integrator=integrator, speculate=bool(args.speculate),
+                               link=link if owner_form else None)
     # AB1/AB2 start-up and first-use allocations: the snapshot renaming (qg.py
     # TwoLayerLoop) allocates its spare slot buffers during the first steps, a
     # hipMalloc each — outside the timed steps.  Then warm-up steps until
@@ -252,9 +273,13 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     # idle gap before a 16-step warm-up, profiles/r05_qg_copy)
     for _ in range(args.driver_warmup):
         loop.step()
-    tw = time.perf_counter()
-    while time.perf_counter() - tw < args.driver_warm_s:
-        loop.step()
+    if owner_form:  # every rank takes the same steps (each is a collective)
+        for _ in range(OWNER_WARM_STEPS):
+            loop.step()
+    else:
+        tw = time.perf_counter()
+        while time.perf_counter() - tw < args.driver_warm_s:
+            loop.step()
     loop.flush()
     ctx.synchronize()
     torch.cuda.synchronize(dev)
@@ -286,6 +311,12 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
     out = {"ms_per_pde_step": ms, "steps": nsteps, "what": what, "clock_ghz_observed": clk,
            # the CFL rule (qg2layersw_raytrace.m:156-165) re-forms the exponential propagators when dt changes
            "dt_changes": int(sum(1 for a, b in zip(loop.dts[nd0 - 1:], timed_dts) if a != b))}
+    if owner_form:
+        loop.settle()
+        out["pde"] = f"owner form (rank 0 steps the PDE, owner weight {args.owner_weight})"
+        ctx.qg_set_stream(bool(args.qg_stream))
+        ctx.set_packet_streams(args.packet_streams)
+        ctx.packets_set(w_in["x"], w_in["k"])
     if integrator == "leapfrog":
         out["packet_steps_per_s"] = n_total * args.substeps / (ms / 1e3)
     else:
@@ -467,6 +498,7 @@ def owner_forecast(ctx, w, args, dev, n_total, full_ms):
 
 
 DRIVER_WARM_S = 0.3  # seconds of untimed driver steps before each driver-step measurement
+OWNER_WARM_STEPS = 100  # ... in the owner form, a step count (every step is a collective)
 FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9  # fp64 VALU lane-ops/s (78.6 TFLOP/s spec counts an FMA as 2)
 LDS_CYCLES_PEAK = 256 * 2.4e9               # LDS-array cycles/s over the chip (one array per CU, 2.4 GHz)
 # fp64 operations one packet-step of the reference arithmetic needs (each +, -, *, /, sqrt, floor one op;
@@ -640,6 +672,12 @@ def parse_args(argv=None):
                     help="then driver steps for this many seconds, untimed (a GPU back from idle; 0: none)")
     ap.add_argument("--driver-warmup", type=int, default=16,
                     help="untimed driver steps before the timed ones (start-up, spare snapshot buffers)")
+    ap.add_argument("--driver-pde", choices=["replicated", "owner"], default="replicated",
+                    help="N > 1 driver step: every rank steps the PDE (replicated), or rank 0 steps it and broadcasts "
+                         "the top-layer qk + dt (owner form, qg.py OwnerLink; its N = 1 forecast is "
+                         "driver_step_forecast.owner)")
+    ap.add_argument("--owner-weight", type=float, default=0.0,
+                    help="owner form: rank 0's packets per packet of another rank (dist.owner_bounds)")
     ap.add_argument("--ode23-steps", type=int, default=8,
                     help="then this many driver steps with the reference's ode23 packet integrator (0: skip)")
     ap.add_argument("--gather", action="store_true",

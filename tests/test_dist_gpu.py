@@ -180,18 +180,22 @@ def test_sharded_driver_files_equal_single_process(ctx, tmp_path, drv, world, pd
         assert len(a) > 0 and a == b, name
 
 
-def test_bench_gpus_2_strong_scaling_line(tmp_path):
+@pytest.mark.parametrize("driver", ["none", "owner"])
+def test_bench_gpus_2_strong_scaling_line(tmp_path, driver):
     """`bench.py --gpus 2` with no torch.distributed environment launches two
     ranks as a child torch.distributed.run (gloo: both share GPU 0) and relays
-    rank 0's line: n_gpus 2, the metric's 1e6 packets split 5e5 per GPU."""
+    rank 0's line: n_gpus 2, the metric's 1e6 packets split 5e5 per GPU; with
+    `--driver-pde owner` also the driver step in the PDE-owner form."""
     import json
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
                                                             "MASTER_PORT")}
     env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"
+    extra = ["--driver-steps", "0"] if driver == "none" else ["--driver-steps", "5", "--driver-warmup", "4",
+                                                              "--driver-pde", "owner", "--owner-weight", "0.25",
+                                                              "--no-forecast"]
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-                        "--steps", "3", "--warmup", "1", "--driver-steps", "0", "--ode23-steps", "0",
-                        "--no-cpu-baseline", "--gather"], cwd=str(tmp_path), env=env, capture_output=True, text=True,
-                       timeout=240)
+                        "--steps", "3", "--warmup", "1", "--ode23-steps", "0", "--no-cpu-baseline", "--gather"] + extra,
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
     # every rank's own last lines (a failing rank's traceback sits mid-stream, before the launcher's report)
     assert r.returncode == 0, _rank_report(r.stderr)
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
@@ -200,3 +204,6 @@ def test_bench_gpus_2_strong_scaling_line(tmp_path):
     assert out["n_gpus"] == 2 and out["scaling"] == "strong"
     assert out["config"]["packets_total"] == 1_000_000 and out["config"]["packets_per_gpu"] == 500_000
     assert out["value"] > 0 and out["finite"] and out["gathered_finite"]
+    if driver == "owner":
+        d = out["driver_step"]
+        assert d["pde"].startswith("owner form") and d["ms_per_pde_step"] > 0
