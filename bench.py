@@ -259,6 +259,7 @@ def driver_step(ctx, w, args, dev, distributed, n_total, integrator="leapfrog", 
         loop = sw.ReceiverLoop(link, ens, 0.25 * (L / nx) / U0, 0.0, nsub=args.substeps)
     else:
         if owner_form:
+            link.bind_owner(ctx)
             link.seed(ctx)
         loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
                                integrator=integrator, speculate=bool(args.speculate),
@@ -455,7 +456,7 @@ def owner_forecast(ctx, w, args, dev, n_total, full_ms):
             U0 = model.max_speed()
             ens = ensemble(n0)  # (n0 = 0: an empty ensemble — the context then holds no packets, as the owner's)
             loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=args.substeps,
-                                   speculate=bool(args.speculate), link=OneGPU(nx))
+                                   speculate=bool(args.speculate), link=OneGPU(nx).bind_owner(ctx))
             legs[("o", n0)] = _time_loop(ctx, loop, args, dev, nsteps)
             loop.settle()
         return legs[("o", n0)]

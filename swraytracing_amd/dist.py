@@ -225,6 +225,19 @@ class OwnerLink:
         dist.broadcast(t, src=self.owner, group=self.dt_group)
         return float(t[0])
 
+    def bind_owner(self, ctx):
+        """The owner's link runs on the context's packet stream (device form):
+        the export is ordered after the QG stream by the library's own events,
+        the broadcast follows it in stream order, and no stream of the
+        library ever waits on a torch stream's event (tools/owner_legs.py
+        --owner-export: a link stream of its own made the owner's step 1.1-2x
+        slower and erratic while packet launches held the GPU).  A PDE owner
+        without packets has nothing else on that stream."""
+        if self.device:
+            import torch
+            self.stream = torch.cuda.ExternalStream(ctx.stream())
+        return self
+
     def _next(self):
         return (self.cur + 1) % self.nbuf
 

@@ -516,6 +516,8 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
     if link is not None:
         link.seed(ctx)
     owner = link is None or rank == 0  # this rank steps the PDE
+    if link is not None and owner:
+        link.bind_owner(ctx)
     if not owner:
         ctx.qg_set_stream(False)  # (snapshots in series with the packets, as in qg2layersw_raytrace)
         ctx.set_packet_streams(1)
@@ -646,6 +648,8 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     if rank == 0:
         write_field(model.q(), os.path.join(out_dir, "pv"))
         write_field(np.array([[t]]), os.path.join(out_dir, "pv_time"))
+    if link is not None and rank == 0:
+        link.bind_owner(ctx)
     if link is not None and rank != 0:
         # a receiving rank runs its snapshots on the packet stream: beside its
         # packet launches the transforms run several times slower (they find

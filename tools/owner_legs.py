@@ -37,9 +37,9 @@ def main():
     ap.add_argument("--nbuf", type=int, default=5)
     ap.add_argument("--recv-qg-stream", type=int, default=0, help="receiver legs: snapshots on the QG stream (1)")
     ap.add_argument("--recv-streams", type=int, default=1, help="receiver legs: packet streams (1 or 2)")
-    ap.add_argument("--owner-export", choices=["link", "packet", "none"], default="link",
-                    help="owner legs: order the export before the link stream (the driver), the packet stream, "
-                         "or no export at all")
+    ap.add_argument("--owner-export", choices=["link", "packet", "none"], default="packet",
+                    help="owner legs: the link on a torch stream of its own, on the packet stream (the driver's, "
+                         "OwnerLink.bind_owner), or no export at all")
     ap.add_argument("--micro", type=int, nargs="*", default=[],
                     help="packet counts: time snapshot_qk alone, the packet interval alone, and both, back to back")
     a = ap.parse_args()
@@ -144,8 +144,7 @@ def main():
         ens = ensemble(n0)
         link = OneGPU(nx)
         if a.owner_export == "packet":
-            pk = ctx.stream()
-            link._export = lambda c_, b, dt=0.0: c_.qg_export(b.data_ptr(), stream=pk, tail=dt, fenced=True)
+            link.bind_owner(ctx)
         elif a.owner_export == "none":
             link.publish = lambda c_, dt: None
         loop = sw.TwoLayerLoop(model, ens, 0.25 * (L / nx) / U0, U0, 0.25, 0.0, nsub=5, link=link)
