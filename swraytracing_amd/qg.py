@@ -248,10 +248,18 @@ def _owner_setup(world, pde, owner_weight, nx, Npackets, link_buffers="auto"):
 
     from .dist import OwnerLink, owner_bounds
     device = {"auto": None, "device": True, "host": False}[link_buffers]
-    return OwnerLink(nx, dist.get_backend(), device=device), owner_bounds(Npackets, world, owner_weight)
+    w0 = owner_weight_for(world) if owner_weight is None else owner_weight
+    return OwnerLink(nx, dist.get_backend(), device=device), owner_bounds(Npackets, world, w0)
 
 
-OWNER_WEIGHT = 0.5  # packets of the PDE owner per packet of a receiving rank (bench.py driver_step_forecast "owner")
+def owner_weight_for(world):
+    """The PDE owner's packets per packet of a receiving rank, from the
+    measured one-GPU legs of bench.py's driver_step_forecast["owner"]
+    (profiles/r06_final): with 2 ranks the owner's PDE leaves room for
+    packets (best w = 0.5), from 4 ranks on the receivers' share is what
+    bounds the step and the owner's PDE already takes about as long as it
+    (best w = 0: the owner holds no packets)."""
+    return 0.5 if world <= 2 else 0.0
 
 
 class TwoLayerLoop:
@@ -474,7 +482,7 @@ class ReceiverLoop:
 def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_days, U_g, f, Cg, *,
                   out_dir="data", nsub=4, max_steps=None, seed=146, verbose=False, r_drag=0.1,
                   packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None,
-                  pde="owner", owner_weight=OWNER_WEIGHT, link_buffers="auto"):
+                  pde="owner", owner_weight=None, link_buffers="auto"):
     """qgsw_raytrace.m:1-180 with the PDE and the packets on the GPU.
 
     Writes ``out_dir``/packet_x.bin, packet_k.bin, packet_time.bin, pv.bin,
@@ -589,7 +597,7 @@ def qgsw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_da
 def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_delay_Fr_days, U_g, f, Cg, *,
                         out_dir="data", nsub=5, max_steps=None, seed=5, verbose=False,
                         packet_intervals=1, integrator="leapfrog", fresh=True, ctx: Context | None = None,
-                        pde="owner", owner_weight=OWNER_WEIGHT, link_buffers="auto"):
+                        pde="owner", owner_weight=None, link_buffers="auto"):
     """qg2layersw_raytrace.m:1-247 with the PDE and the packets on the GPU
     (adaptive CFL :156-165, packets on layer 1 with u += shear_strength and
     interpolate's 2*nx y-period).  Same packet outputs as :func:`qgsw_raytrace`;
@@ -599,7 +607,8 @@ def qg2layersw_raytrace(nx, Npackets, near_inertial_factor, T_Fr_days, packet_de
     Sharded (torch.distributed, world > 1): ``pde="owner"`` (default) — rank 0
     steps the PDE and sends each step's top-layer qk and dt to the other
     ranks, which only build snapshots and advance packets; rank 0 holds
-    ``owner_weight`` packets per packet of another rank (dist.owner_bounds).
+    ``owner_weight`` packets per packet of another rank (dist.owner_bounds;
+    default owner_weight_for(world)).
     ``pde="replicated"``: every rank steps the same PDE, packets split evenly.
     Both write the single-process files byte for byte.  ``link_buffers``: the
     owner link's buffers ("auto": on the device with nccl, on the host with
