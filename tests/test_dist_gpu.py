@@ -149,9 +149,9 @@ def _rank_report(stderr, tail=40):
     ("qg2", 4, "owner", 0.5, "ode23", "host"),
     ("qg2", 2, "owner", 0.0, "ode23", "host"),  # the owner holds no packets: it only joins the collectives
     ("qg1", 2, "owner", 0.5, "leapfrog", "host"),
-    # the nccl form of the link (device buffers, export / snapshot ordered by
-    # events on the link's stream, dt on a gloo side group) over gloo's
-    # CUDA-tensor broadcast: RCCL itself needs one GPU per rank
+    # the nccl form of the link (device buffers, the export and the
+    # receivers' snapshots fenced on the host, dt on a gloo side group) over
+    # gloo's CUDA-tensor broadcast: RCCL itself needs one GPU per rank
     ("qg2", 2, "owner", 0.5, "leapfrog", "device"),
     ("qg2", 4, "owner", 0.25, "leapfrog", "device"),
     ("qg2", 2, "owner", 0.5, "ode23", "device"),
