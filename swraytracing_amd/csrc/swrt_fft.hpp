@@ -400,26 +400,39 @@ struct LdsRowPlanes {
   }
 };
 
-template <class Sink>
-__device__ __forceinline__ void spectra_to(int64_t idx, const double2* fk, int n, int mode, double K_d2, double kscale,
-                                           int with_psi, Sink out, int sx, int sy) {
-  const int64_t nn = (int64_t)n * n;
-  if (idx >= nn) return;
+// spectra_to in two halves, so a kernel can issue the loads of several
+// elements before any arithmetic: spectra_fetch reads the half-plane
+// coefficient of full-spectrum index idx (and where it came from),
+// spectra_emit turns it into the packed plane values.
+struct SpecIn {
+  double2 q;
+  int hx, hy;
+  bool cj, inband;
+};
+__device__ __forceinline__ SpecIn spectra_fetch(int64_t idx, const double2* fk, int n, int sx, int sy) {
   const int sh_ = __ffs(n) - 1;  // n is a power of two
   const int c = (int)idx & (n - 1), r = (int)idx >> sh_;
   const int kmax = n / 2 - 1;
   const int kx = signed_k(r, n), ky = signed_k(c, n);
+  SpecIn in;
+  in.inband = (kx >= -kmax && kx <= kmax && ky >= -kmax && ky <= kmax);
+  // Half-plane representative (kx', ky' >= 0 side) and whether to conjugate.
+  in.hx = kx;
+  in.hy = ky;
+  in.cj = false;
+  if (ky < 0 || (ky == 0 && kx < 0)) { in.hx = -kx; in.hy = -ky; in.cj = true; }
+  in.q = in.inband ? fk[(int64_t)(in.hx + kmax) * sx + (int64_t)in.hy * sy] : make_double2(0.0, 0.0);
+  return in;
+}
+template <class Sink>
+__device__ __forceinline__ void spectra_emit(const SpecIn& in, int64_t idx, int mode, double K_d2, double kscale,
+                                             int with_psi, Sink out) {
   double2 z[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) z[q] = make_double2(0.0, 0.0);
-  const bool inband = (kx >= -kmax && kx <= kmax && ky >= -kmax && ky <= kmax);
-  if (inband) {
-    // Half-plane representative (kx', ky' >= 0 side) and whether to conjugate.
-    int hx = kx, hy = ky;
-    bool cj = false;
-    if (ky < 0 || (ky == 0 && kx < 0)) { hx = -kx; hy = -ky; cj = true; }
-    double2 q = fk[(int64_t)(hx + kmax) * sx + (int64_t)hy * sy];
-    const double kxs = (double)hx * kscale, kys = (double)hy * kscale;
+  if (in.inband) {
+    const double2 q = in.q;
+    const double kxs = (double)in.hx * kscale, kys = (double)in.hy * kscale;
     double2 ps;
     if (mode == 0) {
       ps = q;
@@ -430,12 +443,12 @@ __device__ __forceinline__ void spectra_to(int64_t idx, const double2* fk, int n
     const double2 u = mul_mik(kys, ps);
     const double2 v = mul_ik(kxs, ps);
     double2 a[7] = {u, v, mul_ik(kxs, u), mul_ik(kys, u), mul_ik(kxs, v), mul_ik(kys, v), ps};
-    if (hx == 0 && hy == 0) {
+    if (in.hx == 0 && in.hy == 0) {
       // DC: only its real part reaches the real output of k2g.
 #pragma unroll
       for (int t = 0; t < 7; ++t) a[t].y = 0.0;
     }
-    if (cj) {
+    if (in.cj) {
 #pragma unroll
       for (int t = 0; t < 7; ++t) a[t].y = -a[t].y;
     }
@@ -449,6 +462,12 @@ __device__ __forceinline__ void spectra_to(int64_t idx, const double2* fk, int n
   out(1, idx, z[1]);
   out(2, idx, z[2]);
   if (with_psi) out(3, idx, z[3]);
+}
+template <class Sink>
+__device__ __forceinline__ void spectra_to(int64_t idx, const double2* fk, int n, int mode, double K_d2, double kscale,
+                                           int with_psi, Sink out, int sx, int sy) {
+  if (idx >= (int64_t)n * n) return;
+  spectra_emit(spectra_fetch(idx, fk, n, sx, sy), idx, mode, K_d2, kscale, with_psi, out);
 }
 __device__ __forceinline__ void spectra_at(int64_t idx, const double2* fk, int n, int mode, double K_d2, double kscale,
                                            int with_psi, double2* Z, int sx, int sy) {
@@ -476,8 +495,13 @@ __global__ void __launch_bounds__(1024) spectra_rows_kernel(const double2* fk, i
   const int nb = with_psi ? 4 : 3;
   const int64_t nn = (int64_t)n * n;
   const int r = blockIdx.x;
-  for (int e = threadIdx.x; e < n; e += blockDim.x)
-    spectra_to((int64_t)e + (int64_t)n * r, fk, n, mode, K_d2, kscale, with_psi, LdsRowPlanes{rows, n}, sx, sy);
+  // a lane's elements (at most 2: blockDim >= 3n/4): both loads in flight before either's arithmetic
+  const int e0 = threadIdx.x, e1 = threadIdx.x + blockDim.x;
+  const SpecIn in0 = spectra_fetch((int64_t)e0 + (int64_t)n * r, fk, n, sx, sy);
+  SpecIn in1;
+  if (e1 < n) in1 = spectra_fetch((int64_t)e1 + (int64_t)n * r, fk, n, sx, sy);
+  if (e0 < n) spectra_emit(in0, (int64_t)e0 + (int64_t)n * r, mode, K_d2, kscale, with_psi, LdsRowPlanes{rows, n});
+  if (e1 < n) spectra_emit(in1, (int64_t)e1 + (int64_t)n * r, mode, K_d2, kscale, with_psi, LdsRowPlanes{rows, n});
   __syncthreads();
   const int q = n >> 2;
   fft_stages_one_buffer(rows + (threadIdx.x / q) * n, threadIdx.x % q, n, logn, tw, 1);
@@ -572,7 +596,8 @@ __global__ void __launch_bounds__(256) pack_pairs_kernel(const double2* T, int n
 // for bit, without the 12.6 MB round trip of the transformed planes (512^2).
 // Loads: lanes c, c+1, ... of one plane read a row's CY adjacent columns
 // (contiguous); consecutive groups run on one XCD (its L2 shares the rows'
-// 128-B lines).  Stores: the CY records of one x are contiguous (y fastest).
+// 128-B lines).  Stores: the CY records of one x are contiguous (y fastest),
+// and consecutive lanes store consecutive 16-B chunks of them.
 // blockDim 3*CY*n/4 <= 1024, dynamic LDS 3*CY*(n+1) double2, n/CY % 8 == 0.
 template <int CY>
 __global__ void __launch_bounds__(1024) fft_cols_pack_kernel(const double2* Z, int n, int logn, const double2* tw,
@@ -598,22 +623,29 @@ __global__ void __launch_bounds__(1024) fft_cols_pack_kernel(const double2* Z, i
   __syncthreads();
   fft_stages_one_buffer(sbuf + (t / quarter) * ld, t % quarter, n, logn, tw, 1);
   const int hi = npad - n - 2;
-  for (int e = t; e < n * CY; e += blockDim.x) {
-    const int x = e / CY, cy = e - (e / CY) * CY, y = y0 + cy;
-    const double2 a = sbuf[(0 * CY + cy) * ld + x], b = sbuf[(1 * CY + cy) * ld + x],
-                  cc = sbuf[(2 * CY + cy) * ld + x];
-    const double rec[6] = {a.x + shear, a.y, b.x, b.y, cc.x, -b.x};
+  // chunk f = (x, r): the r-th 16 B of row x's CY contiguous records (record
+  // cy = r / 3, part m = r % 3: {u + shear, v}, {u_x, u_y}, {v_x, -u_x}), so
+  // consecutive lanes store consecutive 16 B of a row
+  constexpr int RW = 3 * CY;
+  for (int f = t; f < n * RW; f += blockDim.x) {
+    const int x = f / RW, r = f - x * RW, cy = r / 3, m = r - 3 * cy, y = y0 + cy;
+    const double2 b = sbuf[(1 * CY + cy) * ld + x];
+    double2 v;
+    if (m == 0) {
+      const double2 a = sbuf[(0 * CY + cy) * ld + x];
+      v = make_double2(a.x + shear, a.y);
+    } else if (m == 1) {
+      v = b;
+    } else {
+      v = make_double2(sbuf[(2 * CY + cy) * ld + x].x, -b.x);
+    }
     const int px[3] = {x + 2, x >= n - 2 ? x + 2 - n : -1, x < hi ? x + 2 + n : -1};
     const int py[3] = {y + 2, y >= n - 2 ? y + 2 - n : -1, y < hi ? y + 2 + n : -1};
     for (int i = 0; i < 3; ++i) {
       if (px[i] < 0) continue;
       for (int j = 0; j < 3; ++j) {
         if (py[j] < 0) continue;
-        // a record is 48 B at a multiple of 48 B: three 16-B stores
-        double2* d = reinterpret_cast<double2*>(nodes + ((int64_t)px[i] * npad + py[j]) * 6);
-        d[0] = make_double2(rec[0], rec[1]);
-        d[1] = make_double2(rec[2], rec[3]);
-        d[2] = make_double2(rec[4], rec[5]);
+        reinterpret_cast<double2*>(nodes + ((int64_t)px[i] * npad + py[j]) * 6)[m] = v;
       }
     }
   }

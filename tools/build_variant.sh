@@ -8,5 +8,5 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 mkdir -p build/var
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -Wall "$@" \
-  -o "build/var/$name.so" swraytracing_amd/csrc/swrt_api.hip
+  -o "build/var/$name.so" swraytracing_amd/csrc/swrt_api.hip -x none build/obj/*.o  # host TUs (build() made them)
 echo "built build/var/$name.so"
