@@ -413,8 +413,8 @@ def _owner_links():
             super().__init__(nx, "nccl", nbuf=nbuf)
             self.fixed_dt = dt
 
-        def _bcast(self, b):
-            pass
+        def _bcast(self, b, async_op=False):
+            return None
 
         def _send_dt(self, dt):
             pass

@@ -135,6 +135,26 @@ def allreduce_max_fn(backend: str = "nccl", group=None):
     return lambda v: max_over_ranks(v, backend=backend, group=group)
 
 
+def _host_wait(work):
+    """Block the host until an asynchronous collective has completed, without
+    queueing a device-side wait on any stream (Work.wait() on "nccl" would make
+    the current stream wait on RCCL's); then surface its error, if any."""
+    import time
+    while not work.is_completed():
+        time.sleep(0)
+    with _default_stream():
+        work.wait()
+
+
+def _default_stream():
+    import contextlib
+
+    import torch
+    if not torch.cuda.is_available():
+        return contextlib.nullcontext()
+    return torch.cuda.stream(torch.cuda.default_stream())
+
+
 class OwnerLink:
     """The PDE-owner driver's per-step hand-off (qg2layersw_raytrace.m:152-197
     sharded with the PDE on ONE rank): the packets read only the top layer of
@@ -145,17 +165,19 @@ class OwnerLink:
     stepping the replicated 2-layer PDE.
 
     "nccl" (RCCL over xGMI): the half plane goes by one broadcast of a device
-    buffer per step on a stream of its own (a non-blocking torch stream), so
-    it runs beside the owner's next PDE step and the receivers' packet
-    launches; swrt_qg_export fills the buffer on the QG stream and
-    swrt_snapshot_qk reads it, each ordered against that stream by events —
-    no host synchronisation on the device data.  dt, which a receiving host
-    needs to queue its packets, goes by a host-side broadcast on a gloo group
-    (reading it back from the device would wait behind the packet launches
-    that hold the GPU).  "gloo": both through one host buffer.  Two buffers in
-    turn: the current step's and the previous step's qk (the first active
-    step's grid_U(prev_qk)); swrt_snapshot_qk orders the next fill of a
-    buffer after its read."""
+    buffer per step, with dt appended to it; dt also goes by a host-side
+    broadcast on a gloo group, because a receiving host needs it to queue its
+    packets and reading it back from the device would wait behind the packet
+    launches that hold the GPU.  "gloo": one host buffer carries both.
+    ``nbuf`` buffers in turn (the latest qk, the previous one, and the ones a
+    receiver has not read yet).  No stream of the library ever waits on a
+    torch or RCCL stream: the owner's export into a buffer is fenced on the
+    host against the broadcast that last read it, the owner's broadcast is
+    asynchronous (its completion polled on the host, never waited for on the
+    packet stream), and a receiver's snapshot reads a buffer only after the
+    host has seen its broadcast complete (ReceiverLoop).  A cross-stream wait
+    on ROCm costs 0.1-0.2 ms per step while packet launches hold the GPU
+    (tools/owner_legs.py)."""
 
     def __init__(self, nx, backend, owner=0, group=None, device=None, nbuf=5):
         """``device``: device buffers (default: with "nccl"); True with
@@ -197,15 +219,16 @@ class OwnerLink:
             # on the link stream (see swrt_qg_export dst_mode 2)
             i = next(k for k, x in enumerate(self.bufs) if x is b)
             if self._sent is not None and self._sent[i] is not None:
-                self._sent[i].synchronize()
+                _host_wait(self._sent[i])
+                self._sent[i] = None
             ctx.qg_export(b.data_ptr(), which=0, layer=0, stream=self.stream.cuda_stream, tail=dt, fenced=True)
         else:
             ctx.qg_export(b.numpy(), which=0, layer=0, tail=dt)
 
-    def _bcast(self, b):
+    def _bcast(self, b, async_op=False):
         import torch.distributed as dist
         with self._on_stream():
-            dist.broadcast(b, src=self.owner, group=self.group)
+            return dist.broadcast(b, src=self.owner, group=self.group, async_op=async_op)
 
     def _send_dt(self, dt):
         if not self.device:
@@ -251,12 +274,12 @@ class OwnerLink:
         i = self._next()
         b = self.bufs[i]
         self._export(ctx, b, dt)
-        self._bcast(b)
-        if self._sent is not None:  # (the broadcast's completion, for the buffer's next export)
-            import torch
-            if self._sent[i] is None:
-                self._sent[i] = torch.cuda.Event()
-            self._sent[i].record(self.stream)
+        # asynchronous: RCCL's stream waits for the export queued so far on
+        # self.stream, and nothing waits for RCCL's stream on the device; the
+        # buffer's next export polls the work on the host (_export)
+        work = self._bcast(b, async_op=self._sent is not None)
+        if self._sent is not None:
+            self._sent[i] = work
         self.cur = i
         self._send_dt(dt)
 
@@ -277,6 +300,10 @@ class OwnerLink:
         if self._dt_work is not None:
             self._dt_work.wait()
             self._dt_work = None
+        for i, w in enumerate(self._sent or []):
+            if w is not None:
+                _host_wait(w)
+                self._sent[i] = None
 
     def snapshot(self, ctx, slot, which, L, K_d2, shear, k_scale, ny_period, fenced=False):
         """grid_U of the latest (which 0) or the previous (1) qk into `slot`.
