@@ -596,7 +596,10 @@ int swrt_clock_ghz_stamps(const uint64_t* stamps, int64_t waves, double realtime
  *   from its own step size, and attempts taken from a gated guess (queued
  *   before the previous attempt's error was known), summed over the calls.
  * SWRT_DEBUG_ODE23_SPLIT_RUNS (get only): swrt_ode23_run calls whose attempts
- *   ran as two part launches on the two packet streams. */
+ *   ran as two part launches on the two packet streams.
+ * SWRT_DEBUG_ODE23_FIRST_CHAINED (get only): ode23 calls that took the first
+ *   step size and first attempt the previous call queued behind their chained
+ *   stage 1 (t0 = 0, tfinal = tmax and RelTol as that call assumed). */
 #define SWRT_DEBUG_HAZARD_CHECK 1
 #define SWRT_DEBUG_SPIN_US 2
 #define SWRT_DEBUG_LEGACY_PARK 3
@@ -609,6 +612,7 @@ int swrt_clock_ghz_stamps(const uint64_t* stamps, int64_t waves, double realtime
 #define SWRT_DEBUG_ODE23_FIRST_TAKEN 11
 #define SWRT_DEBUG_ODE23_GUESSES_TAKEN 12
 #define SWRT_DEBUG_ODE23_SPLIT_RUNS 13
+#define SWRT_DEBUG_ODE23_FIRST_CHAINED 14
 int swrt_debug_set(swrt_ctx* ctx, int key, int64_t value);
 int swrt_debug_get(swrt_ctx* ctx, int key, int64_t* value_out);
 

@@ -137,6 +137,7 @@ DEBUG_ODE23_CHAINED = 10
 DEBUG_ODE23_FIRST_TAKEN = 11
 DEBUG_ODE23_GUESSES_TAKEN = 12
 DEBUG_ODE23_SPLIT_RUNS = 13
+DEBUG_ODE23_FIRST_CHAINED = 14
 
 _lib = None
 

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <map>
 #include <new>
@@ -35,6 +36,9 @@ using namespace swrt;
 namespace {
 
 constexpr int kMaxStepsPerLaunch = 64;  // bound one launch's run time
+// a host copy of an attempt workgroup's error max not yet written (no max of
+// non-negative doubles, NaN included, has this bit pattern)
+constexpr unsigned long long kHpartEmpty = ~0ull;
 constexpr int kXkaMargin = 3;           // xka_tile_kernel: drift margin (cells) of a tile's window
 #ifndef SWRT_TILE
 #define SWRT_TILE 16
@@ -317,7 +321,23 @@ struct swrt_ctx {
     uint64_t wgen[2] = {0, 0};
     double alpha = 0.0, f = 0.0, Cg = 0.0, thr = 0.0, bump = 0.0;
     int64_t taken = 0;  // calls that took it (SWRT_DEBUG_ODE23_CHAINED)
+    // the next call's first attempt, queued behind its stage 1 from the
+    // device's own step size for t0 = 0, tfinal = tmax and `rtol`
+    // (ode23_chain_first): its max slot, each part's workgroups, the split
+    bool first_q = false;
+    int first_slot = -1;
+    unsigned first_wg[2] = {0, 0};
+    bool split = false;
+    double rtol = 0.0, tfinal = 0.0, tmax = 0.0;
+    int64_t first_taken = 0;  // calls that took it (SWRT_DEBUG_ODE23_FIRST_CHAINED)
   } o_chain;
+  // the chained first attempt's part 1 is queued on sx[0] and not joined
+  // (b_pending stays 0, so the QG calls between two intervals do not join
+  // it): a call that drops the chain, or an ode23 call that does not take the
+  // attempt, joins it first (chain_join)
+  bool chain_b = false;
+  hipEvent_t chain_ev[2] = {nullptr, nullptr};
+  bool chain_first = true;  // SWRT_ODE23_CHAIN_FIRST=0 (environment, A/B runs): stage 1 alone is chained
   uint64_t slot_wgen = 0;  // Slot::wgen source
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
@@ -462,10 +482,13 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
 // (swrt_ode23_run_hooked): it would race the interval's attempts in flight.
 #define HOOK_REFUSE \
   if (c->in_hook) return fail(c, SWRT_ERR_STATE, "this call may touch the packets: not allowed inside an ode23 hook");
-#define GUARD_BEGIN_KEEP_SPLIT \
-  HOOK_REFUSE                  \
-  try {                        \
-    c->o_chain.queued = false;
+#define GUARD_BEGIN_KEEP_SPLIT                  \
+  HOOK_REFUSE                                   \
+  try {                                         \
+    {                                           \
+      const int crc_ = chain_drop(c);           \
+      if (crc_) return crc_;                    \
+    }
 #define GUARD_BEGIN_KEEP_CHAIN    \
   try {                           \
     {                             \
@@ -473,10 +496,13 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
       if (jrc_) return jrc_;      \
       hz_api(c);                  \
     }
-#define GUARD_BEGIN            \
-  HOOK_REFUSE                  \
-  GUARD_BEGIN_KEEP_CHAIN       \
-  c->o_chain.queued = false;
+#define GUARD_BEGIN              \
+  HOOK_REFUSE                    \
+  GUARD_BEGIN_KEEP_CHAIN         \
+  {                              \
+    const int crc_ = chain_drop(c); \
+    if (crc_) return crc_;       \
+  }
 #define GUARD_END(ctx)                                                \
   }                                                                   \
   catch (const std::bad_alloc&) {                                     \
@@ -499,6 +525,27 @@ int join_b(swrt_ctx* c) {
   }
   c->b_pending = 0;
   return SWRT_OK;
+}
+
+// Order a chained first attempt's part 1 (sx[0]) before the packet stream's
+// next work: the attempt is dropped, or its call runs another.
+int chain_join(swrt_ctx* c) {
+  if (!c->chain_b) return SWRT_OK;
+  c->chain_b = false;
+  HIPCHK(c, hipEventRecord(c->jx[0], c->sx[0]));
+  HIPCHK(c, hipStreamWaitEvent(c->stream0, c->jx[0], 0));
+  if (c->hz.on) {
+    c->hz.record(c->jx[0], 1);
+    c->hz.wait(0, c->jx[0]);
+  }
+  return SWRT_OK;
+}
+
+// A queued ode23 chain dropped (the packets may change).
+int chain_drop(swrt_ctx* c) {
+  c->o_chain.queued = false;
+  c->o_chain.first_q = false;
+  return chain_join(c);
 }
 
 // Hazard checker (swrt_hazard.hpp): the packet-state buffers of the context.
@@ -564,6 +611,7 @@ int sync_sx(swrt_ctx* c) {
       if (c->hz.on) c->hz.sync(i + 1);
     }
   c->b_pending = 0;
+  c->chain_b = false;
   return SWRT_OK;
 }
 
@@ -1419,11 +1467,13 @@ int swrt_create(int device, swrt_ctx** out) {
   ok = ok && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) == hipSuccess &&
        hipStreamCreateWithFlags(&c->sx[0], hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t& e : c->jx) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+  for (hipEvent_t& e : c->chain_ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   ok = ok && hipHostMalloc((void**)&c->dev_err, sizeof(int) * 4, hipHostMallocMapped) == hipSuccess &&
        hipHostGetDevicePointer((void**)&c->dev_err_d, c->dev_err, 0) == hipSuccess;
   if (c->dev_err) std::memset(c->dev_err, 0, sizeof(int) * 4);
   c->stream0 = c->stream;
   if (const char* e = getenv("SWRT_HAZARD_CHECK")) c->hz.on = atoi(e) != 0;
+  if (const char* e = getenv("SWRT_ODE23_CHAIN_FIRST")) c->chain_first = atoi(e) != 0;
   if (!ok) {
     swrt_destroy(c);
     return SWRT_ERR_HIP;
@@ -1492,6 +1542,8 @@ void swrt_destroy(swrt_ctx* c) {
     if (p) (void)hipFree(p);
   for (auto e : c->timing.ev) (void)hipEventDestroy(e);
   if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+  for (hipEvent_t e : c->chain_ev)
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->jx)
     if (e) (void)hipEventDestroy(e);
   if (c->qstream) (void)hipStreamDestroy(c->qstream);
@@ -2601,7 +2653,7 @@ int swrt_synchronize(swrt_ctx* c) {
 
 int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
   if (!c) return SWRT_ERR_ARG;
-  c->o_chain.queued = false;
+  if (int rc = chain_drop(c)) return rc;
   switch (key) {
     case SWRT_DEBUG_HAZARD_CHECK:
       if (value != 0 && value != 1) return fail(c, SWRT_ERR_ARG, "hazard check must be 0 or 1");
@@ -2665,6 +2717,7 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
     case SWRT_DEBUG_ODE23_FIRST_TAKEN: *value_out = c->o23_first_taken; return SWRT_OK;
     case SWRT_DEBUG_ODE23_GUESSES_TAKEN: *value_out = c->o23_guesses_taken; return SWRT_OK;
     case SWRT_DEBUG_ODE23_SPLIT_RUNS: *value_out = c->o23_split_runs; return SWRT_OK;
+    case SWRT_DEBUG_ODE23_FIRST_CHAINED: *value_out = c->o_chain.first_taken; return SWRT_OK;
     default: return fail(c, SWRT_ERR_ARG, "unknown debug key");
   }
 }
@@ -3541,8 +3594,12 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   }
   if (!c->o_hmax) HIPCHK(c, hipHostMalloc(&c->o_hmax, 3 * sizeof(unsigned long long)));
   if (!c->o_hpart) {
-    HIPCHK(c, hipHostMalloc((void**)&c->o_hpart, 6 * kMaxBins * sizeof(unsigned long long), hipHostMallocMapped));
+    // coherent (fine-grained): the attempt kernels' stores reach host memory
+    // without the system-scope release of a separate event marker
+    HIPCHK(c, hipHostMalloc((void**)&c->o_hpart, 6 * kMaxBins * sizeof(unsigned long long),
+                            hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(c, hipHostGetDevicePointer((void**)&c->o_hpart_d, c->o_hpart, 0));
+    std::fill(c->o_hpart, c->o_hpart + 6 * kMaxBins, kHpartEmpty);
   }
   if (!c->o_shown) {
     HIPCHK(c, hipMalloc((void**)&c->o_coef, 8 * sizeof(double)));
@@ -3615,16 +3672,17 @@ namespace {
 // one ode23 stage over all packets: the LDS-tiled kernel when the packets are
 // binned by the tile kernel's 16x16-cell tiles, else one lane per packet
 template <int STAGE, bool TWO, bool V5>
-void ode23_tile_launch(swrt_ctx* c, const Ode23Args& a, unsigned grid, const int* starts, int ntx, hipStream_t st) {
+void ode23_tile_launch(swrt_ctx* c, const Ode23Args& a, unsigned grid, const int* starts, int ntx, hipStream_t st,
+                       hipEvent_t stop) {
   if constexpr (STAGE == 0) {
     if (a.coef) {  // coefficients from device memory (swrt_ode23_run's first attempt)
-      hipLaunchKernelGGL((tile_ode23_kernel<0, TWO, kTile, kMargin, kTileThreads, V5, true>), dim3(grid),
-                         dim3(kTileThreads), 0, st, a, starts, ntx);
+      hipExtLaunchKernelGGL((tile_ode23_kernel<0, TWO, kTile, kMargin, kTileThreads, V5, true>), dim3(grid),
+                            dim3(kTileThreads), 0, st, nullptr, stop, 0, a, starts, ntx);
       return;
     }
   }
-  hipLaunchKernelGGL((tile_ode23_kernel<STAGE, TWO, kTile, kMargin, kTileThreads, V5>), dim3(grid),
-                     dim3(kTileThreads), 0, st, a, starts, ntx);
+  hipExtLaunchKernelGGL((tile_ode23_kernel<STAGE, TWO, kTile, kMargin, kTileThreads, V5>), dim3(grid),
+                        dim3(kTileThreads), 0, st, nullptr, stop, 0, a, starts, ntx);
 }
 
 // swrt_ode23_run may split each attempt into two part launches (the even and
@@ -3642,10 +3700,16 @@ bool ode23_split_ok(swrt_ctx* c) {
 
 // part -1: one launch over every tile on the packet stream; 0 / 1: that part
 // of a split attempt (part 1 on sx[0]).  *wg_out: the workgroups of the tile
-// launch (each stores its max to a.hpart), 0 for the per-packet kernels.
+// launch (each stores its max to a.hpart, whose host copy is first marked
+// empty), 0 for the per-packet kernels.  `stop`: an event the tile launch
+// itself completes (*stop_done = true) — no marker between consecutive
+// attempts (a separate event record cost ~7 us of idle stream per launch,
+// profiles/r06_ode23); the per-packet kernels leave it to the caller.
 template <int STAGE>
-int ode23_launch(swrt_ctx* c, const Ode23Args& a0, int part = -1, unsigned* wg_out = nullptr) {
+int ode23_launch(swrt_ctx* c, const Ode23Args& a0, int part = -1, unsigned* wg_out = nullptr,
+                 hipEvent_t stop = nullptr, bool* stop_done = nullptr) {
   if (wg_out) *wg_out = 0;
+  if (stop_done) *stop_done = false;
   const int ntx = (int)((c->slot[0].nx + kTile - 1) / kTile);
   if (part >= 0 && !ode23_split_ok(c)) return fail(c, SWRT_ERR_STATE, "ode23 split attempt without a split binning");
   if (use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx * ntx) {
@@ -3676,14 +3740,19 @@ int ode23_launch(swrt_ctx* c, const Ode23Args& a0, int part = -1, unsigned* wg_o
     } else {
       a.order = c->o_order;
     }
+    if (a.hpart) {
+      unsigned long long* hh = c->o_hpart + (a.hpart - c->o_hpart_d);
+      std::fill(hh, hh + grid, kHpartEmpty);
+    }
     const bool v5 = c->slot[0].div_free && (a.nslots == 1 || c->slot[1].div_free);
     if (a.nslots == 2) {
-      if (v5) ode23_tile_launch<STAGE, true, true>(c, a, grid, starts, ntx, st);
-      else ode23_tile_launch<STAGE, true, false>(c, a, grid, starts, ntx, st);
+      if (v5) ode23_tile_launch<STAGE, true, true>(c, a, grid, starts, ntx, st, stop);
+      else ode23_tile_launch<STAGE, true, false>(c, a, grid, starts, ntx, st, stop);
     } else {
-      if (v5) ode23_tile_launch<STAGE, false, true>(c, a, grid, starts, ntx, st);
-      else ode23_tile_launch<STAGE, false, false>(c, a, grid, starts, ntx, st);
+      if (v5) ode23_tile_launch<STAGE, false, true>(c, a, grid, starts, ntx, st, stop);
+      else ode23_tile_launch<STAGE, false, false>(c, a, grid, starts, ntx, st, stop);
     }
+    if (stop_done) *stop_done = stop != nullptr;
   } else if constexpr (STAGE == 0) {  // one lane per packet: the three stage launches
     const dim3 grid(nblocks(c->n, 256)), block(256);
     Ode23Args b = a0;
@@ -3777,7 +3846,7 @@ int swrt_ode23_accept(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
   if (c->in_hook) return fail(c, SWRT_ERR_STATE, "this call may touch the packets: not allowed inside an ode23 hook");
   HIPCHK_RC(lost_check(c));
-  c->o_chain.queued = false;
+  HIPCHK_RC(chain_drop(c));
   if (!c->o_ynx) return fail(c, SWRT_ERR_STATE, "no ode23 step attempted");
   std::swap(c->dx, c->o_ynx);
   std::swap(c->dk, c->o_ynk);
@@ -3796,14 +3865,20 @@ bool same_bits(double a, double b) { return std::memcmp(&a, &b, sizeof(double)) 
 // call's stage 1 — re-binning when due, in-tile sort, f at t = 0 — queued on
 // the accepted packets with the armed slots as slots 0 / 1, so the device runs
 // it while the host returns and prepares that call.  The next call takes it
-// only if it would compute exactly that (ode23_chain_take).  (Chaining the
-// first step size and a whole first attempt as well measured no faster,
-// profiles/r05_chain.)
-int ode23_chain_queue(swrt_ctx* c, double tmax, double f, double Cg, int nslots, double thr, double bump) {
+// only if it would compute exactly that (ode23_chain_take).  Behind stage 1
+// go the next call's first step size and its first attempt, as that call
+// would queue them (ode23_chain_first), taken only if the call's t0, tfinal
+// and RelTol are the ones assumed.  (Round 5 chained an unsplit first attempt,
+// 186 us against 123 us split, and measured no faster: profiles/r05_chain.)
+int ode23_chain_first(swrt_ctx* c, int sl_f1, double tmax, double f, double Cg, double thr, double bump,
+                      double rtol);
+int ode23_chain_queue(swrt_ctx* c, double tmax, double f, double Cg, int nslots, double thr, double bump,
+                      double rtol) {
   swrt_ctx::O23Chain& ch = c->o_chain;
   const bool want = ch.want;
   ch.want = false;
   ch.queued = false;
+  ch.first_q = false;
   if (!want || nslots != 2 || ch.sa < 0 || ch.sb < 0 || ch.sa == ch.sb || c->packets_lost) return SWRT_OK;
   if (!c->slot[ch.sa].set || !c->slot[ch.sb].set || c->slot[ch.sa].nx != c->slot[ch.sb].nx) return SWRT_OK;
   slot_writes_wait(c);  // e.g. the hook's snapshot into slot sb on the QG stream
@@ -3811,11 +3886,15 @@ int ode23_chain_queue(swrt_ctx* c, double tmax, double f, double Cg, int nslots,
   for (int i = 0; i < SWRT_MAX_SLOTS; ++i) saved[i] = c->slot[i];
   c->slot[0] = saved[ch.sa];
   c->slot[1] = saved[ch.sb];
-  const int rc = ode23_f1_queue(c, 0.0, tmax, f, Cg, 2, thr, bump);
+  int rc = ode23_f1_queue(c, 0.0, tmax, f, Cg, 2, thr, bump);
+  const int sl_f1 = c->o_dmax_cur;
+  if (!rc) {
+    c->o_dmax_cur = (sl_f1 + 1) % 3;
+    rc = ode23_chain_first(c, sl_f1, tmax, f, Cg, thr, bump, rtol);
+  }
   for (int i = 0; i < SWRT_MAX_SLOTS; ++i) c->slot[i] = saved[i];
   if (rc) return rc;
-  ch.dmax_slot = c->o_dmax_cur;
-  c->o_dmax_cur = (ch.dmax_slot + 1) % 3;
+  ch.dmax_slot = sl_f1;
   for (int i = 0; i < 2; ++i) {
     const Slot& s = c->slot[i == 0 ? ch.sa : ch.sb];
     ch.nodes[i] = s.nodes;
@@ -3900,12 +3979,16 @@ class DeviceExec final : public O23Exec {
       // whole max passes, so does every part (err = absh * max is monotone)
       a.gate = gate_slot >= 0 ? c->o_dmax + 3 * p + gate_slot : nullptr;
       a.hpart = c->o_hpart_d + (size_t)(3 * p + sl) * kMaxBins;
-      HIPCHK_RC((ode23_launch<0>(c, a, split ? p : -1, &wg[p][sl])));
       const hipStream_t st = p == 0 ? c->stream : c->sx[0];
-      if (wg[p][sl] == 0)  // the per-packet stage kernels (never split): copy the max
-        HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl, c->o_dmax + sl, sizeof(unsigned long long), hipMemcpyDeviceToHost,
-                                 st));
-      HIPCHK(c, hipEventRecord(p == 0 ? c->o_ev[sl] : c->o_evb[sl], st));
+      const hipEvent_t ev = p == 0 ? c->o_ev[sl] : c->o_evb[sl];
+      bool attached = false;
+      HIPCHK_RC((ode23_launch<0>(c, a, split ? p : -1, &wg[p][sl], ev, &attached)));
+      if (!attached) {
+        if (wg[p][sl] == 0)  // the per-packet stage kernels (never split): copy the max
+          HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl, c->o_dmax + sl, sizeof(unsigned long long),
+                                   hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipEventRecord(ev, st));
+      }
     }
     c->o_dmax_cur = (sl + 1) % 3;
     *slot = sl;
@@ -3913,18 +3996,36 @@ class DeviceExec final : public O23Exec {
   }
   // the device's first attempt, from its own step size (before the hook)
   int queue_first() { return launch(0, 1, 0.0, 0.0, 0.0, -1, 0.0, 0.0, &first_slot, c->o_coef); }
+  int first() const { return first_slot; }
+  unsigned workgroups(int p, int sl) const { return wg[p][sl]; }
+  // the first attempt the previous call queued (ode23_chain_first): its slot
+  // and workgroups; the hook then waits for the first wait_max, so the
+  // controller queues its next guess before the hook's host work
+  void adopt_first(int sl, const unsigned wg_[2]) {
+    first_slot = sl;
+    wg[0][sl] = wg_[0];
+    wg[1][sl] = wg_[1];
+    defer_hook = true;
+  }
+
+  int run_hook() {
+    // the hook may call the library (e.g. the next QG step on the QG stream);
+    // it must not touch the packets (c->in_hook refuses those calls).  Its
+    // calls must not join the extra stream's attempt parts into the packet
+    // stream (they run on), so the split is hidden from them and re-marked after.
+    hook_due = false;
+    c->b_pending = 0;
+    c->in_hook = true;
+    hook(hook_user);
+    c->in_hook = false;
+    if (split) c->b_pending = 1;
+    return SWRT_OK;
+  }
 
   int stage1(double* raw) override {
     if (hook) {
-      // the hook may call the library (e.g. the next QG step on the QG stream);
-      // it must not touch the packets (c->in_hook refuses those calls).  Its
-      // calls must not join the extra stream's attempt parts into the packet
-      // stream (they run on), so the split is hidden from them and re-marked after.
-      c->b_pending = 0;
-      c->in_hook = true;
-      hook(hook_user);
-      c->in_hook = false;
-      if (split) c->b_pending = 1;
+      hook_due = true;
+      if (!defer_hook) HIPCHK_RC(run_hook());
     }
     HIPCHK(c, hipEventSynchronize(c->o_ev[sl_f1]));
     if (dev_first)
@@ -3948,6 +4049,7 @@ class DeviceExec final : public O23Exec {
   // the raw error max of the attempt in slot sl: the bit-pattern max (= the
   // value max of these non-negative doubles, as the device's atomicMax)
   int wait_max(int sl, double* out) override {
+    if (hook_due) HIPCHK_RC(run_hook());
     unsigned long long m = 0;
     for (int p = 0; p < P; ++p) {
       // (polling hipEventQuery instead: 1.802 / 1.831 vs 1.849 / 1.805 ms, noise; profiles/r05_ode23)
@@ -3956,8 +4058,15 @@ class DeviceExec final : public O23Exec {
       if (g == 0) {
         m = std::max(m, c->o_hmax[sl]);
       } else {
-        const unsigned long long* hp = c->o_hpart + (size_t)(3 * p + sl) * kMaxBins;
-        for (unsigned i = 0; i < g; ++i) m = std::max(m, hp[i]);
+        // the launch's own completion event carries no system-scope release:
+        // each workgroup's store to the coherent host copy may land a moment
+        // after it, so an entry still marked empty is awaited
+        const volatile unsigned long long* hp = c->o_hpart + (size_t)(3 * p + sl) * kMaxBins;
+        for (unsigned i = 0; i < g; ++i) {
+          unsigned long long v = hp[i];
+          if (v == kHpartEmpty) HIPCHK_RC(await_hpart(hp + i, p, &v));
+          m = std::max(m, v);
+        }
       }
     }
     if (c->hz.on) {  // debug: the host-mapped maxima against the device's atomicMax slots
@@ -3970,6 +4079,18 @@ class DeviceExec final : public O23Exec {
       if (d != m) return fail(c, SWRT_ERR_STATE, "ode23: host-mapped error max differs from the device's");
     }
     std::memcpy(out, &m, sizeof(double));
+    return SWRT_OK;
+  }
+  int await_hpart(const volatile unsigned long long* e, int p, unsigned long long* out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while ((*out = *e) == kHpartEmpty) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+        HIPCHK(c, hipStreamSynchronize(p == 0 ? c->stream : c->sx[0]));
+        if ((*out = *e) == kHpartEmpty)
+          return fail(c, SWRT_ERR_STATE, "ode23: a workgroup's error max never reached host memory");
+        break;
+      }
+    }
     return SWRT_OK;
   }
   // The extra stream's part launches ordered before the packet stream's next
@@ -4005,11 +4126,69 @@ class DeviceExec final : public O23Exec {
   int first_slot = -1;
   void (*hook)(void*);
   void* hook_user;
+  bool defer_hook = false, hook_due = false;
   struct Set {
     double *x, *k, *F;
   } S[3];
   unsigned wg[2][3] = {};  // workgroups of each part's launch in each slot (0: the max was copied)
 };
+
+// The next call's first step size and first attempt, queued behind the stage
+// 1 the chain just queued (slots arranged as that call's 0 / 1): what
+// swrt_ode23_run_hooked queues for t0 = 0, tfinal = tmax and `rtol`, on the
+// tile path only.  Part 1 of a split attempt stays unjoined (c->chain_b); the
+// slots' use mark of this call covers it (c->tail_ev, after sx[0] has waited
+// for the packet stream's tail).
+int ode23_chain_first(swrt_ctx* c, int sl_f1, double tmax, double f, double Cg, double thr, double bump,
+                      double rtol) {
+  swrt_ctx::O23Chain& ch = c->o_chain;
+  ch.first_q = false;
+  const int ntx_ = (int)((c->slot[0].nx + kTile - 1) / kTile);
+  if (!c->chain_first || !(use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx_ * ntx_))
+    return SWRT_OK;
+  const bool split = ode23_split_ok(c);
+  const double t0 = 0.0, tfinal = tmax;
+  const double tdir = std::copysign(1.0, tfinal - t0);
+  const double rtol_c = std::max(rtol, 100 * 2.220446049250313e-16);
+  const double htspan = std::fabs(tfinal - t0);
+  const double hmax = 0.1 * htspan;
+  const double c0 = 0.8 * std::pow(rtol_c, 1.0 / 3.0);
+  hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax, htspan,
+                     16 * o23_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3, split ? 3 : 0);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
+  if (split) {
+    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->o_ev[sl_f1], 0));
+    if (c->hz.on) {
+      c->hz.record(c->o_ev[sl_f1], 0);
+      c->hz.wait(1, c->o_ev[sl_f1]);
+    }
+  }
+  Ode23Args base;
+  int rc;
+  if ((rc = ode23_prepare(c, 2, base, tmax, f, Cg, thr, bump))) return rc;
+  DeviceExec ex(c, base, split, true, sl_f1, nullptr, nullptr);
+  if ((rc = ex.queue_first())) return rc;
+  ch.first_slot = ex.first();
+  for (int p = 0; p < 2; ++p) ch.first_wg[p] = ex.workgroups(p, ch.first_slot);
+  if (split) {
+    HIPCHK(c, hipEventRecord(c->chain_ev[0], c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->chain_ev[0], 0));
+    HIPCHK(c, hipEventRecord(c->chain_ev[1], c->sx[0]));
+    if (c->hz.on) {
+      c->hz.record(c->chain_ev[0], 0);
+      c->hz.wait(1, c->chain_ev[0]);
+    }
+    c->tail_ev = c->chain_ev[1];
+    c->chain_b = true;
+  }
+  ch.first_q = true;
+  ch.split = split;
+  ch.rtol = rtol;
+  ch.tfinal = tfinal;
+  ch.tmax = tmax;  // (the attempt's alpha = t / tmax; stage 1's alpha(0) does not see it)
+  return SWRT_OK;
+}
 }  // namespace
 
 int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
@@ -4031,9 +4210,17 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
   // stage 1 (with this call's re-binning and in-tile sort), its max in slot
   // sl_f1: queued by the previous call when it was chained to this one
   int sl_f1;
-  if (ode23_chain_take(c, t0, tmax, f, Cg, nslots, thr, bump)) {
-    sl_f1 = c->o_chain.dmax_slot;
-    ++c->o_chain.taken;
+  // the chained first attempt is a candidate if this call asks for the first
+  // attempt it assumed; anything else joins its part 1 before touching the packets
+  swrt_ctx::O23Chain& ch = c->o_chain;
+  const bool first_cand = ch.first_q && same_bits(t0, 0.0) && same_bits(tfinal, ch.tfinal) &&
+                          same_bits(tmax, ch.tmax) && same_bits(rtol, ch.rtol);
+  ch.first_q = false;
+  const bool taken = ode23_chain_take(c, t0, tmax, f, Cg, nslots, thr, bump);
+  if (!(taken && first_cand)) HIPCHK_RC(chain_join(c));
+  if (taken) {
+    sl_f1 = ch.dmax_slot;
+    ++ch.taken;
   } else {
     if ((rc = ode23_f1_queue(c, t0, tmax, f, Cg, nslots, thr, bump))) return rc;
     sl_f1 = c->o_dmax_cur;
@@ -4050,36 +4237,51 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
   const bool dev_first = use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx_ * ntx_;
   // Two part launches per attempt when the binning allows (split implies dev_first).
   const bool split = ode23_split_ok(c);
-  if (dev_first) {
-    // (part 1's slots start at zero, cleared here; each launch then clears its next one)
-    hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax, htspan,
-                       16 * o23_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3,
-                       split ? 3 : 0);
-    HIPCHK(c, hipGetLastError());
+  const bool first_chained = taken && first_cand && dev_first && split == ch.split;
+  if (first_chained) {
+    // queued by the previous call: stage 1, the first step (and stage 1's
+    // event after it), the fork and the first attempt, whose part 1 is now
+    // this call's pending split
+    c->chain_b = false;
+    if (split) c->b_pending = 1;
+    ++ch.first_taken;
   } else {
-    HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl_f1, c->o_dmax + sl_f1, sizeof(unsigned long long),
-                             hipMemcpyDeviceToHost, c->stream));
-  }
-  HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
-  if (split) {
-    HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->fork_ev, 0));
-    if (c->hz.on) {
-      c->hz.record(c->fork_ev, 0);
-      c->hz.wait(1, c->fork_ev);
+    HIPCHK_RC(chain_join(c));
+    if (dev_first) {
+      // (part 1's slots start at zero, cleared here; each launch then clears its next one)
+      hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax,
+                         htspan, 16 * o23_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3,
+                         split ? 3 : 0);
+      HIPCHK(c, hipGetLastError());
+    } else {
+      HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl_f1, c->o_dmax + sl_f1, sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost, c->stream));
     }
-    c->b_pending = 1;  // joined into the packet stream before anything else reads the packets (join_b)
+    HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
+    if (split) {
+      // the fork is stage 1's own event (one marker in front of the first attempt, not two)
+      HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->o_ev[sl_f1], 0));
+      if (c->hz.on) {
+        c->hz.record(c->o_ev[sl_f1], 0);
+        c->hz.wait(1, c->o_ev[sl_f1]);
+      }
+      c->b_pending = 1;  // joined into the packet stream before anything else reads the packets (join_b)
+    }
   }
   DeviceExec ex(c, base, split, dev_first, sl_f1, hook, hook_user);
-  // the first attempt from the device's coefficients, queued now; the
-  // caller's hook then runs (host work that overlaps stage 1 and this attempt)
-  if (dev_first && (rc = ex.queue_first())) return rc;
+  // the first attempt from the device's coefficients, queued now (or by the
+  // previous call); the caller's hook then runs (host work that overlaps
+  // stage 1 and this attempt)
+  if (first_chained)
+    ex.adopt_first(ch.first_slot, ch.first_wg);
+  else if (dev_first && (rc = ex.queue_first()))
+    return rc;
   O23Stats st;
   int64_t nts = 0;
   rc = ode23_control(ex, t0, tfinal, rtol, atol, ts_out, ts_cap, &nts, &st);
   if (rc == kO23BelowHmin) return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
   if (rc) return rc;
-  if ((rc = ode23_chain_queue(c, tmax, f, Cg, nslots, thr, bump))) return rc;
+  if ((rc = ode23_chain_queue(c, tmax, f, Cg, nslots, thr, bump, rtol))) return rc;
   *nts_out = nts;
   if (stats3_out) {
     stats3_out[0] = st.steps;

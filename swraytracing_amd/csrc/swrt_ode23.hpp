@@ -511,7 +511,8 @@ __global__ void __launch_bounds__(NT, 4) tile_ode23_kernel(Ode23Args a, const in
       for (int w = 1; w < NT / 64; ++w) b = fmax(b, red[w]);
       const unsigned long long bits = (unsigned long long)__double_as_longlong(b);
       atomicMax(a.dmax, bits);
-      if (a.hpart) a.hpart[blockIdx.x] = bits;
+      // system scope: the host reads it after the launch's own completion event
+      if (a.hpart) __hip_atomic_store(a.hpart + blockIdx.x, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

@@ -87,16 +87,11 @@ def test_checker_catches_the_pre_third_buffer_race(debug_ctx):
     """The ordering before the third packet buffers (test-only switch): the
     launch after a sort launch writes the buffer that sort launch's extra-
     stream parts gather from.  With the checker on, that launch is refused
-    (SWRT_ERR_STATE naming both accesses) before it is queued; with the
-    checker off and the spin schedule, the race really changes the result —
-    the adversarial schedule exposes it, and the fixed ordering (test above)
-    survives the same schedule."""
+    (SWRT_ERR_STATE naming both accesses) before it is queued."""
     import swraytracing_amd as sw
     ctx, L = debug_ctx
     bench, w = _bench_workload(ctx, 300_000)
     ctx.set_locality(20, 0)
-    ctx.set_packet_streams(1)
-    x1, k1 = _run_calls(ctx, bench, w, 6)
     ctx.set_packet_streams(2)
     ctx.debug_set(L.DEBUG_LEGACY_PARK, 1)
     ctx.debug_set(L.DEBUG_HAZARD_CHECK, 1)
@@ -107,12 +102,27 @@ def test_checker_catches_the_pre_third_buffer_race(debug_ctx):
     msg = str(ei.value)
     assert "SWRT_ERR_STATE" in msg and "hazard" in msg and "sort launch" in msg, msg
     ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
+    ctx.debug_set(L.DEBUG_LEGACY_PARK, 0)
     ctx.synchronize()
-    # unchecked, under the spin schedule: the race corrupts the packets (a
-    # race: the spin before each extra-stream part makes it all but certain;
-    # longer spins are tried if a schedule happened to miss it — one did, once
-    # in round 6's first session, gpurun_out r6a; every other run corrupts at
-    # the first spin)
+
+
+def test_the_pre_third_buffer_race_is_real(debug_ctx):
+    """The race the checker refuses above changes the result when it is let
+    run: with the checker off and a spin kernel before each extra-stream part,
+    the legacy ordering corrupts the packets, and the fixed ordering survives
+    the same schedule with the one-stream bits.  A demonstration, so it can
+    only show the race when the two packet streams really run side by side.
+    ROCm multiplexes streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4
+    here), and two streams sharing one run in order; twice in round 6 every
+    spin missed, in sessions that had created other streams first.  The test
+    then skips rather than claim a race it could not show."""
+    ctx, L = debug_ctx
+    bench, w = _bench_workload(ctx, 300_000)
+    ctx.set_locality(20, 0)
+    ctx.set_packet_streams(1)
+    x1, k1 = _run_calls(ctx, bench, w, 6)
+    ctx.set_packet_streams(2)
+    ctx.debug_set(L.DEBUG_LEGACY_PARK, 1)
     corrupted = False
     for spin in (200, 2000, 5000, 10000):
         ctx.debug_set(L.DEBUG_SPIN_US, spin)
@@ -120,11 +130,12 @@ def test_checker_catches_the_pre_third_buffer_race(debug_ctx):
         if not (_bits_equal(x1, xr) and _bits_equal(k1, kr)):
             corrupted = True
             break
-    assert corrupted
     # the fixed ordering under the same schedule: the one-stream bits
     ctx.debug_set(L.DEBUG_LEGACY_PARK, 0)
     xf, kf = _run_calls(ctx, bench, w, 6)
     assert _bits_equal(x1, xf) and _bits_equal(k1, kf)
+    if not corrupted:
+        pytest.skip("the two packet streams did not overlap under any spin schedule (shared hardware queue?)")
 
 
 def test_single_launch_after_split_calls_joins_first(debug_ctx):

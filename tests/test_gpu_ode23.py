@@ -212,7 +212,10 @@ def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
     taken (plain, with the hazard checker modelling its launches, and for an
     interval of another length: alpha(0) = 0 all the same) or dropped — by a
     rewrite of a slot it read (even with the same data), by a call that may
-    touch the packets, or by another RelTol."""
+    touch the packets, or by another RelTol.  Behind its stage 1 the chain
+    also queues the next call's first step size and first (split) attempt;
+    that call takes them only for the t0, tfinal and RelTol they assumed
+    (DEBUG_ODE23_FIRST_CHAINED), else joins and discards them."""
     from swraytracing_amd import _lib as L
     c = qg_case
     nx, Lx, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
@@ -224,22 +227,24 @@ def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
     tmax = 30 * c["dt"]
     bump = orc.BUMP_QG
 
-    def run(arm, between=None, rtol2=1e-3, tfinal2=tmax, hz=0, rtol1=1e-3):
+    def run(arm, between=None, rtol2=1e-3, tfinal2=tmax, hz=0, rtol1=1e-3, tmax2=tmax):
         for s in range(3):
             ctx.set_field_grid(s, _planes(flows[s]), nx, Lx)
         ctx.debug_set(L.DEBUG_HAZARD_CHECK, hz)
         try:
             ctx.packets_set(x, k)
             n0 = ctx.debug_get(L.DEBUG_ODE23_CHAINED)
+            f0 = ctx.debug_get(L.DEBUG_ODE23_FIRST_CHAINED)
             hook = (lambda: ctx.ode23_chain_next(1, 2)) if arm else None
             ts1, _ = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, rtol1, 1e-6, bump, hook=hook)
             ctx.swap_slots(0, 1)
             ctx.swap_slots(1, 2)  # the armed slots 1 / 2 are now slots 0 / 1
             if between is not None:
                 between()
-            ts2, st2 = ctx.ode23_run(0.0, tfinal2, tmax, f, Cg, 2, rtol2, 1e-6, bump)
+            ts2, st2 = ctx.ode23_run(0.0, tfinal2, tmax2, f, Cg, 2, rtol2, 1e-6, bump)
             taken = ctx.debug_get(L.DEBUG_ODE23_CHAINED) - n0
-            return ts1, ts2, *ctx.packets_get(), taken, st2
+            first = ctx.debug_get(L.DEBUG_ODE23_FIRST_CHAINED) - f0
+            return ts1, ts2, *ctx.packets_get(), taken, st2, first
         finally:
             ctx.debug_set(L.DEBUG_HAZARD_CHECK, 0)
 
@@ -251,29 +256,39 @@ def test_ode23_chain_taken_only_when_exact(ctx, qg_case):
         assert a[5] == b[5]  # steps, failed, attempts of the second interval
 
     ref = run(False)
-    assert ref[4] == 0 and len(ref[0]) > 5 and len(ref[1]) > 5
+    assert ref[4] == 0 and ref[6] == 0 and len(ref[0]) > 5 and len(ref[1]) > 5
     for hz in (0, 1):
         chained = run(True, hz=hz)
-        assert chained[4] == 1
+        assert chained[4] == 1 and chained[6] == 1
         same(chained, ref)
+    # a host synchronisation between the calls keeps the chain (and ends part 1)
+    synced = run(True, between=ctx.synchronize)
+    assert synced[4] == 1 and synced[6] == 1
+    same(synced, ref)
     rewrite = run(True, between=lambda: ctx.set_field_grid(1, _planes(flows[2]), nx, Lx))
-    assert rewrite[4] == 0
+    assert rewrite[4] == 0 and rewrite[6] == 0
     same(rewrite, ref)
     touched = run(True, between=lambda: ctx.packets_get())
-    assert touched[4] == 0
+    assert touched[4] == 0 and touched[6] == 0
     same(touched, ref)
     # another RelTol: another stage-1 input (AbsTol/RelTol), dropped
     other = run(True, rtol2=1e-4)
-    assert other[4] == 0
+    assert other[4] == 0 and other[6] == 0
     same(other, run(False, rtol2=1e-4))
     # tight tolerances: rejected attempts in both intervals, chain taken
     tight = run(True, rtol1=1e-7, rtol2=1e-7)
-    assert tight[4] == 1 and tight[5]["failed"] > 0
+    assert tight[4] == 1 and tight[6] == 1 and tight[5]["failed"] > 0
     same(tight, run(False, rtol1=1e-7, rtol2=1e-7))
-    # another interval length (same tmax, t0 = 0): the same stage 1, taken
+    # another interval length (same tmax, t0 = 0): the same stage 1, taken;
+    # the first attempt assumed tfinal = tmax: joined and discarded
     half = run(True, tfinal2=0.5 * tmax)
-    assert half[4] == 1
+    assert half[4] == 1 and half[6] == 0
     same(half, run(False, tfinal2=0.5 * tmax))
+    # the same tfinal over another tmax (the attempt's alpha = t / tmax): stage
+    # 1 taken (alpha(0) = 0), the first attempt discarded
+    longer = run(True, tmax2=2 * tmax)
+    assert longer[4] == 1 and longer[6] == 0
+    same(longer, run(False, tmax2=2 * tmax))
 
 
 def test_ode23_driver_path_at_scale_matches_oracle(fresh_ctx, qg_case, oracle_lib):
@@ -301,7 +316,8 @@ def test_ode23_driver_path_at_scale_matches_oracle(fresh_ctx, qg_case, oracle_li
     k = c["k"][rng.integers(0, c["k"].shape[0], n)]
     tmax = 40 * c["dt"]  # MaxStep 4 dt: the controller rejects some steps at the default tolerances
     bump = orc.BUMP_QG
-    keys = (L.DEBUG_ODE23_CHAINED, L.DEBUG_ODE23_FIRST_TAKEN, L.DEBUG_ODE23_GUESSES_TAKEN, L.DEBUG_ODE23_SPLIT_RUNS)
+    keys = (L.DEBUG_ODE23_CHAINED, L.DEBUG_ODE23_FIRST_TAKEN, L.DEBUG_ODE23_GUESSES_TAKEN, L.DEBUG_ODE23_SPLIT_RUNS,
+            L.DEBUG_ODE23_FIRST_CHAINED)
     ctx.set_locality(4, 0)
     for s in range(3):
         ctx.set_field_grid(s, planes[s], nx, Lx)
@@ -312,8 +328,8 @@ def test_ode23_driver_path_at_scale_matches_oracle(fresh_ctx, qg_case, oracle_li
     ctx.swap_slots(1, 2)  # the armed slots 1 / 2 are now slots 0 / 1
     ts2, st2 = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump)
     xg, kg = ctx.packets_get()
-    chained, first, guesses, split = [ctx.debug_get(key) - b for key, b in zip(keys, before)]
-    assert split == 2 and first == 2 and chained == 1, (split, first, chained)
+    chained, first, guesses, split, first_chained = [ctx.debug_get(key) - b for key, b in zip(keys, before)]
+    assert split == 2 and first == 2 and chained == 1 and first_chained == 1, (split, first, chained, first_chained)
     assert guesses >= 1 and st1["failed"] + st2["failed"] >= 1, (guesses, st1, st2)
     dx = Lx / nx
     rhs = [cbind.raytracing_rhs(planes[i], planes[i + 1], f, Cg, tmax, nx, nx, dx, bump) for i in (0, 1)]

@@ -607,10 +607,11 @@ def _speculative_driver_run(ctx, speculate, integrator="leapfrog"):
     loop.flush()
     import swraytracing_amd._lib as L_
     chained = ctx.debug_get(L_.DEBUG_ODE23_CHAINED)
+    first_chained = ctx.debug_get(L_.DEBUG_ODE23_FIRST_CHAINED)
     qk_pending = model.qk  # the committed step while a speculative one is queued
     loop.settle()
     xs, ks = ens.state()
-    return model.qk, qk_pending, xs, ks, list(loop.dts), U0s, model.t, model.steps, chained
+    return model.qk, qk_pending, xs, ks, list(loop.dts), U0s, model.t, model.steps, chained, first_chained
 
 
 @pytest.mark.parametrize("integrator", ["leapfrog", "ode23"])
@@ -638,6 +639,9 @@ def test_qg2_speculative_steps_bit_identical(fresh_ctx, integrator):
         # call (swrt_ode23_chain_next); the forced dt change drops one chain
         # (a fresh snapshot rewrites slot 1) and the plain loop never arms it
         assert a[8] == 0 and 8 <= b[8] <= 10, (a[8], b[8])
+        # and the first attempt behind each chained stage 1, but at the dt
+        # change (the chain assumed tfinal = the previous dt)
+        assert a[9] == 0 and b[8] - 1 <= b[9] <= b[8], (a[9], b[9])
 
 
 @pytest.mark.parametrize("nx", [64, 512])
