@@ -679,7 +679,7 @@ def parse_args(argv=None):
                          "driver_step_forecast.owner)")
     ap.add_argument("--owner-weight", type=float, default=0.0,
                     help="owner form: rank 0's packets per packet of another rank (dist.owner_bounds)")
-    ap.add_argument("--ode23-steps", type=int, default=8,
+    ap.add_argument("--ode23-steps", type=int, default=16,
                     help="then this many driver steps with the reference's ode23 packet integrator (0: skip)")
     ap.add_argument("--gather", action="store_true",
                     help="after timing, gather all trajectories to rank 0 (one all_gather)")
