@@ -338,6 +338,15 @@ struct swrt_ctx {
   bool chain_b = false;
   hipEvent_t chain_ev[2] = {nullptr, nullptr};
   bool chain_first = true;  // SWRT_ODE23_CHAIN_FIRST=0 (environment, A/B runs): stage 1 alone is chained
+  // the packet stream got work since the last split launch's part 0 that the
+  // next split launch's part 1 (on sx[0]) must follow: that launch forks (an
+  // event marker, ~7 us of idle on each stream).  Only consecutive split
+  // launches of swrt_advance / swrt_advance_intervals with nothing in between
+  // skip it: part p of a binning owns the same tiles at every launch, so
+  // stream order alone orders a part's launches (launch_tiles).
+  // SWRT_FORK_ALWAYS=1 (environment, A/B runs): fork at every split launch.
+  bool s0_dirty = true;
+  bool fork_always = false;
   uint64_t slot_wgen = 0;  // Slot::wgen source
   Timing timing;
   int timing_every = 1;     // bracket every k-th leapfrog launch with HIP events (0: off)
@@ -426,6 +435,7 @@ void slot_writes_wait(swrt_ctx* c, unsigned mask = kAllSlots) {
     if (Slot& s = c->slot[i]; (mask >> i & 1u) && s.wpend) {
       (void)hipStreamWaitEvent(c->stream, s.wev, 0);
       s.wpend = false;
+      c->s0_dirty = true;
     }
 }
 
@@ -495,6 +505,7 @@ int fail(swrt_ctx* c, int code, const std::string& msg) {
       const int jrc_ = join_b(c); \
       if (jrc_) return jrc_;      \
       hz_api(c);                  \
+      c->s0_dirty = true;         \
     }
 #define GUARD_BEGIN              \
   HOOK_REFUSE                    \
@@ -875,14 +886,15 @@ constexpr int kOde23RebinEvery = SWRT_ODE23_REBIN;
 // launch's is seen to touch the other stream's tiles.  Checked on a copy of
 // the checker state, committed only if every access is ordered: a hazard
 // refuses the launch before anything is queued.
-int hz_tile_launch(swrt_ctx* c, const TileArgs& t, const TileShare* parts, int nparts, bool zero_counts) {
+int hz_tile_launch(swrt_ctx* c, const TileArgs& t, const TileShare* parts, int nparts, bool zero_counts,
+                   bool fork = true) {
   HazardChecker h = c->hz;
   if (zero_counts) {  // the next-binning counts' memset, on the packet stream before the parts
     const uint64_t tm = h.op(0);
     if (!h.access(0, tm, t.next_counts, kHzWrite, HzRegion::all(), "the next-binning counts' memset"))
       return fail(c, SWRT_ERR_STATE, h.err);
   }
-  if (nparts > 1) {
+  if (nparts > 1 && fork) {
     h.record(c->fork_ev, 0);
     for (int i = 1; i < nparts; ++i) h.wait(i, c->fork_ev);
   }
@@ -967,11 +979,16 @@ int launch_tiles(swrt_ctx* c, F kernel, int nt, TileArgs t, bool zero_counts) {
     if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, &t.sh, 1, zero_counts));
     if (zero_counts) HIPCHK(c, hipMemsetAsync(t.next_counts, 0, sizeof(int) * ntiles, c->stream));
     launch_k(c, kernel, dim3((unsigned)share_grid(t.sh)), dim3(nt), t);
+    c->s0_dirty = true;  // every tile on the packet stream
     return SWRT_OK;
   }
   const TileShare sh[2] = {TileShare{ntiles, 0, 2, skew ? kShareSkew : kShareEven},
                            TileShare{ntiles, 1, 2, skew ? kShareSkew : kShareEven}};
-  if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, sh, 2, zero_counts));
+  // the fork: only when the packet stream has had other work since the last
+  // split launch (s0_dirty), the counts' memset included; the hazard checker
+  // models exactly the orderings the launch queues
+  const bool fork = c->s0_dirty || zero_counts || skew || c->fork_always;
+  if (c->hz.on) HIPCHK_RC(hz_tile_launch(c, t, sh, 2, zero_counts, fork));
   if (zero_counts) HIPCHK(c, hipMemsetAsync(t.next_counts, 0, sizeof(int) * ntiles, c->stream));
   // Part p takes the same slots at every launch of a binning (the product
   // rule, kShareEven): a stream's consecutive part launches own the same
@@ -979,8 +996,11 @@ int launch_tiles(swrt_ctx* c, F kernel, int nt, TileArgs t, bool zero_counts) {
   // start while stream 1's previous one still runs.  A launch with another
   // mapping races it unless joined first — the checker, which enumerates the
   // slots each part takes, refuses it (round 4's hang, profiles/r04_stream_split).
-  HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->fork_ev, 0));
+  if (fork) {
+    HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->fork_ev, 0));
+  }
+  c->s0_dirty = false;
   t.sh = sh[0];
   hipExtLaunchKernelGGL(kernel, dim3((unsigned)share_grid(sh[0])), dim3(nt), 0, c->stream, c->kev0, nullptr, 0, t);
   if (c->debug_spin_us > 0)
@@ -998,6 +1018,7 @@ int launch_tiles(swrt_ctx* c, F kernel, int nt, TileArgs t, bool zero_counts) {
 // hazard checker.
 int leap_launch_prep(swrt_ctx* c, const StepArgs& a) {
   HIPCHK_RC(join_b(c));
+  c->s0_dirty = true;
   if (!c->hz.on) return SWRT_OK;
   HazardChecker& h = c->hz;
   const uint64_t t = h.op(0);
@@ -1114,6 +1135,7 @@ int tile_cells(const swrt_ctx* c, int64_t nx) {
 // which the scan ranks the tile order.
 int rebin(swrt_ctx* c, bool indirect, int tile = 0, int lanes = kTileThreads) {
   if (int rc = join_b(c)) return rc;  // the second stream's half launches wrote packets this pass reads
+  c->s0_dirty = true;  // a new binning: the next split launch forks
   const Slot& s = c->slot[0];
   const FieldView v = view_of(s);
   BinGeom g;
@@ -1399,6 +1421,7 @@ int ensure_history(swrt_ctx* c, int64_t new_frames) {
   const int64_t need = (c->hframes + new_frames) * per;
   if (new_frames <= 0 || need <= c->hcap) return SWRT_OK;
   if (int rc = join_b(c)) return rc;  // the second stream may still write frames into the old buffers
+  c->s0_dirty = true;
   const int64_t ncap = std::max<int64_t>(need, 2 * c->hcap);
   double *nx_ = nullptr, *nk_ = nullptr;
   HIPCHK(c, hipMalloc(&nx_, sizeof(double) * ncap));
@@ -1474,6 +1497,7 @@ int swrt_create(int device, swrt_ctx** out) {
   c->stream0 = c->stream;
   if (const char* e = getenv("SWRT_HAZARD_CHECK")) c->hz.on = atoi(e) != 0;
   if (const char* e = getenv("SWRT_ODE23_CHAIN_FIRST")) c->chain_first = atoi(e) != 0;
+  if (const char* e = getenv("SWRT_FORK_ALWAYS")) c->fork_always = atoi(e) != 0;
   if (!ok) {
     swrt_destroy(c);
     return SWRT_ERR_HIP;
@@ -1989,6 +2013,7 @@ int swrt_packets_get_device(swrt_ctx* c, double* x_dev, double* k_dev, int64_t l
 
 int swrt_set_timing(swrt_ctx* c, int every) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (every < 0) return fail(c, SWRT_ERR_ARG, "timing interval must be >= 0");
   c->timing_every = every;
   c->launch_count = 0;
@@ -1997,6 +2022,7 @@ int swrt_set_timing(swrt_ctx* c, int every) {
 
 int swrt_set_gather_mode(swrt_ctx* c, int mode) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (mode != 0 && mode != 1) return fail(c, SWRT_ERR_ARG, "gather mode must be 0 or 1");
   c->gather_mode = mode;
   return SWRT_OK;
@@ -2004,6 +2030,7 @@ int swrt_set_gather_mode(swrt_ctx* c, int mode) {
 
 int swrt_set_packet_streams(swrt_ctx* c, int streams) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (streams != 1 && streams != 2) return fail(c, SWRT_ERR_ARG, "packet streams must be 1 or 2");
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = join_b(c)) return rc;
@@ -2015,6 +2042,7 @@ int swrt_set_packet_streams(swrt_ctx* c, int streams) {
 
 int swrt_set_sparse_tiles(swrt_ctx* c, int mode) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (mode < 0 || mode > 2) return fail(c, SWRT_ERR_ARG, "sparse tiles must be 0 (auto), 1 (never) or 2 (always)");
   c->sparse_mode = mode;
   c->bin_valid = false;  // the tile order of the next binning is sized for the launch shape
@@ -2025,6 +2053,7 @@ int swrt_set_sparse_tiles(swrt_ctx* c, int mode) {
 
 int swrt_set_kernel(swrt_ctx* c, int variant) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (variant < 0 || variant > 2) return fail(c, SWRT_ERR_ARG, "kernel variant must be 0..2");
   c->kernel = variant;
   c->bin_valid = false;
@@ -2035,6 +2064,7 @@ int swrt_set_kernel(swrt_ctx* c, int variant) {
 
 int swrt_set_locality(swrt_ctx* c, int64_t rebin_every, int64_t tile) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (rebin_every < 0 || tile < 0) return fail(c, SWRT_ERR_ARG, "negative locality parameter");
   c->rebin_every = rebin_every;
   c->tile = tile;
@@ -2131,6 +2161,7 @@ int swrt_history_get(swrt_ctx* c, int64_t first, int64_t count, double* hist_x, 
 
 int swrt_history_reset(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   c->hframes = 0;
   c->steps_done = 0;
   return SWRT_OK;
@@ -2643,6 +2674,7 @@ int swrt_check_arith(swrt_ctx* c, int64_t n, uint64_t seed, int64_t* mismatches3
 
 int swrt_synchronize(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   HIPCHK(c, hipSetDevice(c->device));
   if (int rc = sync_sx(c)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2653,6 +2685,7 @@ int swrt_synchronize(swrt_ctx* c) {
 
 int swrt_debug_set(swrt_ctx* c, int key, int64_t value) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (int rc = chain_drop(c)) return rc;
   switch (key) {
     case SWRT_DEBUG_HAZARD_CHECK:
@@ -2724,6 +2757,7 @@ int swrt_debug_get(swrt_ctx* c, int key, int64_t* value_out) {
 
 int swrt_qg_set_fused(swrt_ctx* c, int on) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   if (on != 0 && on != 1) return fail(c, SWRT_ERR_ARG, "on must be 0 or 1");
   int rc = swrt_synchronize(c);
@@ -2736,6 +2770,7 @@ int swrt_qg_set_fused(swrt_ctx* c, int on) {
 
 int swrt_qg_set_stream(swrt_ctx* c, int separate) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (c->qg.spec) return fail(c, SWRT_ERR_STATE, "a speculative QG step is pending (swrt_qg_resolve first)");
   if (separate != 0 && separate != 1) return fail(c, SWRT_ERR_ARG, "separate must be 0 or 1");
   int rc = swrt_synchronize(c);
@@ -2747,6 +2782,7 @@ int swrt_qg_set_stream(swrt_ctx* c, int separate) {
 int swrt_get_stream(swrt_ctx* c, void** out) {
   if (!c || !out) return SWRT_ERR_ARG;
   if (int rc = join_b(c)) return rc;  // work queued on it by the caller sees every packet
+  c->s0_dirty = true;                   // ... and the next split launch follows that work
   *out = (void*)c->stream;
   return SWRT_OK;
 }
@@ -3844,6 +3880,7 @@ int swrt_ode23_attempt(swrt_ctx* c, double t, double h, double tnew, double tmax
 
 int swrt_ode23_accept(swrt_ctx* c) {
   if (!c) return SWRT_ERR_ARG;
+  c->s0_dirty = true;  // (conservative: settings and syncs may precede packet-stream work)
   if (c->in_hook) return fail(c, SWRT_ERR_STATE, "this call may touch the packets: not allowed inside an ode23 hook");
   HIPCHK_RC(lost_check(c));
   HIPCHK_RC(chain_drop(c));
