@@ -334,7 +334,7 @@ int swrt_ode23_accept(swrt_ctx* ctx);
  * attempts} go to stats3_out (may be NULL).  If the step size falls below
  * hmin (MATLAB's "unable to meet integration tolerances") the packets are
  * left at the last accepted time and SWRT_ERR_STATE is returned.  Single rank: a sharded ensemble needs the error norm's
- * allreduce between attempts (swraytracing_amd.integrate.ode23_packets). */
+ * max over the ranks (swrt_ode23_run_sharded). */
 int swrt_ode23_run(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                    double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
                    int64_t* stats3_out);
@@ -348,6 +348,22 @@ int swrt_ode23_run(swrt_ctx* ctx, double t0, double tfinal, double tmax, double 
 int swrt_ode23_run_hooked(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                           double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
                           int64_t* stats3_out, void (*hook)(void*), void* hook_user);
+/* swrt_ode23_run_hooked for packets sharded over ranks: the
+ * error norm is a max over every packet of every rank, so each max this
+ * rank's stages produce — stage 1's, then every attempt's the controller
+ * consumes — goes through reduce(&value, reduce_user), which replaces it in
+ * place with the max over the ranks (the caller's collective, e.g. an RCCL
+ * all_reduce) and returns 0 (else SWRT_ERR_STATE).  Every rank then takes the
+ * same steps: one reduce per stage 1 and per consumed attempt, in the same
+ * order on every rank (the order swraytracing_amd.integrate's controller
+ * reduces in, so a rank without packets can run that one).  The first step
+ * size comes from the reduced stage-1 max, so it is not guessed on the
+ * device; a device-gated guess runs only if this rank's max passes its gate,
+ * which the global max passing implies.  reduce NULL: swrt_ode23_run_hooked. */
+int swrt_ode23_run_sharded(swrt_ctx* ctx, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
+                           double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
+                           int64_t* stats3_out, void (*hook)(void*), void* hook_user,
+                           int (*reduce)(double* value, void* reduce_user), void* reduce_user);
 /* Chain the next swrt_ode23_run(_hooked) to the one running (or the next to
  * run): when it ends, it queues the next call's stage 1 (re-binning when due,
  * in-tile sort, f at t = 0) on the accepted packets with slot_a / slot_b as

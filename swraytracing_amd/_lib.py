@@ -34,6 +34,7 @@ _INT = ctypes.c_int
 _P = ctypes.POINTER(ctypes.c_double)
 _VP = ctypes.c_void_p
 _HOOK = ctypes.CFUNCTYPE(None, ctypes.c_void_p)  # void (*)(void*)
+_REDUCE = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_void_p)  # int (*)(double*, void*)
 
 class QGParams(ctypes.Structure):
     """swrt_qg_params (include/swrt.h)."""
@@ -90,6 +91,8 @@ SIGNATURES = {
                               ctypes.POINTER(_I)]),
     "swrt_ode23_run_hooked": (_INT, [_VP, _D, _D, _D, _D, _D, _INT, _D, _D, _D, _P, _I, ctypes.POINTER(_I),
                                      ctypes.POINTER(_I), _HOOK, _VP]),
+    "swrt_ode23_run_sharded": (_INT, [_VP, _D, _D, _D, _D, _D, _INT, _D, _D, _D, _P, _I, ctypes.POINTER(_I),
+                                      ctypes.POINTER(_I), _HOOK, _VP, _REDUCE, _VP]),
     "swrt_ode23_chain_next": (_INT, [_VP, _INT, _INT]),
     "swrt_ode23_replay": (_INT, [_D, _D, _D, _D, _INT, _P, _I, _P, _I, ctypes.POINTER(_I), _P, _I,
                                  ctypes.POINTER(_I), ctypes.POINTER(_I)]),
@@ -211,6 +214,7 @@ class Context:
         self._h = h
         self.device = device
         self._ode23_cb = self._ode23_hook = self._ode23_raised = None  # ode23_run's hook callback
+        self._ode23_red_cb = self._ode23_reduce = None  # ... and its reduce callback (sharded runs)
         self.timing_every = 1  # swrt_set_timing's setting (the library default)
 
     def close(self):
@@ -506,20 +510,23 @@ class Context:
     def ode23_accept(self):
         self._chk(self._L.swrt_ode23_accept(self._h), "swrt_ode23_accept")
 
-    def ode23_run(self, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_cap=10_000, hook=None):
+    def ode23_run(self, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_cap=10_000, hook=None, reduce=None):
         """swrt_ode23_run: the whole ode23 call with the controller in the
         library.  Returns (accepted times, {steps, failed, attempts,
         accepted}); `accepted` counts every accepted time, and a warning is
         raised when more than ts_cap were accepted (the list then holds the
         first ts_cap only).  ``hook``: a callable run once after the first
         launches are queued (swrt_ode23_run_hooked; QG calls only, never the
-        packets); an exception it raises is re-raised after the call."""
+        packets).  ``reduce``: a callable float -> float, the max over the
+        ranks of a sharded run (swrt_ode23_run_sharded; called once for stage
+        1 and once per attempt, the same order on every rank).  An exception
+        either raises is re-raised after the call."""
         ts = np.empty(ts_cap)
         nts = _I()
         st = (_I * 3)()
         args = (self._h, float(t0), float(tfinal), float(tmax), float(f), float(Cg), int(nslots), float(rtol),
                 float(atol), float(bump), _p(ts), int(ts_cap), ctypes.byref(nts), st)
-        if hook is None:
+        if hook is None and reduce is None:
             self._chk(self._L.swrt_ode23_run(*args), "swrt_ode23_run")
         else:
             # one ctypes callback per context (made once), calling this call's hook
@@ -527,17 +534,36 @@ class Context:
                 def _call(_user):
                     h, self._ode23_hook = self._ode23_hook, None
                     try:
-                        h()
+                        if h is not None:
+                            h()
                     except BaseException as e:  # ctypes would print and drop it
                         self._ode23_raised = e
                 self._ode23_cb = _HOOK(_call)
             self._ode23_hook, self._ode23_raised = hook, None
-            rc = self._L.swrt_ode23_run_hooked(*args, self._ode23_cb, None)
+            if reduce is None:
+                rc = self._L.swrt_ode23_run_hooked(*args, self._ode23_cb if hook is not None else _HOOK(), None)
+                name = "swrt_ode23_run_hooked"
+            else:
+                if self._ode23_red_cb is None:
+                    def _red(vp, _user):
+                        try:
+                            vp[0] = float(self._ode23_reduce(vp[0]))
+                            return 0
+                        except BaseException as e:
+                            if self._ode23_raised is None:
+                                self._ode23_raised = e
+                            return 1
+                    self._ode23_red_cb = _REDUCE(_red)
+                self._ode23_reduce = reduce
+                rc = self._L.swrt_ode23_run_sharded(*args, self._ode23_cb if hook is not None else _HOOK(), None,
+                                                    self._ode23_red_cb, None)
+                self._ode23_reduce = None
+                name = "swrt_ode23_run_sharded"
             self._ode23_hook = None
             raised, self._ode23_raised = self._ode23_raised, None
             if raised is not None:
                 raise raised
-            self._chk(rc, "swrt_ode23_run_hooked")
+            self._chk(rc, name)
         # ts_cap bounds the recorded times only (the interval always completes)
         if nts.value > ts_cap:
             import warnings

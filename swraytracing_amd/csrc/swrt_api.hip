@@ -3910,7 +3910,7 @@ bool same_bits(double a, double b) { return std::memcmp(&a, &b, sizeof(double)) 
 int ode23_chain_first(swrt_ctx* c, int sl_f1, double tmax, double f, double Cg, double thr, double bump,
                       double rtol);
 int ode23_chain_queue(swrt_ctx* c, double tmax, double f, double Cg, int nslots, double thr, double bump,
-                      double rtol) {
+                      double rtol, bool with_first) {
   swrt_ctx::O23Chain& ch = c->o_chain;
   const bool want = ch.want;
   ch.want = false;
@@ -3927,7 +3927,7 @@ int ode23_chain_queue(swrt_ctx* c, double tmax, double f, double Cg, int nslots,
   const int sl_f1 = c->o_dmax_cur;
   if (!rc) {
     c->o_dmax_cur = (sl_f1 + 1) % 3;
-    rc = ode23_chain_first(c, sl_f1, tmax, f, Cg, thr, bump, rtol);
+    if (with_first) rc = ode23_chain_first(c, sl_f1, tmax, f, Cg, thr, bump, rtol);
   }
   for (int i = 0; i < SWRT_MAX_SLOTS; ++i) c->slot[i] = saved[i];
   if (rc) return rc;
@@ -3989,9 +3989,9 @@ namespace {
 class DeviceExec final : public O23Exec {
  public:
   DeviceExec(swrt_ctx* c_, const Ode23Args& base_, bool split_, bool dev_first_, int sl_f1_, void (*hook_)(void*),
-             void* hook_user_)
+             void* hook_user_, int (*reduce_)(double*, void*) = nullptr, void* reduce_user_ = nullptr)
       : c(c_), base(base_), split(split_), P(split_ ? 2 : 1), dev_first(dev_first_), sl_f1(sl_f1_), hook(hook_),
-        hook_user(hook_user_),
+        hook_user(hook_user_), reduce(reduce_), reduce_user(reduce_user_),
         S{{c_->dx, c_->dk, c_->oF[0]}, {c_->o_ynx, c_->o_ynk, c_->oF[3]}, {c_->o_spx, c_->o_spk, c_->o_spF}} {}
 
   // queue an attempt (coef: its coefficients from device memory, the first attempt)
@@ -4069,7 +4069,14 @@ class DeviceExec final : public O23Exec {
       std::memcpy(raw, &c->o_shown[0], sizeof(double));
     else
       std::memcpy(raw, c->o_hmax + sl_f1, sizeof(double));
-    return dev_err_check(c);
+    HIPCHK_RC(dev_err_check(c));
+    return global_max(raw);
+  }
+  // a sharded run: this rank's max -> the max over every rank (the caller's
+  // collective, e.g. an RCCL all_reduce), in place
+  int global_max(double* v) {
+    if (reduce && reduce(v, reduce_user) != 0) return fail(c, SWRT_ERR_STATE, "ode23: the reduce callback failed");
+    return SWRT_OK;
   }
   bool first_attempt(double absh, double h, double tnew, const double cf[8], int* slot) override {
     if (!dev_first) return false;
@@ -4116,7 +4123,7 @@ class DeviceExec final : public O23Exec {
       if (d != m) return fail(c, SWRT_ERR_STATE, "ode23: host-mapped error max differs from the device's");
     }
     std::memcpy(out, &m, sizeof(double));
-    return SWRT_OK;
+    return global_max(out);
   }
   int await_hpart(const volatile unsigned long long* e, int p, unsigned long long* out) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -4163,6 +4170,8 @@ class DeviceExec final : public O23Exec {
   int first_slot = -1;
   void (*hook)(void*);
   void* hook_user;
+  int (*reduce)(double*, void*);
+  void* reduce_user;
   bool defer_hook = false, hook_due = false;
   struct Set {
     double *x, *k, *F;
@@ -4231,6 +4240,14 @@ int ode23_chain_first(swrt_ctx* c, int sl_f1, double tmax, double f, double Cg, 
 int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
                           double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
                           int64_t* stats3_out, void (*hook)(void*), void* hook_user) {
+  return swrt_ode23_run_sharded(c, t0, tfinal, tmax, f, Cg, nslots, rtol, atol, bump, ts_out, ts_cap, nts_out,
+                                stats3_out, hook, hook_user, nullptr, nullptr);
+}
+
+int swrt_ode23_run_sharded(swrt_ctx* c, double t0, double tfinal, double tmax, double f, double Cg, int nslots,
+                           double rtol, double atol, double bump, double* ts_out, int64_t ts_cap, int64_t* nts_out,
+                           int64_t* stats3_out, void (*hook)(void*), void* hook_user,
+                           int (*reduce)(double*, void*), void* reduce_user) {
   if (!c) return SWRT_ERR_ARG;
   if (!ts_out || ts_cap < 1 || !nts_out) return fail(c, SWRT_ERR_ARG, "ts_out / ts_cap / nts_out");
   if (c->in_hook) return fail(c, SWRT_ERR_STATE, "an ode23 hook may not start another ode23 call");
@@ -4270,9 +4287,12 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
   // without a host round trip; the controller then computes the same and
   // checks it against the kernel's mapped copy (the tile path only: its
   // attempt kernel reads device coefficients).
+  // (not in a sharded run: the device would take the first step size from
+  // this rank's stage-1 max, the controller takes it from every rank's)
   const int ntx_ = (int)((c->slot[0].nx + kTile - 1) / kTile);
-  const bool dev_first = use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx_ * ntx_;
-  // Two part launches per attempt when the binning allows (split implies dev_first).
+  const bool dev_first =
+      !reduce && use_tile_kernel(c) && c->bin_valid && !c->src_pending && c->nbins == ntx_ * ntx_;
+  // Two part launches per attempt when the binning allows.
   const bool split = ode23_split_ok(c);
   const bool first_chained = taken && first_cand && dev_first && split == ch.split;
   if (first_chained) {
@@ -4305,7 +4325,7 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
       c->b_pending = 1;  // joined into the packet stream before anything else reads the packets (join_b)
     }
   }
-  DeviceExec ex(c, base, split, dev_first, sl_f1, hook, hook_user);
+  DeviceExec ex(c, base, split, dev_first, sl_f1, hook, hook_user, reduce, reduce_user);
   // the first attempt from the device's coefficients, queued now (or by the
   // previous call); the caller's hook then runs (host work that overlaps
   // stage 1 and this attempt)
@@ -4318,7 +4338,7 @@ int swrt_ode23_run_hooked(swrt_ctx* c, double t0, double tfinal, double tmax, do
   rc = ode23_control(ex, t0, tfinal, rtol, atol, ts_out, ts_cap, &nts, &st);
   if (rc == kO23BelowHmin) return fail(c, SWRT_ERR_STATE, "ode23: step size below hmin");
   if (rc) return rc;
-  if ((rc = ode23_chain_queue(c, tmax, f, Cg, nslots, thr, bump, rtol))) return rc;
+  if ((rc = ode23_chain_queue(c, tmax, f, Cg, nslots, thr, bump, rtol, reduce == nullptr))) return rc;
   *nts_out = nts;
   if (stats3_out) {
     stats3_out[0] = st.steps;

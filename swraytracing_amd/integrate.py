@@ -85,22 +85,22 @@ def ode23_packets(ctx: Context, tspan, tmax, f, Cg, nslots=2, rtol=1e-3, atol=1e
     unpinned).  Returns the accepted times.
 
     ``controller``: "library" runs this same controller inside the C library
-    (swrt_ode23_run: no interpreter between attempts), "python" the loop
-    below; default "library" unless ``allreduce_max`` is given (the sharded
-    error norm needs the Python hook).  Same steps and bits either way.
+    (swrt_ode23_run: no interpreter between attempts; with ``allreduce_max``
+    swrt_ode23_run_sharded, which reduces stage 1's and every attempt's max
+    through it), "python" the loop below (the one a rank without packets
+    runs: the same reductions in the same order); default "library" for a
+    Context.  Same steps and bits either way.
 
     ``hook``: a callable (QG calls only, never the packets) run once while
     the interval's first launches run — the library controller calls it
     after stage 1 and the first attempt are queued (swrt_ode23_run_hooked),
     the Python loop after stage 1."""
     if controller is None:
-        controller = "python" if allreduce_max is not None else "library"
+        controller = "library" if hasattr(ctx, "ode23_run") else "python"
     if controller == "library":
-        if allreduce_max is not None:
-            raise ValueError("the library controller has no allreduce hook (use controller='python')")
         try:
             ts, st = ctx.ode23_run(float(tspan[0]), float(tspan[1]), tmax, f, Cg, nslots, rtol, atol, bump,
-                                   hook=hook)
+                                   hook=hook, reduce=allreduce_max)
         except SwrtError as e:
             if "below hmin" in str(e):
                 raise RuntimeError(str(e)) from e

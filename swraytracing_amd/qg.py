@@ -364,7 +364,7 @@ class TwoLayerLoop:
                     self.model.step_speculative(dt)
                     self.model.snapshot_speculative(self.SPEC_SLOT, ny_period=ny)
                     self._spec_snap = True
-                    if self.chain and self.ens.world == 1:  # (a sharded interval runs the Python controller)
+                    if self.chain:  # (sharded too: swrt_ode23_run_sharded takes a chained stage 1)
                         # the next interval reads this one's end snapshot (slot
                         # 1) and the one just queued: its stage 1 is queued as
                         # this interval ends (taken only if still exact)

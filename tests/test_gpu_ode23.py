@@ -433,3 +433,50 @@ def test_ode23_chain_dropped_by_a_qg_snapshot_rewrite(fresh_ctx, qg_case):
         for u, v in zip(a[:4], ref[:4]):
             np.testing.assert_array_equal(u, v)
         assert a[5] == ref[5]
+
+
+def test_ode23_run_sharded_reduce_steps_and_bits(fresh_ctx, qg_case):
+    """swrt_ode23_run_sharded (the library controller of a sharded run): with
+    an identity reduce — one rank — the same times, counts and packet bits as
+    swrt_ode23_run, though its first step size is not guessed on the device.
+    The reduce is called once for stage 1 and once per attempt; a reduce that
+    raises surfaces its exception."""
+    ctx = fresh_ctx
+    c = qg_case
+    nx, Lx, f, Cg = c["nx"], c["L"], c["f"], c["Cg"]
+    flows = [c["flow"], {n: np.asarray(v) * 1.3 for n, v in c["flow"].items()}]
+    rng = np.random.default_rng(37)
+    n = 70_000
+    x = rng.uniform(-Lx / 2, Lx / 2, (n, 2))
+    k = c["k"][rng.integers(0, c["k"].shape[0], n)]
+    tmax = 30 * c["dt"]
+    bump = orc.BUMP_QG
+    ctx.set_locality(4, 0)
+    for s in range(2):
+        ctx.set_field_grid(s, _planes(flows[s]), nx, Lx)
+
+    def run(reduce):
+        ctx.packets_set(x, k)
+        ts, st = ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump, reduce=reduce)
+        return ts, st, *ctx.packets_get()
+
+    calls = []
+
+    def ident(v):
+        calls.append(v)
+        return v
+
+    a = run(None)
+    b = run(ident)
+    np.testing.assert_array_equal(a[0], b[0])
+    assert (a[1]["steps"], a[1]["failed"], a[1]["attempts"]) == (b[1]["steps"], b[1]["failed"], b[1]["attempts"])
+    np.testing.assert_array_equal(a[2], b[2])
+    np.testing.assert_array_equal(a[3], b[3])
+    assert len(calls) == 1 + b[1]["attempts"] and all(v >= 0 for v in calls)
+
+    def boom(v):
+        raise KeyError("reduce failed on purpose")
+
+    ctx.packets_set(x, k)
+    with pytest.raises(KeyError, match="on purpose"):
+        ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump, reduce=boom)
