@@ -3904,8 +3904,9 @@ bool same_bits(double a, double b) { return std::memcmp(&a, &b, sizeof(double)) 
 // it while the host returns and prepares that call.  The next call takes it
 // only if it would compute exactly that (ode23_chain_take).  Behind stage 1
 // go the next call's first step size and its first attempt, as that call
-// would queue them (ode23_chain_first), taken only if the call's t0, tfinal
-// and RelTol are the ones assumed.  (Round 5 chained an unsplit first attempt,
+// would queue them (ode23_chain_first), taken only if the call's t0, tfinal,
+// tmax and RelTol are the ones assumed (never in a sharded run: its first
+// step size comes from every rank's stage 1).  (Round 5 chained an unsplit first attempt,
 // 186 us against 123 us split, and measured no faster: profiles/r05_chain.)
 int ode23_chain_first(swrt_ctx* c, int sl_f1, double tmax, double f, double Cg, double thr, double bump,
                       double rtol);
