@@ -480,3 +480,37 @@ def test_ode23_run_sharded_reduce_steps_and_bits(fresh_ctx, qg_case):
     ctx.packets_set(x, k)
     with pytest.raises(KeyError, match="on purpose"):
         ctx.ode23_run(0.0, tmax, tmax, f, Cg, 2, 1e-3, 1e-6, bump, reduce=boom)
+
+
+def test_ode23_driver_longer_run_same_files_with_and_without_chaining(tmp_path, monkeypatch):
+    """The 2-layer driver with the reference's ode23 over 48 PDE steps (its
+    CFL rule, re-binning every 2nd interval, 70,000 packets so every attempt
+    is split): the chained stage 1 and first attempt
+    (defaults), the chained stage 1 alone (SWRT_ODE23_CHAIN_FIRST=0) and no
+    chain at all (SWRT_ODE23_CHAIN=0) write the same packet_x / packet_k /
+    packet_time / pv files, byte for byte."""
+    import swraytracing_amd as sw
+    from swraytracing_amd import _lib as L
+    out = {}
+    for name, env in (("first", {}), ("stage1", {"SWRT_ODE23_CHAIN_FIRST": "0"}), ("off", {"SWRT_ODE23_CHAIN": "0"})):
+        for k_, v in (("SWRT_ODE23_CHAIN_FIRST", None), ("SWRT_ODE23_CHAIN", None)):
+            monkeypatch.delenv(k_, raising=False)
+        for k_, v in env.items():
+            monkeypatch.setenv(k_, v)
+        c = sw.Context(0)
+        try:
+            d = tmp_path / name
+            sw.qg2layersw_raytrace(128, 70_000, 4.0, 10.0, 0.0, 0.2, 3.0, 1.0, out_dir=str(d), max_steps=48, seed=9,
+                                   integrator="ode23", ctx=c)
+            out[name] = ({n: (d / n).read_bytes() for n in ("packet_x.bin", "packet_k.bin", "packet_time.bin",
+                                                              "pv.bin")},
+                         c.debug_get(L.DEBUG_ODE23_CHAINED), c.debug_get(L.DEBUG_ODE23_FIRST_CHAINED))
+        finally:
+            c.close()
+    files, chained, first = out["first"]
+    assert chained >= 30 and first >= 30, (chained, first)
+    assert out["stage1"][1] >= 30 and out["stage1"][2] == 0
+    assert out["off"][1] == 0 and out["off"][2] == 0
+    for name in ("stage1", "off"):
+        for fn, b in files.items():
+            assert len(b) > 0 and out[name][0][fn] == b, (name, fn)
