@@ -264,3 +264,31 @@ def test_owner_link_hands_every_step_to_every_rank(world):
         p.join(120)
         assert p.exitcode == 0
     assert q.get(timeout=10)
+
+
+def test_host_wait_polls_without_a_device_wait():
+    """dist._host_wait (the owner's fence before refilling a link buffer):
+    polls Work.is_completed on the host until the broadcast has completed,
+    then calls Work.wait once (outside any stream of the library) to surface
+    its error — never a device-side wait before completion."""
+    from swraytracing_amd.dist import _host_wait
+
+    class Work:
+        def __init__(self, polls, fail=False):
+            self.polls, self.fail, self.log = polls, fail, []
+
+        def is_completed(self):
+            self.log.append("poll")
+            self.polls -= 1
+            return self.polls < 0
+
+        def wait(self):
+            self.log.append("wait")
+            if self.fail:
+                raise RuntimeError("broadcast failed")
+
+    w = Work(3)
+    _host_wait(w)
+    assert w.log == ["poll"] * 4 + ["wait"]
+    with pytest.raises(RuntimeError, match="broadcast failed"):
+        _host_wait(Work(0, fail=True))
