@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <map>
@@ -305,9 +306,17 @@ struct swrt_ctx {
   // swrt_ode23_run's first attempt: its coefficients from the device's own
   // step-size computation (ode23_first_step_kernel), and the host-mapped copy
   // {raw, absh, h, tnew, coefficients} the host checks its computation against
+  // (coherent; shown[12]: the launch's ticket, stored after the values)
   double* o_coef = nullptr;
   double* o_shown = nullptr;
   double* o_shown_d = nullptr;
+  uint64_t o_ticket = 0;  // the last first-step launch's ticket
+  // SWRT_ODE23_MARKERS=1 (environment, A/B runs): swrt_ode23_run's launches
+  // as before round 6's last change — an event marker after the first-step
+  // kernel and after the chained first attempt's part 0, a join recorded on
+  // the extra stream at the end of a split call, and the host waiting for
+  // each launch's event before reading its maxima
+  bool o23_markers = false;
   // the next swrt_ode23_run's stage 1, queued at the end of this one
   // (swrt_ode23_chain_next): armed with the slots the next call reads as its
   // slots 0 / 1; `queued` holds what it was computed from, and any API call
@@ -328,6 +337,7 @@ struct swrt_ctx {
     int first_slot = -1;
     unsigned first_wg[2] = {0, 0};
     bool split = false;
+    uint64_t first_ticket = 0;
     double rtol = 0.0, tfinal = 0.0, tmax = 0.0;
     int64_t first_taken = 0;  // calls that took it (SWRT_DEBUG_ODE23_FIRST_CHAINED)
   } o_chain;
@@ -1491,13 +1501,15 @@ int swrt_create(int device, swrt_ctx** out) {
        hipStreamCreateWithFlags(&c->sx[0], hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t& e : c->jx) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
   for (hipEvent_t& e : c->chain_ev) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-  ok = ok && hipHostMalloc((void**)&c->dev_err, sizeof(int) * 4, hipHostMallocMapped) == hipSuccess &&
+  ok = ok && hipHostMalloc((void**)&c->dev_err, sizeof(int) * 4, hipHostMallocMapped | hipHostMallocCoherent) ==
+                 hipSuccess &&
        hipHostGetDevicePointer((void**)&c->dev_err_d, c->dev_err, 0) == hipSuccess;
   if (c->dev_err) std::memset(c->dev_err, 0, sizeof(int) * 4);
   c->stream0 = c->stream;
   if (const char* e = getenv("SWRT_HAZARD_CHECK")) c->hz.on = atoi(e) != 0;
   if (const char* e = getenv("SWRT_ODE23_CHAIN_FIRST")) c->chain_first = atoi(e) != 0;
   if (const char* e = getenv("SWRT_FORK_ALWAYS")) c->fork_always = atoi(e) != 0;
+  if (const char* e = getenv("SWRT_ODE23_MARKERS")) c->o23_markers = atoi(e) != 0;
   if (!ok) {
     swrt_destroy(c);
     return SWRT_ERR_HIP;
@@ -3639,8 +3651,9 @@ int ode23_prepare(swrt_ctx* c, int nslots, Ode23Args& a, double tmax, double f, 
   }
   if (!c->o_shown) {
     HIPCHK(c, hipMalloc((void**)&c->o_coef, 8 * sizeof(double)));
-    HIPCHK(c, hipHostMalloc((void**)&c->o_shown, 12 * sizeof(double), hipHostMallocMapped));
+    HIPCHK(c, hipHostMalloc((void**)&c->o_shown, 13 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(c, hipHostGetDevicePointer((void**)&c->o_shown_d, c->o_shown, 0));
+    std::memset(c->o_shown, 0, 13 * sizeof(double));  // (ticket 0: never a launch's)
   }
   for (hipEvent_t& e : c->o_ev)
     if (!e) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -3981,6 +3994,28 @@ int swrt_ode23_run(swrt_ctx* c, double t0, double tfinal, double tmax, double f,
 }
 
 namespace {
+// The first-step kernel (the first attempt's step size on the device) on the
+// packet stream, stage 1's max slot event o_ev[sl_f1] attached to it: the
+// first attempt's part 0 follows it with no marker between them, part 1 waits
+// for that event, and the host reads the step size once the launch's ticket
+// has reached shown[12] (DeviceExec::stage1).  SWRT_ODE23_MARKERS=1: a marker
+// after it instead (~7-12 us of idle GPU before the first attempt,
+// profiles/r06_ode23).
+int ode23_first_step_queue(swrt_ctx* c, int sl_f1, double c0, double hmax, double htspan, double t0, double tfinal,
+                           bool split, uint64_t* ticket) {
+  const double tdir = std::copysign(1.0, tfinal - t0);
+  const uint64_t tk = ++c->o_ticket;
+  const hipEvent_t stop = c->o23_markers ? nullptr : c->o_ev[sl_f1];
+  // (part 1's slots start at zero, cleared here; each launch then clears its next one)
+  hipExtLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, nullptr, stop, 0,
+                        c->o_dmax + sl_f1, c0, hmax, htspan, 16 * o23_spacing(t0), tdir, t0, tfinal, c->o_coef,
+                        c->o_shown_d, c->o_dmax + 3, split ? 3 : 0, (unsigned long long)tk);
+  HIPCHK(c, hipGetLastError());
+  if (c->o23_markers) HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
+  *ticket = tk;
+  return SWRT_OK;
+}
+
 // swrt_ode23_run's stages for the controller (ode23_control, swrt_ode23_ctl.cpp):
 // each attempt one tile launch — two part launches when the binning allows
 // (ode23_split_ok), part 1 on the extra packet stream, part p keeping max
@@ -4029,6 +4064,7 @@ class DeviceExec final : public O23Exec {
       }
     }
     c->o_dmax_cur = (sl + 1) % 3;
+    if (P == 2) b_last = sl;  // the extra stream's last work
     *slot = sl;
     return SWRT_OK;
   }
@@ -4041,6 +4077,7 @@ class DeviceExec final : public O23Exec {
   // controller queues its next guess before the hook's host work
   void adopt_first(int sl, const unsigned wg_[2]) {
     first_slot = sl;
+    if (P == 2) b_last = sl;
     wg[0][sl] = wg_[0];
     wg[1][sl] = wg_[1];
     defer_hook = true;
@@ -4065,10 +4102,12 @@ class DeviceExec final : public O23Exec {
       hook_due = true;
       if (!defer_hook) HIPCHK_RC(run_hook());
     }
-    HIPCHK(c, hipEventSynchronize(c->o_ev[sl_f1]));
-    if (dev_first)
+    // (the first-step kernel's values: read once its ticket is in, no event wait)
+    if (!dev_first || c->o23_markers) HIPCHK(c, hipEventSynchronize(c->o_ev[sl_f1]));
+    if (dev_first) {
+      HIPCHK_RC(await_shown());
       std::memcpy(raw, &c->o_shown[0], sizeof(double));
-    else
+    } else
       std::memcpy(raw, c->o_hmax + sl_f1, sizeof(double));
     HIPCHK_RC(dev_err_check(c));
     return global_max(raw);
@@ -4097,15 +4136,19 @@ class DeviceExec final : public O23Exec {
     if (hook_due) HIPCHK_RC(run_hook());
     unsigned long long m = 0;
     for (int p = 0; p < P; ++p) {
-      // (polling hipEventQuery instead: 1.802 / 1.831 vs 1.849 / 1.805 ms, noise; profiles/r05_ode23)
-      HIPCHK(c, hipEventSynchronize(p == 0 ? c->o_ev[sl] : c->o_evb[sl]));
       const unsigned g = wg[p][sl];
+      // The tile launches' maxima are polled in host memory, every workgroup
+      // storing its own at its end: no wait for the launch's event, whose
+      // host wake-up trailed the kernel by ~10-20 us (the end of an interval
+      // waits for it, profiles/r06_ode23).  The per-packet kernels' copied
+      // max is read after its event.
+      // (polling hipEventQuery instead: 1.802 / 1.831 vs 1.849 / 1.805 ms, noise; profiles/r05_ode23)
+      if (g == 0 || c->o23_markers) HIPCHK(c, hipEventSynchronize(p == 0 ? c->o_ev[sl] : c->o_evb[sl]));
       if (g == 0) {
         m = std::max(m, c->o_hmax[sl]);
       } else {
-        // the launch's own completion event carries no system-scope release:
-        // each workgroup's store to the coherent host copy may land a moment
-        // after it, so an entry still marked empty is awaited
+        // (after an event too: the launch's own completion event carries no
+        // system-scope release, so a store may land a moment after it)
         const volatile unsigned long long* hp = c->o_hpart + (size_t)(3 * p + sl) * kMaxBins;
         for (unsigned i = 0; i < g; ++i) {
           unsigned long long v = hp[i];
@@ -4126,6 +4169,22 @@ class DeviceExec final : public O23Exec {
     std::memcpy(out, &m, sizeof(double));
     return global_max(out);
   }
+  // the first-step launch's values, once its ticket is in shown[12] (its
+  // event has completed; the values may land a moment after it)
+  void expect_ticket(uint64_t t) { ticket = t; }
+  int await_shown() {
+    const volatile unsigned long long* tk = reinterpret_cast<const volatile unsigned long long*>(c->o_shown + 12);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*tk != ticket) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (*tk != ticket) return fail(c, SWRT_ERR_STATE, "ode23: the first step size never reached host memory");
+        break;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return SWRT_OK;
+  }
   int await_hpart(const volatile unsigned long long* e, int p, unsigned long long* out) {
     const auto t0 = std::chrono::steady_clock::now();
     while ((*out = *e) == kHpartEmpty) {
@@ -4142,8 +4201,25 @@ class DeviceExec final : public O23Exec {
   // work; set `cur` becomes the packets (and F1), the others the spares.
   int finish(int cur, bool failed) override {
     if (split) {
-      c->b_pending = 1;
-      HIPCHK_RC(join_b(c));
+      if (!failed && b_last >= 0 && !c->o23_markers) {
+        // the join is the extra stream's last launch's own event (a marker
+        // recorded there would put ~7 us between the last attempt and the
+        // next work); none once it has completed
+        const hipEvent_t ev = c->o_evb[b_last];
+        const hipError_t q = hipEventQuery(ev);
+        if (q == hipErrorNotReady)
+          HIPCHK(c, hipStreamWaitEvent(c->stream0, ev, 0));
+        else
+          HIPCHK(c, q);
+        c->b_pending = 0;
+        if (c->hz.on) {
+          c->hz.record(ev, 1);
+          c->hz.wait(0, ev);
+        }
+      } else {
+        c->b_pending = 1;
+        HIPCHK_RC(join_b(c));
+      }
     }
     if (failed) HIPCHK(c, hipStreamSynchronize(c->stream));  // a queued guess may still be running
     const int o1 = (cur + 1) % 3, o2 = (cur + 2) % 3;
@@ -4174,6 +4250,8 @@ class DeviceExec final : public O23Exec {
   int (*reduce)(double*, void*);
   void* reduce_user;
   bool defer_hook = false, hook_due = false;
+  uint64_t ticket = 0;
+  int b_last = -1;  // the max slot of the last part-1 launch (its event: the extra stream's last work)
   struct Set {
     double *x, *k, *F;
   } S[3];
@@ -4195,15 +4273,12 @@ int ode23_chain_first(swrt_ctx* c, int sl_f1, double tmax, double f, double Cg, 
     return SWRT_OK;
   const bool split = ode23_split_ok(c);
   const double t0 = 0.0, tfinal = tmax;
-  const double tdir = std::copysign(1.0, tfinal - t0);
   const double rtol_c = std::max(rtol, 100 * 2.220446049250313e-16);
   const double htspan = std::fabs(tfinal - t0);
   const double hmax = 0.1 * htspan;
   const double c0 = 0.8 * std::pow(rtol_c, 1.0 / 3.0);
-  hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax, htspan,
-                     16 * o23_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3, split ? 3 : 0);
-  HIPCHK(c, hipGetLastError());
-  HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
+  uint64_t ticket = 0;
+  HIPCHK_RC(ode23_first_step_queue(c, sl_f1, c0, hmax, htspan, t0, tfinal, split, &ticket));
   if (split) {
     HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->o_ev[sl_f1], 0));
     if (c->hz.on) {
@@ -4216,15 +4291,23 @@ int ode23_chain_first(swrt_ctx* c, int sl_f1, double tmax, double f, double Cg, 
   if ((rc = ode23_prepare(c, 2, base, tmax, f, Cg, thr, bump))) return rc;
   DeviceExec ex(c, base, split, true, sl_f1, nullptr, nullptr);
   if ((rc = ex.queue_first())) return rc;
+  ch.first_ticket = ticket;
   ch.first_slot = ex.first();
   for (int p = 0; p < 2; ++p) ch.first_wg[p] = ex.workgroups(p, ch.first_slot);
   if (split) {
-    HIPCHK(c, hipEventRecord(c->chain_ev[0], c->stream));
-    HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->chain_ev[0], 0));
+    // one event after both parts: sx[0] waits for part 0's own (attached)
+    // event, so no marker lands on the packet stream between the attempt and
+    // the next call's next one
+    hipEvent_t p0 = c->chain_ev[0];
+    if (ch.first_wg[0] != 0 && !c->o23_markers)
+      p0 = c->o_ev[ch.first_slot];
+    else
+      HIPCHK(c, hipEventRecord(p0, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->sx[0], p0, 0));
     HIPCHK(c, hipEventRecord(c->chain_ev[1], c->sx[0]));
     if (c->hz.on) {
-      c->hz.record(c->chain_ev[0], 0);
-      c->hz.wait(1, c->chain_ev[0]);
+      c->hz.record(p0, 0);
+      c->hz.wait(1, p0);
     }
     c->tail_ev = c->chain_ev[1];
     c->chain_b = true;
@@ -4255,7 +4338,6 @@ int swrt_ode23_run_sharded(swrt_ctx* c, double t0, double tfinal, double tmax, d
   GUARD_BEGIN_KEEP_CHAIN
   HIPCHK_RC(lost_check(c));
   SlotUse slot_use(c, false, kSlots01);
-  const double tdir = std::copysign(1.0, tfinal - t0);
   const double rtol_c = std::max(rtol, 100 * 2.220446049250313e-16);
   const double thr = atol / rtol_c;
   const double htspan = std::fabs(tfinal - t0);
@@ -4296,7 +4378,9 @@ int swrt_ode23_run_sharded(swrt_ctx* c, double t0, double tfinal, double tmax, d
   // Two part launches per attempt when the binning allows.
   const bool split = ode23_split_ok(c);
   const bool first_chained = taken && first_cand && dev_first && split == ch.split;
+  uint64_t ticket = 0;  // the first-step launch's (dev_first)
   if (first_chained) {
+    ticket = ch.first_ticket;
     // queued by the previous call: stage 1, the first step (and stage 1's
     // event after it), the fork and the first attempt, whose part 1 is now
     // this call's pending split
@@ -4306,16 +4390,12 @@ int swrt_ode23_run_sharded(swrt_ctx* c, double t0, double tfinal, double tmax, d
   } else {
     HIPCHK_RC(chain_join(c));
     if (dev_first) {
-      // (part 1's slots start at zero, cleared here; each launch then clears its next one)
-      hipLaunchKernelGGL(ode23_first_step_kernel, dim3(1), dim3(64), 0, c->stream, c->o_dmax + sl_f1, c0, hmax,
-                         htspan, 16 * o23_spacing(t0), tdir, t0, tfinal, c->o_coef, c->o_shown_d, c->o_dmax + 3,
-                         split ? 3 : 0);
-      HIPCHK(c, hipGetLastError());
+      HIPCHK_RC(ode23_first_step_queue(c, sl_f1, c0, hmax, htspan, t0, tfinal, split, &ticket));
     } else {
       HIPCHK(c, hipMemcpyAsync(c->o_hmax + sl_f1, c->o_dmax + sl_f1, sizeof(unsigned long long),
                                hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
     }
-    HIPCHK(c, hipEventRecord(c->o_ev[sl_f1], c->stream));
     if (split) {
       // the fork is stage 1's own event (one marker in front of the first attempt, not two)
       HIPCHK(c, hipStreamWaitEvent(c->sx[0], c->o_ev[sl_f1], 0));
@@ -4327,6 +4407,7 @@ int swrt_ode23_run_sharded(swrt_ctx* c, double t0, double tfinal, double tmax, d
     }
   }
   DeviceExec ex(c, base, split, dev_first, sl_f1, hook, hook_user, reduce, reduce_user);
+  ex.expect_ticket(ticket);
   // the first attempt from the device's coefficients, queued now (or by the
   // previous call); the caller's hook then runs (host work that overlaps
   // stage 1 and this attempt)

@@ -106,7 +106,8 @@ __global__ void __launch_bounds__(1024) bin_scan_kernel(int* counts, int nbins, 
     }
     if (threadIdx.x == 0) {
       starts[nbins] = 0;
-      *err = 1;
+      // coherent host memory, read after events that carry no system-scope release
+      __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (order != nullptr)
       for (int b = threadIdx.x; b < nbins; b += blockDim.x) order[b] = b;

@@ -79,10 +79,14 @@ struct Ode23Args {
 // them, to host-mapped `shown`, against which the host checks its own
 // computation of the same.  `clear`/`nclear`: max slots zeroed on the way
 // (a split run's part-1 slots; no memset launch in front of the first
-// attempt).  One lane; plain vector stores.
+// attempt).  One lane; plain vector stores.  `shown` is coherent host memory
+// and the launch's own completion event carries no system-scope release: the
+// values go first, then `ticket` to shown[12] by a system-scope release
+// store, and the host reads them once it sees its ticket there.
 __global__ void ode23_first_step_kernel(const unsigned long long* dmax, double c0, double hmax, double htspan,
                                         double hmin0, double tdir, double t0, double tfinal, double* coef,
-                                        double* shown, unsigned long long* clear, int nclear) {
+                                        double* shown, unsigned long long* clear, int nclear,
+                                        unsigned long long ticket) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   for (int i = 0; i < nclear; ++i) clear[i] = 0ull;
   const unsigned long long bits = *dmax;
@@ -98,6 +102,8 @@ __global__ void ode23_first_step_kernel(const unsigned long long* dmax, double c
   shown[2] = h;
   shown[3] = tnew;
   for (int i = 0; i < 8; ++i) shown[4 + i] = cf[i];
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(shown + 12), ticket, __ATOMIC_RELEASE,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __device__ __forceinline__ void ode_rhs(const Ode23Args& a, const double ys[4], double fo[4]) {
