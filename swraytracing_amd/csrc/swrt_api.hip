@@ -1178,9 +1178,9 @@ int rebin(swrt_ctx* c, bool indirect, int tile = 0, int lanes = kTileThreads) {
     ++h.epoch;  // a new partition of the packets into tiles
   }
   if (!keys_valid) {
-    // (the last scan left the counts zero unless a counting launch has run
-    // since: no memset then, one launch fewer in front of the count)
-    if (!c->counts_zero) HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * nbins, c->stream));
+    // (skipping this memset when the last scan left the counts zero broke
+    // three GPU tests deterministically, profiles/r06_ode23/README.md: kept)
+    HIPCHK(c, hipMemsetAsync(c->bins, 0, sizeof(int) * nbins, c->stream));
     hipLaunchKernelGGL(bin_count_kernel, dim3(grid), dim3(256), sizeof(int) * nbins, c->stream, g, c->dx, n,
                        nbins, c->keys, c->bins);
     HIPCHK(c, hipGetLastError());
