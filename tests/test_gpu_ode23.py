@@ -486,14 +486,16 @@ def test_ode23_driver_longer_run_same_files_with_and_without_chaining(tmp_path, 
     """The 2-layer driver with the reference's ode23 over 48 PDE steps (its
     CFL rule, re-binning every 2nd interval, 70,000 packets so every attempt
     is split): the chained stage 1 and first attempt
-    (defaults), the chained stage 1 alone (SWRT_ODE23_CHAIN_FIRST=0) and no
-    chain at all (SWRT_ODE23_CHAIN=0) write the same packet_x / packet_k /
-    packet_time / pv files, byte for byte."""
+    (defaults), the chained stage 1 alone (SWRT_ODE23_CHAIN_FIRST=0), no
+    chain at all (SWRT_ODE23_CHAIN=0) and the launches with event markers
+    and event waits (SWRT_ODE23_MARKERS=1) write the same packet_x /
+    packet_k / packet_time / pv files, byte for byte."""
     import swraytracing_amd as sw
     from swraytracing_amd import _lib as L
     out = {}
-    for name, env in (("first", {}), ("stage1", {"SWRT_ODE23_CHAIN_FIRST": "0"}), ("off", {"SWRT_ODE23_CHAIN": "0"})):
-        for k_, v in (("SWRT_ODE23_CHAIN_FIRST", None), ("SWRT_ODE23_CHAIN", None)):
+    for name, env in (("first", {}), ("stage1", {"SWRT_ODE23_CHAIN_FIRST": "0"}), ("off", {"SWRT_ODE23_CHAIN": "0"}),
+                      ("markers", {"SWRT_ODE23_MARKERS": "1"})):
+        for k_, v in (("SWRT_ODE23_CHAIN_FIRST", None), ("SWRT_ODE23_CHAIN", None), ("SWRT_ODE23_MARKERS", None)):
             monkeypatch.delenv(k_, raising=False)
         for k_, v in env.items():
             monkeypatch.setenv(k_, v)
@@ -511,6 +513,7 @@ def test_ode23_driver_longer_run_same_files_with_and_without_chaining(tmp_path, 
     assert chained >= 30 and first >= 30, (chained, first)
     assert out["stage1"][1] >= 30 and out["stage1"][2] == 0
     assert out["off"][1] == 0 and out["off"][2] == 0
-    for name in ("stage1", "off"):
+    assert out["markers"][1] >= 30 and out["markers"][2] >= 30
+    for name in ("stage1", "off", "markers"):
         for fn, b in files.items():
             assert len(b) > 0 and out[name][0][fn] == b, (name, fn)
