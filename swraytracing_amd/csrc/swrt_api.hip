@@ -4048,6 +4048,16 @@ class DeviceExec final : public O23Exec {
     a.ynk = S[to].k;
     attempt_coeffs(a, ta, ha, tnewa);
     const int sl = c->o_dmax_cur;
+    // The host polls a slot's maxima without waiting for the launch's event
+    // (wait_max), so a launch whose maxima were never read (a guess its
+    // gate discarded; in a sharded run one that ran on this rank's part of
+    // the max) must have finished before its slot's host copy is re-marked
+    // empty for this launch.  Its events still hold that launch.
+    if (unread[sl]) {
+      HIPCHK(c, hipEventSynchronize(c->o_ev[sl]));
+      if (P == 2) HIPCHK(c, hipEventSynchronize(c->o_evb[sl]));
+    }
+    unread[sl] = true;
     a.gate_scale = gscale;
     a.gate_limit = glimit;
     for (int p = 0; p < P; ++p) {
@@ -4082,6 +4092,7 @@ class DeviceExec final : public O23Exec {
   // controller queues its next guess before the hook's host work
   void adopt_first(int sl, const unsigned wg_[2]) {
     first_slot = sl;
+    unread[sl] = true;
     if (P == 2) b_last = sl;
     wg[0][sl] = wg_[0];
     wg[1][sl] = wg_[1];
@@ -4139,6 +4150,7 @@ class DeviceExec final : public O23Exec {
   // value max of these non-negative doubles, as the device's atomicMax)
   int wait_max(int sl, double* out) override {
     if (hook_due) HIPCHK_RC(run_hook());
+    unread[sl] = false;
     unsigned long long m = 0;
     for (int p = 0; p < P; ++p) {
       const unsigned g = wg[p][sl];
@@ -4257,6 +4269,7 @@ class DeviceExec final : public O23Exec {
   bool defer_hook = false, hook_due = false;
   uint64_t ticket = 0;
   int b_last = -1;  // the max slot of the last part-1 launch (its event: the extra stream's last work)
+  bool unread[3] = {false, false, false};  // a launch in this slot whose maxima wait_max has not read
   struct Set {
     double *x, *k, *F;
   } S[3];
